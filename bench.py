@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark: all-sources SPF on the 100x100 grid (BASELINE.json metric).
+
+A "step" = one all-sources pass: every node of the topology is a source, the
+sources are split in contiguous blocks over the ranks (one process per GPU,
+strong scaling: total work is fixed), each rank runs ONE engine launch over its
+block through the C-ABI (openr_spf_solve_device) on device-resident buffers.
+Inputs (CSR replica, source list) are resident in HBM before the timed region;
+outputs (u64 distances + next-hop bitsets) are written to HBM.
+
+Timed region: barrier + synchronize, K steps, barrier + synchronize; the max
+over ranks is reported. The RCCL all-gather of the result shards is measured
+after the timed region and reported separately ("gather"), see DESIGN.md.
+
+roofline.achieved = algorithmic bytes per launch / mean kernel duration, with
+B(src) = 4(V+1) + 8E + V(8 + ceil(deg(src)/8))  (SURVEY.md §8d).
+cpu_baseline = the CPU oracle (C restatement of LinkState::runSpf) on a bounded
+sample of the same sources, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "all-sources SPF solves/sec + edge relax/s (% HBM roofline), 10k-node grid, 1-8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def build_topology(name: str):
+    from openr_amd import topology as T
+
+    if name == "grid100":
+        return T.grid_fast(100), {"workload": "grid100-all-sources", "nodes": 10000, "links": 19800}
+    if name == "fabric":
+        g = T.fabric(5000)
+        return g, {"workload": "fabric5000-all-sources", "nodes": g.num_nodes, "links": g.num_links}
+    if name == "wan":
+        g = T.wan(1000, 3000, 64, seed=1)
+        return g, {"workload": "wan1k-all-sources", "nodes": g.num_nodes, "links": g.num_links}
+    raise SystemExit(f"unknown --topology {name}")
+
+
+def algorithmic_bytes(g, sources: np.ndarray) -> int:
+    """Σ B(src), B = 4(V+1) + 8E + V(8 + ceil(deg(src)/8))."""
+    V, E = g.num_nodes, g.num_dir_edges
+    deg = np.array([len(set(g.col[g.row_ptr[u]:g.row_ptr[u + 1]].tolist())) for u in range(V)], dtype=np.int64)
+    per = 4 * (V + 1) + 8 * E + V * (8 + (deg[sources] + 7) // 8)
+    return int(per.sum())
+
+
+def cpu_baseline(g, seconds: float, use_metric: bool):
+    from oracle import Oracle
+
+    o = Oracle(g)
+    V = g.num_nodes
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a small strided sample, then size the timed sample to ~`seconds`
+    probe = np.arange(0, V, max(1, V // 32), dtype=np.uint32)[:32]
+    t0 = time.perf_counter()
+    o.all_sources(probe, use_metric, nthreads=1, want_dist=True, want_nh=False)
+    per_solve_1t = (time.perf_counter() - t0) / len(probe)
+    n = int(min(V, max(nthreads, seconds * nthreads / max(per_solve_1t, 1e-9))))
+    sample = np.linspace(0, V - 1, n).astype(np.uint32)
+    t0 = time.perf_counter()
+    o.all_sources(sample, use_metric, nthreads=nthreads, want_dist=True, want_nh=True)
+    dt = time.perf_counter() - t0
+    try:
+        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        cpu_model = "unknown"
+    return {
+        "value": n / dt,
+        "unit": "solves/s",
+        "cores": nthreads,
+        "kind": "port",
+        "sample": f"{n} of {V} sources (evenly spaced), dist+next-hops, {nthreads} pthreads, {dt:.1f}s; {cpu_model}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--topology", default="grid100", choices=["grid100", "fabric", "wan"])
+    ap.add_argument("--no-metric", action="store_true", help="hop-count SPF (useLinkMetric=false)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from openr_amd.engine import SpfEngine
+
+    g, cfg = build_topology(args.topology)
+    V = g.num_nodes
+    eng = SpfEngine([local_rank])
+    eng.set_graph(g)
+    nb = eng.nh_bytes
+    use_metric = not args.no_metric
+
+    # contiguous source blocks per rank (shard.py semantics)
+    from openr_amd.shard import shard_range
+
+    lo, hi = shard_range(V, rank, world)
+    n_local = hi - lo
+    src = torch.arange(lo, hi, dtype=torch.int32, device=dev)
+    d_dist = torch.empty((n_local, V), dtype=torch.int64, device=dev)
+    d_nh = torch.empty((n_local, V, nb), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.solve_device(src.data_ptr(), n_local, d_dist.data_ptr(), d_nh.data_ptr(), nb, use_metric,
+                         stream=stream.cuda_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness spot check (grid: Manhattan distances) outside the timed region
+    if args.topology == "grid100" and n_local:
+        n = 100
+        rows = [0, n_local - 1]
+        host = d_dist[rows].cpu().numpy().view(np.uint64)
+        a = np.arange(V)
+        for r, s in zip(rows, [lo, hi - 1]):
+            exp = np.abs(s % n - a % n) + np.abs(s // n - a // n)
+            assert np.array_equal(host[rows.index(r)].astype(np.int64), exp), "bench result check failed"
+
+    gather = None
+    if world > 1 and not args.no_gather:
+        from openr_amd.shard import allgather_results
+
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = time.perf_counter()
+        allgather_results(d_dist, d_nh, V, world)
+        torch.cuda.synchronize(dev)
+        gms = (time.perf_counter() - tg) * 1e3
+        t = torch.tensor([gms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gather = {"ms": float(t.item()), "bytes": int(V * V * (8 + nb)),
+                  "gather_inclusive_value": V / (elapsed / args.steps + float(t.item()) / 1e3)}
+
+    solves_total = V * args.steps
+    value = solves_total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    sources_local = np.arange(lo, hi)
+    bytes_launch = algorithmic_bytes(g, sources_local) if n_local else 0
+    mean_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    achieved = bytes_launch / mean_kernel_s / 1e9 if mean_kernel_s > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("topology") == args.topology and tj.get("n_sources") == n_local:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (reference benchmark grid generator, unit metrics)",
+            "config": dict(cfg, **{"sources_per_step": V, "use_link_metric": use_metric,
+                                   "parallelism": f"source-sharded x{world}"}),
+            "edge_relax_per_s": value * g.num_dir_edges,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel_ms_mean": mean_kernel_s * 1e3,
+                "bytes_per_launch": bytes_launch,
+            },
+        }
+        if gather is not None:
+            out["gather"] = gather
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(g, args.cpu_seconds, use_metric)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

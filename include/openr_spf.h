@@ -1,0 +1,153 @@
+/*
+ * openr_spf.h — C-ABI of the MI355X-native SPF engine for OpenR's Decision module.
+ *
+ * This is the drop-in boundary under openr::LinkState. Each entry point names
+ * the reference interface it replaces:
+ *
+ *   openr_spf_set_graph        LinkState topology mirror; call wherever the reference
+ *                              clears its SPF memo: updateAdjacencyDatabase
+ *                              (LinkState.cpp:714-717), deleteAdjacencyDatabase
+ *                              (:730-731), decrementHolds (:509-512)
+ *   openr_spf_solve            LinkState::runSpf(src, useLinkMetric)  (LinkState.cpp:808-882,
+ *                              LinkState.h:436-443), batched over sources; the memoized
+ *                              LinkState::getSpfResult (LinkState.cpp:793-803) and the
+ *                              per-neighbour LFA solves of SpfSolver::getNextHopsWithMetric
+ *                              (Decision.cpp:1170-1204) are batches of this call
+ *   openr_spf_solve_ignore     LinkState::runSpf(src, true, linksToIgnore) as used by
+ *                              getKthPaths k>=2 (LinkState.cpp:769-779) and per-link-failure
+ *                              what-if sweeps; one (source, ignore-set) pair per solve
+ *   openr_spf_solve_device     the same on device-resident buffers and a caller stream
+ *                              (batched prefetch / benchmarks / multi-GPU shards)
+ *   openr_spf_last_error       glog CHECK / exception text of the reference
+ *
+ * Conventions
+ *   - All functions return 0 (OPENR_SPF_OK) or a negative errno-style code; no C++
+ *     exception crosses the ABI. openr_spf_last_error() returns a thread-local message.
+ *   - Host output buffers are caller-owned. Device memory is library-owned except in
+ *     openr_spf_solve_device, where every pointer is device memory owned by the caller.
+ *   - A context is single-threaded (one per LinkState, matching the reference's
+ *     threading: everything in Decision runs on one event-base thread). Host-buffer calls
+ *     are synchronous on return.
+ *   - There is no CPU fallback: if the HIP runtime or a device is unavailable,
+ *     openr_spf_create fails with OPENR_SPF_ENODEV.
+ *
+ * Semantics (bit-exact with LinkState::runSpf for strictly positive metrics)
+ *   dist[s][v]   u64 shortest distance (NodeSpfResult::metric), UINT64_MAX if v is not
+ *                in the SpfResult (unreachable). dist[s][src] = 0.
+ *   nh[s][v][b]  next-hop set of v as a bitset over the source's DISTINCT neighbours in
+ *                CSR row order: bit i (byte i/8, bit i%8) <-> the i-th distinct `col`
+ *                value of row src (openr_spf_neighbor_map). nh bits of src itself are 0.
+ *   tight[s][w]  (OPENR_SPF_EMIT_TIGHT) bit e of the E-bit mask is set iff directed edge e
+ *                u->v is on a shortest path: usable, dist[u]+w(e)==dist[v], and u may
+ *                expand (u==src or !node_overloaded[u]). NodeSpfResult::pathLinks(v) is
+ *                the tight in-edges of v ordered by (dist[u], name_rank[u]) then by
+ *                position of e in row u.
+ *   A directed edge is usable iff edge_up[e] and link_id[e] is not in the solve's
+ *   ignore set. Overloaded nodes other than the source are reached but never expanded.
+ *   Metrics of usable edges must lie in [1, 2^31-1] when OPENR_SPF_USE_LINK_METRIC is
+ *   set (the i32 Adjacency.metric range); zero or wrapped-negative metrics make the
+ *   reference's pop order history-dependent and are rejected with OPENR_SPF_ENOTSUP.
+ */
+#ifndef OPENR_SPF_H
+#define OPENR_SPF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OPENR_SPF_ABI_VERSION 1
+
+enum {
+  OPENR_SPF_OK = 0,
+  OPENR_SPF_EIO = -5,       /* HIP runtime error */
+  OPENR_SPF_ENOMEM = -12,   /* host or device allocation failed */
+  OPENR_SPF_ENODEV = -19,   /* no usable GPU / HIP runtime */
+  OPENR_SPF_EINVAL = -22,   /* bad argument (null, out of range, no graph set) */
+  OPENR_SPF_E2BIG = -7,     /* graph too large for the engine (see openr_spf_limits) */
+  OPENR_SPF_ENOTSUP = -95,  /* metric outside [1, 2^31-1] on a usable edge */
+};
+
+enum {
+  OPENR_SPF_USE_LINK_METRIC = 1u << 0, /* runSpf useLinkMetric; else every hop costs 1 */
+  OPENR_SPF_EMIT_TIGHT = 1u << 1,      /* fill tight[] (pathLinks reconstruction)      */
+};
+
+typedef struct openr_spf_ctx openr_spf_ctx;
+
+/* CSR mirror of LinkState::linkMap_ (LinkState.h:456-467). Row u lists u's
+   directed edges in LinkState::linksFromNode(u) iteration order. Every link id
+   appears exactly twice (u->v and v->u). Arrays are copied by set_graph. */
+typedef struct {
+  uint32_t num_nodes;               /* V */
+  uint32_t num_dir_edges;           /* E */
+  uint32_t num_links;               /* L: link ids are in [0, L) */
+  const uint32_t* row_ptr;          /* [V+1] */
+  const uint32_t* col;              /* [E] neighbour node id */
+  const uint64_t* metric;           /* [E] Link::getMetricFromNode(u) (hold-aware value()) */
+  const uint32_t* link_id;          /* [E] undirected link id */
+  const uint8_t* edge_up;           /* [E] Link::isUp() */
+  const uint8_t* node_overloaded;   /* [V] LinkState::isNodeOverloaded() */
+  const uint32_t* name_rank;        /* [V] rank of the node name under std::string < */
+} openr_spf_graph;
+
+typedef struct {
+  uint32_t max_nodes;       /* largest V the engine accepts */
+  uint32_t max_nh_bits;     /* largest distinct degree (next-hop bitset width) */
+} openr_spf_limits_t;
+
+typedef struct {
+  uint64_t spf_runs;        /* logical SPFs solved (fb303 decision.spf_runs) */
+  uint64_t batches;         /* solve calls */
+  double last_batch_ms;     /* wall time of the last host-buffer solve (decision.spf_ms) */
+  double last_kernel_ms;    /* device time of the last solve's kernels */
+} openr_spf_stats_t;
+
+int openr_spf_abi_version(void);
+const char* openr_spf_last_error(void);
+void openr_spf_limits(openr_spf_limits_t* out);
+
+/* device_ids: n_devices HIP ordinals (NULL -> the current device). Sources of one
+   solve call are split in contiguous blocks across the devices. */
+int openr_spf_create(const int* device_ids, int n_devices, openr_spf_ctx** out);
+void openr_spf_destroy(openr_spf_ctx* ctx);
+
+int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* graph);
+
+/* Minimum nh_bytes for the current graph: ceil(max distinct degree / 8), >= 1. */
+int openr_spf_nh_bytes(const openr_spf_ctx* ctx, uint32_t* out_nh_bytes);
+
+/* Distinct neighbours of src in row order (next-hop bit i -> out_nbrs[i]). */
+int openr_spf_neighbor_map(const openr_spf_ctx* ctx, uint32_t src, uint32_t* out_nbrs,
+                           uint32_t capacity, uint32_t* out_count);
+
+/* Batched SPF from sources[0..n): dist [n][V]; nh [n][V][nh_bytes] (nh_bytes >=
+   openr_spf_nh_bytes, or nh == NULL); tight [n][ceil(E/64)] or NULL. */
+int openr_spf_solve(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n,
+                    uint32_t flags, uint64_t* dist, uint8_t* nh, uint32_t nh_bytes,
+                    uint64_t* tight);
+
+/* As openr_spf_solve with a per-solve ignore set: solve i ignores the links
+   ignore_links[ignore_ptr[i] .. ignore_ptr[i+1]) (ignore_ptr has n+1 entries). */
+int openr_spf_solve_ignore(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n,
+                           uint32_t flags, const uint32_t* ignore_ptr,
+                           const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
+                           uint32_t nh_bytes, uint64_t* tight);
+
+/* Device-buffer form on device `device_index` of the context (an index into the
+   device_ids given to create). All pointers are device memory; d_ignore_ptr may be
+   NULL (no ignore sets); d_nh / d_tight may be NULL. `stream` is a hipStream_t
+   (NULL = the context's own stream). Asynchronous: returns after enqueueing. */
+int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index,
+                           const uint32_t* d_sources, uint32_t n, uint32_t flags,
+                           const uint32_t* d_ignore_ptr, const uint32_t* d_ignore_links,
+                           uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes,
+                           uint64_t* d_tight, void* stream);
+
+int openr_spf_get_stats(const openr_spf_ctx* ctx, openr_spf_stats_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPENR_SPF_H */

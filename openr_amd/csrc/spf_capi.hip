@@ -1,0 +1,494 @@
+// spf_capi.hip — host side of the C-ABI declared in include/openr_spf.h.
+//
+// Owns the per-device CSR replicas (one DevGraph per GPU of the context), picks the
+// kernel for a solve (uniform-cost BFS or settle-safe buckets), splits a batch of
+// sources across the context's devices and moves results. There is deliberately no
+// CPU path: every solve runs on the GPU or fails with an error code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/openr_spf.h"
+#include "spf_kernels.h"
+
+using namespace openr_spf;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(OPENR_SPF_EIO, "%s failed: %s", #expr, hipGetErrorString(_e));       \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Device {
+  int ordinal = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  DevGraph g;
+  // scratch for host-buffer solves
+  DevBuf<uint32_t> src, ign_ptr, ign_links;
+  DevBuf<uint64_t> dist, tight;
+  DevBuf<uint8_t> nh;
+};
+
+void free_graph(DevGraph& g) {
+  void* ptrs[] = {g.row, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  g = DevGraph{};
+}
+
+}  // namespace
+
+struct openr_spf_ctx {
+  std::vector<Device> devs;
+  bool has_graph = false;
+  uint32_t V = 0, E = 0, L = 0;
+  std::vector<uint32_t> row_ptr, col;
+  uint32_t nh_bits = 0;         // max distinct degree
+  uint32_t w_min = 0, w_max = 0;
+  bool metric_ok = true;        // every usable metric in [1, 2^31-1]
+  uint32_t group_lanes = 4;
+  openr_spf_stats_t stats{};
+};
+
+namespace {
+
+struct Plan {
+  bool bfs = true;
+  uint64_t cost = 1;
+  uint32_t delta = 1;
+  bool dist64 = false;
+  int nh_mode = kNhByte;
+};
+
+int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
+  const bool use_metric = (flags & OPENR_SPF_USE_LINK_METRIC) != 0;
+  if (use_metric && !ctx->metric_ok)
+    return fail(OPENR_SPF_ENOTSUP,
+                "usable edge metric outside [1, 2^31-1]: the reference's (metric, name) pop order is "
+                "history-dependent for such metrics and the engine does not emulate it");
+  p->nh_mode = nh_mode_for_bits(ctx->nh_bits);
+  if (p->nh_mode < 0) return fail(OPENR_SPF_E2BIG, "max distinct degree %u exceeds 256", ctx->nh_bits);
+  if (!use_metric || ctx->w_min == ctx->w_max) {
+    p->bfs = true;
+    p->cost = use_metric ? std::max<uint32_t>(ctx->w_min, 1u) : 1u;
+    if (!bfs_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode))
+      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident BFS kernel", ctx->V);
+  } else {
+    p->bfs = false;
+    p->delta = ctx->w_min;
+    p->dist64 = (uint64_t)ctx->V * ctx->w_max >= 0xFFFFFFFFull;
+    if (!bucket_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64))
+      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident bucket kernel", ctx->V);
+  }
+  return OPENR_SPF_OK;
+}
+
+hipError_t launch(const openr_spf_ctx* ctx, const Device& d, const Plan& p, const SolveArgs& a,
+                  hipStream_t s) {
+  LaunchInfo info;
+  if (p.bfs) return launch_bfs(d.g, a, p.cost, p.nh_mode, (int)ctx->group_lanes, d.num_cus, s, &info);
+  return launch_bucket(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+}
+
+int check_solve_args(const openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint64_t* dist,
+                     uint8_t* nh, uint32_t nh_bytes) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (n && (!sources || !dist)) return fail(OPENR_SPF_EINVAL, "null sources or dist");
+  const uint32_t need = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
+  if (nh && nh_bytes < need) return fail(OPENR_SPF_EINVAL, "nh_bytes %u < required %u", nh_bytes, need);
+  return OPENR_SPF_OK;
+}
+
+int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
+               const uint32_t* ignore_ptr, const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
+               uint32_t nh_bytes, uint64_t* tight) {
+  int rc = check_solve_args(ctx, sources, n, dist, nh, nh_bytes);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < n; ++i)
+    if (sources[i] >= ctx->V) return fail(OPENR_SPF_EINVAL, "source %u out of range (V=%u)", sources[i], ctx->V);
+  if (ignore_ptr) {
+    if (ignore_ptr[0] != 0) return fail(OPENR_SPF_EINVAL, "ignore_ptr[0] must be 0");
+    for (uint32_t i = 0; i < n; ++i)
+      if (ignore_ptr[i + 1] < ignore_ptr[i]) return fail(OPENR_SPF_EINVAL, "ignore_ptr not monotone");
+    if (ignore_ptr[n] && !ignore_links) return fail(OPENR_SPF_EINVAL, "null ignore_links");
+  }
+  Plan plan;
+  rc = make_plan(ctx, flags, ignore_ptr != nullptr, &plan);
+  if (rc) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t V = ctx->V, tw = (ctx->E + 63u) / 64u;
+  const uint32_t nd = (uint32_t)ctx->devs.size();
+  const uint32_t per = (n + nd - 1) / std::max<uint32_t>(nd, 1);
+  std::vector<uint32_t> rebased;
+  for (uint32_t di = 0; di < nd; ++di) {
+    Device& d = ctx->devs[di];
+    const uint32_t b = std::min(n, di * per), e = std::min(n, b + per), m = e - b;
+    if (!m) continue;
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(d.src.reserve(m));
+    HIP_TRY(d.dist.reserve((size_t)m * V));
+    if (nh) HIP_TRY(d.nh.reserve((size_t)m * V * nh_bytes));
+    if (tight) HIP_TRY(d.tight.reserve((size_t)m * tw));
+    HIP_TRY(hipMemcpyAsync(d.src.p, sources + b, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    SolveArgs a{};
+    a.sources = d.src.p;
+    a.n = m;
+    if (ignore_ptr) {
+      const uint32_t lb = ignore_ptr[b], le = ignore_ptr[e];
+      rebased.resize(m + 1);
+      for (uint32_t i = 0; i <= m; ++i) rebased[i] = ignore_ptr[b + i] - lb;
+      HIP_TRY(d.ign_ptr.reserve(m + 1));
+      HIP_TRY(d.ign_links.reserve(std::max<uint32_t>(le - lb, 1u)));
+      HIP_TRY(hipMemcpy(d.ign_ptr.p, rebased.data(), (m + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+      if (le > lb)
+        HIP_TRY(hipMemcpyAsync(d.ign_links.p, ignore_links + lb, (le - lb) * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, d.stream));
+      a.ign_ptr = d.ign_ptr.p;
+      a.ign_links = d.ign_links.p;
+    }
+    a.dist = d.dist.p;
+    a.nh = nh ? d.nh.p : nullptr;
+    a.nh_bytes = nh_bytes;
+    a.tight = tight ? d.tight.p : nullptr;
+    a.nh_bits = ctx->nh_bits;
+    HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
+    HIP_TRY(launch(ctx, d, plan, a, d.stream));
+    HIP_TRY(hipEventRecord(d.ev_end, d.stream));
+    HIP_TRY(hipMemcpyAsync(dist + (size_t)b * V, d.dist.p, (size_t)m * V * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, d.stream));
+    if (nh)
+      HIP_TRY(hipMemcpyAsync(nh + (size_t)b * V * nh_bytes, d.nh.p, (size_t)m * V * nh_bytes,
+                             hipMemcpyDeviceToHost, d.stream));
+    if (tight)
+      HIP_TRY(hipMemcpyAsync(tight + (size_t)b * tw, d.tight.p, (size_t)m * tw * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, d.stream));
+  }
+  double kms = 0.0;
+  for (uint32_t di = 0; di < nd; ++di) {
+    Device& d = ctx->devs[di];
+    const uint32_t b = std::min(n, di * per), e = std::min(n, b + per);
+    if (e <= b) continue;
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
+    kms = std::max(kms, (double)ms);
+  }
+  ctx->stats.spf_runs += n;
+  ctx->stats.batches += 1;
+  ctx->stats.last_kernel_ms = kms;
+  ctx->stats.last_batch_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return OPENR_SPF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int openr_spf_abi_version(void) { return OPENR_SPF_ABI_VERSION; }
+
+const char* openr_spf_last_error(void) { return g_last_error.c_str(); }
+
+void openr_spf_limits(openr_spf_limits_t* out) {
+  if (!out) return;
+  // Largest V whose LDS-resident BFS state (<= 8 next-hop bits, no ignore set) fits a CU.
+  uint32_t lo = 1, hi = 65535;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) / 2;
+    if (bfs_lds_bytes(mid, 0, false, kNhByte)) lo = mid;
+    else hi = mid - 1;
+  }
+  out->max_nodes = lo;
+  out->max_nh_bits = 256;
+}
+
+int openr_spf_create(const int* device_ids, int n_devices, openr_spf_ctx** out) {
+  if (!out) return fail(OPENR_SPF_EINVAL, "null out");
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0)
+    return fail(OPENR_SPF_ENODEV, "no HIP device available (%s); the engine has no CPU path",
+                e == hipSuccess ? "count=0" : hipGetErrorString(e));
+  std::vector<int> ids;
+  if (!device_ids || n_devices <= 0) {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    ids.push_back(cur);
+  } else {
+    for (int i = 0; i < n_devices; ++i) {
+      if (device_ids[i] < 0 || device_ids[i] >= count)
+        return fail(OPENR_SPF_EINVAL, "device id %d out of range (count=%d)", device_ids[i], count);
+      ids.push_back(device_ids[i]);
+    }
+  }
+  auto* ctx = new (std::nothrow) openr_spf_ctx();
+  if (!ctx) return fail(OPENR_SPF_ENOMEM, "out of host memory");
+  for (int id : ids) {
+    Device d;
+    d.ordinal = id;
+    hipDeviceProp_t prop;
+    if (hipSetDevice(id) != hipSuccess || hipGetDeviceProperties(&prop, id) != hipSuccess ||
+        hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&d.ev_begin) != hipSuccess || hipEventCreate(&d.ev_end) != hipSuccess) {
+      openr_spf_destroy(ctx);
+      return fail(OPENR_SPF_ENODEV, "failed to initialise HIP device %d", id);
+    }
+    d.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    ctx->devs.push_back(d);
+  }
+  *out = ctx;
+  return OPENR_SPF_OK;
+}
+
+void openr_spf_destroy(openr_spf_ctx* ctx) {
+  if (!ctx) return;
+  for (Device& d : ctx->devs) {
+    (void)hipSetDevice(d.ordinal);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    free_graph(d.g);
+    d.src.release();
+    d.ign_ptr.release();
+    d.ign_links.release();
+    d.dist.release();
+    d.tight.release();
+    d.nh.release();
+    if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
+    if (d.ev_end) (void)hipEventDestroy(d.ev_end);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete ctx;
+}
+
+int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
+  if (!ctx || !gr) return fail(OPENR_SPF_EINVAL, "null argument");
+  const uint32_t V = gr->num_nodes, E = gr->num_dir_edges, L = gr->num_links;
+  if (!gr->row_ptr || !gr->node_overloaded || !gr->name_rank || (E && (!gr->col || !gr->metric || !gr->link_id ||
+                                                                      !gr->edge_up)))
+    return fail(OPENR_SPF_EINVAL, "null graph array");
+  if (V >= kEdgeDown) return fail(OPENR_SPF_E2BIG, "too many nodes");
+  if (gr->row_ptr[0] != 0 || gr->row_ptr[V] != E) return fail(OPENR_SPF_EINVAL, "row_ptr must span [0, E]");
+  for (uint32_t u = 0; u < V; ++u)
+    if (gr->row_ptr[u + 1] < gr->row_ptr[u]) return fail(OPENR_SPF_EINVAL, "row_ptr not monotone at %u", u);
+
+  std::vector<uint32_t> adj(E), w(E), win(E), rev(E), lid(E), owner(E);
+  std::vector<uint16_t> nbr(E);
+  std::vector<uint8_t> ovl(V);
+  // link id -> its two directed edges
+  std::vector<uint32_t> first(L, UINT32_MAX), second(L, UINT32_MAX);
+  uint32_t nh_bits = 0, w_min = UINT32_MAX, w_max = 0;
+  bool metric_ok = true;
+  std::vector<uint32_t> seen_stamp(V, UINT32_MAX), seen_idx(V, 0);
+  for (uint32_t u = 0; u < V; ++u) {
+    ovl[u] = gr->node_overloaded[u] ? 1 : 0;
+    uint32_t nd = 0;
+    for (uint32_t e = gr->row_ptr[u]; e < gr->row_ptr[u + 1]; ++e) {
+      const uint32_t v = gr->col[e], l = gr->link_id[e];
+      if (v >= V) return fail(OPENR_SPF_EINVAL, "col[%u]=%u out of range", e, v);
+      if (l >= L) return fail(OPENR_SPF_EINVAL, "link_id[%u]=%u out of range", e, l);
+      owner[e] = u;
+      if (seen_stamp[v] != u) {
+        seen_stamp[v] = u;
+        seen_idx[v] = nd++;
+      }
+      nbr[e] = (uint16_t)std::min<uint32_t>(seen_idx[v], 0xFFFFu);
+      if (first[l] == UINT32_MAX) first[l] = e;
+      else if (second[l] == UINT32_MAX) second[l] = e;
+      else return fail(OPENR_SPF_EINVAL, "link %u appears more than twice", l);
+      lid[e] = l;
+      const bool up = gr->edge_up[e] != 0;
+      adj[e] = v | (up ? 0u : kEdgeDown);
+      const uint64_t m = gr->metric[e];
+      w[e] = (uint32_t)std::min<uint64_t>(m, 0xFFFFFFFFull);
+      if (up) {
+        if (m == 0 || m > 0x7FFFFFFFull) metric_ok = false;
+        else {
+          w_min = std::min<uint32_t>(w_min, (uint32_t)m);
+          w_max = std::max<uint32_t>(w_max, (uint32_t)m);
+        }
+      }
+    }
+    nh_bits = std::max(nh_bits, nd);
+  }
+  for (uint32_t l = 0; l < L; ++l) {
+    if (first[l] == UINT32_MAX) continue;  // unused id
+    const uint32_t a = first[l], b = second[l];
+    if (b == UINT32_MAX) return fail(OPENR_SPF_EINVAL, "link %u has a single direction", l);
+    if (gr->col[a] != owner[b] || gr->col[b] != owner[a])
+      return fail(OPENR_SPF_EINVAL, "link %u directions do not mirror each other", l);
+    if ((gr->edge_up[a] != 0) != (gr->edge_up[b] != 0))
+      return fail(OPENR_SPF_EINVAL, "link %u edge_up differs by direction (Link::isUp is per link)", l);
+    rev[a] = b;
+    rev[b] = a;
+  }
+  for (uint32_t e = 0; e < E; ++e) win[e] = w[rev[e]];
+  if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
+  if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
+
+  for (Device& d : ctx->devs) {
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    free_graph(d.g);
+    DevGraph g;
+    g.V = V;
+    g.E = E;
+    g.L = L;
+    auto up = [&](auto** dst, const auto* srcp, size_t count) -> hipError_t {
+      using T = std::remove_pointer_t<std::remove_pointer_t<decltype(dst)>>;
+      hipError_t err = hipMalloc(reinterpret_cast<void**>(dst), std::max<size_t>(count, 1) * sizeof(T));
+      if (err != hipSuccess) return err;
+      if (count) err = hipMemcpy(*dst, srcp, count * sizeof(T), hipMemcpyHostToDevice);
+      return err;
+    };
+    hipError_t err = up(&g.row, gr->row_ptr, V + 1);
+    if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
+    if (err == hipSuccess) err = up(&g.w, w.data(), E);
+    if (err == hipSuccess) err = up(&g.win, win.data(), E);
+    if (err == hipSuccess) err = up(&g.rev, rev.data(), E);
+    if (err == hipSuccess) err = up(&g.lid, lid.data(), E);
+    if (err == hipSuccess) err = up(&g.nbr, nbr.data(), E);
+    if (err == hipSuccess) err = up(&g.ovl, ovl.data(), V);
+    d.g = g;
+    if (err != hipSuccess) {
+      ctx->has_graph = false;
+      return fail(OPENR_SPF_ENOMEM, "graph upload failed: %s", hipGetErrorString(err));
+    }
+  }
+  ctx->V = V;
+  ctx->E = E;
+  ctx->L = L;
+  ctx->row_ptr.assign(gr->row_ptr, gr->row_ptr + V + 1);
+  ctx->col.assign(gr->col, gr->col + E);
+  ctx->nh_bits = nh_bits;
+  ctx->w_min = w_min;
+  ctx->w_max = w_max;
+  ctx->metric_ok = metric_ok;
+  const uint32_t avg = V ? (E + V - 1) / V : 1;
+  uint32_t gl = 1;
+  while (gl < avg && gl < 64) gl <<= 1;
+  ctx->group_lanes = gl;
+  ctx->has_graph = true;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_nh_bytes(const openr_spf_ctx* ctx, uint32_t* out) {
+  if (!ctx || !out) return fail(OPENR_SPF_EINVAL, "null argument");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set");
+  *out = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_neighbor_map(const openr_spf_ctx* ctx, uint32_t src, uint32_t* out_nbrs, uint32_t capacity,
+                           uint32_t* out_count) {
+  if (!ctx || !out_count) return fail(OPENR_SPF_EINVAL, "null argument");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set");
+  if (src >= ctx->V) return fail(OPENR_SPF_EINVAL, "source out of range");
+  uint32_t n = 0;
+  for (uint32_t e = ctx->row_ptr[src]; e < ctx->row_ptr[src + 1]; ++e) {
+    const uint32_t v = ctx->col[e];
+    bool dup = false;
+    for (uint32_t f = ctx->row_ptr[src]; f < e && !dup; ++f) dup = ctx->col[f] == v;
+    if (dup) continue;
+    if (out_nbrs && n < capacity) out_nbrs[n] = v;
+    ++n;
+  }
+  *out_count = n;
+  if (out_nbrs && n > capacity) return fail(OPENR_SPF_EINVAL, "capacity %u < %u neighbours", capacity, n);
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_solve(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags, uint64_t* dist,
+                    uint8_t* nh, uint32_t nh_bytes, uint64_t* tight) {
+  return solve_host(ctx, sources, n, flags, nullptr, nullptr, dist, nh, nh_bytes, tight);
+}
+
+int openr_spf_solve_ignore(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
+                           const uint32_t* ignore_ptr, const uint32_t* ignore_links, uint64_t* dist,
+                           uint8_t* nh, uint32_t nh_bytes, uint64_t* tight) {
+  if (!ignore_ptr) return fail(OPENR_SPF_EINVAL, "null ignore_ptr");
+  return solve_host(ctx, sources, n, flags, ignore_ptr, ignore_links, dist, nh, nh_bytes, tight);
+}
+
+int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n,
+                           uint32_t flags, const uint32_t* d_ignore_ptr, const uint32_t* d_ignore_links,
+                           uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes, uint64_t* d_tight, void* stream) {
+  int rc = check_solve_args(ctx, d_sources, n, d_dist, d_nh, nh_bytes);
+  if (rc) return rc;
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  Plan plan;
+  rc = make_plan(ctx, flags, d_ignore_ptr != nullptr, &plan);
+  if (rc) return rc;
+  Device& d = ctx->devs[device_index];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  SolveArgs a{};
+  a.sources = d_sources;
+  a.n = n;
+  a.ign_ptr = d_ignore_ptr;
+  a.ign_links = d_ignore_links;
+  a.dist = d_dist;
+  a.nh = d_nh;
+  a.nh_bytes = nh_bytes;
+  a.tight = d_tight;
+  a.nh_bits = ctx->nh_bits;
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  HIP_TRY(launch(ctx, d, plan, a, s));
+  ctx->stats.spf_runs += n;
+  ctx->stats.batches += 1;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_get_stats(const openr_spf_ctx* ctx, openr_spf_stats_t* out) {
+  if (!ctx || !out) return fail(OPENR_SPF_EINVAL, "null argument");
+  *out = ctx->stats;
+  return OPENR_SPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// spf_kernels.h — device-side graph layout and kernel launchers of the SPF engine.
+//
+// One workgroup owns one solve at a time (persistent loop over the batch): the
+// per-solve state (levels / distances, next-hop bitsets, frontier) lives in LDS,
+// the CSR mirror is streamed from L2/HBM and shared by every workgroup.
+// See DESIGN.md "Kernels" for the roofline accounting.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace openr_spf {
+
+// Device copy of the CSR mirror (include/openr_spf.h openr_spf_graph), packed for
+// the kernels. Built once per openr_spf_set_graph on every device of the context.
+struct DevGraph {
+  uint32_t V = 0, E = 0, L = 0;
+  uint32_t* row = nullptr;     // [V+1]
+  uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
+  uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
+  uint32_t* win = nullptr;     // [E] metric of the reverse edge (col -> row owner)
+  uint32_t* rev = nullptr;     // [E] index of the reverse edge
+  uint32_t* lid = nullptr;     // [E] undirected link id
+  uint16_t* nbr = nullptr;     // [E] distinct-neighbour index of col within its row
+  uint8_t* ovl = nullptr;      // [V] overloaded
+};
+
+constexpr uint32_t kEdgeDown = 0x80000000u;
+constexpr uint32_t kBlock = 256;
+
+// Next-hop bitset storage classes in LDS (chosen from the max distinct degree).
+enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, kNhW8 = 5 };
+int nh_mode_for_bits(uint32_t bits);            // -1 if > 256 bits
+uint32_t nh_mode_lds_bytes(int mode, uint32_t V);
+
+struct SolveArgs {
+  const uint32_t* sources;
+  uint32_t n;
+  const uint32_t* ign_ptr;    // nullable
+  const uint32_t* ign_links;
+  uint64_t* dist;             // [n][V]
+  uint8_t* nh;                // nullable [n][V][nh_bytes]
+  uint32_t nh_bytes;
+  uint64_t* tight;            // nullable [n][ceil(E/64)] (zeroed by the launcher)
+  uint32_t nh_bits;           // bits that are meaningful (max distinct degree)
+};
+
+struct LaunchInfo {
+  uint32_t lds_bytes = 0;
+  uint32_t grid = 0;
+  const char* kernel = "";
+};
+
+// Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels.
+hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode,
+                      int group_lanes, int num_cus, hipStream_t s, LaunchInfo* info);
+
+// General positive metrics: buckets of width delta = min usable metric (Dial /
+// delta-stepping with settle-safe buckets) and a pull pass for next-hops.
+hipError_t launch_bucket(const DevGraph& g, const SolveArgs& a, uint32_t delta, bool dist64,
+                         int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
+
+// LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
+uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode);
+uint32_t bucket_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
+constexpr uint32_t kMaxLds = 160 * 1024;
+
+}  // namespace openr_spf

@@ -1,0 +1,207 @@
+"""ctypes binding of the SPF engine's C-ABI (include/openr_spf.h).
+
+``SpfEngine`` is a thin, typed wrapper: every call goes straight to
+libopenr_spf.so and every failure raises ``SpfError`` with the library's
+message. There is no Python or CPU implementation of the solve behind it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libopenr_spf.so")
+
+USE_LINK_METRIC = 1
+EMIT_TIGHT = 2
+
+OK, EIO, ENOMEM, ENODEV, EINVAL, E2BIG, ENOTSUP = 0, -5, -12, -19, -22, -7, -95
+
+# Exported symbols of include/openr_spf.h (checked by tests/test_capi_symbols.py).
+EXPORTS = (
+    "openr_spf_abi_version",
+    "openr_spf_last_error",
+    "openr_spf_limits",
+    "openr_spf_create",
+    "openr_spf_destroy",
+    "openr_spf_set_graph",
+    "openr_spf_nh_bytes",
+    "openr_spf_neighbor_map",
+    "openr_spf_solve",
+    "openr_spf_solve_ignore",
+    "openr_spf_solve_device",
+    "openr_spf_get_stats",
+)
+
+
+class SpfError(RuntimeError):
+    def __init__(self, code: int, msg: str) -> None:
+        super().__init__(f"openr_spf error {code}: {msg}")
+        self.code = code
+
+
+class SpfGraph(ctypes.Structure):
+    _fields_ = [
+        ("num_nodes", ctypes.c_uint32),
+        ("num_dir_edges", ctypes.c_uint32),
+        ("num_links", ctypes.c_uint32),
+        ("row_ptr", ctypes.POINTER(ctypes.c_uint32)),
+        ("col", ctypes.POINTER(ctypes.c_uint32)),
+        ("metric", ctypes.POINTER(ctypes.c_uint64)),
+        ("link_id", ctypes.POINTER(ctypes.c_uint32)),
+        ("edge_up", ctypes.POINTER(ctypes.c_uint8)),
+        ("node_overloaded", ctypes.POINTER(ctypes.c_uint8)),
+        ("name_rank", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+class SpfLimits(ctypes.Structure):
+    _fields_ = [("max_nodes", ctypes.c_uint32), ("max_nh_bits", ctypes.c_uint32)]
+
+
+class SpfStats(ctypes.Structure):
+    _fields_ = [
+        ("spf_runs", ctypes.c_uint64),
+        ("batches", ctypes.c_uint64),
+        ("last_batch_ms", ctypes.c_double),
+        ("last_kernel_ms", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def load_library():
+    """Load libopenr_spf.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    l = ctypes.CDLL(LIB_PATH)
+    vp, u32, P = ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER
+    l.openr_spf_abi_version.restype = ctypes.c_int
+    l.openr_spf_last_error.restype = ctypes.c_char_p
+    l.openr_spf_limits.argtypes = [P(SpfLimits)]
+    l.openr_spf_limits.restype = None
+    l.openr_spf_create.argtypes = [vp, ctypes.c_int, P(vp)]
+    l.openr_spf_destroy.argtypes = [vp]
+    l.openr_spf_destroy.restype = None
+    l.openr_spf_set_graph.argtypes = [vp, P(SpfGraph)]
+    l.openr_spf_nh_bytes.argtypes = [vp, P(u32)]
+    l.openr_spf_neighbor_map.argtypes = [vp, u32, vp, u32, P(u32)]
+    l.openr_spf_solve.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp]
+    l.openr_spf_solve_ignore.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, u32, vp]
+    l.openr_spf_solve_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
+    l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
+    for name in EXPORTS:
+        if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy"):
+            getattr(l, name).restype = ctypes.c_int
+    _lib = l
+    return l
+
+
+def _check(rc: int) -> None:
+    if rc != OK:
+        msg = _lib.openr_spf_last_error()
+        raise SpfError(rc, msg.decode() if msg else "")
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+class SpfEngine:
+    """One engine context (= one LinkState's device-side SPF backend)."""
+
+    def __init__(self, device_ids: Optional[Sequence[int]] = None) -> None:
+        self._lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        if device_ids:
+            ids = (ctypes.c_int * len(device_ids))(*device_ids)
+            rc = self._lib.openr_spf_create(ctypes.cast(ids, ctypes.c_void_p), len(device_ids), ctypes.byref(self._ctx))
+        else:
+            rc = self._lib.openr_spf_create(None, 0, ctypes.byref(self._ctx))
+        _check(rc)
+        self.g = None
+        self._gs = None
+        self.nh_bytes = 1
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.openr_spf_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self) -> None:  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_graph(self, g) -> None:
+        self._gs = g.ctypes_struct(SpfGraph)
+        _check(self._lib.openr_spf_set_graph(self._ctx, ctypes.byref(self._gs)))
+        self.g = g
+        nb = ctypes.c_uint32()
+        _check(self._lib.openr_spf_nh_bytes(self._ctx, ctypes.byref(nb)))
+        self.nh_bytes = int(nb.value)
+
+    def neighbor_map(self, src: int) -> np.ndarray:
+        n = ctypes.c_uint32()
+        _check(self._lib.openr_spf_neighbor_map(self._ctx, src, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(int(n.value), 1), dtype=np.uint32)
+        _check(self._lib.openr_spf_neighbor_map(self._ctx, src, _p(out), out.shape[0], ctypes.byref(n)))
+        return out[: int(n.value)]
+
+    def solve(self, sources: Sequence[int], use_link_metric: bool = True, want_nh: bool = True,
+              want_tight: bool = False, ignore: Optional[Sequence[Sequence[int]]] = None,
+              nh_bytes: Optional[int] = None) -> Tuple[np.ndarray, Optional[np.ndarray], Optional[np.ndarray]]:
+        """Batched SPF. Returns (dist[n,V] u64, nh[n,V,nh_bytes] u8 | None, tight[n,ceil(E/64)] u64 | None)."""
+        g = self.g
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        n, V = int(src.shape[0]), g.num_nodes
+        nb = self.nh_bytes if nh_bytes is None else nh_bytes
+        dist = np.empty((n, V), dtype=np.uint64)
+        nh = np.empty((n, V, nb), dtype=np.uint8) if want_nh else None
+        tw = (g.num_dir_edges + 63) // 64
+        tight = np.empty((n, max(tw, 1)), dtype=np.uint64) if want_tight else None
+        flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if want_tight else 0)
+        if ignore is None:
+            rc = self._lib.openr_spf_solve(self._ctx, _p(src), n, flags, _p(dist), _p(nh), nb, _p(tight))
+        else:
+            ptr = np.zeros(n + 1, dtype=np.uint32)
+            ptr[1:] = np.cumsum([len(x) for x in ignore])
+            links = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in ignore])
+                                         if ptr[-1] else np.zeros(1, dtype=np.uint32), dtype=np.uint32)
+            rc = self._lib.openr_spf_solve_ignore(self._ctx, _p(src), n, flags, _p(ptr), _p(links), _p(dist),
+                                                  _p(nh), nb, _p(tight))
+        _check(rc)
+        return dist, nh, tight
+
+    def solve_device(self, d_sources: int, n: int, d_dist: int, d_nh: int = 0, nh_bytes: int = 0,
+                     use_link_metric: bool = True, stream: int = 0, device_index: int = 0,
+                     d_ignore_ptr: int = 0, d_ignore_links: int = 0, d_tight: int = 0) -> None:
+        """Device-pointer form (ints are raw device addresses, e.g. torch data_ptr())."""
+        flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if d_tight else 0)
+        vp = ctypes.c_void_p
+        _check(self._lib.openr_spf_solve_device(self._ctx, device_index, vp(d_sources), n, flags,
+                                                vp(d_ignore_ptr or None), vp(d_ignore_links or None), vp(d_dist),
+                                                vp(d_nh or None), nh_bytes or self.nh_bytes, vp(d_tight or None),
+                                                vp(stream or None)))
+
+    def stats(self) -> SpfStats:
+        s = SpfStats()
+        _check(self._lib.openr_spf_get_stats(self._ctx, ctypes.byref(s)))
+        return s
+
+
+def limits() -> SpfLimits:
+    l = load_library()
+    s = SpfLimits()
+    l.openr_spf_limits(ctypes.byref(s))
+    return s

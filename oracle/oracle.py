@@ -1,0 +1,157 @@
+"""ctypes wrapper over liboracle_spf.so — CPU ORACLE, test infrastructure only.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
+use this module, and only as the checker / the timed CPU port. It restates
+/root/reference/openr/decision/LinkState.cpp:762-882 (see spf_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Set
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle_spf.so")
+U64_MAX = 0xFFFFFFFFFFFFFFFF
+
+
+class OracleGraph(ctypes.Structure):
+    _fields_ = [
+        ("num_nodes", ctypes.c_uint32),
+        ("num_dir_edges", ctypes.c_uint32),
+        ("num_links", ctypes.c_uint32),
+        ("row_ptr", ctypes.POINTER(ctypes.c_uint32)),
+        ("col", ctypes.POINTER(ctypes.c_uint32)),
+        ("metric", ctypes.POINTER(ctypes.c_uint64)),
+        ("link_id", ctypes.POINTER(ctypes.c_uint32)),
+        ("edge_up", ctypes.POINTER(ctypes.c_uint8)),
+        ("node_overloaded", ctypes.POINTER(ctypes.c_uint8)),
+        ("name_rank", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+_lib = None
+
+
+def build() -> None:
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        l = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.POINTER
+        l.oracle_run_spf.restype = ctypes.c_int64
+        l.oracle_run_spf.argtypes = [P(OracleGraph), ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+        l.oracle_kth_paths.restype = ctypes.c_int64
+        l.oracle_kth_paths.argtypes = [P(OracleGraph), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+        l.oracle_all_sources.restype = ctypes.c_int
+        l.oracle_all_sources.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+        l.oracle_num_distinct_neighbors.restype = ctypes.c_uint32
+        l.oracle_num_distinct_neighbors.argtypes = [P(OracleGraph), ctypes.c_uint32]
+        _lib = l
+    return _lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+@dataclass
+class SpfRun:
+    dist: np.ndarray  # u64 [V]
+    nh: np.ndarray  # u8 [V, nh_bytes]
+    order: np.ndarray  # settle order (u32)
+    pl_ptr: np.ndarray
+    pl_edge: np.ndarray
+
+    def reachable(self) -> np.ndarray:
+        return self.dist != np.uint64(U64_MAX)
+
+
+class Oracle:
+    """Reference-faithful SPF/KSP over a CSR mirror (topology.CsrGraph)."""
+
+    def __init__(self, g) -> None:
+        self.g = g
+        self._s = g.ctypes_struct(OracleGraph)
+        self.nh_bytes = g.nh_bytes()
+
+    def run_spf(self, src: int, use_link_metric: bool = True,
+                ignore_links: Optional[Sequence[int]] = None) -> SpfRun:
+        g = self.g
+        V, E = g.num_nodes, g.num_dir_edges
+        ign = None
+        if ignore_links:
+            ign = np.zeros((g.num_links + 63) // 64 + 1, dtype=np.uint64)
+            for l in ignore_links:
+                ign[l >> 6] |= np.uint64(1 << (l & 63))
+        dist = np.empty(V, dtype=np.uint64)
+        nh = np.zeros((V, self.nh_bytes), dtype=np.uint8)
+        order = np.zeros(V, dtype=np.uint32)
+        pl_ptr = np.zeros(V + 1, dtype=np.uint32)
+        pl_edge = np.zeros(max(E, 1), dtype=np.uint32)
+        n = lib().oracle_run_spf(ctypes.byref(self._s), src, int(use_link_metric), _ptr(ign), _ptr(dist),
+                                 _ptr(nh), self.nh_bytes, _ptr(order), _ptr(pl_ptr), _ptr(pl_edge))
+        if n < 0:
+            raise RuntimeError(f"oracle_run_spf failed ({n})")
+        return SpfRun(dist, nh, order[:n].copy(), pl_ptr, pl_edge[: pl_ptr[V]].copy())
+
+    def kth_paths(self, src: int, dest: int, k: int) -> List[List[int]]:
+        g = self.g
+        E = max(g.num_dir_edges, 1)
+        pptr = np.zeros(E + 2, dtype=np.uint32)
+        edges = np.zeros(E + 1, dtype=np.uint32)
+        n = lib().oracle_kth_paths(ctypes.byref(self._s), src, dest, k, _ptr(pptr), E + 1, _ptr(edges), E + 1)
+        if n < 0:
+            raise RuntimeError("oracle_kth_paths failed")
+        return [edges[pptr[i] : pptr[i + 1]].tolist() for i in range(n)]
+
+    def all_sources(self, sources: Sequence[int], use_link_metric: bool = True, nthreads: int = 1,
+                    want_dist: bool = True, want_nh: bool = True):
+        g = self.g
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        n = src.shape[0]
+        dist = np.empty((n, g.num_nodes), dtype=np.uint64) if want_dist else None
+        nh = np.zeros((n, g.num_nodes, self.nh_bytes), dtype=np.uint8) if want_nh else None
+        rc = lib().oracle_all_sources(ctypes.byref(self._s), _ptr(src), n, int(use_link_metric), _ptr(dist),
+                                      _ptr(nh), self.nh_bytes, nthreads)
+        if rc != 0:
+            raise RuntimeError("oracle_all_sources failed")
+        return dist, nh
+
+    # --- helpers mirroring the reference's SpfResult view -------------------
+    def next_hop_names(self, src: int, run: SpfRun, v: int) -> Set[str]:
+        nbrs = self.g.distinct_neighbors(src)
+        out = set()
+        for i, nb in enumerate(nbrs):
+            if (run.nh[v, i >> 3] >> (i & 7)) & 1:
+                out.add(self.g.names[nb])
+        return out
+
+    def spf_result(self, src: int, use_link_metric: bool = True,
+                   ignore_links: Optional[Sequence[int]] = None) -> Dict[str, Dict]:
+        """SpfResult-like dict: name -> {metric, nextHops, pathLinks[(link, prevName)]}."""
+        run = self.run_spf(src, use_link_metric, ignore_links)
+        owner = self.g.edge_owner()
+        res = {}
+        for v in np.nonzero(run.reachable())[0].tolist():
+            pls = run.pl_edge[run.pl_ptr[v] : run.pl_ptr[v + 1]].tolist()
+            res[self.g.names[v]] = {
+                "metric": int(run.dist[v]),
+                "nextHops": self.next_hop_names(src, run, v),
+                "pathLinks": [(int(self.g.link_id[e]), self.g.names[int(owner[e])]) for e in pls],
+            }
+        return res
