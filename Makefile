@@ -11,7 +11,15 @@ ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_capi.hip
 ENGINE_HDRS := $(CSRC)/spf_kernels.h include/openr_spf.h
 ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_capi.o
 
-all: $(ENGINE) oracle
+HOST := $(LIBDIR)/libopenr_decision.so
+HOST_SRCS := $(CSRC)/host/LinkState.cpp
+HOST_HDRS := $(CSRC)/host/LinkState.h include/openr_spf.h
+CXX ?= g++
+CC ?= gcc
+CXXFLAGS ?= -O2 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+CPPTEST := tests/cpp/build/linkstate_test
+
+all: $(ENGINE) $(HOST) oracle $(CPPTEST)
 
 $(LIBDIR):
 	mkdir -p $@
@@ -22,11 +30,22 @@ $(LIBDIR)/%.o: $(CSRC)/%.hip $(ENGINE_HDRS) | $(LIBDIR)
 $(ENGINE): $(ENGINE_OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ENGINE_OBJS)
 
+# C++ host mirror of openr::LinkState over the C-ABI (links the engine)
+$(HOST): $(HOST_SRCS) $(HOST_HDRS) $(ENGINE)
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) -L$(LIBDIR) -lopenr_spf -Wl,-rpath,'$$ORIGIN'
+
+# C++ tests of the host mirror (oracle linked as the checker)
+$(CPPTEST): tests/cpp/linkstate_test.cpp $(HOST) oracle/spf_oracle.c oracle/spf_oracle.h
+	mkdir -p tests/cpp/build
+	$(CC) -O2 -g -std=c11 -c oracle/spf_oracle.c -o tests/cpp/build/spf_oracle.o
+	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/linkstate_test.cpp tests/cpp/build/spf_oracle.o \
+	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf $(LIBDIR)
+	rm -rf $(LIBDIR) tests/cpp/build
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -125,7 +125,8 @@ def main():
     src = torch.arange(lo, hi, dtype=torch.int32, device=dev)
     d_dist = torch.empty((n_local, V), dtype=torch.int64, device=dev)
     d_nh = torch.empty((n_local, V, nb), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(device=dev)  # a real (non-null) stream shared by launches and events
+    torch.cuda.set_stream(stream)
 
     def step():
         eng.solve_device(src.data_ptr(), n_local, d_dist.data_ptr(), d_nh.data_ptr(), nb, use_metric,

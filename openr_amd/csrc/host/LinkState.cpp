@@ -1,0 +1,679 @@
+// LinkState.cpp — host mirror of openr::LinkState (see LinkState.h).
+//
+// Topology bookkeeping restates the reference behaviour (LinkState.cpp:54-760):
+// bidirectional link formation, hold-down values, change detection and memo
+// invalidation happen at the same points with the same results, so that
+// linksFromNode() iterates in the same order as the reference on the same
+// standard library. runSpf is the GPU engine behind include/openr_spf.h.
+#include "LinkState.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <sstream>
+
+#include "../../../include/openr_spf.h"
+
+namespace openr {
+
+// ---------------------------------------------------------------------------
+// counters
+// ---------------------------------------------------------------------------
+SpfCounters& SpfCounters::get() {
+  static SpfCounters c;
+  return c;
+}
+void SpfCounters::addSpfRun(double ms, uint64_t runs) {
+  runs_ += runs;
+  msSum_ += ms;
+  samples_ += 1;
+}
+void SpfCounters::reset() { *this = SpfCounters(); }
+
+// ---------------------------------------------------------------------------
+// HoldableValue (reference LinkState.cpp:54-125)
+// ---------------------------------------------------------------------------
+template <class T>
+HoldableValue<T>::HoldableValue(T val) : val_(val) {}
+
+template <class T>
+void HoldableValue<T>::operator=(T val) {
+  val_ = val;
+  heldVal_.reset();
+  holdTtl_ = 0;
+}
+
+template <class T>
+const T& HoldableValue<T>::value() const {
+  return heldVal_ ? *heldVal_ : val_;
+}
+
+template <class T>
+bool HoldableValue<T>::hasHold() const {
+  return heldVal_.has_value();
+}
+
+template <class T>
+bool HoldableValue<T>::decrementTtl() {
+  if (!heldVal_) return false;
+  if (--holdTtl_ != 0) return false;
+  heldVal_.reset();
+  return true;
+}
+
+template <class T>
+bool HoldableValue<T>::updateValue(T val, LinkStateMetric holdUpTtl, LinkStateMetric holdDownTtl) {
+  if (val == val_) return false;  // same value: no-op
+  if (hasHold()) {
+    // a second change during a hold falls back to a fast update
+    heldVal_.reset();
+    holdTtl_ = 0;
+  } else {
+    holdTtl_ = isChangeBringingUp(val) ? holdUpTtl : holdDownTtl;
+    if (holdTtl_ != 0) heldVal_ = val_;
+  }
+  val_ = val;
+  return !hasHold();
+}
+
+template <>
+bool HoldableValue<bool>::isChangeBringingUp(bool val) const {
+  return val_ && !val;  // overload cleared
+}
+
+template <>
+bool HoldableValue<LinkStateMetric>::isChangeBringingUp(LinkStateMetric val) const {
+  return val < val_;  // metric improved
+}
+
+template class HoldableValue<LinkStateMetric>;
+template class HoldableValue<bool>;
+
+// ---------------------------------------------------------------------------
+// Link (reference LinkState.cpp:127-377)
+// ---------------------------------------------------------------------------
+namespace {
+using NamePair = std::pair<std::string, std::string>;
+std::pair<NamePair, NamePair> orderEnds(const std::string& n1, const std::string& if1, const std::string& n2,
+                                        const std::string& if2) {
+  return std::minmax(NamePair(n1, if1), NamePair(n2, if2));
+}
+}  // namespace
+
+Link::Link(const std::string& area, const std::string& nodeName1, const std::string& if1,
+           const std::string& nodeName2, const std::string& if2)
+    : area_(area),
+      orderedNames_(orderEnds(nodeName1, if1, nodeName2, if2)),
+      hash(std::hash<std::pair<NamePair, NamePair>>()(orderedNames_)) {
+  ends_[0].node = nodeName1;
+  ends_[0].iface = if1;
+  ends_[1].node = nodeName2;
+  ends_[1].iface = if2;
+}
+
+Link::Link(const std::string& area, const std::string& nodeName1, const thrift::Adjacency& adj1,
+           const std::string& nodeName2, const thrift::Adjacency& adj2)
+    : Link(area, nodeName1, adj1.ifName, nodeName2, adj2.ifName) {
+  const thrift::Adjacency* adjs[2] = {&adj1, &adj2};
+  for (int i = 0; i < 2; ++i) {
+    End& end = ends_[i];
+    // i32 Adjacency.metric -> u64 LinkStateMetric (negative values wrap)
+    end.metric = static_cast<LinkStateMetric>(adjs[i]->metric);
+    end.overload = adjs[i]->isOverloaded;
+    end.adjLabel = adjs[i]->adjLabel;
+    end.nhV4 = adjs[i]->nextHopV4;
+    end.nhV6 = adjs[i]->nextHopV6;
+  }
+}
+
+int Link::sideOf(const std::string& nodeName) const {
+  if (ends_[0].node == nodeName) return 0;
+  if (ends_[1].node == nodeName) return 1;
+  throw std::invalid_argument(nodeName);
+}
+
+const std::string& Link::getOtherNodeName(const std::string& nodeName) const {
+  return ends_[1 - sideOf(nodeName)].node;
+}
+const std::string& Link::firstNodeName() const { return orderedNames_.first.first; }
+const std::string& Link::secondNodeName() const { return orderedNames_.second.first; }
+const std::string& Link::getIfaceFromNode(const std::string& nodeName) const {
+  return ends_[sideOf(nodeName)].iface;
+}
+LinkStateMetric Link::getMetricFromNode(const std::string& nodeName) const {
+  return ends_[sideOf(nodeName)].metric.value();
+}
+int32_t Link::getAdjLabelFromNode(const std::string& nodeName) const { return ends_[sideOf(nodeName)].adjLabel; }
+bool Link::getOverloadFromNode(const std::string& nodeName) const {
+  return ends_[sideOf(nodeName)].overload.value();
+}
+const thrift::BinaryAddress& Link::getNhV4FromNode(const std::string& nodeName) const {
+  return ends_[sideOf(nodeName)].nhV4;
+}
+const thrift::BinaryAddress& Link::getNhV6FromNode(const std::string& nodeName) const {
+  return ends_[sideOf(nodeName)].nhV6;
+}
+void Link::setNhV4FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV4) {
+  ends_[sideOf(nodeName)].nhV4 = nhV4;
+}
+void Link::setNhV6FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV6) {
+  ends_[sideOf(nodeName)].nhV6 = nhV6;
+}
+void Link::setHoldUpTtl(LinkStateMetric ttl) { holdUpTtl_ = ttl; }
+
+bool Link::isUp() const {
+  return holdUpTtl_ == 0 && !ends_[0].overload.value() && !ends_[1].overload.value();
+}
+
+bool Link::decrementHolds() {
+  bool expired = false;
+  if (holdUpTtl_ != 0) expired |= (--holdUpTtl_ == 0);
+  for (End& end : ends_) {
+    expired |= end.metric.decrementTtl();
+    expired |= end.overload.decrementTtl();
+  }
+  return expired;
+}
+
+bool Link::hasHolds() const {
+  if (holdUpTtl_ != 0) return true;
+  for (const End& end : ends_)
+    if (end.metric.hasHold() || end.overload.hasHold()) return true;
+  return false;
+}
+
+bool Link::setMetricFromNode(const std::string& nodeName, LinkStateMetric d, LinkStateMetric holdUpTtl,
+                             LinkStateMetric holdDownTtl) {
+  return ends_[sideOf(nodeName)].metric.updateValue(d, holdUpTtl, holdDownTtl);
+}
+
+void Link::setAdjLabelFromNode(const std::string& nodeName, int32_t adjLabel) {
+  ends_[sideOf(nodeName)].adjLabel = adjLabel;
+}
+
+bool Link::setOverloadFromNode(const std::string& nodeName, bool overload, LinkStateMetric holdUpTtl,
+                               LinkStateMetric holdDownTtl) {
+  const bool wasUp = isUp();
+  ends_[sideOf(nodeName)].overload.updateValue(overload, holdUpTtl, holdDownTtl);
+  // simplex overloads are not modelled: only an up/down flip changes topology
+  return wasUp != isUp();
+}
+
+bool Link::operator<(const Link& other) const {
+  if (hash != other.hash) return hash < other.hash;
+  return orderedNames_ < other.orderedNames_;
+}
+
+bool Link::operator==(const Link& other) const { return hash == other.hash && orderedNames_ == other.orderedNames_; }
+
+std::string Link::toString() const {
+  std::ostringstream os;
+  os << area_ << " - " << ends_[0].node << "%" << ends_[0].iface << " <---> " << ends_[1].node << "%"
+     << ends_[1].iface;
+  return os.str();
+}
+
+std::string Link::directionalToString(const std::string& fromNode) const {
+  const int s = sideOf(fromNode);
+  std::ostringstream os;
+  os << area_ << " - " << ends_[s].node << "%" << ends_[s].iface << " ---> " << ends_[1 - s].node << "%"
+     << ends_[1 - s].iface;
+  return os.str();
+}
+
+// ---------------------------------------------------------------------------
+// engine handle
+// ---------------------------------------------------------------------------
+class SpfEngineHandle {
+ public:
+  SpfEngineHandle() {
+    int dev = -1;
+    if (const char* e = std::getenv("OPENR_SPF_DEVICE")) dev = std::atoi(e);
+    int rc = dev >= 0 ? openr_spf_create(&dev, 1, &ctx_) : openr_spf_create(nullptr, 0, &ctx_);
+    check(rc, "openr_spf_create");
+  }
+  ~SpfEngineHandle() { openr_spf_destroy(ctx_); }
+  SpfEngineHandle(const SpfEngineHandle&) = delete;
+  SpfEngineHandle& operator=(const SpfEngineHandle&) = delete;
+
+  static void check(int rc, const char* what) {
+    if (rc != OPENR_SPF_OK)
+      throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) + "): " + openr_spf_last_error());
+  }
+  openr_spf_ctx* ctx() { return ctx_; }
+  const void* owner = nullptr;   // LinkState whose graph is loaded
+  uint64_t generation = 0;       // its mirror generation
+
+ private:
+  openr_spf_ctx* ctx_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// LinkState (reference LinkState.cpp:379-803)
+// ---------------------------------------------------------------------------
+LinkState::LinkState(const std::string& area) : area_(area) {}
+
+size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const { return l->hash; }
+bool LinkState::LinkPtrLess::operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const {
+  return *lhs < *rhs;
+}
+bool LinkState::LinkPtrEqual::operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const {
+  return *lhs == *rhs;
+}
+
+bool LinkState::pathAInPathB(Path const& a, Path const& b) {
+  if (a.size() > b.size()) return false;
+  for (size_t start = 0; start + a.size() <= b.size(); ++start) {
+    size_t k = 0;
+    while (k < a.size() && *a[k] == *b[start + k]) ++k;
+    if (k == a.size()) return true;
+  }
+  return false;
+}
+
+std::optional<LinkState::Path> LinkState::traceOnePath(std::string const& src, std::string const& dest,
+                                                       SpfResult const& result, LinkSet& linksToIgnore) const {
+  if (src == dest) return Path{};
+  for (auto const& pl : result.at(dest).pathLinks()) {
+    if (!linksToIgnore.insert(pl.link).second) continue;  // link already used by a path
+    if (auto path = traceOnePath(src, pl.prevNode, result, linksToIgnore)) {
+      path->push_back(pl.link);
+      return path;
+    }
+  }
+  return std::nullopt;
+}
+
+void LinkState::addLink(std::shared_ptr<Link> link) {
+  if (!linkMap_[link->firstNodeName()].insert(link).second || !linkMap_[link->secondNodeName()].insert(link).second ||
+      !allLinks_.insert(link).second)
+    throw std::logic_error("addLink: duplicate link " + link->toString());
+  markMirrorDirty();
+}
+
+void LinkState::removeLink(std::shared_ptr<Link> link) {
+  if (!linkMap_.at(link->firstNodeName()).erase(link) || !linkMap_.at(link->secondNodeName()).erase(link) ||
+      !allLinks_.erase(link))
+    throw std::logic_error("removeLink: unknown link " + link->toString());
+  markMirrorDirty();
+}
+
+void LinkState::removeNode(const std::string& nodeName) {
+  auto it = linkMap_.find(nodeName);
+  if (it == linkMap_.end()) return;  // node never had links (empty adjacency db)
+  for (auto const& link : it->second) {
+    if (!linkMap_.at(link->getOtherNodeName(nodeName)).erase(link) || !allLinks_.erase(link))
+      throw std::logic_error("removeNode: inconsistent link map for " + nodeName);
+  }
+  linkMap_.erase(it);
+  nodeOverloads_.erase(nodeName);
+  markMirrorDirty();
+}
+
+const LinkState::LinkSet& LinkState::linksFromNode(const std::string& nodeName) const {
+  static const LinkSet kEmpty;
+  auto it = linkMap_.find(nodeName);
+  return it == linkMap_.end() ? kEmpty : it->second;
+}
+
+std::vector<std::shared_ptr<Link>> LinkState::orderedLinksFromNode(const std::string& nodeName) const {
+  const LinkSet& set = linksFromNode(nodeName);
+  std::vector<std::shared_ptr<Link>> links(set.begin(), set.end());
+  std::sort(links.begin(), links.end(), LinkPtrLess{});
+  return links;
+}
+
+bool LinkState::updateNodeOverloaded(const std::string& nodeName, bool isOverloaded, LinkStateMetric holdUpTtl,
+                                     LinkStateMetric holdDownTtl) {
+  markMirrorDirty();
+  auto it = nodeOverloads_.find(nodeName);
+  if (it != nodeOverloads_.end()) return it->second.updateValue(isOverloaded, holdUpTtl, holdDownTtl);
+  nodeOverloads_.emplace(nodeName, HoldableValue<bool>{isOverloaded});
+  return false;  // a new node is not a topology change
+}
+
+bool LinkState::isNodeOverloaded(const std::string& nodeName) const {
+  auto it = nodeOverloads_.find(nodeName);
+  return it != nodeOverloads_.end() && it->second.value();
+}
+
+LinkState::LinkStateChange LinkState::decrementHolds() {
+  LinkStateChange change;
+  for (auto& link : allLinks_) change.topologyChanged |= link->decrementHolds();
+  for (auto& kv : nodeOverloads_) change.topologyChanged |= kv.second.decrementTtl();
+  if (change.topologyChanged) {
+    spfResults_.clear();
+    kthPathResults_.clear();
+    markMirrorDirty();
+  }
+  return change;
+}
+
+bool LinkState::hasHolds() const {
+  for (auto& link : allLinks_)
+    if (link->hasHolds()) return true;
+  for (auto& kv : nodeOverloads_)
+    if (kv.second.hasHold()) return true;
+  return false;
+}
+
+std::shared_ptr<Link> LinkState::maybeMakeLink(const std::string& nodeName, const thrift::Adjacency& adj) const {
+  // a Link exists only if the other end advertises the reverse adjacency
+  auto it = adjacencyDatabases_.find(adj.otherNodeName);
+  if (it == adjacencyDatabases_.end()) return nullptr;
+  for (const auto& back : it->second.adjacencies) {
+    if (back.otherNodeName == nodeName && adj.otherIfName == back.ifName && adj.ifName == back.otherIfName)
+      return std::make_shared<Link>(area_, nodeName, adj, adj.otherNodeName, back);
+  }
+  return nullptr;
+}
+
+std::vector<std::shared_ptr<Link>> LinkState::getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const {
+  std::vector<std::shared_ptr<Link>> links;
+  links.reserve(adjDb.adjacencies.size());
+  for (const auto& adj : adjDb.adjacencies)
+    if (auto link = maybeMakeLink(adjDb.thisNodeName, adj)) links.push_back(std::move(link));
+  std::sort(links.begin(), links.end(), LinkPtrLess{});
+  return links;
+}
+
+LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyDatabase const& newDb,
+                                                              LinkStateMetric holdUpTtl,
+                                                              LinkStateMetric holdDownTtl) {
+  LinkStateChange change;
+  const std::string nodeName = newDb.thisNodeName;
+  markMirrorDirty();
+
+  thrift::AdjacencyDatabase prior(std::move(adjacencyDatabases_[nodeName]));
+  adjacencyDatabases_[nodeName] = newDb;
+
+  // both sides ordered by <hash, names> so one merge pass finds adds/removes/updates
+  const auto oldLinks = orderedLinksFromNode(nodeName);
+  const auto newLinks = getOrderedLinkSet(newDb);
+
+  change.topologyChanged |= updateNodeOverloaded(nodeName, newDb.isOverloaded, holdUpTtl, holdDownTtl);
+  change.nodeLabelChanged = prior.nodeLabel != newDb.nodeLabel;
+
+  size_t ni = 0, oi = 0;
+  while (ni < newLinks.size() || oi < oldLinks.size()) {
+    const bool takeNew = ni < newLinks.size() && (oi == oldLinks.size() || *newLinks[ni] < *oldLinks[oi]);
+    const bool takeOld = !takeNew && oi < oldLinks.size() && (ni == newLinks.size() || *oldLinks[oi] < *newLinks[ni]);
+    if (takeNew) {  // link came up (possibly held down)
+      newLinks[ni]->setHoldUpTtl(holdUpTtl);
+      change.topologyChanged |= newLinks[ni]->isUp();
+      addLink(newLinks[ni]);
+      ++ni;
+      continue;
+    }
+    if (takeOld) {  // link went away
+      change.topologyChanged |= oldLinks[oi]->isUp();
+      removeLink(oldLinks[oi]);
+      ++oi;
+      continue;
+    }
+    // same link on both sides: update the object we already hold
+    Link& cur = *oldLinks[oi];
+    const Link& upd = *newLinks[ni];
+    if (upd.getMetricFromNode(nodeName) != cur.getMetricFromNode(nodeName))
+      change.topologyChanged |= cur.setMetricFromNode(nodeName, upd.getMetricFromNode(nodeName), holdUpTtl,
+                                                      holdDownTtl);
+    if (upd.getOverloadFromNode(nodeName) != cur.getOverloadFromNode(nodeName))
+      change.topologyChanged |= cur.setOverloadFromNode(nodeName, upd.getOverloadFromNode(nodeName), holdUpTtl,
+                                                        holdDownTtl);
+    if (upd.getAdjLabelFromNode(nodeName) != cur.getAdjLabelFromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setAdjLabelFromNode(nodeName, upd.getAdjLabelFromNode(nodeName));
+    }
+    if (upd.getNhV4FromNode(nodeName) != cur.getNhV4FromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setNhV4FromNode(nodeName, upd.getNhV4FromNode(nodeName));
+    }
+    if (upd.getNhV6FromNode(nodeName) != cur.getNhV6FromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setNhV6FromNode(nodeName, upd.getNhV6FromNode(nodeName));
+    }
+    ++ni;
+    ++oi;
+  }
+  if (change.topologyChanged) {
+    spfResults_.clear();
+    kthPathResults_.clear();
+  }
+  return change;
+}
+
+LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& nodeName) {
+  LinkStateChange change;
+  auto it = adjacencyDatabases_.find(nodeName);
+  if (it != adjacencyDatabases_.end()) {
+    removeNode(nodeName);
+    adjacencyDatabases_.erase(it);
+    spfResults_.clear();
+    kthPathResults_.clear();
+    markMirrorDirty();
+    change.topologyChanged = true;
+  }
+  return change;
+}
+
+std::optional<LinkStateMetric> LinkState::getMetricFromAToB(std::string const& a, std::string const& b,
+                                                            bool useLinkMetric) const {
+  if (a == b) return 0;
+  auto const& res = getSpfResult(a, useLinkMetric);
+  auto it = res.find(b);
+  if (it == res.end()) return std::nullopt;
+  return it->second.metric();
+}
+
+LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
+  LinkStateMetric best = 0;
+  for (auto const& kv : getSpfResult(nodeName, false)) best = std::max(best, kv.second.metric());
+  return best;
+}
+
+std::vector<LinkState::Path> const& LinkState::getKthPaths(const std::string& src, const std::string& dest,
+                                                           size_t k) const {
+  if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");  // CHECK_GE(k, 1)
+  const auto key = std::make_tuple(src, dest, k);
+  auto it = kthPathResults_.find(key);
+  if (it != kthPathResults_.end()) return it->second;
+  LinkSet ignore;
+  for (size_t i = 1; i < k; ++i)
+    for (auto const& path : getKthPaths(src, dest, i))
+      for (auto const& link : path) ignore.insert(link);
+  std::vector<Path> paths;
+  SpfResult fresh;
+  const SpfResult* res = nullptr;
+  if (ignore.empty()) {
+    res = &getSpfResult(src, true);
+  } else {
+    fresh = runSpf(src, true, ignore);
+    res = &fresh;
+  }
+  if (res->count(dest)) {
+    LinkSet visited;
+    auto path = traceOnePath(src, dest, *res, visited);
+    while (path && !path->empty()) {
+      paths.push_back(std::move(*path));
+      path = traceOnePath(src, dest, *res, visited);
+    }
+  }
+  return kthPathResults_.emplace(key, std::move(paths)).first->second;
+}
+
+LinkState::SpfResult const& LinkState::getSpfResult(const std::string& nodeName, bool useLinkMetric) const {
+  const auto key = std::make_pair(nodeName, useLinkMetric);
+  auto it = spfResults_.find(key);
+  if (it == spfResults_.end()) it = spfResults_.emplace(key, runSpf(nodeName, useLinkMetric)).first;
+  return it->second;
+}
+
+void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric) const {
+  std::vector<std::string> missing;
+  for (auto const& n : nodes)
+    if (!spfResults_.count(std::make_pair(n, useLinkMetric))) missing.push_back(n);
+  if (missing.empty()) return;
+  auto results = runSpfBatch(missing, useLinkMetric, std::vector<const LinkSet*>(missing.size(), nullptr));
+  for (size_t i = 0; i < missing.size(); ++i)
+    spfResults_.emplace(std::make_pair(missing[i], useLinkMetric), std::move(results[i]));
+}
+
+// ---------------------------------------------------------------------------
+// CSR mirror + engine-backed runSpf
+// ---------------------------------------------------------------------------
+const LinkState::CsrMirror& LinkState::csrMirror() const {
+  if (!mirrorDirty_) return mirror_;
+  CsrMirror m;
+  // node set: every node with an adjacency database or a link; ids in name order
+  for (auto const& kv : adjacencyDatabases_) m.names.push_back(kv.first);
+  for (auto const& kv : linkMap_)
+    if (!adjacencyDatabases_.count(kv.first)) m.names.push_back(kv.first);
+  std::sort(m.names.begin(), m.names.end());
+  const uint32_t V = (uint32_t)m.names.size();
+  for (uint32_t i = 0; i < V; ++i) m.id.emplace(m.names[i], i);
+  m.nameRank.resize(V);
+  for (uint32_t i = 0; i < V; ++i) m.nameRank[i] = i;
+  std::unordered_map<const Link*, uint32_t> linkIds;
+  m.rowPtr.assign(V + 1, 0);
+  m.overloaded.assign(V, 0);
+  for (uint32_t u = 0; u < V; ++u) {
+    const std::string& name = m.names[u];
+    m.overloaded[u] = isNodeOverloaded(name) ? 1 : 0;
+    // row order == linksFromNode(u) iteration order (pathLinks order among parallel links)
+    for (auto const& link : linksFromNode(name)) {
+      auto ins = linkIds.emplace(link.get(), (uint32_t)m.links.size());
+      if (ins.second) m.links.push_back(link);
+      m.col.push_back(m.id.at(link->getOtherNodeName(name)));
+      m.metric.push_back(link->getMetricFromNode(name));
+      m.linkId.push_back(ins.first->second);
+      m.edgeUp.push_back(link->isUp() ? 1 : 0);
+      m.edgeOwner.push_back(u);
+    }
+    m.rowPtr[u + 1] = (uint32_t)m.col.size();
+  }
+  mirror_ = std::move(m);
+  mirrorDirty_ = false;
+  ++mirrorGeneration_;
+  return mirror_;
+}
+
+std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,
+                                                         const std::vector<const LinkSet*>& ignores) const {
+  const auto t0 = std::chrono::steady_clock::now();
+  const CsrMirror& m = csrMirror();
+  std::vector<SpfResult> out(srcs.size());
+  // sources unknown to the graph: the reference pops only the source itself
+  std::vector<uint32_t> ids;
+  std::vector<size_t> slot;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    auto it = m.id.find(srcs[i]);
+    if (it == m.id.end()) {
+      out[i].emplace(srcs[i], NodeSpfResult(0));
+    } else {
+      ids.push_back(it->second);
+      slot.push_back(i);
+    }
+  }
+  if (!ids.empty()) {
+    if (!engine_) engine_ = std::make_shared<SpfEngineHandle>();
+    if (engine_->owner != this || engine_->generation != mirrorGeneration_) {
+      openr_spf_graph g{};
+      g.num_nodes = (uint32_t)m.names.size();
+      g.num_dir_edges = (uint32_t)m.col.size();
+      g.num_links = (uint32_t)m.links.size();
+      g.row_ptr = m.rowPtr.data();
+      g.col = m.col.data();
+      g.metric = m.metric.data();
+      g.link_id = m.linkId.data();
+      g.edge_up = m.edgeUp.data();
+      g.node_overloaded = m.overloaded.data();
+      g.name_rank = m.nameRank.data();
+      SpfEngineHandle::check(openr_spf_set_graph(engine_->ctx(), &g), "openr_spf_set_graph");
+      engine_->owner = this;
+      engine_->generation = mirrorGeneration_;
+    }
+    const uint32_t V = (uint32_t)m.names.size(), E = (uint32_t)m.col.size(), tw = (E + 63) / 64;
+    uint32_t nb = 1;
+    SpfEngineHandle::check(openr_spf_nh_bytes(engine_->ctx(), &nb), "openr_spf_nh_bytes");
+    const size_t n = ids.size();
+    std::vector<uint64_t> dist(n * V), tight(n * std::max<uint32_t>(tw, 1));
+    std::vector<uint8_t> nh(n * V * nb);
+    const uint32_t flags = (useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u) | (uint32_t)OPENR_SPF_EMIT_TIGHT;
+    bool anyIgnore = false;
+    for (size_t k = 0; k < n; ++k) anyIgnore |= ignores[slot[k]] && !ignores[slot[k]]->empty();
+    if (anyIgnore) {
+      std::unordered_map<const Link*, uint32_t> lid;
+      for (uint32_t l = 0; l < m.links.size(); ++l) lid.emplace(m.links[l].get(), l);
+      std::vector<uint32_t> ptr(n + 1, 0), links;
+      for (size_t k = 0; k < n; ++k) {
+        if (const LinkSet* ign = ignores[slot[k]]) {
+          for (auto const& link : *ign) {
+            // match by link identity (LinkPtrEqual), not pointer
+            for (auto const& cand : linksFromNode(link->firstNodeName())) {
+              if (*cand == *link) {
+                auto f = lid.find(cand.get());
+                if (f != lid.end()) links.push_back(f->second);
+                break;
+              }
+            }
+          }
+        }
+        ptr[k + 1] = (uint32_t)links.size();
+      }
+      if (links.empty()) links.push_back(0);
+      SpfEngineHandle::check(openr_spf_solve_ignore(engine_->ctx(), ids.data(), (uint32_t)n, flags, ptr.data(),
+                                                    links.data(), dist.data(), nh.data(), nb, tight.data()),
+                             "openr_spf_solve_ignore");
+    } else {
+      SpfEngineHandle::check(
+          openr_spf_solve(engine_->ctx(), ids.data(), (uint32_t)n, flags, dist.data(), nh.data(), nb, tight.data()),
+          "openr_spf_solve");
+    }
+    // materialise SpfResult: nextHops from the bitsets, pathLinks from tight edges
+    // ordered by the predecessor's settle order (dist, name) then row position.
+    std::vector<uint32_t> nbrs(V ? V : 1);
+    std::vector<uint32_t> order;
+    for (size_t k = 0; k < n; ++k) {
+      const uint32_t src = ids[k];
+      uint32_t nn = 0;
+      SpfEngineHandle::check(openr_spf_neighbor_map(engine_->ctx(), src, nbrs.data(), (uint32_t)nbrs.size(), &nn),
+                             "openr_spf_neighbor_map");
+      const uint64_t* d = dist.data() + k * V;
+      const uint8_t* h = nh.data() + k * (size_t)V * nb;
+      const uint64_t* t = tight.data() + k * (size_t)std::max<uint32_t>(tw, 1);
+      SpfResult& res = out[slot[k]];
+      res.reserve(V);
+      for (uint32_t v = 0; v < V; ++v) {
+        if (d[v] == UINT64_MAX) continue;
+        NodeSpfResult r(d[v]);
+        const uint8_t* hv = h + (size_t)v * nb;
+        for (uint32_t i = 0; i < nn; ++i)
+          if ((hv[i >> 3] >> (i & 7)) & 1u) r.addNextHop(m.names[nbrs[i]]);
+        res.emplace(m.names[v], std::move(r));
+      }
+      order.clear();
+      for (uint32_t e = 0; e < E; ++e)
+        if ((t[e >> 6] >> (e & 63)) & 1ull) order.push_back(e);
+      std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t ux = m.edgeOwner[x], uy = m.edgeOwner[y];
+        if (d[ux] != d[uy]) return d[ux] < d[uy];
+        if (m.nameRank[ux] != m.nameRank[uy]) return m.nameRank[ux] < m.nameRank[uy];
+        return x < y;
+      });
+      for (uint32_t e : order) {
+        const uint32_t u = m.edgeOwner[e], v = m.col[e];
+        res.at(m.names[v]).addPath(m.links[m.linkId[e]], m.names[u]);
+      }
+    }
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  SpfCounters::get().addSpfRun(ms, srcs.size());  // decision.spf_runs counts logical SPFs
+  return out;
+}
+
+LinkState::SpfResult LinkState::runSpf(const std::string& src, bool useLinkMetric, const LinkSet& linksToIgnore) const {
+  auto v = runSpfBatch({src}, useLinkMetric, {&linksToIgnore});
+  return std::move(v[0]);
+}
+
+}  // namespace openr

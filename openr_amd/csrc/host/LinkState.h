@@ -1,0 +1,339 @@
+// LinkState.h — C++ host mirror of openr::LinkState with the SPF on the GPU engine.
+//
+// Public surface and semantics follow /root/reference/openr/decision/LinkState.h
+// (HoldableValue :36-58, Link :82-175, LinkState :177-469) so that Decision's callers
+// (SpfSolver, Decision.cpp) compile against it unchanged. What differs is below the
+// surface: LinkState::runSpf (reference LinkState.cpp:808-882) is a call through the
+// C-ABI in include/openr_spf.h on a CSR mirror of linkMap_, and results are
+// materialised from the engine's dense outputs (distances, next-hop bitsets,
+// tight-edge mask). There is no CPU Dijkstra here.
+//
+// Thrift types: this standalone build carries minimal structs with the fields of
+// openr/if/Lsdb.thrift:71-129 (Adjacency, AdjacencyDatabase) and Network.thrift
+// BinaryAddress. In the real tree the generated types replace them.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <limits>
+#include <map>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+namespace openr {
+// folly::hash::hash_128_to_64 (CityHash Hash128to64), folly rev 1540c39c.
+inline uint64_t hash_128_to_64(uint64_t upper, uint64_t lower) {
+  const uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= (a >> 47);
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= (b >> 47);
+  b *= kMul;
+  return b;
+}
+}  // namespace openr
+
+namespace std {
+// folly provides these for the reference (folly/hash/Hash.h): hash_combine of the
+// element hashes. Link::hash, and with it linksFromNode() iteration order, depend on it.
+template <class A, class B>
+struct hash<pair<A, B>> {
+  size_t operator()(const pair<A, B>& p) const {
+    return openr::hash_128_to_64(std::hash<A>()(p.first), std::hash<B>()(p.second));
+  }
+};
+template <class... T>
+struct hash<tuple<T...>> {
+  size_t operator()(const tuple<T...>& t) const {
+    size_t h = 0;
+    bool first = true;
+    std::apply(
+        [&](const auto&... e) {
+          ((h = first ? (first = false, std::hash<std::decay_t<decltype(e)>>()(e))
+                      : openr::hash_128_to_64(h, std::hash<std::decay_t<decltype(e)>>()(e))),
+           ...);
+        },
+        t);
+    return h;
+  }
+};
+}  // namespace std
+
+namespace openr {
+
+using LinkStateMetric = uint64_t;
+
+namespace thrift {
+struct BinaryAddress {
+  std::string addr;
+  std::optional<std::string> ifName;
+  bool operator==(const BinaryAddress& o) const { return addr == o.addr && ifName == o.ifName; }
+  bool operator!=(const BinaryAddress& o) const { return !(*this == o); }
+};
+
+struct Adjacency {
+  std::string otherNodeName;
+  std::string ifName;
+  BinaryAddress nextHopV6;
+  BinaryAddress nextHopV4;
+  int32_t metric = 0;
+  int32_t adjLabel = 0;
+  bool isOverloaded = false;
+  int32_t rtt = 0;
+  int64_t timestamp = 0;
+  int64_t weight = 1;
+  std::string otherIfName;
+};
+
+struct AdjacencyDatabase {
+  std::string thisNodeName;
+  bool isOverloaded = false;
+  std::vector<Adjacency> adjacencies;
+  int32_t nodeLabel = 0;
+  std::string area;
+};
+}  // namespace thrift
+
+// fb303-style counters of the SPF path: decision.spf_runs (COUNT) and decision.spf_ms
+// (AVG), as recorded by the reference at LinkState.cpp:815 and :880.
+struct SpfCounters {
+  static SpfCounters& get();
+  void addSpfRun(double ms, uint64_t runs = 1);
+  void reset();
+  uint64_t spfRuns() const { return runs_; }
+  double spfMsAvg() const { return samples_ ? msSum_ / (double)samples_ : 0.0; }
+
+ private:
+  uint64_t runs_ = 0, samples_ = 0;
+  double msSum_ = 0.0;
+};
+
+template <class T>
+class HoldableValue {
+ public:
+  explicit HoldableValue(T val);
+  void operator=(T val);
+  const T& value() const;
+  bool hasHold() const;
+  // return true if the call changed value()
+  bool decrementTtl();
+  bool updateValue(T val, LinkStateMetric holdUpTtl, LinkStateMetric holdDownTtl);
+
+ private:
+  bool isChangeBringingUp(T val) const;
+  T val_;
+  std::optional<T> heldVal_;
+  LinkStateMetric holdTtl_{0};
+};
+
+class Link {
+ public:
+  Link(const std::string& area, const std::string& nodeName1, const std::string& if1,
+       const std::string& nodeName2, const std::string& if2);
+  Link(const std::string& area, const std::string& nodeName1, const thrift::Adjacency& adj1,
+       const std::string& nodeName2, const thrift::Adjacency& adj2);
+
+ private:
+  // one end of the link, as advertised by that end's node
+  struct End {
+    std::string node, iface;
+    HoldableValue<LinkStateMetric> metric{1};
+    HoldableValue<bool> overload{false};
+    int32_t adjLabel{0};
+    thrift::BinaryAddress nhV4, nhV6;
+  };
+  const std::string area_;
+  End ends_[2];
+  LinkStateMetric holdUpTtl_{0};
+  const std::pair<std::pair<std::string, std::string>, std::pair<std::string, std::string>> orderedNames_;
+
+  int sideOf(const std::string& nodeName) const;  // throws std::invalid_argument
+
+ public:
+  const size_t hash{0};
+
+  void setHoldUpTtl(LinkStateMetric ttl);
+  bool isUp() const;
+  bool decrementHolds();
+  bool hasHolds() const;
+  const std::string& getArea() const { return area_; }
+  const std::string& getOtherNodeName(const std::string& nodeName) const;
+  const std::string& firstNodeName() const;
+  const std::string& secondNodeName() const;
+  const std::string& getIfaceFromNode(const std::string& nodeName) const;
+  LinkStateMetric getMetricFromNode(const std::string& nodeName) const;
+  int32_t getAdjLabelFromNode(const std::string& nodeName) const;
+  bool getOverloadFromNode(const std::string& nodeName) const;
+  const thrift::BinaryAddress& getNhV4FromNode(const std::string& nodeName) const;
+  const thrift::BinaryAddress& getNhV6FromNode(const std::string& nodeName) const;
+  void setNhV4FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV4);
+  void setNhV6FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV6);
+  bool setMetricFromNode(const std::string& nodeName, LinkStateMetric d, LinkStateMetric holdUpTtl,
+                         LinkStateMetric holdDownTtl);
+  void setAdjLabelFromNode(const std::string& nodeName, int32_t adjLabel);
+  bool setOverloadFromNode(const std::string& nodeName, bool overload, LinkStateMetric holdUpTtl,
+                           LinkStateMetric holdDownTtl);
+  bool operator<(const Link& other) const;
+  bool operator==(const Link& other) const;
+  std::string toString() const;
+  std::string directionalToString(const std::string& fromNode) const;
+};
+
+class SpfEngineHandle;  // RAII owner of an openr_spf_ctx (LinkState.cpp)
+
+class LinkState {
+ public:
+  explicit LinkState(const std::string& area);
+
+  struct LinkPtrHash {
+    size_t operator()(const std::shared_ptr<Link>& l) const;
+  };
+  struct LinkPtrLess {
+    bool operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const;
+  };
+  struct LinkPtrEqual {
+    bool operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const;
+  };
+  using LinkSet = std::unordered_set<std::shared_ptr<Link>, LinkPtrHash, LinkPtrEqual>;
+
+  class NodeSpfResult {
+   public:
+    class PathLink {
+     public:
+      PathLink(std::shared_ptr<Link> const& l, std::string const& n) : link(l), prevNode(n) {}
+      std::shared_ptr<Link> const link;
+      std::string const prevNode;
+    };
+    explicit NodeSpfResult(LinkStateMetric m) : metric_(m) {}
+    void reset(LinkStateMetric newMetric) {
+      metric_ = newMetric;
+      pathLinks_.clear();
+      nextHops_.clear();
+    }
+    std::vector<PathLink> const& pathLinks() const { return pathLinks_; }
+    std::unordered_set<std::string> const& nextHops() const { return nextHops_; }
+    LinkStateMetric metric() const { return metric_; }
+    void addPath(std::shared_ptr<Link> const& link, std::string const& prevNode) {
+      pathLinks_.emplace_back(link, prevNode);
+    }
+    void addNextHops(std::unordered_set<std::string> const& toInsert) {
+      nextHops_.insert(toInsert.begin(), toInsert.end());
+    }
+    void addNextHop(std::string const& toInsert) { nextHops_.insert(toInsert); }
+
+   private:
+    LinkStateMetric metric_{std::numeric_limits<LinkStateMetric>::max()};
+    std::vector<PathLink> pathLinks_;
+    std::unordered_set<std::string> nextHops_;
+  };
+
+  using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
+  using Path = std::vector<std::shared_ptr<Link>>;
+
+  // memoized per (node, useLinkMetric) until the next topology change
+  SpfResult const& getSpfResult(const std::string& nodeName, bool useLinkMetric = true) const;
+
+  // Batched prefetch (new): one engine launch fills the memo for every node in
+  // `nodes` (e.g. me + neighbours for LFA, or all nodes for all-sources route build).
+  void prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
+
+  std::vector<LinkState::Path> const& getKthPaths(const std::string& src, const std::string& dest,
+                                                  size_t k) const;
+
+  class LinkStateChange {
+   public:
+    LinkStateChange() = default;
+    LinkStateChange(bool topo, bool link, bool node)
+        : topologyChanged(topo), linkAttributesChanged(link), nodeLabelChanged(node) {}
+    bool operator==(LinkStateChange const& other) const {
+      return topologyChanged == other.topologyChanged && linkAttributesChanged == other.linkAttributesChanged &&
+             nodeLabelChanged == other.nodeLabelChanged;
+    }
+    bool topologyChanged{false};
+    bool linkAttributesChanged{false};
+    bool nodeLabelChanged{false};
+  };
+
+  LinkStateChange decrementHolds();
+  LinkStateChange updateAdjacencyDatabase(thrift::AdjacencyDatabase const& adjacencyDb,
+                                          LinkStateMetric holdUpTtl = 0, LinkStateMetric holdDownTtl = 0);
+  LinkStateChange deleteAdjacencyDatabase(const std::string& nodeName);
+
+  std::optional<LinkStateMetric> getMetricFromAToB(std::string const& a, std::string const& b,
+                                                   bool useLinkMetric = true) const;
+  std::optional<LinkStateMetric> getHopsFromAToB(std::string const& a, std::string const& b) const {
+    return getMetricFromAToB(a, b, false);
+  }
+  LinkStateMetric getMaxHopsToNode(const std::string& nodeName) const;
+  const std::string& getArea() const { return area_; }
+  bool hasNode(const std::string& nodeName) const { return adjacencyDatabases_.count(nodeName) != 0; }
+  const LinkSet& linksFromNode(const std::string& nodeName) const;
+  bool isNodeOverloaded(const std::string& nodeName) const;
+  bool hasHolds() const;
+  size_t numLinks() const { return allLinks_.size(); }
+  size_t numNodes() const { return linkMap_.size(); }
+  std::unordered_map<std::string, thrift::AdjacencyDatabase> const& getAdjacencyDatabases() const {
+    return adjacencyDatabases_;
+  }
+  static bool pathAInPathB(Path const& a, Path const& b);
+
+  // --- engine mirror (introspection for tests and benchmarks) ---------------
+  struct CsrMirror {
+    std::vector<std::string> names;  // sorted: id == rank under std::string operator<
+    std::unordered_map<std::string, uint32_t> id;
+    std::vector<uint32_t> rowPtr, col, linkId;
+    std::vector<uint64_t> metric;
+    std::vector<uint8_t> edgeUp, overloaded;
+    std::vector<uint32_t> nameRank;
+    std::vector<std::shared_ptr<Link>> links;  // link id -> Link
+    std::vector<uint32_t> edgeOwner;
+  };
+  const CsrMirror& csrMirror() const;
+
+ private:
+  const std::string area_;
+  mutable std::unordered_map<std::pair<std::string, bool>, SpfResult> spfResults_;
+  mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<LinkState::Path>>
+      kthPathResults_;
+
+  std::optional<Path> traceOnePath(std::string const& src, std::string const& dest, SpfResult const& result,
+                                   LinkSet& linksToIgnore) const;
+  void addLink(std::shared_ptr<Link> link);
+  void removeLink(std::shared_ptr<Link> link);
+  void removeNode(const std::string& nodeName);
+  bool updateNodeOverloaded(const std::string& nodeName, bool isOverloaded, LinkStateMetric holdUpTtl,
+                            LinkStateMetric holdDownTtl);
+  SpfResult runSpf(const std::string& src, bool useLinkMetric, const LinkSet& linksToIgnore = {}) const;
+  std::vector<SpfResult> runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,
+                                     const std::vector<const LinkSet*>& ignores) const;
+  std::shared_ptr<Link> maybeMakeLink(const std::string& nodeName, const thrift::Adjacency& adj) const;
+  std::vector<std::shared_ptr<Link>> getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const;
+  std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;
+  void markMirrorDirty() { mirrorDirty_ = true; }
+
+  std::unordered_map<std::string, LinkSet> linkMap_;
+  LinkSet allLinks_;
+  std::unordered_map<std::string, HoldableValue<bool>> nodeOverloads_;
+  std::unordered_map<std::string, thrift::AdjacencyDatabase> adjacencyDatabases_;
+
+  mutable CsrMirror mirror_;
+  mutable bool mirrorDirty_ = true;
+  mutable uint64_t mirrorGeneration_ = 0;
+  mutable std::shared_ptr<SpfEngineHandle> engine_;
+};
+
+}  // namespace openr
+
+namespace std {
+template <>
+struct hash<openr::Link> {
+  size_t operator()(openr::Link const& link) const { return link.hash; }
+};
+}  // namespace std

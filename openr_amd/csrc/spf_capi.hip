@@ -71,11 +71,11 @@ struct Device {
   // scratch for host-buffer solves
   DevBuf<uint32_t> src, ign_ptr, ign_links;
   DevBuf<uint64_t> dist, tight;
-  DevBuf<uint8_t> nh;
+  DevBuf<uint8_t> nh, ovf;
 };
 
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
+  void* ptrs[] = {g.row, g.row2, g.ovl_bits, g.ell, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -197,6 +197,8 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh_bytes = nh_bytes;
     a.tight = tight ? d.tight.p : nullptr;
     a.nh_bits = ctx->nh_bits;
+    HIP_TRY(d.ovf.reserve(m));
+    a.ovf = d.ovf.p;
     HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
     HIP_TRY(launch(ctx, d, plan, a, d.stream));
     HIP_TRY(hipEventRecord(d.ev_end, d.stream));
@@ -300,6 +302,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.dist.release();
     d.tight.release();
     d.nh.release();
+    d.ovf.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -369,6 +372,18 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     rev[b] = a;
   }
   for (uint32_t e = 0; e < E; ++e) win[e] = w[rev[e]];
+  std::vector<uint2> row2(V);
+  std::vector<uint4> ell(V);
+  for (uint32_t u = 0; u < V; ++u) {
+    uint32_t x[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
+    for (uint32_t j = 0; j < 4 && gr->row_ptr[u] + j < gr->row_ptr[u + 1]; ++j) x[j] = adj[gr->row_ptr[u] + j];
+    ell[u] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  std::vector<uint32_t> ovl_bits((V + 31) / 32 + 1, 0);
+  for (uint32_t u = 0; u < V; ++u) {
+    row2[u] = make_uint2(gr->row_ptr[u], gr->row_ptr[u + 1]);
+    if (ovl[u]) ovl_bits[u >> 5] |= 1u << (u & 31u);
+  }
   if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
 
@@ -388,6 +403,9 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
       return err;
     };
     hipError_t err = up(&g.row, gr->row_ptr, V + 1);
+    if (err == hipSuccess) err = up(&g.row2, row2.data(), V);
+    if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
+    if (err == hipSuccess) err = up(&g.ell, ell.data(), V);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
     if (err == hipSuccess) err = up(&g.win, win.data(), E);
@@ -410,9 +428,12 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->w_min = w_min;
   ctx->w_max = w_max;
   ctx->metric_ok = metric_ok;
+  // lanes per frontier node: enough that one pass of kBfsEdgesPerLane edges per lane
+  // covers an average row (grid: 1 lane x 4 edges; fabric: 8 lanes x 4 edges)
   const uint32_t avg = V ? (E + V - 1) / V : 1;
+  const uint32_t per_lane = (avg + kBfsEdgesPerLane - 1) / kBfsEdgesPerLane;
   uint32_t gl = 1;
-  while (gl < avg && gl < 64) gl <<= 1;
+  while (gl < per_lane && gl < 64) gl <<= 1;
   ctx->group_lanes = gl;
   ctx->has_graph = true;
   return OPENR_SPF_OK;
@@ -478,6 +499,8 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bytes = nh_bytes;
   a.tight = d_tight;
   a.nh_bits = ctx->nh_bits;
+  HIP_TRY(d.ovf.reserve(n));
+  a.ovf = d.ovf.p;
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;

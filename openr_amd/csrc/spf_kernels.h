@@ -16,6 +16,9 @@ namespace openr_spf {
 struct DevGraph {
   uint32_t V = 0, E = 0, L = 0;
   uint32_t* row = nullptr;     // [V+1]
+  uint2* row2 = nullptr;       // [V] (row[u], row[u+1]) in one 8-byte load
+  uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
+  uint4* ell = nullptr;        // [V] first 4 edges of each row (adj encoding, kEdgeDown-padded)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
   uint32_t* win = nullptr;     // [E] metric of the reverse edge (col -> row owner)
@@ -27,6 +30,8 @@ struct DevGraph {
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
 constexpr uint32_t kBlock = 256;
+constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
+constexpr uint32_t kBfsTargetWgs = 6;     // fast-path BFS sizes its LDS for this many workgroups per CU
 
 // Next-hop bitset storage classes in LDS (chosen from the max distinct degree).
 enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, kNhW8 = 5 };
@@ -43,6 +48,7 @@ struct SolveArgs {
   uint32_t nh_bytes;
   uint64_t* tight;            // nullable [n][ceil(E/64)] (zeroed by the launcher)
   uint32_t nh_bits;           // bits that are meaningful (max distinct degree)
+  uint8_t* ovf;               // [n] scratch: BFS deeper than the u8 level range (re-run with u16)
 };
 
 struct LaunchInfo {

@@ -47,6 +47,11 @@ struct Nh<kNhByte> {  // <= 8 bits: four nodes per dword
   static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
     return j == 0 ? (nh[v >> 2] >> ((v & 3u) * 8u)) & 0xFFu : 0u;
   }
+  struct Val { uint32_t x; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu}; }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+    if (s.x) atomicOr(&nh[v >> 2], s.x << ((v & 3u) * 8u));
+  }
 };
 
 template <>
@@ -61,6 +66,11 @@ struct Nh<kNhHalf> {  // <= 16 bits: two nodes per dword
   }
   static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
     return j < 2 ? (nh[v >> 1] >> ((v & 1u) * 16u + 8u * j)) & 0xFFu : 0u;
+  }
+  struct Val { uint32_t x; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu}; }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+    if (s.x) atomicOr(&nh[v >> 1], s.x << ((v & 1u) * 16u));
   }
 };
 
@@ -79,6 +89,18 @@ struct NhWords {  // W dwords per node
   }
   static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
     return j < 4u * W ? (nh[v * W + (j >> 2)] >> (8u * (j & 3u))) & 0xFFu : 0u;
+  }
+  struct Val { uint32_t x[W]; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) {
+    Val r;
+#pragma unroll
+    for (int k = 0; k < W; ++k) r.x[k] = nh[u * W + k];
+    return r;
+  }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+#pragma unroll
+    for (int k = 0; k < W; ++k)
+      if (s.x[k]) atomicOr(&nh[v * W + k], s.x[k]);
   }
 };
 template <> struct Nh<kNhW1> : NhWords<1> {};
@@ -116,23 +138,27 @@ __device__ __forceinline__ void load_ignore(uint32_t* ign, uint32_t words, const
   (void)words;
 }
 
+template <typename LT>
 struct BfsLayout {
-  uint32_t order, lvl, vis, prev, nh, ign, total;
+  uint32_t lvl, nh, ring, ovl, ign, total;
 };
 
-__host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words) {
-  BfsLayout l;
-  uint32_t off = 16;  // control words
+// ring = frontier queue (power of two, wraps) in the fast path, or the full BFS-order
+// array (capacity V, never wraps) in the fallback path.
+template <typename LT>
+__host__ __device__ inline BfsLayout<LT> bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
+                                                    uint32_t ring_cap) {
+  BfsLayout<LT> l;
+  uint32_t off = 16;  // control: append counters [0..2], overflow flag [3]
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
     return o;
   };
-  l.order = take(2u * V);
-  l.lvl = take(2u * V);
-  l.vis = take(4u * ((V + 31u) / 32u));
-  l.prev = take(4u * ((V + 31u) / 32u));
+  l.lvl = take((uint32_t)sizeof(LT) * (V + 4u));
   l.nh = take(4u * nh_words);
+  l.ring = take(2u * ring_cap);
+  l.ovl = take(4u * ((V + 31u) / 32u));
   l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
   l.total = off;
   return l;
@@ -163,112 +189,211 @@ __host__ __device__ inline BucketLayout bucket_layout(uint32_t V, uint32_t L, bo
 // ---------------------------------------------------------------------------
 // Uniform-cost kernel: level-synchronous BFS
 // ---------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, uint64_t cost,
-                                                     uint32_t glog, uint32_t has_ign) {
+// LDS per solve: lvl[] (LT, all-ones = not reached), next-hop bitsets, and the
+// frontier queue. Level L expands queue slots [head, tail): groups of G lanes per
+// frontier node, K edges per lane loaded ahead (rows of degree <= 4 come from one
+// 16-byte ELL load when G == 1). Edge u->v is tight iff lvl[v] > L; the first
+// arrival claims v with a CAS on the lvl word (back edges cost one plain LDS read),
+// fresh nodes are appended with one LDS atomic per wave per pass. One barrier per
+// level; append counters are triple-buffered.
+//   RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent
+//                 levels exceed the ring, or whose depth exceeds 253, sets ovf[sid].
+//   RING = false: LT = u16, queue = full BFS order (capacity V); re-runs flagged solves.
+template <typename LT>
+struct LvlOps;
+template <>
+struct LvlOps<uint8_t> {
+  static constexpr uint32_t kPer = 4, kBits = 8, kUnset = 0xFFu;
+};
+template <>
+struct LvlOps<uint16_t> {
+  static constexpr uint32_t kPer = 2, kBits = 16, kUnset = 0xFFFFu;
+};
+
+// 0: v settled at a level <= L (not tight); 1: tight, already reached at L+1; 2: tight & first.
+template <typename LT>
+__device__ __forceinline__ uint32_t claim_level(uint32_t* lvl_w, uint32_t v, uint32_t L) {
+  using O = LvlOps<LT>;
+  const uint32_t w = v / O::kPer, shift = (v % O::kPer) * O::kBits, mask = O::kUnset << shift;
+  uint32_t old = lvl_w[w];
+  for (;;) {
+    const uint32_t cur = (old & mask) >> shift;
+    if (cur <= L) return 0;
+    if (cur == L + 1u) return 1;
+    const uint32_t prev = atomicCAS(&lvl_w[w], old, (old & ~mask) | ((L + 1u) << shift));
+    if (prev == old) return 2;
+    old = prev;
+  }
+}
+
+// Exclusive prefix of a small per-lane count (< 8) across the wave, via 3 ballots.
+__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t c, uint32_t* total) {
+  const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+  const unsigned long long lt = (1ull << __lane_id()) - 1ull;
+  *total = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  return (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+}
+
+template <int MODE, int K, typename LT, bool RING, bool ELL>
+__global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog,
+                                                     uint32_t has_ign, uint32_t ring_cap, uint32_t rerun) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   using N = Nh<MODE>;
+  using O = LvlOps<LT>;
   const uint32_t V = g.V, tid = threadIdx.x;
   const uint32_t nh_words = N::words(V);
-  const BfsLayout lay = bfs_layout(V, g.L, has_ign != 0, nh_words);
+  const BfsLayout<LT> lay = bfs_layout<LT>(V, g.L, has_ign != 0, nh_words, ring_cap);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
-  uint16_t* order = reinterpret_cast<uint16_t*>(base + lay.order);
-  uint16_t* lvl = reinterpret_cast<uint16_t*>(base + lay.lvl);
-  uint32_t* vis = reinterpret_cast<uint32_t*>(base + lay.vis);
-  uint32_t* prev = reinterpret_cast<uint32_t*>(base + lay.prev);
+  LT* lvl = reinterpret_cast<LT*>(base + lay.lvl);
+  uint32_t* lvl_w = reinterpret_cast<uint32_t*>(base + lay.lvl);
   uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
+  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
+  uint32_t* ovl = reinterpret_cast<uint32_t*>(base + lay.ovl);
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
-  const uint32_t vis_words = (V + 31u) / 32u;
+  const uint32_t bit_words = (V + 31u) / 32u;
+  const uint32_t lvl_words = (V + O::kPer - 1u) / O::kPer + 1u;
   const uint32_t ign_words = (g.L + 31u) / 32u;
   const uint32_t G = 1u << glog, ngroups = kBlock >> glog;
   const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
   const uint32_t tight_words = (g.E + 63u) / 64u;
+  const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
+
+  for (uint32_t i = tid; i < bit_words; i += kBlock) ovl[i] = g.ovl_bits[i];
 
   for (uint32_t sid = blockIdx.x; sid < a.n; sid += gridDim.x) {
+    if (rerun && !a.ovf[sid]) continue;  // block-uniform
     const uint32_t src = a.sources[sid];
-    for (uint32_t i = tid; i < vis_words; i += kBlock) {
-      vis[i] = 0;
-      prev[i] = 0;
-    }
+    for (uint32_t i = tid; i < lvl_words; i += kBlock) lvl_w[i] = 0xFFFFFFFFu;
     for (uint32_t i = tid; i < nh_words; i += kBlock) nh[i] = 0;
     if (has_ign)
       for (uint32_t i = tid; i < ign_words; i += kBlock) ign[i] = 0;
+    if (tid == 0) ctl[0] = ctl[1] = ctl[2] = ctl[3] = 0;
     __syncthreads();
     if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
     if (tid == 0) {
-      vis[src >> 5] |= 1u << (src & 31u);
-      prev[src >> 5] |= 1u << (src & 31u);
-      order[0] = (uint16_t)src;
       lvl[src] = 0;
-      ctl[1] = 1;
+      ring[0] = (uint16_t)src;
     }
     __syncthreads();
-
-    uint32_t head = 0, tail = 1, level = 0;
     uint64_t* trow = a.tight ? a.tight + (size_t)sid * tight_words : nullptr;
+
+    uint32_t head = 0, tail = 1, L = 0;
+    bool overflow = false;  // block-uniform
     while (head < tail) {
+      if (RING && L + 1u >= O::kUnset) {  // next level not representable in u8
+        overflow = true;
+        break;
+      }
+      uint32_t* cnt = &ctl[L % 3u];
+      if (tid == 0) ctl[(L + 1u) % 3u] = 0;  // last read two barriers ago
       for (uint32_t fb = head; fb < tail; fb += ngroups) {
         const uint32_t idx = fb + group;
-        uint32_t u = 0, beg = 0, end = 0;
+        uint32_t u = src, beg = 0, end = 0;
+        uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
         if (idx < tail) {
-          u = order[idx];
-          // overloaded nodes other than the source are sinks (LinkState.cpp:831-838)
-          if (u == src || !g.ovl[u]) {
-            beg = g.row[u];
-            end = g.row[u + 1];
+          u = ring[RING ? (idx & rmask) : idx];
+          if (u == src || !test_bit(ovl, u)) {  // overloaded non-source nodes are sinks
+            const uint2 r = g.row2[u];
+            beg = r.x;
+            end = r.y;
+            if (ELL) ell = g.ell[u];
           }
         }
-        for (uint32_t k = 0;; ++k) {
-          const uint32_t e = beg + lane_g + k * G;
-          const bool has = e < end;
-          if (!__any(has)) break;
-          bool fresh = false;
-          uint32_t v = 0;
-          if (has) {
-            const uint32_t av = g.adj[e];
-            if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e]))) {
-              v = av;
-              if (!test_bit(prev, v)) {  // v not settled at a level <= current
-                const uint32_t bit = 1u << (v & 31u);
-                fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
-                if (u == src)
-                  N::or_bit(nh, v, g.nbr[e]);  // directly connected: nextHops = {v}
-                else
-                  N::or_from(nh, v, u);  // addNextHops(nh(u))
-                if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
-              }
+        const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
+        // pass p covers edges beg + lane_g + (p*K + j)*G; with ELL the first pass reads `ell`
+        for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
+          uint32_t av[K], lv[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t e = e0 + j * G;
+            if (ELL && e0 == beg) {
+              av[j] = j == 0 ? ell.x : j == 1 ? ell.y : j == 2 ? ell.z : ell.w;
+            } else {
+              av[j] = e < end ? g.adj[e] : kEdgeDown;
+            }
+            lv[j] = (has_ign && e < end) ? g.lid[e] : 0u;
+          }
+          uint32_t st[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t e = e0 + j * G;
+            const uint32_t v = av[j] & ~kEdgeDown;
+            st[j] = 0;
+            if (!(av[j] & kEdgeDown) && e < end && !(has_ign && test_bit(ign, lv[j])))
+              st[j] = claim_level<LT>(lvl_w, v, L);
+          }
+          uint32_t nfresh = 0;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t e = e0 + j * G;
+            if (st[j]) {  // tight edge: first or equal-cost arrival (LinkState.cpp:857-873)
+              const uint32_t v = av[j] & ~kEdgeDown;
+              if (u == src)
+                N::or_bit(nh, v, g.nbr[e]);  // directly connected: nextHops = {v}
+              else
+                N::or_val(nh, v, nhu);       // addNextHops(nh(u))
+              if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+              nfresh += st[j] >> 1;
             }
           }
-          const uint32_t slot = wave_append(fresh, &ctl[1]);
-          if (fresh) {
-            order[slot] = (uint16_t)v;
-            lvl[v] = (uint16_t)(level + 1u);
+          uint32_t total;
+          uint32_t slot = wave_prefix_small(nfresh, &total);
+          uint32_t wbase = 0;
+          if (total) {
+            const int leader = __ffsll((long long)__ballot(nfresh != 0)) - 1;
+            if ((int)__lane_id() == leader) wbase = atomicAdd(cnt, total);
+            wbase = __shfl(wbase, leader);
+          }
+          slot += tail + wbase;
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            if (st[j] == 2u) {
+              const uint32_t v = av[j] & ~kEdgeDown;
+              if (!RING) {
+                ring[slot] = (uint16_t)v;
+              } else if (slot - head < ring_cap) {
+                ring[slot & rmask] = (uint16_t)v;
+              } else {
+                ctl[3] = 1;  // two adjacent levels exceed the ring
+              }
+              ++slot;
+            }
           }
         }
-      }
-      __syncthreads();
-      const uint32_t new_tail = ctl[1];
-      for (uint32_t i = tail + tid; i < new_tail; i += kBlock) {
-        const uint32_t v = order[i];
-        atomicOr(&prev[v >> 5], 1u << (v & 31u));
       }
       __syncthreads();
       head = tail;
-      tail = new_tail;
-      ++level;
+      tail += *cnt;
+      ++L;
+      if (RING && ctl[3]) {  // ring overflow; ctl[3] is uniform after the barrier
+        overflow = true;
+        break;
+      }
+    }
+    if (RING && overflow) {  // re-run by the u16 / full-order variant
+      if (tid == 0) a.ovf[sid] = 1;
+      __syncthreads();
+      continue;
     }
 
     uint64_t* drow = a.dist + (size_t)sid * V;
-    for (uint32_t v = tid; v < V; v += kBlock)
-      drow[v] = test_bit(vis, v) ? (uint64_t)lvl[v] * cost : ~0ull;
+    for (uint32_t v = tid; v < V; v += kBlock) {
+      const uint32_t l = lvl[v];
+      drow[v] = l != O::kUnset ? (uint64_t)l * cost : ~0ull;
+    }
     if (a.nh) {
       const uint32_t nb = a.nh_bytes;
       uint8_t* nrow = a.nh + (size_t)sid * V * nb;
-      const uint32_t total = V * nb;
-      for (uint32_t i = tid; i < total; i += kBlock) {
-        const uint32_t v = i / nb, j = i - v * nb;
-        nrow[i] = (uint8_t)N::byte(nh, v, j);
+      if (MODE == kNhByte && nb == 1 && ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0) {
+        uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+        for (uint32_t i = tid; i < V / 4u; i += kBlock) nrow32[i] = nh[i];
+      } else {
+        const uint32_t total = V * nb;
+        for (uint32_t i = tid; i < total; i += kBlock) {
+          const uint32_t v = i / nb, j = i - v * nb;
+          nrow[i] = (uint8_t)N::byte(nh, v, j);
+        }
       }
     }
     __syncthreads();
@@ -465,8 +590,9 @@ int nh_mode_for_bits(uint32_t bits) {
 uint32_t nh_mode_lds_bytes(int mode, uint32_t V) { return 4u * nh_words_for(mode, V); }
 
 uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode) {
+  // the full-order u16 variant must fit (it re-runs solves the fast path flags)
   if (V > 65535u) return 0;
-  uint32_t t = bfs_layout(V, L, has_ignore, nh_words_for(nh_mode, V)).total;
+  uint32_t t = bfs_layout<uint16_t>(V, L, has_ignore, nh_words_for(nh_mode, V), V).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -476,37 +602,80 @@ uint32_t bucket_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, 
   return t <= kMaxLds ? t : 0;
 }
 
+namespace {
+template <int MODE, typename LT, bool RING, bool ELL>
+hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                              uint32_t ring_cap, uint32_t rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
+  constexpr int K = (int)kBfsEdgesPerLane;
+  const uint32_t lds = bfs_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), ring_cap).total;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus);
+  auto k = bfs_kernel<MODE, K, LT, RING, ELL>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  if (info && !rerun) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = RING ? "bfs_kernel<ring,u8>" : "bfs_kernel<full,u16>";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun);
+  return hipGetLastError();
+}
+
+// Fast path: u8 levels + a ring sized so that kBfsTargetWgs workgroups fit a CU.
+// It cannot be used when its ring would be smaller than kMinRing entries; then the
+// full-order u16 variant runs directly.
+uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode) {
+  const uint32_t fixed = bfs_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), 0).total;
+  const uint32_t budget = kMaxLds / kBfsTargetWgs;
+  if (fixed >= budget) return 0;
+  uint32_t cap = 1;
+  while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
+  return cap >= 256u ? cap : 0u;
+}
+
+template <int MODE, bool ELL>
+hipError_t launch_bfs_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                           int num_cus, hipStream_t s, LaunchInfo* info) {
+  const uint32_t cap = fast_ring_cap(g, has_ign, MODE);
+  if (!cap) return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, 0, num_cus, s, info);
+  const bool may_overflow = g.V > cap || g.V > 254u;
+  if (may_overflow) {
+    if (!a.ovf) return hipErrorInvalidValue;
+    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
+    if (err != hipSuccess) return err;
+  }
+  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELL>(g, a, cost, glog, has_ign, cap, 0, num_cus, s, info);
+  if (err != hipSuccess || !may_overflow) return err;
+  return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, 1, num_cus, s, info);
+}
+}  // namespace
+
 hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, int group_lanes,
                       int num_cus, hipStream_t s, LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
-  const uint32_t lds = bfs_lds_bytes(g.V, g.L, has_ign, nh_mode);
-  if (!lds) return hipErrorInvalidValue;
+  if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
+  if (a.tight) {
+    hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((g.E + 63u) / 64u) * 8u, s);
+    if (err != hipSuccess) return err;
+  }
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
-  const uint32_t grid = blocks_for(a.n, lds, num_cus);
-  if (info) {
-    info->lds_bytes = lds;
-    info->grid = grid;
-    info->kernel = "bfs_kernel";
-  }
-#define OPENR_BFS_CASE(M)                                                                        \
-  case M: {                                                                                      \
-    auto k = bfs_kernel<M>;                                                                      \
-    hipError_t err = launch_common(k, lds, grid, s, a, g);                                       \
-    if (err != hipSuccess) return err;                                                           \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, s, g, a, cost, glog, (uint32_t)has_ign); \
-    return hipGetLastError();                                                                    \
-  }
+  const bool ell = glog == 0 && g.ell != nullptr;
+#define OPENR_BFS_MODE(M)                                                                   \
+  case M:                                                                                   \
+    return ell ? launch_bfs_mode<M, true>(g, a, cost, glog, has_ign, num_cus, s, info)      \
+               : launch_bfs_mode<M, false>(g, a, cost, glog, has_ign, num_cus, s, info);
   switch (nh_mode) {
-    OPENR_BFS_CASE(kNhByte)
-    OPENR_BFS_CASE(kNhHalf)
-    OPENR_BFS_CASE(kNhW1)
-    OPENR_BFS_CASE(kNhW2)
-    OPENR_BFS_CASE(kNhW4)
-    OPENR_BFS_CASE(kNhW8)
+    OPENR_BFS_MODE(kNhByte)
+    OPENR_BFS_MODE(kNhHalf)
+    OPENR_BFS_MODE(kNhW1)
+    OPENR_BFS_MODE(kNhW2)
+    OPENR_BFS_MODE(kNhW4)
+    OPENR_BFS_MODE(kNhW8)
   }
-#undef OPENR_BFS_CASE
+#undef OPENR_BFS_MODE
   return hipErrorInvalidValue;
 }
 

@@ -1,0 +1,600 @@
+// linkstate_test.cpp — tests of the C++ host mirror of openr::LinkState.
+//
+// Transcribes /root/reference/openr/decision/tests/LinkStateTest.cpp and the
+// LinkState-level expectations of DecisionTest.cpp (file:line per test), plus
+// oracle cross-checks (the oracle is linked here as the checker only).
+//   linkstate_test cpu   -> host-only tests (no GPU needed)
+//   linkstate_test gpu   -> tests that run SPF on the engine
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../oracle/spf_oracle.h"
+#include "../../openr_amd/csrc/host/LinkState.h"
+
+using namespace openr;
+
+static int g_failures = 0, g_checks = 0;
+#define EXPECT_TRUE(c)                                                   \
+  do {                                                                   \
+    ++g_checks;                                                          \
+    if (!(c)) {                                                          \
+      ++g_failures;                                                      \
+      std::fprintf(stderr, "  FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+    }                                                                    \
+  } while (0)
+#define EXPECT_FALSE(c) EXPECT_TRUE(!(c))
+#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
+#define EXPECT_THROW(stmt)  \
+  do {                      \
+    bool thrown = false;    \
+    try {                   \
+      stmt;                 \
+    } catch (...) {         \
+      thrown = true;        \
+    }                       \
+    EXPECT_TRUE(thrown);    \
+  } while (0)
+
+struct TestCase {
+  const char* name;
+  bool gpu;
+  std::function<void()> fn;
+};
+static std::vector<TestCase>& registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+struct Reg {
+  Reg(const char* n, bool gpu, std::function<void()> f) { registry().push_back({n, gpu, std::move(f)}); }
+};
+#define TEST_CPU(name) \
+  static void name();  \
+  static Reg reg_##name(#name, false, name);  \
+  static void name()
+#define TEST_GPU(name) \
+  static void name();  \
+  static Reg reg_##name(#name, true, name);  \
+  static void name()
+
+static const std::string kArea = "0";
+
+static thrift::Adjacency createAdjacency(const std::string& otherNode, const std::string& ifName,
+                                         const std::string& otherIfName, int32_t metric, int32_t adjLabel = 0) {
+  thrift::Adjacency a;
+  a.otherNodeName = otherNode;
+  a.ifName = ifName;
+  a.otherIfName = otherIfName;
+  a.metric = metric;
+  a.adjLabel = adjLabel;
+  a.nextHopV6.addr = "fe80::" + otherNode;
+  a.nextHopV4.addr = "10.0.0." + otherNode;
+  return a;
+}
+
+static thrift::AdjacencyDatabase createAdjDb(const std::string& node, std::vector<thrift::Adjacency> adjs,
+                                             int32_t nodeLabel) {
+  thrift::AdjacencyDatabase db;
+  db.thisNodeName = node;
+  db.adjacencies = std::move(adjs);
+  db.nodeLabel = nodeLabel;
+  db.area = kArea;
+  return db;
+}
+
+// getLinkState fixture builder (DecisionTestUtils.cpp:16-42)
+static LinkState getLinkState(const std::vector<std::pair<int, std::vector<std::pair<int, int>>>>& adjMap) {
+  LinkState ls(kArea);
+  for (auto const& [node, adjList] : adjMap) {
+    std::vector<thrift::Adjacency> adjs;
+    std::map<int, int> numParallel;
+    for (auto const& [adj, weight] : adjList) {
+      const int k = numParallel[adj]++;
+      adjs.push_back(createAdjacency(std::to_string(adj), std::to_string(node) + "/" + std::to_string(adj) + "/" +
+                                                             std::to_string(k),
+                                     std::to_string(adj) + "/" + std::to_string(node) + "/" + std::to_string(k),
+                                     weight, (node << 16) + adj));
+    }
+    ls.updateAdjacencyDatabase(createAdjDb(std::to_string(node), adjs, node), 0, 0);
+  }
+  return ls;
+}
+
+static std::vector<std::pair<int, std::vector<std::pair<int, int>>>> unit(
+    const std::vector<std::pair<int, std::vector<int>>>& m) {
+  std::vector<std::pair<int, std::vector<std::pair<int, int>>>> r;
+  for (auto const& [n, adjs] : m) {
+    std::vector<std::pair<int, int>> w;
+    for (int a : adjs) w.emplace_back(a, 1);
+    r.emplace_back(n, w);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// LinkStateTest.cpp:22-83
+TEST_CPU(HoldableValueTest_BasicOperation) {
+  HoldableValue<bool> hv{true};
+  EXPECT_TRUE(hv.value());
+  EXPECT_FALSE(hv.hasHold());
+  EXPECT_FALSE(hv.decrementTtl());
+  const LinkStateMetric holdUpTtl = 10, holdDownTtl = 5;
+  EXPECT_FALSE(hv.updateValue(false, holdUpTtl, holdDownTtl));
+  for (LinkStateMetric i = 0; i < holdUpTtl - 1; ++i) {
+    EXPECT_TRUE(hv.hasHold());
+    EXPECT_TRUE(hv.value());
+    EXPECT_FALSE(hv.decrementTtl());
+  }
+  EXPECT_TRUE(hv.decrementTtl());
+  EXPECT_FALSE(hv.hasHold());
+  EXPECT_FALSE(hv.value());
+  EXPECT_FALSE(hv.updateValue(false, holdUpTtl, holdDownTtl));
+  EXPECT_FALSE(hv.hasHold());
+  EXPECT_FALSE(hv.value());
+  EXPECT_FALSE(hv.updateValue(true, holdUpTtl, holdDownTtl));
+  for (LinkStateMetric i = 0; i < holdDownTtl - 1; ++i) {
+    EXPECT_TRUE(hv.hasHold());
+    EXPECT_FALSE(hv.value());
+    EXPECT_FALSE(hv.decrementTtl());
+  }
+  EXPECT_TRUE(hv.decrementTtl());
+  EXPECT_FALSE(hv.hasHold());
+  EXPECT_TRUE(hv.value());
+  EXPECT_FALSE(hv.updateValue(false, holdUpTtl, holdDownTtl));
+  EXPECT_TRUE(hv.hasHold());
+  EXPECT_TRUE(hv.value());
+  EXPECT_FALSE(hv.decrementTtl());
+  EXPECT_TRUE(hv.updateValue(true, holdUpTtl, holdDownTtl));
+  EXPECT_FALSE(hv.hasHold());
+  EXPECT_TRUE(hv.value());
+
+  HoldableValue<LinkStateMetric> hvLsm{10};
+  EXPECT_EQ(10u, hvLsm.value());
+  EXPECT_FALSE(hvLsm.hasHold());
+  EXPECT_FALSE(hvLsm.decrementTtl());
+  EXPECT_FALSE(hvLsm.updateValue(5, holdUpTtl, holdDownTtl));
+  for (LinkStateMetric i = 0; i < holdUpTtl - 1; ++i) {
+    EXPECT_TRUE(hvLsm.hasHold());
+    EXPECT_EQ(10u, hvLsm.value());
+    EXPECT_FALSE(hvLsm.decrementTtl());
+  }
+  EXPECT_TRUE(hvLsm.decrementTtl());
+  EXPECT_FALSE(hvLsm.hasHold());
+  EXPECT_EQ(5u, hvLsm.value());
+}
+
+// LinkStateTest.cpp:85-137
+TEST_CPU(LinkTest_BasicOperation) {
+  std::string n1 = "node1";
+  auto adj1 = createAdjacency(n1, "if1", "if2", 1, 1);
+  std::string n2 = "node2";
+  auto adj2 = createAdjacency(n2, "if2", "if1", 1, 2);
+  Link l1(kArea, n1, adj1, n2, adj2);
+  EXPECT_EQ(kArea, l1.getArea());
+  EXPECT_EQ(n2, l1.getOtherNodeName(n1));
+  EXPECT_EQ(n1, l1.getOtherNodeName(n2));
+  EXPECT_THROW(l1.getOtherNodeName("node3"));
+  EXPECT_EQ(adj1.ifName, l1.getIfaceFromNode(n1));
+  EXPECT_EQ(adj2.ifName, l1.getIfaceFromNode(n2));
+  EXPECT_THROW(l1.getIfaceFromNode("node3"));
+  EXPECT_EQ((LinkStateMetric)adj1.metric, l1.getMetricFromNode(n1));
+  EXPECT_EQ((LinkStateMetric)adj2.metric, l1.getMetricFromNode(n2));
+  EXPECT_THROW(l1.getMetricFromNode("node3"));
+  EXPECT_EQ(adj1.adjLabel, l1.getAdjLabelFromNode(n1));
+  EXPECT_EQ(adj2.adjLabel, l1.getAdjLabelFromNode(n2));
+  EXPECT_THROW(l1.getAdjLabelFromNode("node3"));
+  EXPECT_FALSE(l1.getOverloadFromNode(n1));
+  EXPECT_FALSE(l1.getOverloadFromNode(n2));
+  EXPECT_TRUE(l1.isUp());
+  EXPECT_TRUE(l1.setMetricFromNode(n1, 2, 0, 0));
+  EXPECT_EQ(2u, l1.getMetricFromNode(n1));
+  EXPECT_TRUE(l1.setOverloadFromNode(n2, true, 0, 0));
+  EXPECT_FALSE(l1.getOverloadFromNode(n1));
+  EXPECT_TRUE(l1.getOverloadFromNode(n2));
+  EXPECT_FALSE(l1.isUp());
+  Link l2(kArea, n2, adj2, n1, adj1);
+  EXPECT_TRUE(l1 == l2);
+  EXPECT_FALSE(l1 < l2);
+  EXPECT_FALSE(l2 < l1);
+  std::string n3 = "node3";
+  auto adj3 = createAdjacency(n2, "if3", "if2", 1, 1);
+  Link l3(kArea, n1, adj1, n3, adj3);
+  EXPECT_FALSE(l1 == l3);
+  EXPECT_TRUE(l1 < l3 || l3 < l1);
+}
+
+static bool sameLinks(const LinkState::LinkSet& set, std::vector<Link> want) {
+  if (set.size() != want.size()) return false;
+  for (auto const& w : want) {
+    bool found = false;
+    for (auto const& l : set) found |= (*l == w);
+    if (!found) return false;
+  }
+  return true;
+}
+
+// LinkStateTest.cpp:139-200
+TEST_CPU(LinkStateTest_BasicOperation) {
+  std::string n1 = "node1", n2 = "node2", n3 = "node3";
+  auto adj12 = createAdjacency(n2, "if2", "if1", 1, 1);
+  auto adj13 = createAdjacency(n3, "if3", "if1", 1, 1);
+  auto adj21 = createAdjacency(n1, "if1", "if2", 1, 1);
+  auto adj23 = createAdjacency(n3, "if3", "if2", 1, 1);
+  auto adj31 = createAdjacency(n1, "if1", "if3", 1, 1);
+  auto adj32 = createAdjacency(n2, "if2", "if3", 1, 1);
+  Link l1(kArea, n1, adj12, n2, adj21);
+  Link l2(kArea, n2, adj23, n3, adj32);
+  Link l3(kArea, n3, adj31, n1, adj13);
+  auto adjDb1 = createAdjDb(n1, {adj12, adj13}, 1);
+  auto adjDb2 = createAdjDb(n2, {adj21, adj23}, 2);
+  auto adjDb3 = createAdjDb(n3, {adj31, adj32}, 3);
+  LinkState state{kArea};
+  EXPECT_EQ(kArea, state.getArea());
+  EXPECT_FALSE(state.updateAdjacencyDatabase(adjDb1, 0, 0).topologyChanged);
+  EXPECT_TRUE(state.updateAdjacencyDatabase(adjDb2, 0, 0).topologyChanged);
+  EXPECT_TRUE(state.updateAdjacencyDatabase(adjDb3, 0, 0).topologyChanged);
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n1), {l1, l3}));
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n2), {l1, l2}));
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n3), {l2, l3}));
+  EXPECT_TRUE(state.linksFromNode("node4").empty());
+  EXPECT_FALSE(state.isNodeOverloaded(n1));
+  adjDb1.isOverloaded = true;
+  EXPECT_TRUE(state.updateAdjacencyDatabase(adjDb1, 0, 0).topologyChanged);
+  EXPECT_TRUE(state.isNodeOverloaded(n1));
+  EXPECT_FALSE(state.updateAdjacencyDatabase(adjDb1, 0, 0).topologyChanged);
+  adjDb1.isOverloaded = false;
+  EXPECT_TRUE(state.updateAdjacencyDatabase(adjDb1, 0, 0).topologyChanged);
+  EXPECT_FALSE(state.isNodeOverloaded(n1));
+  adjDb1 = createAdjDb(n1, {adj13}, 1);
+  EXPECT_TRUE(state.updateAdjacencyDatabase(adjDb1, 0, 0).topologyChanged);
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n1), {l3}));
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n2), {l2}));
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n3), {l2, l3}));
+  EXPECT_TRUE(state.deleteAdjacencyDatabase(n1).topologyChanged);
+  EXPECT_TRUE(state.linksFromNode(n1).empty());
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n2), {l2}));
+  EXPECT_TRUE(sameLinks(state.linksFromNode(n3), {l2}));
+}
+
+// LinkStateTest.cpp:202-242
+TEST_CPU(LinkStateTest_pathAInPathB) {
+  auto l1 = std::make_shared<Link>(kArea, "1", "1/2", "2", "2/1");
+  auto l2 = std::make_shared<Link>(kArea, "2", "2/3", "3", "3/2");
+  auto l3 = std::make_shared<Link>(kArea, "1", "1/3", "3", "3/1");
+  LinkState::Path p1, p2;
+  EXPECT_TRUE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_TRUE(LinkState::pathAInPathB(p2, p1));
+  p1.push_back(l1);
+  EXPECT_FALSE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_TRUE(LinkState::pathAInPathB(p2, p1));
+  p2.push_back(l1);
+  EXPECT_TRUE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_TRUE(LinkState::pathAInPathB(p2, p1));
+  p1.push_back(l2);
+  EXPECT_FALSE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_TRUE(LinkState::pathAInPathB(p2, p1));
+  p1.push_back(l3);
+  p2.push_back(l2);
+  EXPECT_FALSE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_TRUE(LinkState::pathAInPathB(p2, p1));
+  p1.clear();
+  p2.clear();
+  p1.push_back(l3);
+  p1.push_back(l2);
+  p2.push_back(l1);
+  EXPECT_FALSE(LinkState::pathAInPathB(p1, p2));
+  EXPECT_FALSE(LinkState::pathAInPathB(p2, p1));
+}
+
+// Hold-down: a link added with holdUpTtl stays down until the hold expires.
+TEST_CPU(LinkStateTest_HoldUpAndMirror) {
+  LinkState ls(kArea);
+  ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 1), 0, 0);
+  auto ch = ls.updateAdjacencyDatabase(createAdjDb("b", {createAdjacency("a", "b/a", "a/b", 4)}, 2), 2, 0);
+  EXPECT_FALSE(ch.topologyChanged);  // held up
+  EXPECT_TRUE(ls.hasHolds());
+  auto const& m = ls.csrMirror();
+  EXPECT_EQ(2u, (unsigned)m.names.size());
+  EXPECT_EQ(2u, (unsigned)m.col.size());
+  EXPECT_EQ(0, (int)m.edgeUp[0]);
+  EXPECT_FALSE(ls.decrementHolds().topologyChanged);
+  EXPECT_TRUE(ls.decrementHolds().topologyChanged);
+  auto const& m2 = ls.csrMirror();
+  EXPECT_EQ(1, (int)m2.edgeUp[0]);
+  EXPECT_EQ(3u, m2.metric[m2.rowPtr[m2.id.at("a")]]);
+  EXPECT_EQ(4u, m2.metric[m2.rowPtr[m2.id.at("b")]]);
+}
+
+// ParallelAdjRingTopologyFixture adjacencies (DecisionTest.cpp:3146-3203)
+static LinkState parallelRing() {
+  LinkState ls(kArea);
+  auto db1 = createAdjDb("1",
+                         {createAdjacency("2", "2/1", "1/1", 11), createAdjacency("2", "2/2", "1/2", 11),
+                          createAdjacency("2", "2/3", "1/3", 20), createAdjacency("3", "3/1", "1/1", 11)},
+                         1);
+  auto db2 = createAdjDb("2",
+                         {createAdjacency("1", "1/1", "2/1", 11), createAdjacency("1", "1/2", "2/2", 11),
+                          createAdjacency("1", "1/3", "2/3", 20), createAdjacency("4", "4/1", "2/1", 11)},
+                         2);
+  auto db3 = createAdjDb("3",
+                         {createAdjacency("1", "1/1", "3/1", 11), createAdjacency("4", "4/1", "3/1", 11),
+                          createAdjacency("4", "4/2", "3/2", 20), createAdjacency("4", "4/3", "3/3", 20)},
+                         3);
+  auto db4 = createAdjDb("4",
+                         {createAdjacency("2", "2/1", "4/1", 11), createAdjacency("3", "3/1", "4/1", 11),
+                          createAdjacency("3", "3/2", "4/2", 20), createAdjacency("3", "3/3", "4/3", 20)},
+                         4);
+  EXPECT_FALSE(ls.updateAdjacencyDatabase(db1).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(db2).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(db3).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(db4).topologyChanged);
+  return ls;
+}
+
+TEST_CPU(LinkStateTest_LinksFromNodeOrder) {
+  // The pathLinks order among parallel links follows linksFromNode() iteration;
+  // with folly's pair hash on libstdc++ node 1 iterates its 1-2 links as 2/2 before 2/1
+  // (what DecisionTest.cpp:3596-3599 relies on). Printed for the record.
+  auto ls = parallelRing();
+  std::string order;
+  for (auto const& l : ls.linksFromNode("1")) order += l->getIfaceFromNode("1") + " ";
+  std::printf("    linksFromNode(1) order: %s\n", order.c_str());
+  size_t p22 = order.find("2/2"), p21 = order.find("2/1");
+  EXPECT_TRUE(p22 != std::string::npos && p21 != std::string::npos);
+}
+
+// ---------------------------------------------------------------------------
+// GPU tests
+// LinkStateTest.cpp:244-284
+TEST_GPU(LinkStateTest_getKthPaths_box) {
+  auto linkState = getLinkState({{1, {{2, 10}, {3, 5}}},
+                                 {2, {{1, 10}, {4, 15}, {4, 35}}},
+                                 {3, {{1, 5}, {4, 20}}},
+                                 {4, {{2, 15}, {3, 20}, {2, 35}}}});
+  auto firstPaths = linkState.getKthPaths("2", "4", 1);
+  EXPECT_EQ(1u, firstPaths.size());
+  EXPECT_EQ(1u, firstPaths.at(0).size());
+  EXPECT_EQ(15u, firstPaths.at(0).at(0)->getMetricFromNode("2"));
+  auto secondPaths = linkState.getKthPaths("2", "4", 2);
+  EXPECT_EQ(2u, secondPaths.size());
+  std::multiset<size_t> sizes;
+  for (auto const& path : secondPaths) {
+    sizes.insert(path.size());
+    std::string next = "2";
+    LinkStateMetric dist = 0;
+    for (auto const& link : path) {
+      dist += link->getMetricFromNode(next);
+      next = link->getOtherNodeName(next);
+    }
+    EXPECT_EQ(35u, dist);
+  }
+  EXPECT_TRUE((sizes == std::multiset<size_t>{1, 3}));
+}
+
+// LinkStateTest.cpp:286-315
+TEST_GPU(LinkStateTest_getKthPaths_mesh) {
+  auto linkState = getLinkState(
+      unit({{1, {2, 2, 3, 3, 4, 4}}, {2, {1, 1, 3, 3, 4, 4}}, {3, {1, 1, 2, 2, 4, 4}}, {4, {1, 1, 2, 2, 3, 3}}}));
+  auto firstPaths = linkState.getKthPaths("2", "4", 1);
+  EXPECT_EQ(2u, firstPaths.size());
+  for (auto const& p : firstPaths) EXPECT_EQ(1u, p.size());
+  auto secondPaths = linkState.getKthPaths("2", "4", 2);
+  EXPECT_EQ(4u, secondPaths.size());
+  for (auto const& p : secondPaths) EXPECT_EQ(2u, p.size());
+  LinkState::LinkSet set;
+  auto all = firstPaths;
+  all.insert(all.end(), secondPaths.begin(), secondPaths.end());
+  for (auto const& path : all)
+    for (auto const& link : path) EXPECT_TRUE(set.insert(link).second);
+}
+
+// LinkStateTest.cpp:318-377
+TEST_GPU(LinkStateTest_getHopCounts) {
+  {
+    auto ls = getLinkState(unit({{1, {2, 3}}, {2, {1, 4}}, {3, {1, 4}}, {4, {2, 3}}}));
+    EXPECT_TRUE(ls.getHopsFromAToB("1", "2") == 1u);
+    EXPECT_TRUE(ls.getHopsFromAToB("1", "4") == 2u);
+    EXPECT_EQ(2u, ls.getMaxHopsToNode("1"));
+  }
+  {
+    auto ls = getLinkState(unit({{1, {2}}, {2, {1, 3}}, {3, {2, 4}}, {4, {3, 5}}, {5, {4}}}));
+    EXPECT_TRUE(ls.getHopsFromAToB("1", "2") == 1u);
+    EXPECT_TRUE(ls.getHopsFromAToB("1", "4") == 3u);
+    EXPECT_TRUE(ls.getHopsFromAToB("2", "3") == 1u);
+    EXPECT_EQ(4u, ls.getMaxHopsToNode("1"));
+    EXPECT_EQ(3u, ls.getMaxHopsToNode("2"));
+    EXPECT_EQ(2u, ls.getMaxHopsToNode("3"));
+  }
+  {
+    auto ls = getLinkState(unit({{1, {2}}, {2, {1, 3}}, {3, {2, 4}}, {4, {3}}, {5, {}}}));
+    EXPECT_FALSE(ls.getHopsFromAToB("1", "5").has_value());
+    EXPECT_TRUE(ls.getHopsFromAToB("2", "3") == 1u);
+    EXPECT_EQ(3u, ls.getMaxHopsToNode("1"));
+    EXPECT_EQ(0u, ls.getMaxHopsToNode("5"));
+  }
+}
+
+// DecisionTest.cpp:3536-3599 (KSP2 on the parallel-adjacency ring): k=1 paths from 1
+// to 4 leave node 1 over adj12_2 (ifName 2/2) and adj13_1 (ifName 3/1); k=2 is empty.
+TEST_GPU(DecisionTest_ParallelAdjRing_Ksp2FirstHops) {
+  auto ls = parallelRing();
+  auto const& k1 = ls.getKthPaths("1", "4", 1);
+  EXPECT_EQ(2u, k1.size());
+  std::set<std::string> firstIfs;
+  for (auto const& p : k1) firstIfs.insert(p.front()->getIfaceFromNode("1"));
+  EXPECT_TRUE((firstIfs == std::set<std::string>{"2/2", "3/1"}));
+  EXPECT_TRUE(ls.getKthPaths("1", "4", 2).empty());
+  auto const& r = ls.getSpfResult("1");
+  EXPECT_EQ(22u, r.at("4").metric());
+  EXPECT_TRUE((r.at("4").nextHops() == std::unordered_set<std::string>{"2", "3"}));
+}
+
+// SimpleRingTopologyFixture counters (DecisionTest.cpp:1826-1827, 2306-2309):
+// 4 base SPFs for 4 sources, then 12 KSP2 second SPFs.
+TEST_GPU(DecisionTest_SimpleRing_SpfRunCounts) {
+  LinkState ls(kArea);
+  ls.updateAdjacencyDatabase(
+      createAdjDb("1", {createAdjacency("2", "1/2", "2/1", 10), createAdjacency("3", "1/3", "3/1", 10)}, 1));
+  ls.updateAdjacencyDatabase(
+      createAdjDb("2", {createAdjacency("1", "2/1", "1/2", 10), createAdjacency("4", "2/4", "4/2", 10)}, 2));
+  ls.updateAdjacencyDatabase(
+      createAdjDb("3", {createAdjacency("1", "3/1", "1/3", 10), createAdjacency("4", "3/4", "4/3", 10)}, 3));
+  ls.updateAdjacencyDatabase(
+      createAdjDb("4", {createAdjacency("2", "4/2", "2/4", 10), createAdjacency("3", "4/3", "3/4", 10)}, 4));
+  SpfCounters::get().reset();
+  const std::vector<std::string> nodes{"1", "2", "3", "4"};
+  for (auto const& n : nodes) ls.getSpfResult(n);
+  EXPECT_EQ(4u, SpfCounters::get().spfRuns());
+  for (auto const& s : nodes)
+    for (auto const& d : nodes)
+      if (s != d) {
+        ls.getKthPaths(s, d, 1);
+        ls.getKthPaths(s, d, 2);
+      }
+  EXPECT_EQ(16u, SpfCounters::get().spfRuns());
+  auto const& r1 = ls.getSpfResult("1");
+  EXPECT_EQ(20u, r1.at("4").metric());
+  EXPECT_TRUE((r1.at("4").nextHops() == std::unordered_set<std::string>{"2", "3"}));
+}
+
+// DecisionTest.cpp:4207-4355 grid, all sources via one batched prefetch
+TEST_GPU(DecisionTest_Grid_ShortestPath) {
+  for (int n : {2, 4, 10, 16}) {
+    LinkState ls(kArea);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        std::vector<thrift::Adjacency> adjs;
+        auto add = [&](int ii, int jj, const char* ifn, const char* oifn) {
+          if (ii < 0 || ii >= n || jj < 0 || jj >= n) return;
+          adjs.push_back(createAdjacency(std::to_string(ii * n + jj), ifn, oifn, 1));
+        };
+        add(i, j + 1, "0/1", "0/3");
+        add(i - 1, j, "0/2", "0/4");
+        add(i, j - 1, "0/3", "0/1");
+        add(i + 1, j, "0/4", "0/2");
+        ls.updateAdjacencyDatabase(createAdjDb(std::to_string(i * n + j), adjs, i * n + j + 1));
+      }
+    std::vector<std::string> all;
+    for (int v = 0; v < n * n; ++v) all.push_back(std::to_string(v));
+    SpfCounters::get().reset();
+    ls.prefetchSpfResults(all);
+    EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());
+    bool ok = true;
+    for (int a = 0; a < n * n; ++a)
+      for (int b = 0; b < n * n; ++b) {
+        auto m = ls.getMetricFromAToB(std::to_string(a), std::to_string(b));
+        const int want = std::abs(a % n - b % n) + std::abs(a / n - b / n);
+        ok &= m.has_value() && *m == (LinkStateMetric)want;
+      }
+    EXPECT_TRUE(ok);
+    EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());  // all served by the memo
+  }
+}
+
+// Random topologies through the full adjacency-database path: every getSpfResult and
+// getKthPaths equals the oracle run on the same CSR mirror (pathLinks order included).
+TEST_GPU(LinkState_RandomOracleParity) {
+  std::mt19937_64 rng(7);
+  for (int trial = 0; trial < 6; ++trial) {
+    const int V = 12 + trial * 9;
+    LinkState ls(kArea);
+    std::vector<std::vector<thrift::Adjacency>> adjs(V);
+    int ifc = 0;
+    auto link = [&](int a, int b, int wa, int wb, bool ovl) {
+      const std::string ia = "if" + std::to_string(ifc++), ib = "if" + std::to_string(ifc++);
+      auto x = createAdjacency(std::to_string(b), ia, ib, wa);
+      x.isOverloaded = ovl;
+      adjs[a].push_back(x);
+      adjs[b].push_back(createAdjacency(std::to_string(a), ib, ia, wb));
+    };
+    for (int v = 1; v < V; ++v) link((int)(rng() % v), v, 1 + rng() % 6, 1 + rng() % 6, false);
+    for (int k = 0; k < V; ++k) {
+      int a = rng() % V, b = rng() % V;
+      if (a != b) link(a, b, 1 + rng() % 6, 1 + rng() % 6, rng() % 10 == 0);
+    }
+    for (int k = 0; k < V / 4; ++k) {  // parallel links
+      int a = rng() % V;
+      if (!adjs[a].empty()) {
+        int b = std::stoi(adjs[a][0].otherNodeName);
+        link(a, b, 1 + rng() % 6, 1 + rng() % 6, false);
+      }
+    }
+    for (int v = 0; v < V; ++v) {
+      auto db = createAdjDb(std::to_string(v), adjs[v], v + 1);
+      db.isOverloaded = rng() % 8 == 0;
+      ls.updateAdjacencyDatabase(db);
+    }
+    auto const& m = ls.csrMirror();
+    oracle_graph og{(uint32_t)m.names.size(), (uint32_t)m.col.size(), (uint32_t)m.links.size(), m.rowPtr.data(),
+                    m.col.data(), m.metric.data(), m.linkId.data(), m.edgeUp.data(), m.overloaded.data(),
+                    m.nameRank.data()};
+    const uint32_t NV = og.num_nodes, NE = og.num_dir_edges;
+    std::vector<uint64_t> dist(NV);
+    std::vector<uint32_t> plp(NV + 1), ple(NE + 1);
+    for (uint32_t s = 0; s < NV; ++s) {
+      for (int useMetric = 0; useMetric < 2; ++useMetric) {
+        auto const& res = ls.getSpfResult(m.names[s], useMetric != 0);
+        int64_t cnt = oracle_run_spf(&og, s, useMetric, nullptr, dist.data(), nullptr, 0, nullptr, plp.data(),
+                                     ple.data());
+        EXPECT_EQ((size_t)cnt, res.size());
+        for (uint32_t v = 0; v < NV; ++v) {
+          auto it = res.find(m.names[v]);
+          if (dist[v] == UINT64_MAX) {
+            EXPECT_TRUE(it == res.end());
+            continue;
+          }
+          if (it == res.end()) {
+            EXPECT_TRUE(false);
+            continue;
+          }
+          EXPECT_EQ(dist[v], it->second.metric());
+          auto const& pls = it->second.pathLinks();
+          bool same = pls.size() == plp[v + 1] - plp[v];
+          for (uint32_t i = 0; same && i < pls.size(); ++i) {
+            const uint32_t e = ple[plp[v] + i];
+            same = pls[i].link.get() == m.links[m.linkId[e]].get() && pls[i].prevNode == m.names[m.edgeOwner[e]];
+          }
+          EXPECT_TRUE(same);
+        }
+      }
+      for (uint32_t d = 0; d < NV; d += 3) {
+        for (uint32_t k = 1; k <= 2; ++k) {
+          auto const& paths = ls.getKthPaths(m.names[s], m.names[d], k);
+          std::vector<uint32_t> pptr(NE + 2), pe(NE + 2);
+          int64_t np = oracle_kth_paths(&og, s, d, k, pptr.data(), NE + 1, pe.data(), NE + 1);
+          EXPECT_EQ((size_t)np, paths.size());
+          bool same = (size_t)np == paths.size();
+          for (int64_t i = 0; same && i < np; ++i) {
+            same = paths[i].size() == pptr[i + 1] - pptr[i];
+            for (uint32_t j = 0; same && j < paths[i].size(); ++j)
+              same = paths[i][j].get() == m.links[m.linkId[pe[pptr[i] + j]]].get();
+          }
+          EXPECT_TRUE(same);
+        }
+      }
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  int ran = 0;
+  for (auto const& t : registry()) {
+    if (t.gpu != (mode == "gpu") && mode != "all") continue;
+    const int before = g_failures;
+    try {
+      t.fn();
+    } catch (const std::exception& e) {
+      ++g_failures;
+      std::fprintf(stderr, "  EXCEPTION in %s: %s\n", t.name, e.what());
+    }
+    std::printf("[%s] %s\n", g_failures == before ? "PASS" : "FAIL", t.name);
+    ++ran;
+  }
+  std::printf("%d tests, %d checks, %d failures\n", ran, g_checks, g_failures);
+  return g_failures ? 1 : 0;
+}

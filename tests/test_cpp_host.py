@@ -1,0 +1,37 @@
+"""Runs the C++ host-mirror tests (tests/cpp/linkstate_test.cpp).
+
+cpu group: HoldableValue / Link / LinkState topology semantics and the CSR mirror
+(LinkStateTest.cpp:22-242); gpu group: SPF, KSP, hop counts, spf_runs counters and
+oracle parity through the C-ABI engine.
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "linkstate_test")
+
+
+def run(group):
+    assert os.path.exists(BIN), "build first: make"
+    p = subprocess.run([BIN, group], capture_output=True, text=True, timeout=600)
+    print(p.stdout)
+    print(p.stderr)
+    assert p.returncode == 0, p.stdout + p.stderr
+    return p.stdout
+
+
+def test_host_mirror_cpu():
+    out = run("cpu")
+    assert "0 failures" in out
+    # pathLinks order among parallel links = linksFromNode order; the DecisionTest
+    # adj12_2 expectation needs 2/2 before 2/1 on node 1.
+    line = [l for l in out.splitlines() if "linksFromNode(1) order" in l][0]
+    assert line.index("2/2") < line.index("2/1")
+
+
+@pytest.mark.gpu
+def test_host_mirror_gpu():
+    out = run("gpu")
+    assert "0 failures" in out

@@ -207,6 +207,19 @@ def test_large_metrics_use_u64_distances(eng):
     assert int(dist.max()) > 0xFFFFFFFF
 
 
+def test_deep_bfs_u8_overflow_rerun(eng):
+    """BFS deeper than 253 levels: the u8-level pass flags it, the u16 pass re-runs it."""
+    V = 700
+    names = [f"p{i:04d}" for i in range(V)]
+    links = np.array([(i, i + 1) for i in range(V - 1)])
+    g = T.csr_from_links(names, links)
+    dist, _ = check_against_oracle(eng, g, [0, 1, 350, 699, 100, 0], True, check_pathlinks=True)
+    assert int(dist[0, V - 1]) == V - 1
+    srcs = [0, 699, 5]
+    ignore = [[10], [], [600]]
+    check_against_oracle(eng, g, srcs, True, ignore=ignore)
+
+
 # --- edge cases -------------------------------------------------------------
 def test_single_node_and_isolated(eng):
     g = T.build_csr([T.AdjacencyDatabase("a", []), T.AdjacencyDatabase("b", [])])
