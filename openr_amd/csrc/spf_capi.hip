@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -128,10 +129,20 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   return OPENR_SPF_OK;
 }
 
+// Tuning overrides (benchmarks only): OPENR_SPF_GROUP_LANES=1|2|4|..|64 lanes per
+// frontier node in the BFS kernel.
+int group_lanes_override(int dflt) {
+  const char* e = std::getenv("OPENR_SPF_GROUP_LANES");
+  if (!e) return dflt;
+  int v = std::atoi(e);
+  return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : dflt;
+}
+
 hipError_t launch(const openr_spf_ctx* ctx, const Device& d, const Plan& p, const SolveArgs& a,
                   hipStream_t s) {
   LaunchInfo info;
-  if (p.bfs) return launch_bfs(d.g, a, p.cost, p.nh_mode, (int)ctx->group_lanes, d.num_cus, s, &info);
+  if (p.bfs)
+    return launch_bfs(d.g, a, p.cost, p.nh_mode, group_lanes_override((int)ctx->group_lanes), d.num_cus, s, &info);
   return launch_bucket(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
 }
 

@@ -23,6 +23,8 @@
 // stream and the result write (DESIGN.md "Roofline").
 #include "spf_kernels.h"
 
+#include <cstdlib>
+
 namespace openr_spf {
 
 namespace {
@@ -626,6 +628,8 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
 // It cannot be used when its ring would be smaller than kMinRing entries; then the
 // full-order u16 variant runs directly.
 uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode) {
+  if (const char* e = std::getenv("OPENR_SPF_BFS_FULL"))  // tuning: force the full-order variant
+    if (e[0] == '1') return 0;
   const uint32_t fixed = bfs_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), 0).total;
   const uint32_t budget = kMaxLds / kBfsTargetWgs;
   if (fixed >= budget) return 0;
