@@ -72,7 +72,7 @@ struct Device {
   // scratch for host-buffer solves
   DevBuf<uint32_t> src, ign_ptr, ign_links;
   DevBuf<uint64_t> dist, tight;
-  DevBuf<uint8_t> nh, ovf;
+  DevBuf<uint8_t> nh, ovf, scratch;
 };
 
 void free_graph(DevGraph& g) {
@@ -136,6 +136,20 @@ int group_lanes_override(int dflt) {
   if (!e) return dflt;
   int v = std::atoi(e);
   return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : dflt;
+}
+
+// Device scratch for the multi-source BFS (level bytes per lane); grown on demand.
+hipError_t prepare_scratch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs& a) {
+  a.scratch = nullptr;
+  a.scratch_bytes = 0;
+  if (!p.bfs) return hipSuccess;
+  const MsPlan ms = plan_msbfs(d.g, a.n, ctx->nh_bits, a.ign_ptr != nullptr, a.tight != nullptr, d.num_cus);
+  if (!ms.use) return hipSuccess;
+  hipError_t e = d.scratch.reserve(ms.scratch);
+  if (e != hipSuccess) return e;
+  a.scratch = d.scratch.p;
+  a.scratch_bytes = d.scratch.cap;
+  return hipSuccess;
 }
 
 hipError_t launch(const openr_spf_ctx* ctx, const Device& d, const Plan& p, const SolveArgs& a,
@@ -210,6 +224,7 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh_bits = ctx->nh_bits;
     HIP_TRY(d.ovf.reserve(m));
     a.ovf = d.ovf.p;
+    HIP_TRY(prepare_scratch(ctx, d, plan, a));
     HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
     HIP_TRY(launch(ctx, d, plan, a, d.stream));
     HIP_TRY(hipEventRecord(d.ev_end, d.stream));
@@ -314,6 +329,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.tight.release();
     d.nh.release();
     d.ovf.release();
+    d.scratch.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -406,6 +422,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     g.V = V;
     g.E = E;
     g.L = L;
+    for (uint32_t u = 0; u < V; ++u) g.max_deg = std::max(g.max_deg, gr->row_ptr[u + 1] - gr->row_ptr[u]);
     auto up = [&](auto** dst, const auto* srcp, size_t count) -> hipError_t {
       using T = std::remove_pointer_t<std::remove_pointer_t<decltype(dst)>>;
       hipError_t err = hipMalloc(reinterpret_cast<void**>(dst), std::max<size_t>(count, 1) * sizeof(T));
@@ -442,7 +459,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   // lanes per frontier node: enough that one pass of kBfsEdgesPerLane edges per lane
   // covers an average row (grid: 1 lane x 4 edges; fabric: 8 lanes x 4 edges)
   const uint32_t avg = V ? (E + V - 1) / V : 1;
-  const uint32_t per_lane = (avg + kBfsEdgesPerLane - 1) / kBfsEdgesPerLane;
+  const uint32_t per_lane = (avg + 2 * kBfsEdgesPerLane - 1) / (2 * kBfsEdgesPerLane);  // fabric: G=4 measured best
   uint32_t gl = 1;
   while (gl < per_lane && gl < 64) gl <<= 1;
   ctx->group_lanes = gl;
@@ -512,6 +529,7 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bits = ctx->nh_bits;
   HIP_TRY(d.ovf.reserve(n));
   a.ovf = d.ovf.p;
+  HIP_TRY(prepare_scratch(ctx, d, plan, a));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;

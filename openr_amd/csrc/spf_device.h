@@ -1,0 +1,132 @@
+// spf_device.h — device helpers shared by the SPF kernels (LDS next-hop bitsets,
+// wave-level compaction, ignore masks). Header-only; included by the .hip files.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spf_kernels.h"
+
+namespace openr_spf {
+namespace dev {
+
+// ---------------------------------------------------------------------------
+// Next-hop bitset storage in LDS
+// ---------------------------------------------------------------------------
+template <int MODE>
+struct Nh;
+
+template <>
+struct Nh<kNhByte> {  // <= 8 bits: four nodes per dword
+  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 3u) / 4u; }
+  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
+    atomicOr(&nh[v >> 2], (1u << b) << ((v & 3u) * 8u));
+  }
+  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
+    uint32_t x = (nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu;
+    if (x) atomicOr(&nh[v >> 2], x << ((v & 3u) * 8u));
+  }
+  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
+    return j == 0 ? (nh[v >> 2] >> ((v & 3u) * 8u)) & 0xFFu : 0u;
+  }
+  struct Val { uint32_t x; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu}; }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+    if (s.x) atomicOr(&nh[v >> 2], s.x << ((v & 3u) * 8u));
+  }
+};
+
+template <>
+struct Nh<kNhHalf> {  // <= 16 bits: two nodes per dword
+  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 1u) / 2u; }
+  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
+    atomicOr(&nh[v >> 1], (1u << b) << ((v & 1u) * 16u));
+  }
+  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
+    uint32_t x = (nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu;
+    if (x) atomicOr(&nh[v >> 1], x << ((v & 1u) * 16u));
+  }
+  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
+    return j < 2 ? (nh[v >> 1] >> ((v & 1u) * 16u + 8u * j)) & 0xFFu : 0u;
+  }
+  struct Val { uint32_t x; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu}; }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+    if (s.x) atomicOr(&nh[v >> 1], s.x << ((v & 1u) * 16u));
+  }
+};
+
+template <int W>
+struct NhWords {  // W dwords per node
+  static __host__ __device__ uint32_t words(uint32_t V) { return V * W; }
+  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
+    atomicOr(&nh[v * W + (b >> 5)], 1u << (b & 31u));
+  }
+  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      uint32_t x = nh[u * W + k];
+      if (x) atomicOr(&nh[v * W + k], x);
+    }
+  }
+  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
+    return j < 4u * W ? (nh[v * W + (j >> 2)] >> (8u * (j & 3u))) & 0xFFu : 0u;
+  }
+  struct Val { uint32_t x[W]; };
+  static __device__ Val load(const uint32_t* nh, uint32_t u) {
+    Val r;
+#pragma unroll
+    for (int k = 0; k < W; ++k) r.x[k] = nh[u * W + k];
+    return r;
+  }
+  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
+#pragma unroll
+    for (int k = 0; k < W; ++k)
+      if (s.x[k]) atomicOr(&nh[v * W + k], s.x[k]);
+  }
+};
+template <> struct Nh<kNhW1> : NhWords<1> {};
+template <> struct Nh<kNhW2> : NhWords<2> {};
+template <> struct Nh<kNhW4> : NhWords<4> {};
+template <> struct Nh<kNhW8> : NhWords<8> {};
+
+__device__ __forceinline__ bool test_bit(const uint32_t* bits, uint32_t i) {
+  return (bits[i >> 5] >> (i & 31u)) & 1u;
+}
+
+// Append `item` for every lane with `fresh` set; one LDS atomic per wave.
+// Returns the slot index for fresh lanes. Must be reached by the whole wave.
+__device__ __forceinline__ uint32_t wave_append(bool fresh, uint32_t* counter) {
+  const unsigned long long m = __ballot(fresh);
+  uint32_t base = 0;
+  if (m) {
+    const int lane = __lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    base += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  }
+  return base;
+}
+
+// Build the per-solve ignore mask (linksToIgnore) in LDS.
+__device__ __forceinline__ void load_ignore(uint32_t* ign, uint32_t words, const SolveArgs& a,
+                                            uint32_t sid, uint32_t L) {
+  const uint32_t b = a.ign_ptr[sid], e = a.ign_ptr[sid + 1];
+  for (uint32_t k = b + threadIdx.x; k < e; k += kBlock) {
+    const uint32_t l = a.ign_links[k];
+    if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
+  }
+  (void)words;
+}
+
+// Exclusive prefix of a small per-lane count (< 8) across the wave, via 3 ballots.
+__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t c, uint32_t* total) {
+  const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+  const unsigned long long lt = (1ull << __lane_id()) - 1ull;
+  *total = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+  return (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+}
+
+}  // namespace dev
+}  // namespace openr_spf

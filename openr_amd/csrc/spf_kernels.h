@@ -15,6 +15,7 @@ namespace openr_spf {
 // the kernels. Built once per openr_spf_set_graph on every device of the context.
 struct DevGraph {
   uint32_t V = 0, E = 0, L = 0;
+  uint32_t max_deg = 0;        // largest row (source expansion must fit the frontier queue)
   uint32_t* row = nullptr;     // [V+1]
   uint2* row2 = nullptr;       // [V] (row[u], row[u+1]) in one 8-byte load
   uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
@@ -38,6 +39,12 @@ enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, k
 int nh_mode_for_bits(uint32_t bits);            // -1 if > 256 bits
 uint32_t nh_mode_lds_bytes(int mode, uint32_t V);
 
+struct LaunchInfo {
+  uint32_t lds_bytes = 0;
+  uint32_t grid = 0;
+  const char* kernel = "";
+};
+
 struct SolveArgs {
   const uint32_t* sources;
   uint32_t n;
@@ -48,14 +55,23 @@ struct SolveArgs {
   uint32_t nh_bytes;
   uint64_t* tight;            // nullable [n][ceil(E/64)] (zeroed by the launcher)
   uint32_t nh_bits;           // bits that are meaningful (max distinct degree)
-  uint8_t* ovf;               // [n] scratch: BFS deeper than the u8 level range (re-run with u16)
+  uint8_t* ovf;               // [n] scratch: solves a faster variant could not finish (re-run flags)
+  uint8_t* scratch;           // multi-source BFS level bytes ([grid][V][lanes]); nullable
+  size_t scratch_bytes;
 };
 
-struct LaunchInfo {
-  uint32_t lds_bytes = 0;
-  uint32_t grid = 0;
-  const char* kernel = "";
+// Bit-parallel multi-source BFS plan (spf_msbfs.hip).
+struct MsPlan {
+  bool use = false;
+  int lanes = 16;
+  uint32_t cap = 0, lds = 0, grid = 0;
+  size_t scratch = 0;  // bytes of SolveArgs::scratch required
 };
+MsPlan plan_msbfs(const DevGraph& g, uint32_t n, uint32_t nh_bits, bool has_ign, bool tight, int num_cus);
+hipError_t launch_msbfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t D, int lanes,
+                        int group_lanes, uint32_t cap, uint8_t* scratch, uint32_t grid, hipStream_t s,
+                        LaunchInfo* info);
+
 
 // Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels.
 hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode,

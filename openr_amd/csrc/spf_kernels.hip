@@ -25,124 +25,17 @@
 
 #include <cstdlib>
 
+#include "spf_device.h"
+
 namespace openr_spf {
 
 namespace {
+using namespace dev;
 
-
-// ---------------------------------------------------------------------------
-// Next-hop bitset storage in LDS
-// ---------------------------------------------------------------------------
-template <int MODE>
-struct Nh;
-
-template <>
-struct Nh<kNhByte> {  // <= 8 bits: four nodes per dword
-  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 3u) / 4u; }
-  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
-    atomicOr(&nh[v >> 2], (1u << b) << ((v & 3u) * 8u));
-  }
-  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
-    uint32_t x = (nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu;
-    if (x) atomicOr(&nh[v >> 2], x << ((v & 3u) * 8u));
-  }
-  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
-    return j == 0 ? (nh[v >> 2] >> ((v & 3u) * 8u)) & 0xFFu : 0u;
-  }
-  struct Val { uint32_t x; };
-  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu}; }
-  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
-    if (s.x) atomicOr(&nh[v >> 2], s.x << ((v & 3u) * 8u));
-  }
-};
-
-template <>
-struct Nh<kNhHalf> {  // <= 16 bits: two nodes per dword
-  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 1u) / 2u; }
-  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
-    atomicOr(&nh[v >> 1], (1u << b) << ((v & 1u) * 16u));
-  }
-  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
-    uint32_t x = (nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu;
-    if (x) atomicOr(&nh[v >> 1], x << ((v & 1u) * 16u));
-  }
-  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
-    return j < 2 ? (nh[v >> 1] >> ((v & 1u) * 16u + 8u * j)) & 0xFFu : 0u;
-  }
-  struct Val { uint32_t x; };
-  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu}; }
-  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
-    if (s.x) atomicOr(&nh[v >> 1], s.x << ((v & 1u) * 16u));
-  }
-};
-
-template <int W>
-struct NhWords {  // W dwords per node
-  static __host__ __device__ uint32_t words(uint32_t V) { return V * W; }
-  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
-    atomicOr(&nh[v * W + (b >> 5)], 1u << (b & 31u));
-  }
-  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      uint32_t x = nh[u * W + k];
-      if (x) atomicOr(&nh[v * W + k], x);
-    }
-  }
-  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
-    return j < 4u * W ? (nh[v * W + (j >> 2)] >> (8u * (j & 3u))) & 0xFFu : 0u;
-  }
-  struct Val { uint32_t x[W]; };
-  static __device__ Val load(const uint32_t* nh, uint32_t u) {
-    Val r;
-#pragma unroll
-    for (int k = 0; k < W; ++k) r.x[k] = nh[u * W + k];
-    return r;
-  }
-  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
-#pragma unroll
-    for (int k = 0; k < W; ++k)
-      if (s.x[k]) atomicOr(&nh[v * W + k], s.x[k]);
-  }
-};
-template <> struct Nh<kNhW1> : NhWords<1> {};
-template <> struct Nh<kNhW2> : NhWords<2> {};
-template <> struct Nh<kNhW4> : NhWords<4> {};
-template <> struct Nh<kNhW8> : NhWords<8> {};
-
-__device__ __forceinline__ bool test_bit(const uint32_t* bits, uint32_t i) {
-  return (bits[i >> 5] >> (i & 31u)) & 1u;
-}
-
-// Append `item` for every lane with `fresh` set; one LDS atomic per wave.
-// Returns the slot index for fresh lanes. Must be reached by the whole wave.
-__device__ __forceinline__ uint32_t wave_append(bool fresh, uint32_t* counter) {
-  const unsigned long long m = __ballot(fresh);
-  uint32_t base = 0;
-  if (m) {
-    const int lane = __lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    base += (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-  }
-  return base;
-}
-
-// Build the per-solve ignore mask (linksToIgnore) in LDS.
-__device__ __forceinline__ void load_ignore(uint32_t* ign, uint32_t words, const SolveArgs& a,
-                                            uint32_t sid, uint32_t L) {
-  const uint32_t b = a.ign_ptr[sid], e = a.ign_ptr[sid + 1];
-  for (uint32_t k = b + threadIdx.x; k < e; k += kBlock) {
-    const uint32_t l = a.ign_links[k];
-    if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
-  }
-  (void)words;
-}
 
 template <typename LT>
 struct BfsLayout {
-  uint32_t lvl, nh, ring, ovl, ign, total;
+  uint32_t lvl, vis, nh, ring, ovl, ign, total;
 };
 
 // ring = frontier queue (power of two, wraps) in the fast path, or the full BFS-order
@@ -158,6 +51,7 @@ __host__ __device__ inline BfsLayout<LT> bfs_layout(uint32_t V, uint32_t L, bool
     return o;
   };
   l.lvl = take((uint32_t)sizeof(LT) * (V + 4u));
+  l.vis = take(4u * ((V + 31u) / 32u));
   l.nh = take(4u * nh_words);
   l.ring = take(2u * ring_cap);
   l.ovl = take(4u * ((V + 31u) / 32u));
@@ -189,74 +83,57 @@ __host__ __device__ inline BucketLayout bucket_layout(uint32_t V, uint32_t L, bo
 }
 
 // ---------------------------------------------------------------------------
-// Uniform-cost kernel: level-synchronous BFS
+// Uniform-cost kernel: level-synchronous BFS (one source per workgroup)
 // ---------------------------------------------------------------------------
-// LDS per solve: lvl[] (LT, all-ones = not reached), next-hop bitsets, and the
-// frontier queue. Level L expands queue slots [head, tail): groups of G lanes per
-// frontier node, K edges per lane loaded ahead (rows of degree <= 4 come from one
-// 16-byte ELL load when G == 1). Edge u->v is tight iff lvl[v] > L; the first
-// arrival claims v with a CAS on the lvl word (back edges cost one plain LDS read),
-// fresh nodes are appended with one LDS atomic per wave per pass. One barrier per
-// level; append counters are triple-buffered.
+// LDS per solve: lvl[] (LT, all-ones = not reached), a visited bitmap, next-hop
+// bitsets and the frontier queue. The source is expanded first (level 0 -> 1, next
+// hops = the neighbour itself); then level L expands queue slots [head, tail):
+// groups of G lanes per frontier node, K edges per lane loaded ahead (rows of degree
+// <= 4 come from one 16-byte ELL load when G == 1). Edge u->v is tight iff
+// lvl[v] > L (all tight preds of v sit on level L); the tight arrival ORs nh(u) into
+// nh(v) and stores lvl[v] = L+1 (idempotent); ds_or_rtn on the visited bitmap elects
+// the one arrival that appends v (one LDS atomic per wave per pass for the slots).
+// One barrier per level; append counters are triple-buffered.
 //   RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent
 //                 levels exceed the ring, or whose depth exceeds 253, sets ovf[sid].
-//   RING = false: LT = u16, queue = full BFS order (capacity V); re-runs flagged solves.
+//   RING = false: LT = u16, queue = full BFS order (capacity V).
+// rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
 template <typename LT>
 struct LvlOps;
 template <>
 struct LvlOps<uint8_t> {
-  static constexpr uint32_t kPer = 4, kBits = 8, kUnset = 0xFFu;
+  static constexpr uint32_t kUnset = 0xFFu;
 };
 template <>
 struct LvlOps<uint16_t> {
-  static constexpr uint32_t kPer = 2, kBits = 16, kUnset = 0xFFFFu;
+  static constexpr uint32_t kUnset = 0xFFFFu;
 };
 
-// 0: v settled at a level <= L (not tight); 1: tight, already reached at L+1; 2: tight & first.
-template <typename LT>
-__device__ __forceinline__ uint32_t claim_level(uint32_t* lvl_w, uint32_t v, uint32_t L) {
-  using O = LvlOps<LT>;
-  const uint32_t w = v / O::kPer, shift = (v % O::kPer) * O::kBits, mask = O::kUnset << shift;
-  uint32_t old = lvl_w[w];
-  for (;;) {
-    const uint32_t cur = (old & mask) >> shift;
-    if (cur <= L) return 0;
-    if (cur == L + 1u) return 1;
-    const uint32_t prev = atomicCAS(&lvl_w[w], old, (old & ~mask) | ((L + 1u) << shift));
-    if (prev == old) return 2;
-    old = prev;
-  }
-}
-
-// Exclusive prefix of a small per-lane count (< 8) across the wave, via 3 ballots.
-__device__ __forceinline__ uint32_t wave_prefix_small(uint32_t c, uint32_t* total) {
-  const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
-  const unsigned long long lt = (1ull << __lane_id()) - 1ull;
-  *total = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-  return (uint32_t)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
-}
-
-template <int MODE, int K, typename LT, bool RING, bool ELL>
+template <int MODE, int K, typename LT, bool RING, bool ELL, bool GENERIC>
 __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog,
-                                                     uint32_t has_ign, uint32_t ring_cap, uint32_t rerun) {
+                                                     uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun) {
+  // GENERIC = false: no ignore set and no tight-edge output (compile-time), the
+  // all-sources / prefetch case; GENERIC = true handles both at run time.
+  const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   using N = Nh<MODE>;
   using O = LvlOps<LT>;
-  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6;
   const uint32_t nh_words = N::words(V);
   const BfsLayout<LT> lay = bfs_layout<LT>(V, g.L, has_ign != 0, nh_words, ring_cap);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
   LT* lvl = reinterpret_cast<LT*>(base + lay.lvl);
   uint32_t* lvl_w = reinterpret_cast<uint32_t*>(base + lay.lvl);
+  uint32_t* vis = reinterpret_cast<uint32_t*>(base + lay.vis);
   uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
   uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
   uint32_t* ovl = reinterpret_cast<uint32_t*>(base + lay.ovl);
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
   const uint32_t bit_words = (V + 31u) / 32u;
-  const uint32_t lvl_words = (V + O::kPer - 1u) / O::kPer + 1u;
+  const uint32_t lvl_words = ((uint32_t)sizeof(LT) * (V + 4u)) / 4u;
   const uint32_t ign_words = (g.L + 31u) / 32u;
-  const uint32_t G = 1u << glog, ngroups = kBlock >> glog;
+  const uint32_t G = 1u << glog, ngroups = kBlock >> glog, groups_per_wave = 64u >> glog;
   const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
   const uint32_t tight_words = (g.E + 63u) / 64u;
   const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
@@ -264,23 +141,49 @@ __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, ui
   for (uint32_t i = tid; i < bit_words; i += kBlock) ovl[i] = g.ovl_bits[i];
 
   for (uint32_t sid = blockIdx.x; sid < a.n; sid += gridDim.x) {
-    if (rerun && !a.ovf[sid]) continue;  // block-uniform
+    if (rerun && a.ovf[sid] != rerun) continue;  // block-uniform
     const uint32_t src = a.sources[sid];
     for (uint32_t i = tid; i < lvl_words; i += kBlock) lvl_w[i] = 0xFFFFFFFFu;
+    for (uint32_t i = tid; i < bit_words; i += kBlock) vis[i] = 0;
     for (uint32_t i = tid; i < nh_words; i += kBlock) nh[i] = 0;
     if (has_ign)
       for (uint32_t i = tid; i < ign_words; i += kBlock) ign[i] = 0;
-    if (tid == 0) ctl[0] = ctl[1] = ctl[2] = ctl[3] = 0;
+    if (tid < 4) ctl[tid] = 0;
     __syncthreads();
     if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
     if (tid == 0) {
       lvl[src] = 0;
-      ring[0] = (uint16_t)src;
+      vis[src >> 5] = 1u << (src & 31u);
     }
     __syncthreads();
-    uint64_t* trow = a.tight ? a.tight + (size_t)sid * tight_words : nullptr;
+    uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
 
-    uint32_t head = 0, tail = 1, L = 0;
+    // level 0: expand the source; a directly connected node's next hop is itself
+    {
+      const uint2 rs = g.row2[src];
+      for (uint32_t e0 = rs.x; e0 < rs.y; e0 += kBlock) {
+        const uint32_t e = e0 + tid;
+        bool fresh = false;
+        uint32_t v = 0;
+        if (e < rs.y) {
+          const uint32_t av = g.adj[e];
+          v = av & ~kEdgeDown;
+          if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e])) && v != src) {
+            const uint32_t bit = 1u << (v & 31u);
+            fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
+            lvl[v] = (LT)1;
+            N::or_bit(nh, v, g.nbr[e]);
+            if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+          }
+        }
+        // level-0 appends count in ctl[0]; level L >= 1 uses ctl[L % 3] (ctl[1] first)
+        const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
+        if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap checked by the host
+      }
+    }
+    __syncthreads();
+
+    uint32_t head = 1, tail = 1u + ctl[0], L = 1;
     bool overflow = false;  // block-uniform
     while (head < tail) {
       if (RING && L + 1u >= O::kUnset) {  // next level not representable in u8
@@ -290,12 +193,13 @@ __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, ui
       uint32_t* cnt = &ctl[L % 3u];
       if (tid == 0) ctl[(L + 1u) % 3u] = 0;  // last read two barriers ago
       for (uint32_t fb = head; fb < tail; fb += ngroups) {
+        if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
         const uint32_t idx = fb + group;
-        uint32_t u = src, beg = 0, end = 0;
+        uint32_t u = 0, beg = 0, end = 0;
         uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
         if (idx < tail) {
           u = ring[RING ? (idx & rmask) : idx];
-          if (u == src || !test_bit(ovl, u)) {  // overloaded non-source nodes are sinks
+          if (!test_bit(ovl, u)) {  // overloaded non-source nodes are sinks (LinkState.cpp:831-838)
             const uint2 r = g.row2[u];
             beg = r.x;
             end = r.y;
@@ -303,7 +207,6 @@ __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, ui
           }
         }
         const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
-        // pass p covers edges beg + lane_g + (p*K + j)*G; with ELL the first pass reads `ell`
         for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
           uint32_t av[K], lv[K];
 #pragma unroll
@@ -316,41 +219,33 @@ __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, ui
             }
             lv[j] = (has_ign && e < end) ? g.lid[e] : 0u;
           }
-          uint32_t st[K];
+          uint32_t fresh_mask = 0;
 #pragma unroll
           for (int j = 0; j < K; ++j) {
             const uint32_t e = e0 + j * G;
             const uint32_t v = av[j] & ~kEdgeDown;
-            st[j] = 0;
-            if (!(av[j] & kEdgeDown) && e < end && !(has_ign && test_bit(ign, lv[j])))
-              st[j] = claim_level<LT>(lvl_w, v, L);
-          }
-          uint32_t nfresh = 0;
-#pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const uint32_t e = e0 + j * G;
-            if (st[j]) {  // tight edge: first or equal-cost arrival (LinkState.cpp:857-873)
-              const uint32_t v = av[j] & ~kEdgeDown;
-              if (u == src)
-                N::or_bit(nh, v, g.nbr[e]);  // directly connected: nextHops = {v}
-              else
-                N::or_val(nh, v, nhu);       // addNextHops(nh(u))
+            const bool ok = !(av[j] & kEdgeDown) && e < end && !(has_ign && test_bit(ign, lv[j]));
+            if (ok && (uint32_t)lvl[v] > L) {
+              // tight edge: first or equal-cost arrival (LinkState.cpp:857-873)
+              const uint32_t bit = 1u << (v & 31u);
+              fresh_mask |= (atomicOr(&vis[v >> 5], bit) & bit) ? 0u : (1u << j);
+              lvl[v] = (LT)(L + 1u);
+              N::or_val(nh, v, nhu);  // addNextHops(nh(u))
               if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
-              nfresh += st[j] >> 1;
             }
           }
           uint32_t total;
-          uint32_t slot = wave_prefix_small(nfresh, &total);
+          uint32_t slot = wave_prefix_small((uint32_t)__popc(fresh_mask), &total);
           uint32_t wbase = 0;
           if (total) {
-            const int leader = __ffsll((long long)__ballot(nfresh != 0)) - 1;
+            const int leader = __ffsll((long long)__ballot(fresh_mask != 0)) - 1;
             if ((int)__lane_id() == leader) wbase = atomicAdd(cnt, total);
             wbase = __shfl(wbase, leader);
           }
           slot += tail + wbase;
 #pragma unroll
           for (int j = 0; j < K; ++j) {
-            if (st[j] == 2u) {
+            if ((fresh_mask >> j) & 1u) {
               const uint32_t v = av[j] & ~kEdgeDown;
               if (!RING) {
                 ring[slot] = (uint16_t)v;
@@ -374,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void bfs_kernel(DevGraph g, SolveArgs a, ui
       }
     }
     if (RING && overflow) {  // re-run by the u16 / full-order variant
-      if (tid == 0) a.ovf[sid] = 1;
+      if (tid == 0) a.ovf[sid] = (uint8_t)(rerun + 1u);
       __syncthreads();
       continue;
     }
@@ -611,7 +506,8 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   constexpr int K = (int)kBfsEdgesPerLane;
   const uint32_t lds = bfs_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), ring_cap).total;
   const uint32_t grid = blocks_for(a.n, lds, num_cus);
-  auto k = bfs_kernel<MODE, K, LT, RING, ELL>;
+  const bool generic = has_ign || a.tight != nullptr;
+  auto k = generic ? bfs_kernel<MODE, K, LT, RING, ELL, true> : bfs_kernel<MODE, K, LT, RING, ELL, false>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
@@ -635,23 +531,24 @@ uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode) {
   if (fixed >= budget) return 0;
   uint32_t cap = 1;
   while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
-  return cap >= 256u ? cap : 0u;
+  return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
 }
 
 template <int MODE, bool ELL>
 hipError_t launch_bfs_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                           int num_cus, hipStream_t s, LaunchInfo* info) {
+                           uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // ring/u8 variant first (or as the re-run of flagged multi-source batches); solves it
+  // flags are re-run by the full-order u16 variant on the same stream
   const uint32_t cap = fast_ring_cap(g, has_ign, MODE);
-  if (!cap) return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, 0, num_cus, s, info);
+  if (!cap)
+    return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, first_rerun, num_cus, s,
+                                                          info);
   const bool may_overflow = g.V > cap || g.V > 254u;
-  if (may_overflow) {
-    if (!a.ovf) return hipErrorInvalidValue;
-    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
-    if (err != hipSuccess) return err;
-  }
-  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELL>(g, a, cost, glog, has_ign, cap, 0, num_cus, s, info);
+  hipError_t err =
+      launch_bfs_variant<MODE, uint8_t, true, ELL>(g, a, cost, glog, has_ign, cap, first_rerun, num_cus, s, info);
   if (err != hipSuccess || !may_overflow) return err;
-  return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, 1, num_cus, s, info);
+  return launch_bfs_variant<MODE, uint16_t, false, ELL>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u, num_cus,
+                                                        s, info);
 }
 }  // namespace
 
@@ -660,17 +557,29 @@ hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int 
   const bool has_ign = a.ign_ptr != nullptr;
   if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
+  if (!a.ovf) return hipErrorInvalidValue;
+  hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
+  if (err != hipSuccess) return err;
   if (a.tight) {
-    hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((g.E + 63u) / 64u) * 8u, s);
+    err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((g.E + 63u) / 64u) * 8u, s);
     if (err != hipSuccess) return err;
   }
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   const bool ell = glog == 0 && g.ell != nullptr;
-#define OPENR_BFS_MODE(M)                                                                   \
-  case M:                                                                                   \
-    return ell ? launch_bfs_mode<M, true>(g, a, cost, glog, has_ign, num_cus, s, info)      \
-               : launch_bfs_mode<M, false>(g, a, cost, glog, has_ign, num_cus, s, info);
+  // bit-parallel multi-source BFS when eligible; its overflowing batches fall through
+  uint32_t first_rerun = 0;
+  const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
+  if (ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
+    err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
+                       info);
+    if (err != hipSuccess) return err;
+    first_rerun = 1;
+  }
+#define OPENR_BFS_MODE(M)                                                                               \
+  case M:                                                                                               \
+    return ell ? launch_bfs_mode<M, true>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info)      \
+               : launch_bfs_mode<M, false>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
   switch (nh_mode) {
     OPENR_BFS_MODE(kNhByte)
     OPENR_BFS_MODE(kNhHalf)

@@ -8,6 +8,9 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; stop_on_fault $rc; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|error" gpurun_out/gpu_tests.log | tail -3; stop_on_fault $rc
+if grep -qiE "illegal memory access|memory access fault|HSA_STATUS_ERROR|hipErrorLaunchFailure" gpurun_out/gpu_tests.log; then
+  echo "GPU fault reported inside the tests; stopping"; exit 3
+fi
 if [ -z "${SKIP_BENCH:-}" ]; then
   timeout -k 10 400 python -u bench.py ${BENCH_ARGS:---steps 10 --warmup 2} > gpurun_out/bench.log 2>&1
   rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log; stop_on_fault $rc

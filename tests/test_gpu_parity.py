@@ -26,15 +26,22 @@ def eng():
 
 
 def check_against_oracle(eng, g, sources, use_metric=True, ignore=None, check_pathlinks=True):
+    """Both engine paths vs the oracle: the plain solve (eligible for the bit-parallel
+    multi-source kernel) and, with check_pathlinks, the tight-edge solve (per-source)."""
     eng.set_graph(g)
-    dist, nh, tight = eng.solve(sources, use_metric, want_nh=True, want_tight=check_pathlinks, ignore=ignore)
     o = Oracle(g)
     assert eng.nh_bytes == o.nh_bytes
+    runs = [o.run_spf(int(s), use_metric, ignore[i] if ignore else None) for i, s in enumerate(sources)]
+    dist, nh, _ = eng.solve(sources, use_metric, want_nh=True, want_tight=False, ignore=ignore)
     for i, s in enumerate(sources):
-        run = o.run_spf(int(s), use_metric, ignore[i] if ignore else None)
-        np.testing.assert_array_equal(dist[i], run.dist, err_msg=f"dist src={s}")
-        np.testing.assert_array_equal(nh[i], run.nh, err_msg=f"nh src={s}")
-        if check_pathlinks:
+        np.testing.assert_array_equal(dist[i], runs[i].dist, err_msg=f"dist src={s}")
+        np.testing.assert_array_equal(nh[i], runs[i].nh, err_msg=f"nh src={s}")
+    if check_pathlinks:
+        dist2, nh2, tight = eng.solve(sources, use_metric, want_nh=True, want_tight=True, ignore=ignore)
+        np.testing.assert_array_equal(dist2, dist)
+        np.testing.assert_array_equal(nh2, nh)
+        for i, s in enumerate(sources):
+            run = runs[i]
             pe = tight_in_edges(g, dist[i], tight[i])
             for v in np.nonzero(run.reachable())[0].tolist():
                 want = run.pl_edge[run.pl_ptr[v] : run.pl_ptr[v + 1]].tolist()
@@ -207,8 +214,10 @@ def test_large_metrics_use_u64_distances(eng):
     assert int(dist.max()) > 0xFFFFFFFF
 
 
-def test_deep_bfs_u8_overflow_rerun(eng):
+@pytest.mark.parametrize("ms", ["0", "1"])
+def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, ms):
     """BFS deeper than 253 levels: the u8-level pass flags it, the u16 pass re-runs it."""
+    monkeypatch.setenv("OPENR_SPF_MSBFS", ms)
     V = 700
     names = [f"p{i:04d}" for i in range(V)]
     links = np.array([(i, i + 1) for i in range(V - 1)])
@@ -218,6 +227,38 @@ def test_deep_bfs_u8_overflow_rerun(eng):
     srcs = [0, 699, 5]
     ignore = [[10], [], [600]]
     check_against_oracle(eng, g, srcs, True, ignore=ignore)
+
+
+@pytest.fixture
+def msbfs_on(monkeypatch):
+    monkeypatch.setenv("OPENR_SPF_MSBFS", "1")
+
+
+def test_msbfs_list_overflow_reruns(eng, monkeypatch, msbfs_on):
+    """A frontier larger than the multi-source kernel's list re-runs per source."""
+    monkeypatch.setenv("OPENR_SPF_MS_CAP", "16")
+    g = T.grid_fast(16)
+    dist, _ = check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
+    monkeypatch.setenv("OPENR_SPF_MS_LANES", "8")
+    check_against_oracle(eng, g, list(range(0, g.num_nodes, 3)), True, check_pathlinks=False)
+
+
+@pytest.mark.parametrize("lanes", ["8", "16"])
+def test_msbfs_lane_widths(eng, monkeypatch, lanes, msbfs_on):
+    monkeypatch.setenv("OPENR_SPF_MS_LANES", lanes)
+    for seed in range(3):
+        g = random_graph(200 + seed, 90, 200, 1)
+        check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
+        check_against_oracle(eng, g, list(range(g.num_nodes)), False, check_pathlinks=False)
+
+
+def test_msbfs_matches_per_source(eng, monkeypatch):
+    g = T.grid_fast(20)
+    eng.set_graph(g)
+    d1, n1, _ = eng.solve(range(400), True)
+    monkeypatch.setenv("OPENR_SPF_MSBFS", "1")
+    d2, n2, _ = eng.solve(range(400), True)
+    assert np.array_equal(d1, d2) and np.array_equal(n1, n2)
 
 
 # --- edge cases -------------------------------------------------------------
