@@ -2,14 +2,15 @@
 #   make            -> openr_amd/lib/libopenr_spf.so, oracle/liboracle_spf.so
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-parameter
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-parameter \
+            -mllvm -amdgpu-atomic-optimizer-strategy=None
 LIBDIR := openr_amd/lib
 CSRC := openr_amd/csrc
 
 ENGINE := $(LIBDIR)/libopenr_spf.so
-ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_msbfs.hip $(CSRC)/spf_capi.hip
+ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_bfs.hip $(CSRC)/spf_msbfs.hip $(CSRC)/spf_capi.hip
 ENGINE_HDRS := $(CSRC)/spf_kernels.h $(CSRC)/spf_device.h include/openr_spf.h
-ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_msbfs.o $(LIBDIR)/spf_capi.o
+ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_bfs.o $(LIBDIR)/spf_msbfs.o $(LIBDIR)/spf_capi.o
 
 HOST := $(LIBDIR)/libopenr_decision.so
 HOST_SRCS := $(CSRC)/host/LinkState.cpp

@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark: all-sources SPF on the 100x100 grid (BASELINE.json metric).
 
-A "step" = one all-sources pass: every node of the topology is a source, the
-sources are split in contiguous blocks over the ranks (one process per GPU,
-strong scaling: total work is fixed), each rank runs ONE engine launch over its
-block through the C-ABI (openr_spf_solve_device) on device-resident buffers.
-Inputs (CSR replica, source list) are resident in HBM before the timed region;
-outputs (u64 distances + next-hop bitsets) are written to HBM.
+A "step" = one all-sources pass per rank: every node of the topology is a
+source, one engine launch through the C-ABI (openr_spf_solve_device) on
+device-resident buffers. Inputs (CSR replica, source list) are resident in HBM
+before the timed region; outputs (u64 distances + next-hop bitsets) are written
+to HBM.
+
+Scaling (one process per GPU, --gpus N under torch.distributed.run):
+  weak (default)  per-GPU work is fixed: each rank runs the all-sources SPF of its
+                  own LinkState replica (one OpenR area per GPU: Decision keeps one
+                  LinkState per area, Decision.cpp areaLinkStates_). N x V solves per
+                  step, no collective on the data path.
+  strong          the V sources of ONE topology are split in contiguous blocks over
+                  the ranks (shard.py); the RCCL all-gather of the result shards is
+                  measured after the timed region and reported as "gather".
 
 Timed region: barrier + synchronize, K steps, barrier + synchronize; the max
-over ranks is reported. The RCCL all-gather of the result shards is measured
-after the timed region and reported separately ("gather"), see DESIGN.md.
+over ranks is reported.
 
 roofline.achieved = algorithmic bytes per launch / mean kernel duration, with
 B(src) = 4(V+1) + 8E + V(8 + ceil(deg(src)/8))  (SURVEY.md §8d).
@@ -55,6 +62,9 @@ def algorithmic_bytes(g, sources: np.ndarray) -> int:
 
 
 def cpu_baseline(g, seconds: float, use_metric: bool):
+    """The oracle (C restatement of LinkState::runSpf, oracle/spf_oracle.c) timed on
+    the host cores: the same all-sources workload, repeated passes over an evenly
+    spaced source sample until about `seconds` of wall time."""
     from oracle import Oracle
 
     o = Oracle(g)
@@ -65,11 +75,15 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
     t0 = time.perf_counter()
     o.all_sources(probe, use_metric, nthreads=1, want_dist=True, want_nh=False)
     per_solve_1t = (time.perf_counter() - t0) / len(probe)
-    n = int(min(V, max(nthreads, seconds * nthreads / max(per_solve_1t, 1e-9))))
+    want = max(nthreads, int(seconds * nthreads / max(per_solve_1t, 1e-9)))
+    n = int(min(V, want))
+    passes = max(1, want // n)
     sample = np.linspace(0, V - 1, n).astype(np.uint32)
     t0 = time.perf_counter()
-    o.all_sources(sample, use_metric, nthreads=nthreads, want_dist=True, want_nh=True)
+    for _ in range(passes):
+        o.all_sources(sample, use_metric, nthreads=nthreads, want_dist=True, want_nh=True)
     dt = time.perf_counter() - t0
+    n *= passes
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
@@ -79,7 +93,8 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
         "unit": "solves/s",
         "cores": nthreads,
         "kind": "port",
-        "sample": f"{n} of {V} sources (evenly spaced), dist+next-hops, {nthreads} pthreads, {dt:.1f}s; {cpu_model}",
+        "sample": f"{n} solves ({passes} pass(es) over {n // passes} of {V} sources, evenly spaced), dist+next-hops, "
+                  f"{nthreads} pthreads, {dt:.1f}s; {cpu_model}",
     }
 
 
@@ -93,7 +108,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
     args = ap.parse_args()
 
     import torch
@@ -120,7 +136,7 @@ def main():
     # contiguous source blocks per rank (shard.py semantics)
     from openr_amd.shard import shard_range
 
-    lo, hi = shard_range(V, rank, world)
+    lo, hi = shard_range(V, rank, world) if args.scaling == "strong" else (0, V)
     n_local = hi - lo
     src = torch.arange(lo, hi, dtype=torch.int32, device=dev)
     d_dist = torch.empty((n_local, V), dtype=torch.int64, device=dev)
@@ -166,7 +182,7 @@ def main():
             assert np.array_equal(host[rows.index(r)].astype(np.int64), exp), "bench result check failed"
 
     gather = None
-    if world > 1 and not args.no_gather:
+    if world > 1 and args.scaling == "strong" and not args.no_gather:
         from openr_amd.shard import allgather_results
 
         torch.cuda.synchronize(dev)
@@ -180,7 +196,7 @@ def main():
         gather = {"ms": float(t.item()), "bytes": int(V * V * (8 + nb)),
                   "gather_inclusive_value": V / (elapsed / args.steps + float(t.item()) / 1e3)}
 
-    solves_total = V * args.steps
+    solves_total = (V if args.scaling == "strong" else V * world) * args.steps
     value = solves_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     sources_local = np.arange(lo, hi)
@@ -191,7 +207,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("topology") == args.topology and tj.get("n_sources") == n_local:
+            if tj.get("topology") == args.topology and tj.get("n_sources") in (None, n_local):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -206,12 +222,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (reference benchmark grid generator, unit metrics)",
-            "config": dict(cfg, **{"sources_per_step": V, "use_link_metric": use_metric,
-                                   "parallelism": f"source-sharded x{world}"}),
+            "config": dict(cfg, **{"sources_per_step": solves_total // args.steps, "use_link_metric": use_metric,
+                                   "parallelism": (f"source-sharded x{world}" if args.scaling == "strong"
+                                                   else f"area-per-GPU x{world}")}),
             "edge_relax_per_s": value * g.num_dir_edges,
             "roofline": {
                 "bound": "hbm",

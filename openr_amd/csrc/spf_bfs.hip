@@ -1,0 +1,478 @@
+// spf_bfs.hip — uniform-cost SPF kernel (every usable edge costs the same c: grids and
+// fabrics with unit metrics, and LinkState::runSpf(useLinkMetric=false) hop counts).
+//
+// Semantics (LinkState::runSpf, /root/reference/openr/decision/LinkState.cpp:808-882,
+// closed form for positive metrics): with uniform cost the
+// reference's (metric, name) pop order settles whole BFS levels in turn, and
+//   dist(v) = c * level(v)    (UINT64_MAX if v is never reached)
+//   nh(v)   = OR over tight in-edges u->v of (u == src ? {v} : nh(u))
+// where u->v is tight iff it is usable, u is on level L, v on level L+1, and u may be
+// expanded (u == src or u not overloaded, LinkState.cpp:831-838).
+//
+// Shape: one 256-thread workgroup owns one solve (persistent, dynamically scheduled
+// over the batch). Per solve LDS holds level bytes, next-hop sets and a frontier ring;
+// the CSR mirror is streamed from L2/HBM and shared by every workgroup on the chip.
+// Level L expands ring slots [head, tail): G lanes per frontier node, K edges per lane
+// loaded ahead. An arrival on an edge u->v is tight iff lvl[v] > L; it ORs nh(u) into
+// nh(v) and stores lvl[v] = L+1 (idempotent). The arrival that appends v to the ring is
+// elected by the atomicOr on v's next-hop field (packed modes: the one that saw the
+// field empty) or by a visited bitmap (multi-dword modes). Appends are wave-aggregated
+// (3 ballots + one ds_add per wave per pass). One barrier per level.
+//
+// No MFMA: min-plus relaxation is not a matrix contraction (DESIGN.md "Roofline").
+#include <cstdlib>
+
+#include "spf_device.h"
+#include "spf_kernels.h"
+
+namespace openr_spf {
+
+namespace {
+using namespace dev;
+
+template <typename LT>
+struct BfsLayout {
+  uint32_t lvl, vis, nh, ring, ign, dummy, total;
+};
+
+// ring = frontier queue (power of two, wraps) in the fast path, or the full BFS-order
+// array (capacity V, never wraps) in the fallback path.
+template <typename LT>
+__host__ __device__ inline BfsLayout<LT> bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
+                                                    bool need_vis, uint32_t ring_cap) {
+  BfsLayout<LT> l;
+  uint32_t off = 16;  // control: append counters [0..2], overflow flag [3]
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.lvl = take((uint32_t)sizeof(LT) * (V + 4u));
+  l.vis = need_vis ? take(4u * ((V + 31u) / 32u)) : 0u;
+  l.nh = take(4u * nh_words);
+  l.ring = take(2u * ring_cap);
+  l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
+  l.dummy = take(4u * 64u);  // per-lane sink for the no-op atomics of non-tight edges
+  l.total = off;
+  return l;
+}
+
+template <typename LT>
+struct LvlOps;
+template <>
+struct LvlOps<uint8_t> {
+  static constexpr uint32_t kUnset = 0xFFu;
+};
+template <>
+struct LvlOps<uint16_t> {
+  static constexpr uint32_t kUnset = 0xFFFFu;
+};
+
+// Writes this solve's dist row (u64) and next-hop row from LDS, coalesced.
+template <typename T>
+__device__ __forceinline__ void store_row(T* p, const T& x, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(x, p);  // streamed result rows: keep the CSR resident in L2
+  else
+    *p = x;
+}
+
+template <int MODE, typename LT>
+__device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t V, const LT* lvl,
+                                           const uint32_t* nh, uint64_t cost, bool nt) {
+  using N = Nh<MODE>;
+  using O = LvlOps<LT>;
+  const uint32_t tid = threadIdx.x;
+  uint64_t* drow = a.dist + (size_t)sid * V;
+  if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
+    // two nodes per lane: 16-byte stores
+    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
+    for (uint32_t i = tid; i < V / 2u; i += kBlock) {
+      const uint32_t l0 = lvl[2u * i], l1 = lvl[2u * i + 1u];
+      const uint64_t x0 = l0 != O::kUnset ? (uint64_t)l0 * cost : ~0ull;
+      const uint64_t x1 = l1 != O::kUnset ? (uint64_t)l1 * cost : ~0ull;
+      if (nt) {
+        __builtin_nontemporal_store(x0, &d2[i].x);
+        __builtin_nontemporal_store(x1, &d2[i].y);
+      } else {
+        d2[i] = make_ulonglong2(x0, x1);
+      }
+    }
+  } else {
+    for (uint32_t v = tid; v < V; v += kBlock) {
+      const uint32_t l = lvl[v];
+      store_row<uint64_t>(&drow[v], l != O::kUnset ? (uint64_t)l * cost : ~0ull, nt);
+    }
+  }
+  if (!a.nh) return;
+  const uint32_t nb = a.nh_bytes;
+  uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+  const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
+  if (MODE == kNhNibble && nb == 1 && aligned4) {
+    // four nodes (four nibbles of one half-dword) per lane -> one u32 of four bytes
+    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+    for (uint32_t i = tid; i < V / 4u; i += kBlock) {
+      const uint32_t h = (nh[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
+      store_row<uint32_t>(&nrow32[i], (h & 0xFu) | ((h & 0xF0u) << 4) | ((h & 0xF00u) << 8) | ((h & 0xF000u) << 12), nt);
+    }
+  } else if (MODE == kNhByte && nb == 1 && aligned4) {
+    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+    for (uint32_t i = tid; i < V / 4u; i += kBlock) store_row<uint32_t>(&nrow32[i], nh[i], nt);
+  } else {
+    const uint32_t total = V * nb;
+    for (uint32_t i = tid; i < total; i += kBlock) {
+      const uint32_t v = i / nb, j = i - v * nb;
+      nrow[i] = (uint8_t)N::byte(nh, v, j);
+    }
+  }
+}
+
+// ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
+// the rest from CSR (G == 1); 2 = ELL only (every row has <= 4 edges, no ignore set,
+// no tight-edge output).
+// RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent levels
+//               exceed the ring, or whose depth exceeds 253, sets ovf[sid] for a re-run.
+// RING = false: LT = u16, queue = full BFS order (capacity V).
+// rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
+template <int MODE, int K, typename LT, bool RING, int ELLM, bool GENERIC>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void bfs_kernel(
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog,
+                                                     uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
+                                                     uint32_t work_slot, uint32_t nt) {
+  // GENERIC = false: no ignore set and no tight-edge output (compile time), the
+  // all-sources / prefetch case; GENERIC = true handles both at run time.
+  constexpr bool ELECT = Nh<MODE>::kSingle;
+  const bool has_ign = GENERIC && has_ign_rt != 0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t s_next;
+  using N = Nh<MODE>;
+  using O = LvlOps<LT>;
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6;
+  const uint32_t nh_words = N::words(V);
+  const BfsLayout<LT> lay = bfs_layout<LT>(V, g.L, has_ign, nh_words, !ELECT, ring_cap);
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  LT* lvl = reinterpret_cast<LT*>(base + lay.lvl);
+  uint32_t* lvl_w = reinterpret_cast<uint32_t*>(base + lay.lvl);
+  uint32_t* vis = reinterpret_cast<uint32_t*>(base + lay.vis);
+  uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
+  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
+  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
+  const uint32_t lane = __lane_id();
+  const uint32_t bit_words = (V + 31u) / 32u;
+  const uint32_t lvl_words = ((uint32_t)sizeof(LT) * (V + 4u)) / 4u;
+  const uint32_t ign_words = (g.L + 31u) / 32u;
+  const uint32_t G = 1u << glog, ngroups = kBlock >> glog, groups_per_wave = 64u >> glog;
+  const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
+  const uint32_t tight_words = (g.E + 63u) / 64u;
+  const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
+  uint32_t* work = a.work + work_slot;
+
+  for (uint32_t sid = blockIdx.x; sid < a.n;) {
+    if (!(rerun && a.ovf[sid] != rerun)) {  // block-uniform
+      const uint32_t src = a.sources[sid];
+      for (uint32_t i = tid; i < lvl_words; i += kBlock) lvl_w[i] = 0xFFFFFFFFu;
+      if (!ELECT)
+        for (uint32_t i = tid; i < bit_words; i += kBlock) vis[i] = 0;
+      for (uint32_t i = tid; i < nh_words; i += kBlock) nh[i] = 0;
+      if (has_ign)
+        for (uint32_t i = tid; i < ign_words; i += kBlock) ign[i] = 0;
+      if (tid < 4) ctl[tid] = 0;
+      __syncthreads();
+      if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
+      if (tid == 0) {
+        lvl[src] = 0;
+        if (!ELECT) vis[src >> 5] = 1u << (src & 31u);
+      }
+      __syncthreads();
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+
+      // level 0: expand the source (even when overloaded); a directly connected
+      // node's next hop is the node itself (LinkState.cpp:867-872)
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += kBlock) {
+          const uint32_t e = e0 + tid;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e])) && v != src) {
+              if constexpr (ELECT) {
+                fresh = N::fetch_or_bit(nh, v, g.nbr[e]) == 0u;
+              } else {
+                const uint32_t bit = 1u << (v & 31u);
+                fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
+                N::or_bit(nh, v, g.nbr[e]);
+              }
+              lvl[v] = (LT)1;
+              if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+            }
+          }
+          // level-0 appends count in ctl[0]; level L >= 1 uses ctl[L % 3] (ctl[1] first)
+          const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
+          if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap checked by the host
+        }
+      }
+      __syncthreads();
+
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1;
+      bool overflow = false;  // block-uniform
+      while (head < tail) {
+        if (RING && L + 1u >= O::kUnset) {  // next level not representable in u8
+          overflow = true;
+          break;
+        }
+        uint32_t* cnt = &ctl[L % 3u];
+        if (tid == 0) ctl[(L + 1u) % 3u] = 0;  // last read two barriers ago
+        for (uint32_t fb = head; fb < tail; fb += ngroups) {
+          if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
+          const uint32_t idx = fb + group;
+          const bool live = idx < tail;
+          uint32_t u = 0, beg = 0, end = 0;
+          uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
+          if (live) {
+            u = ring[RING ? (idx & rmask) : idx];
+            if (ELLM == 2) {
+              ell = g.ellt[u];
+            } else {
+              const uint2 r = g.row2t[u];  // empty for overloaded nodes (sinks)
+              beg = r.x;
+              end = r.y;
+              if (ELLM == 1) ell = g.ellt[u];
+            }
+          }
+          if (ELLM == 2 && live) end = 4;  // kEdgeDown-padded ELL slots stand for the row end
+          const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
+          for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; __any(e0 < end); e0 += G * K) {
+            uint32_t av[K], lv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j * G;
+              if (ELLM == 2) {
+                av[j] = j == 0 ? ell.x : j == 1 ? ell.y : j == 2 ? ell.z : ell.w;
+              } else if (ELLM == 1 && e0 == beg) {
+                av[j] = j == 0 ? ell.x : j == 1 ? ell.y : j == 2 ? ell.z : ell.w;
+              } else {
+                av[j] = e < end ? g.adj[e] : kEdgeDown;
+              }
+              lv[j] = (has_ign && e < end) ? g.lid[e] : 0u;
+            }
+            // (1) tight test: the K level reads are issued together (no branches)
+            bool tight[K];
+            uint32_t vv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j * G;
+              vv[j] = av[j] & ~kEdgeDown;
+              const bool ok = !(av[j] & kEdgeDown) && (ELLM == 2 || e < end) && !(has_ign && test_bit(ign, lv[j]));
+              const uint32_t l = lvl[ok ? vv[j] : V];  // lvl[V] is padding
+              tight[j] = ok && l > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
+            }
+            // (2) addNextHops(nh(u)) + election of the appending arrival: K atomics in
+            //     flight together; non-tight edges OR 0 into the lane's own dummy word
+            uint32_t fresh_mask = 0;
+            if constexpr (ELECT) {
+              const uint32_t x = nhu.x;
+              uint32_t old[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                old[j] = atomicOr(tight[j] ? &nh[N::word(vv[j])] : &dummy[lane], tight[j] ? x << N::shift(vv[j]) : 0u);
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                fresh_mask |= (tight[j] && ((old[j] >> N::shift(vv[j])) & N::kMask) == 0u) ? (1u << j) : 0u;
+            } else {
+              uint32_t old[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                old[j] = atomicOr(tight[j] ? &vis[vv[j] >> 5] : &dummy[lane], tight[j] ? 1u << (vv[j] & 31u) : 0u);
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                fresh_mask |= (tight[j] && !((old[j] >> (vv[j] & 31u)) & 1u)) ? (1u << j) : 0u;
+                if (tight[j]) N::or_val(nh, vv[j], nhu);
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              if (trow && tight[j]) {
+                const uint32_t e = e0 + j * G;
+                atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+              }
+            }
+            // (3) wave-aggregated append: 3 ballots + one ds_add per wave
+            uint32_t total;
+            uint32_t slot = wave_prefix_small((uint32_t)__popc(fresh_mask), &total);
+            if (total) {  // wave-uniform
+              const int leader = __ffsll((long long)__ballot(1)) - 1;
+              uint32_t wbase = 0;
+              if ((int)lane == leader) wbase = atomicAdd(cnt, total);
+              slot += tail + __builtin_amdgcn_readfirstlane(wbase);
+              bool lost = false;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                if ((fresh_mask >> j) & 1u) {
+                  if (!RING) {
+                    ring[slot] = (uint16_t)vv[j];
+                  } else if (slot - head < ring_cap) {
+                    ring[slot & rmask] = (uint16_t)vv[j];
+                  } else {
+                    lost = true;  // two adjacent levels exceed the ring
+                  }
+                  ++slot;
+                }
+              }
+              if (RING && __any(lost) && (int)lane == leader) ctl[3] = 1;
+            }
+          }
+        }
+        __syncthreads();
+        head = tail;
+        tail += *cnt;
+        ++L;
+        if (RING && ctl[3]) {  // ring overflow; ctl[3] is uniform after the barrier
+          overflow = true;
+          break;
+        }
+      }
+      if (RING && overflow) {  // re-run by the u16 / full-order variant
+        if (tid == 0) a.ovf[sid] = (uint8_t)(rerun + 1u);
+      } else {
+        write_rows<MODE, LT>(a, sid, V, lvl, nh, cost, nt != 0);
+      }
+    }
+    // next solve: dynamic scheduling (the first gridDim.x solves are static)
+    __syncthreads();  // every lane is done with this solve's LDS and s_next
+    if (tid == 0) s_next = gridDim.x + atomicAdd(work, 1u);
+    __syncthreads();
+    sid = s_next;
+  }
+}
+
+// Fast path: u8 levels + a ring sized so that target workgroups fit a CU.
+// It cannot be used when its ring would be smaller than 256 entries (or than a row);
+// then the full-order u16 variant runs directly.
+uint32_t target_wgs() {
+  if (const char* e = std::getenv("OPENR_SPF_BFS_WGS")) {  // tuning
+    const int v = std::atoi(e);
+    if (v >= 1 && v <= 16) return (uint32_t)v;
+  }
+  return kBfsTargetWgs;
+}
+
+// Result rows are written once and read by the host / the next consumer, never by this
+// kernel: non-temporal stores keep them from evicting the CSR mirror out of L2.
+uint32_t nt_stores() {
+  if (const char* e = std::getenv("OPENR_SPF_NT")) return e[0] == '1' ? 1u : 0u;  // tuning
+  return 1u;
+}
+
+uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode) {
+  if (const char* e = std::getenv("OPENR_SPF_BFS_FULL"))  // tuning: force the full-order variant
+    if (e[0] == '1') return 0;
+  const bool vis = !nh_mode_single(mode);
+  const uint32_t fixed = bfs_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), vis, 0).total;
+  const uint32_t budget = kMaxLds / target_wgs();
+  if (fixed >= budget) return 0;
+  uint32_t cap = 1;
+  while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
+  return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
+}
+
+template <int MODE, typename LT, bool RING, int ELLM>
+hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                              uint32_t ring_cap, uint32_t rerun, uint32_t work_slot, int num_cus, hipStream_t s,
+                              LaunchInfo* info) {
+  constexpr int K = (int)kBfsEdgesPerLane;
+  const bool vis = !Nh<MODE>::kSingle;
+  const uint32_t lds = bfs_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus);
+  const bool generic = has_ign || a.tight != nullptr;
+  auto k = generic ? bfs_kernel<MODE, K, LT, RING, ELLM == 2 ? 1 : ELLM, true>
+                   : bfs_kernel<MODE, K, LT, RING, ELLM, false>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  if (info && !rerun) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = RING ? "bfs_kernel<ring,u8>" : "bfs_kernel<full,u16>";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun,
+                     work_slot, nt_stores());
+  return hipGetLastError();
+}
+
+template <int MODE, int ELLM>
+hipError_t launch_bfs_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                           uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // ring/u8 variant first (or as the re-run of flagged multi-source batches); solves it
+  // flags are re-run by the full-order u16 variant on the same stream
+  const uint32_t cap = fast_ring_cap(g, has_ign, MODE);
+  if (!cap)
+    return launch_bfs_variant<MODE, uint16_t, false, ELLM>(g, a, cost, glog, has_ign, g.V, first_rerun, 1u,
+                                                           num_cus, s, info);
+  const bool may_overflow = g.V > cap || g.V > 254u;
+  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELLM>(g, a, cost, glog, has_ign, cap, first_rerun, 1u,
+                                                                 num_cus, s, info);
+  if (err != hipSuccess || !may_overflow) return err;
+  return launch_bfs_variant<MODE, uint16_t, false, ELLM>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u, 2u,
+                                                         num_cus, s, info);
+}
+}  // namespace
+
+uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode) {
+  // the full-order u16 variant must fit (it re-runs solves the fast path flags)
+  if (V > 65535u) return 0;
+  uint32_t t = bfs_layout<uint16_t>(V, L, has_ignore, nh_words_for(nh_mode, V), !nh_mode_single(nh_mode), V).total;
+  return t <= kMaxLds ? t : 0;
+}
+
+hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, int group_lanes,
+                      int num_cus, hipStream_t s, LaunchInfo* info) {
+  const bool has_ign = a.ign_ptr != nullptr;
+  if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode)) return hipErrorInvalidValue;
+  if (a.n == 0) return hipSuccess;
+  if (!a.ovf || !a.work) return hipErrorInvalidValue;
+  hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
+  if (err != hipSuccess) return err;
+  err = hipMemsetAsync(a.work, 0, kWorkSlots * sizeof(uint32_t), s);
+  if (err != hipSuccess) return err;
+  if (a.tight) {
+    err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((g.E + 63u) / 64u) * 8u, s);
+    if (err != hipSuccess) return err;
+  }
+  uint32_t glog = 0;
+  while ((1 << glog) < group_lanes && glog < 6) ++glog;
+  // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
+  const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
+  // bit-parallel multi-source BFS when eligible (opt-in); its overflowing batches fall through
+  uint32_t first_rerun = 0;
+  const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
+  if (ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
+    err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
+                       info);
+    if (err != hipSuccess) return err;
+    first_rerun = 1;
+  }
+#define OPENR_BFS_MODE(M)                                                                                   \
+  case M:                                                                                                   \
+    return ellm == 2   ? launch_bfs_mode<M, 2>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info)  \
+           : ellm == 1 ? launch_bfs_mode<M, 1>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info)  \
+                       : launch_bfs_mode<M, 0>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  switch (nh_mode) {
+    OPENR_BFS_MODE(kNhNibble)
+    OPENR_BFS_MODE(kNhByte)
+    OPENR_BFS_MODE(kNhHalf)
+    OPENR_BFS_MODE(kNhW1)
+    OPENR_BFS_MODE(kNhW2)
+    OPENR_BFS_MODE(kNhW4)
+    OPENR_BFS_MODE(kNhW8)
+  }
+#undef OPENR_BFS_MODE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace openr_spf

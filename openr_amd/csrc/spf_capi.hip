@@ -73,10 +73,11 @@ struct Device {
   DevBuf<uint32_t> src, ign_ptr, ign_links;
   DevBuf<uint64_t> dist, tight;
   DevBuf<uint8_t> nh, ovf, scratch;
+  DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
 };
 
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row, g.row2, g.ovl_bits, g.ell, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
+  void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -224,6 +225,8 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh_bits = ctx->nh_bits;
     HIP_TRY(d.ovf.reserve(m));
     a.ovf = d.ovf.p;
+    HIP_TRY(d.work.reserve(kWorkSlots));
+    a.work = d.work.p;
     HIP_TRY(prepare_scratch(ctx, d, plan, a));
     HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
     HIP_TRY(launch(ctx, d, plan, a, d.stream));
@@ -330,6 +333,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.nh.release();
     d.ovf.release();
     d.scratch.release();
+    d.work.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -399,16 +403,20 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     rev[b] = a;
   }
   for (uint32_t e = 0; e < E; ++e) win[e] = w[rev[e]];
-  std::vector<uint2> row2(V);
-  std::vector<uint4> ell(V);
+  // transit views: an overloaded node is reached but never expanded unless it is the
+  // source (LinkState.cpp:831-838), so its transit row is empty / all-down
+  std::vector<uint2> row2(V), row2t(V);
+  std::vector<uint4> ellt(V);
   for (uint32_t u = 0; u < V; ++u) {
     uint32_t x[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
-    for (uint32_t j = 0; j < 4 && gr->row_ptr[u] + j < gr->row_ptr[u + 1]; ++j) x[j] = adj[gr->row_ptr[u] + j];
-    ell[u] = make_uint4(x[0], x[1], x[2], x[3]);
+    if (!ovl[u])
+      for (uint32_t j = 0; j < 4 && gr->row_ptr[u] + j < gr->row_ptr[u + 1]; ++j) x[j] = adj[gr->row_ptr[u] + j];
+    ellt[u] = make_uint4(x[0], x[1], x[2], x[3]);
   }
   std::vector<uint32_t> ovl_bits((V + 31) / 32 + 1, 0);
   for (uint32_t u = 0; u < V; ++u) {
     row2[u] = make_uint2(gr->row_ptr[u], gr->row_ptr[u + 1]);
+    row2t[u] = ovl[u] ? make_uint2(gr->row_ptr[u], gr->row_ptr[u]) : row2[u];
     if (ovl[u]) ovl_bits[u >> 5] |= 1u << (u & 31u);
   }
   if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
@@ -432,8 +440,9 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     };
     hipError_t err = up(&g.row, gr->row_ptr, V + 1);
     if (err == hipSuccess) err = up(&g.row2, row2.data(), V);
+    if (err == hipSuccess) err = up(&g.row2t, row2t.data(), V);
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
-    if (err == hipSuccess) err = up(&g.ell, ell.data(), V);
+    if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
     if (err == hipSuccess) err = up(&g.win, win.data(), E);
@@ -529,6 +538,8 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bits = ctx->nh_bits;
   HIP_TRY(d.ovf.reserve(n));
   a.ovf = d.ovf.p;
+  HIP_TRY(d.work.reserve(kWorkSlots));
+  a.work = d.work.p;
   HIP_TRY(prepare_scratch(ctx, d, plan, a));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   HIP_TRY(launch(ctx, d, plan, a, s));

@@ -16,48 +16,43 @@ namespace dev {
 template <int MODE>
 struct Nh;
 
-template <>
-struct Nh<kNhByte> {  // <= 8 bits: four nodes per dword
-  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 3u) / 4u; }
-  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
-    atomicOr(&nh[v >> 2], (1u << b) << ((v & 3u) * 8u));
+// Packed modes (one node's set inside one dword): the first arrival at v is the one
+// whose atomicOr sees v's field empty (every reached node's set is non-empty), so
+// these modes elect the appending arrival without a separate visited bitmap.
+template <uint32_t BITS>
+struct NhPacked {
+  static constexpr bool kSingle = true;
+  static constexpr uint32_t kPer = 32u / BITS;
+  static constexpr uint32_t kMask = BITS == 32 ? 0xFFFFFFFFu : ((1u << (BITS & 31u)) - 1u);
+  static __host__ __device__ uint32_t words(uint32_t V) { return (V + kPer - 1u) / kPer; }
+  static __device__ uint32_t word(uint32_t v) { return v / kPer; }
+  static __device__ uint32_t shift(uint32_t v) { return (v % kPer) * BITS; }
+  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) { atomicOr(&nh[word(v)], (1u << b) << shift(v)); }
+  // OR bit b into v's set; returns the set's previous bits (0 <=> first arrival)
+  static __device__ uint32_t fetch_or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
+    return (atomicOr(&nh[word(v)], (1u << b) << shift(v)) >> shift(v)) & kMask;
   }
   static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
-    uint32_t x = (nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu;
-    if (x) atomicOr(&nh[v >> 2], x << ((v & 3u) * 8u));
+    const uint32_t x = (nh[word(u)] >> shift(u)) & kMask;
+    if (x) atomicOr(&nh[word(v)], x << shift(v));
   }
   static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
-    return j == 0 ? (nh[v >> 2] >> ((v & 3u) * 8u)) & 0xFFu : 0u;
+    return j * 8u < BITS ? (nh[word(v)] >> (shift(v) + 8u * j)) & (BITS < 8 ? kMask : 0xFFu) : 0u;
   }
   struct Val { uint32_t x; };
-  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 2] >> ((u & 3u) * 8u)) & 0xFFu}; }
+  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[word(u)] >> shift(u)) & kMask}; }
   static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
-    if (s.x) atomicOr(&nh[v >> 2], s.x << ((v & 3u) * 8u));
+    if (s.x) atomicOr(&nh[word(v)], s.x << shift(v));
   }
 };
-
-template <>
-struct Nh<kNhHalf> {  // <= 16 bits: two nodes per dword
-  static __host__ __device__ uint32_t words(uint32_t V) { return (V + 1u) / 2u; }
-  static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
-    atomicOr(&nh[v >> 1], (1u << b) << ((v & 1u) * 16u));
-  }
-  static __device__ void or_from(uint32_t* nh, uint32_t v, uint32_t u) {
-    uint32_t x = (nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu;
-    if (x) atomicOr(&nh[v >> 1], x << ((v & 1u) * 16u));
-  }
-  static __device__ uint32_t byte(const uint32_t* nh, uint32_t v, uint32_t j) {
-    return j < 2 ? (nh[v >> 1] >> ((v & 1u) * 16u + 8u * j)) & 0xFFu : 0u;
-  }
-  struct Val { uint32_t x; };
-  static __device__ Val load(const uint32_t* nh, uint32_t u) { return {(nh[u >> 1] >> ((u & 1u) * 16u)) & 0xFFFFu}; }
-  static __device__ void or_val(uint32_t* nh, uint32_t v, const Val& s) {
-    if (s.x) atomicOr(&nh[v >> 1], s.x << ((v & 1u) * 16u));
-  }
-};
+template <> struct Nh<kNhNibble> : NhPacked<4> {};  // <= 4 bits (grids): eight nodes per dword
+template <> struct Nh<kNhByte> : NhPacked<8> {};    // <= 8 bits: four nodes per dword
+template <> struct Nh<kNhHalf> : NhPacked<16> {};   // <= 16 bits: two nodes per dword
+template <> struct Nh<kNhW1> : NhPacked<32> {};     // <= 32 bits: one dword per node
 
 template <int W>
-struct NhWords {  // W dwords per node
+struct NhWords {  // W dwords per node (W >= 2)
+  static constexpr bool kSingle = false;  // arrivals are elected by a visited bitmap
   static __host__ __device__ uint32_t words(uint32_t V) { return V * W; }
   static __device__ void or_bit(uint32_t* nh, uint32_t v, uint32_t b) {
     atomicOr(&nh[v * W + (b >> 5)], 1u << (b & 31u));
@@ -85,7 +80,6 @@ struct NhWords {  // W dwords per node
       if (s.x[k]) atomicOr(&nh[v * W + k], s.x[k]);
   }
 };
-template <> struct Nh<kNhW1> : NhWords<1> {};
 template <> struct Nh<kNhW2> : NhWords<2> {};
 template <> struct Nh<kNhW4> : NhWords<4> {};
 template <> struct Nh<kNhW8> : NhWords<8> {};

@@ -18,8 +18,10 @@ struct DevGraph {
   uint32_t max_deg = 0;        // largest row (source expansion must fit the frontier queue)
   uint32_t* row = nullptr;     // [V+1]
   uint2* row2 = nullptr;       // [V] (row[u], row[u+1]) in one 8-byte load
+  uint2* row2t = nullptr;      // [V] transit row: row2[u], or an empty range when u is overloaded
+                               //     (an overloaded node other than the source is never expanded)
   uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
-  uint4* ell = nullptr;        // [V] first 4 edges of each row (adj encoding, kEdgeDown-padded)
+  uint4* ellt = nullptr;       // [V] first 4 edges of each transit row (adj encoding, kEdgeDown-padded)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
   uint32_t* win = nullptr;     // [E] metric of the reverse edge (col -> row owner)
@@ -32,12 +34,16 @@ struct DevGraph {
 constexpr uint32_t kEdgeDown = 0x80000000u;
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
-constexpr uint32_t kBfsTargetWgs = 6;     // fast-path BFS sizes its LDS for this many workgroups per CU
+constexpr uint32_t kBfsTargetWgs = 8;     // fast-path BFS sizes its LDS for this many workgroups per CU
 
 // Next-hop bitset storage classes in LDS (chosen from the max distinct degree).
-enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, kNhW8 = 5 };
+enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, kNhW8 = 5, kNhNibble = 6 };
 int nh_mode_for_bits(uint32_t bits);            // -1 if > 256 bits
 uint32_t nh_mode_lds_bytes(int mode, uint32_t V);
+uint32_t nh_words_for(int mode, uint32_t V);     // LDS dwords of V next-hop sets
+bool nh_mode_single(int mode);                  // one node's set lives inside one dword
+// persistent grid: workgroups that fit a CU by LDS (<= 8 x 256 threads) x CUs, <= n
+uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus);
 
 struct LaunchInfo {
   uint32_t lds_bytes = 0;
@@ -58,7 +64,9 @@ struct SolveArgs {
   uint8_t* ovf;               // [n] scratch: solves a faster variant could not finish (re-run flags)
   uint8_t* scratch;           // multi-source BFS level bytes ([grid][V][lanes]); nullable
   size_t scratch_bytes;
+  uint32_t* work;             // [kWorkSlots] dynamic-scheduling counters (zeroed by the launcher)
 };
+constexpr uint32_t kWorkSlots = 4;  // one counter per kernel launched for one solve call
 
 // Bit-parallel multi-source BFS plan (spf_msbfs.hip).
 struct MsPlan {
