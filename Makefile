@@ -29,7 +29,7 @@ $(LIBDIR)/%.o: $(CSRC)/%.hip $(ENGINE_HDRS) | $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(ENGINE): $(ENGINE_OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ENGINE_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(ENGINE_OBJS)
 
 # C++ host mirror of openr::LinkState over the C-ABI (links the engine)
 $(HOST): $(HOST_SRCS) $(HOST_HDRS) $(ENGINE)

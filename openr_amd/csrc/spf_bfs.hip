@@ -77,12 +77,30 @@ __device__ __forceinline__ void store_row(T* p, const T& x, bool nt) {
     *p = x;
 }
 
-template <int MODE, typename LT>
-__device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t V, const LT* lvl,
-                                           const uint32_t* nh, uint64_t cost, bool nt) {
+// Sliced classes: slice s owns next-hop bytes [4s, 4s + 4); slice 0 also writes the
+// distance row and zero-fills the bytes past the last slice.
+template <int MODE, typename LT, bool SLICED>
+__device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
+                                           const LT* lvl, const uint32_t* nh, uint64_t cost, bool nt) {
   using N = Nh<MODE>;
   using O = LvlOps<LT>;
   const uint32_t tid = threadIdx.x;
+  if (SLICED) {
+    if (a.nh) {
+      const uint32_t nb = a.nh_bytes, j0 = 4u * slice, zero0 = 4u * a.nsl;
+      uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        const uint32_t w = nh[v];
+        uint8_t* o = nrow + (size_t)v * nb;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4u; ++jj)
+          if (j0 + jj < nb) o[j0 + jj] = (uint8_t)(w >> (8u * jj));
+        if (slice == 0)
+          for (uint32_t j = zero0; j < nb; ++j) o[j] = 0;
+      }
+    }
+    if (slice != 0) return;
+  }
   uint64_t* drow = a.dist + (size_t)sid * V;
   if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
     // two nodes per lane: 16-byte stores
@@ -104,7 +122,7 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
       store_row<uint64_t>(&drow[v], l != O::kUnset ? (uint64_t)l * cost : ~0ull, nt);
     }
   }
-  if (!a.nh) return;
+  if (SLICED || !a.nh) return;
   const uint32_t nb = a.nh_bytes;
   uint8_t* nrow = a.nh + (size_t)sid * V * nb;
   const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
@@ -134,14 +152,15 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
 //               exceed the ring, or whose depth exceeds 253, sets ovf[sid] for a re-run.
 // RING = false: LT = u16, queue = full BFS order (capacity V).
 // rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
-template <int MODE, int K, typename LT, bool RING, int ELLM, bool GENERIC>
+// SLICED: one unit = (solve, 32-bit slice of the next-hop set); arrivals are elected
+// by the visited bitmap (a slice of nh(u) may be empty).
+template <int MODE, int K, typename LT, bool RING, int ELLM, bool GENERIC, bool SLICED>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void bfs_kernel(
-    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog,
-                                                     uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
-                                                     uint32_t work_slot, uint32_t nt) {
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
+    uint32_t work_slot, uint32_t nt) {
   // GENERIC = false: no ignore set and no tight-edge output (compile time), the
   // all-sources / prefetch case; GENERIC = true handles both at run time.
-  constexpr bool ELECT = Nh<MODE>::kSingle;
+  constexpr bool ELECT = Nh<MODE>::kSingle && !SLICED;
   const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_next;
@@ -168,10 +187,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
   const uint32_t tight_words = (g.E + 63u) / 64u;
   const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
   uint32_t* work = a.work + work_slot;
+  const uint32_t nsl = SLICED ? a.nsl : 1u;
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  const uint32_t units = count * nsl;
 
-  for (uint32_t sid = blockIdx.x; sid < a.n;) {
-    if (!(rerun && a.ovf[sid] != rerun)) {  // block-uniform
-      const uint32_t src = a.sources[sid];
+  for (uint32_t unit = blockIdx.x; unit < units;) {
+    const uint32_t k = SLICED ? unit / nsl : unit, slice = SLICED ? unit - k * nsl : 0u;
+    const uint32_t sid = a.perm ? a.perm[first + k] : k;
+    const uint32_t src = a.sources[sid];
+    if (src < V && !(rerun && a.ovf[sid] != rerun)) {  // block-uniform
       for (uint32_t i = tid; i < lvl_words; i += kBlock) lvl_w[i] = 0xFFFFFFFFu;
       if (!ELECT)
         for (uint32_t i = tid; i < bit_words; i += kBlock) vis[i] = 0;
@@ -205,7 +229,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
               } else {
                 const uint32_t bit = 1u << (v & 31u);
                 fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
-                N::or_bit(nh, v, g.nbr[e]);
+                const uint32_t b = g.nbr[e];
+                if (!SLICED) N::or_bit(nh, v, b);
+                else if ((b >> 5) == slice) N::or_bit(nh, v, b & 31u);
               }
               lvl[v] = (LT)1;
               if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
@@ -338,16 +364,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
       }
       if (RING && overflow) {  // re-run by the u16 / full-order variant
-        if (tid == 0) a.ovf[sid] = (uint8_t)(rerun + 1u);
+        if (tid == 0) a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
       } else {
-        write_rows<MODE, LT>(a, sid, V, lvl, nh, cost, nt != 0);
+        write_rows<MODE, LT, SLICED>(a, sid, slice, V, lvl, nh, cost, nt != 0);
       }
     }
-    // next solve: dynamic scheduling (the first gridDim.x solves are static)
-    __syncthreads();  // every lane is done with this solve's LDS and s_next
+    // next unit: dynamic scheduling (the first gridDim.x units are static)
+    __syncthreads();  // every lane is done with this unit's LDS and s_next
     if (tid == 0) s_next = gridDim.x + atomicAdd(work, 1u);
     __syncthreads();
-    sid = s_next;
+    unit = s_next;
   }
 }
 
@@ -369,29 +395,34 @@ uint32_t nt_stores() {
   return 1u;
 }
 
-uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode) {
+uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode, bool sliced) {
   if (const char* e = std::getenv("OPENR_SPF_BFS_FULL"))  // tuning: force the full-order variant
     if (e[0] == '1') return 0;
-  const bool vis = !nh_mode_single(mode);
+  const bool vis = sliced || !nh_mode_single(mode);
   const uint32_t fixed = bfs_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), vis, 0).total;
   const uint32_t budget = kMaxLds / target_wgs();
-  if (fixed >= budget) return 0;
+  if (fixed >= budget) {
+    // fewer workgroups per CU: the largest power-of-two ring that still fits one
+    uint32_t cap = 1;
+    while (fixed + cap * 4u <= kMaxLds && cap < 4096u) cap *= 2u;
+    return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
+  }
   uint32_t cap = 1;
   while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
   return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
 }
 
-template <int MODE, typename LT, bool RING, int ELLM>
+template <int MODE, typename LT, bool RING, int ELLM, bool SLICED>
 hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
                               uint32_t ring_cap, uint32_t rerun, uint32_t work_slot, int num_cus, hipStream_t s,
                               LaunchInfo* info) {
   constexpr int K = (int)kBfsEdgesPerLane;
-  const bool vis = !Nh<MODE>::kSingle;
+  const bool vis = SLICED || !Nh<MODE>::kSingle;
   const uint32_t lds = bfs_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
-  const uint32_t grid = blocks_for(a.n, lds, num_cus);
+  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus);
   const bool generic = has_ign || a.tight != nullptr;
-  auto k = generic ? bfs_kernel<MODE, K, LT, RING, ELLM == 2 ? 1 : ELLM, true>
-                   : bfs_kernel<MODE, K, LT, RING, ELLM, false>;
+  auto k = generic ? bfs_kernel<MODE, K, LT, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
+                   : bfs_kernel<MODE, K, LT, RING, ELLM, false, SLICED>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
@@ -405,73 +436,73 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   return hipGetLastError();
 }
 
-template <int MODE, int ELLM>
+template <int MODE, int ELLM, bool SLICED>
 hipError_t launch_bfs_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
                            uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
   // ring/u8 variant first (or as the re-run of flagged multi-source batches); solves it
   // flags are re-run by the full-order u16 variant on the same stream
-  const uint32_t cap = fast_ring_cap(g, has_ign, MODE);
+  const uint32_t slot = 2u * a.cls;
+  const uint32_t cap = fast_ring_cap(g, has_ign, MODE, SLICED);
   if (!cap)
-    return launch_bfs_variant<MODE, uint16_t, false, ELLM>(g, a, cost, glog, has_ign, g.V, first_rerun, 1u,
-                                                           num_cus, s, info);
+    return launch_bfs_variant<MODE, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun, slot,
+                                                                   num_cus, s, info);
   const bool may_overflow = g.V > cap || g.V > 254u;
-  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELLM>(g, a, cost, glog, has_ign, cap, first_rerun, 1u,
-                                                                 num_cus, s, info);
+  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, cap, first_rerun,
+                                                                         slot, num_cus, s, info);
   if (err != hipSuccess || !may_overflow) return err;
-  return launch_bfs_variant<MODE, uint16_t, false, ELLM>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u, 2u,
-                                                         num_cus, s, info);
+  return launch_bfs_variant<MODE, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u,
+                                                                 slot + 1u, num_cus, s, info);
+}
+
+template <int MODE, bool SLICED>
+hipError_t launch_bfs_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                          uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
+  if (ellm == 2) return launch_bfs_mode<MODE, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  if (ellm == 1) return launch_bfs_mode<MODE, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  return launch_bfs_mode<MODE, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
 }
 }  // namespace
 
-uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode) {
+uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool sliced) {
   // the full-order u16 variant must fit (it re-runs solves the fast path flags)
   if (V > 65535u) return 0;
-  uint32_t t = bfs_layout<uint16_t>(V, L, has_ignore, nh_words_for(nh_mode, V), !nh_mode_single(nh_mode), V).total;
+  const bool vis = sliced || !nh_mode_single(nh_mode);
+  uint32_t t = bfs_layout<uint16_t>(V, L, has_ignore, nh_words_for(nh_mode, V), vis, V).total;
   return t <= kMaxLds ? t : 0;
 }
 
-hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, int group_lanes,
-                      int num_cus, hipStream_t s, LaunchInfo* info) {
+hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, bool sliced,
+                      int group_lanes, int num_cus, hipStream_t s, LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
-  if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode)) return hipErrorInvalidValue;
+  if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode, sliced)) return hipErrorInvalidValue;
+  if (sliced && (nh_mode != kNhW1 || a.nsl < 1u || a.nsl > 8u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  if (!a.ovf || !a.work) return hipErrorInvalidValue;
+  if (!a.ovf || !a.work || a.cls >= kMaxClasses) return hipErrorInvalidValue;
   hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
   if (err != hipSuccess) return err;
-  err = hipMemsetAsync(a.work, 0, kWorkSlots * sizeof(uint32_t), s);
+  err = hipMemsetAsync(a.work + 2u * a.cls, 0, 2u * sizeof(uint32_t), s);
   if (err != hipSuccess) return err;
-  if (a.tight) {
-    err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((g.E + 63u) / 64u) * 8u, s);
-    if (err != hipSuccess) return err;
-  }
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
   const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
-  // bit-parallel multi-source BFS when eligible (opt-in); its overflowing batches fall through
+  // bit-parallel multi-source BFS when eligible (opt-in, single-class batches); its
+  // overflowing batches fall through to the per-source kernels
   uint32_t first_rerun = 0;
   const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
-  if (ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
+  if (!a.perm && !sliced && ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
     err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
                        info);
     if (err != hipSuccess) return err;
     first_rerun = 1;
   }
-#define OPENR_BFS_MODE(M)                                                                                   \
-  case M:                                                                                                   \
-    return ellm == 2   ? launch_bfs_mode<M, 2>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info)  \
-           : ellm == 1 ? launch_bfs_mode<M, 1>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info)  \
-                       : launch_bfs_mode<M, 0>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  if (sliced) return launch_bfs_ell<kNhW1, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
   switch (nh_mode) {
-    OPENR_BFS_MODE(kNhNibble)
-    OPENR_BFS_MODE(kNhByte)
-    OPENR_BFS_MODE(kNhHalf)
-    OPENR_BFS_MODE(kNhW1)
-    OPENR_BFS_MODE(kNhW2)
-    OPENR_BFS_MODE(kNhW4)
-    OPENR_BFS_MODE(kNhW8)
+    case kNhNibble: return launch_bfs_ell<kNhNibble, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhByte: return launch_bfs_ell<kNhByte, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhHalf: return launch_bfs_ell<kNhHalf, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhW1: return launch_bfs_ell<kNhW1, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
   }
-#undef OPENR_BFS_MODE
   return hipErrorInvalidValue;
 }
 

@@ -74,10 +74,11 @@ struct Device {
   DevBuf<uint64_t> dist, tight;
   DevBuf<uint8_t> nh, ovf, scratch;
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
+  DevBuf<uint32_t> perm, part;  // source-class partition of a batch
 };
 
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl};
+  void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl, g.cls};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -94,6 +95,8 @@ struct openr_spf_ctx {
   uint32_t w_min = 0, w_max = 0;
   bool metric_ok = true;        // every usable metric in [1, 2^31-1]
   uint32_t group_lanes = 4;
+  uint32_t cls_mask = 0;        // source classes present among the nodes (SrcClass bits)
+  uint32_t nsl = 1;             // next-hop slices of the sliced class
   openr_spf_stats_t stats{};
 };
 
@@ -118,8 +121,10 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   if (!use_metric || ctx->w_min == ctx->w_max) {
     p->bfs = true;
     p->cost = use_metric ? std::max<uint32_t>(ctx->w_min, 1u) : 1u;
-    if (!bfs_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode))
-      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident BFS kernel", ctx->V);
+    for (int c = 0; c < kNumClasses; ++c)
+      if ((ctx->cls_mask >> c) & 1u)
+        if (!bfs_lds_bytes(ctx->V, ctx->L, has_ign, nh_mode_of_class(c), c == kClsSliced))
+          return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident BFS kernel", ctx->V);
   } else {
     p->bfs = false;
     p->delta = ctx->w_min;
@@ -153,12 +158,37 @@ hipError_t prepare_scratch(const openr_spf_ctx* ctx, Device& d, const Plan& p, S
   return hipSuccess;
 }
 
-hipError_t launch(const openr_spf_ctx* ctx, const Device& d, const Plan& p, const SolveArgs& a,
-                  hipStream_t s) {
+// Uniform-cost solves run per source class (next-hop width): one class -> one launch;
+// several -> a device-side partition of the batch, then one launch per class, the
+// widest first.
+hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs a, hipStream_t s) {
   LaunchInfo info;
-  if (p.bfs)
-    return launch_bfs(d.g, a, p.cost, p.nh_mode, group_lanes_override((int)ctx->group_lanes), d.num_cus, s, &info);
-  return launch_bucket(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+  if (a.tight) {
+    hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((d.g.E + 63u) / 64u) * 8u, s);
+    if (err != hipSuccess) return err;
+  }
+  if (!p.bfs) return launch_bucket(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+  const int gl = group_lanes_override((int)ctx->group_lanes);
+  a.perm = nullptr;
+  a.part = nullptr;
+  a.nsl = ctx->nsl;
+  if (__builtin_popcount(ctx->cls_mask) == 1) {
+    a.cls = (uint32_t)__builtin_ctz(ctx->cls_mask);
+    return launch_bfs(d.g, a, p.cost, nh_mode_of_class((int)a.cls), a.cls == kClsSliced, gl, d.num_cus, s, &info);
+  }
+  hipError_t err = d.perm.reserve(std::max<uint32_t>(a.n, 1u));
+  if (err == hipSuccess) err = d.part.reserve(3u * kMaxClasses);
+  if (err == hipSuccess) err = launch_partition(a.sources, a.n, d.g.cls, d.g.V, d.part.p, d.perm.p, s);
+  if (err != hipSuccess) return err;
+  a.perm = d.perm.p;
+  a.part = d.part.p;
+  for (int c = kNumClasses - 1; c >= 0; --c) {
+    if (!((ctx->cls_mask >> c) & 1u)) continue;
+    a.cls = (uint32_t)c;
+    err = launch_bfs(d.g, a, p.cost, nh_mode_of_class(c), c == kClsSliced, gl, d.num_cus, s, &info);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
 }
 
 int check_solve_args(const openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint64_t* dist,
@@ -273,7 +303,7 @@ void openr_spf_limits(openr_spf_limits_t* out) {
   uint32_t lo = 1, hi = 65535;
   while (lo < hi) {
     uint32_t mid = (lo + hi + 1) / 2;
-    if (bfs_lds_bytes(mid, 0, false, kNhByte)) lo = mid;
+    if (bfs_lds_bytes(mid, 0, false, kNhByte, false)) lo = mid;
     else hi = mid - 1;
   }
   out->max_nodes = lo;
@@ -334,6 +364,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.ovf.release();
     d.scratch.release();
     d.work.release();
+    d.perm.release();
+    d.part.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -420,6 +452,18 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (ovl[u]) ovl_bits[u >> 5] |= 1u << (u & 31u);
   }
   if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
+  // source class of every node (distinct degree -> next-hop width)
+  std::vector<uint8_t> cls(V);
+  uint32_t cls_mask = 0, sliced_deg = 0;
+  for (uint32_t u = 0; u < V; ++u) {
+    uint32_t nd = 0;
+    for (uint32_t e = gr->row_ptr[u]; e < gr->row_ptr[u + 1]; ++e) nd = std::max<uint32_t>(nd, nbr[e] + 1u);
+    const int c = src_class_for_degree(nd);
+    cls[u] = (uint8_t)c;
+    cls_mask |= 1u << c;
+    if (c == kClsSliced) sliced_deg = std::max(sliced_deg, nd);
+  }
+  if (!cls_mask) cls_mask = 1u << kClsNibble;
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
 
   for (Device& d : ctx->devs) {
@@ -450,6 +494,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.lid, lid.data(), E);
     if (err == hipSuccess) err = up(&g.nbr, nbr.data(), E);
     if (err == hipSuccess) err = up(&g.ovl, ovl.data(), V);
+    if (err == hipSuccess) err = up(&g.cls, cls.data(), V);
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;
@@ -465,10 +510,12 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->w_min = w_min;
   ctx->w_max = w_max;
   ctx->metric_ok = metric_ok;
+  ctx->cls_mask = cls_mask;
+  ctx->nsl = std::max<uint32_t>(1u, (sliced_deg + 31u) / 32u);
   // lanes per frontier node: enough that one pass of kBfsEdgesPerLane edges per lane
   // covers an average row (grid: 1 lane x 4 edges; fabric: 8 lanes x 4 edges)
   const uint32_t avg = V ? (E + V - 1) / V : 1;
-  const uint32_t per_lane = (avg + 2 * kBfsEdgesPerLane - 1) / (2 * kBfsEdgesPerLane);  // fabric: G=4 measured best
+  const uint32_t per_lane = (avg + 4 * kBfsEdgesPerLane - 1) / (4 * kBfsEdgesPerLane);  // fabric: G=2 measured best
   uint32_t gl = 1;
   while (gl < per_lane && gl < 64) gl <<= 1;
   ctx->group_lanes = gl;

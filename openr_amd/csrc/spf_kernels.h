@@ -29,6 +29,7 @@ struct DevGraph {
   uint32_t* lid = nullptr;     // [E] undirected link id
   uint16_t* nbr = nullptr;     // [E] distinct-neighbour index of col within its row
   uint8_t* ovl = nullptr;      // [V] overloaded
+  uint8_t* cls = nullptr;      // [V] source class (SrcClass) of each node
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
@@ -65,8 +66,26 @@ struct SolveArgs {
   uint8_t* scratch;           // multi-source BFS level bytes ([grid][V][lanes]); nullable
   size_t scratch_bytes;
   uint32_t* work;             // [kWorkSlots] dynamic-scheduling counters (zeroed by the launcher)
+  // Source classes (next-hop width): when perm != nullptr this launch solves only the
+  // sources of class `cls`: solve k < part[cls] is sid = perm[part[kMaxClasses + cls] + k]
+  // (part / perm in device memory, built by partition_sources or the host).
+  const uint32_t* perm;
+  const uint32_t* part;       // [2 * kMaxClasses]: counts, then offsets
+  uint32_t cls;
+  uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
 };
-constexpr uint32_t kWorkSlots = 4;  // one counter per kernel launched for one solve call
+constexpr uint32_t kWorkSlots = 16;  // dynamic-scheduling counters: 2 per source class
+constexpr uint32_t kMaxClasses = 8;
+
+// Source classes by distinct degree (next-hop bitset width). Classes 0-3 keep a node's
+// set in one LDS dword; class 4 (> 32 neighbours) solves in ceil(deg / 32) slices of 32
+// next-hop bits each, one slice per workgroup pass.
+enum SrcClass : int { kClsNibble = 0, kClsByte = 1, kClsHalf = 2, kClsWord = 3, kClsSliced = 4, kNumClasses = 5 };
+int src_class_for_degree(uint32_t distinct_degree);  // -1 if > 256
+int nh_mode_of_class(int cls);
+// Stable within a class is not required: perm maps class-local index -> sid.
+hipError_t launch_partition(const uint32_t* d_sources, uint32_t n, const uint8_t* d_node_cls, uint32_t V,
+                            uint32_t* d_part, uint32_t* d_perm, hipStream_t s);
 
 // Bit-parallel multi-source BFS plan (spf_msbfs.hip).
 struct MsPlan {
@@ -82,7 +101,8 @@ hipError_t launch_msbfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, ui
 
 
 // Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels.
-hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode,
+// nh_mode = the class's storage (sliced classes: kNhW1 with a.nsl slices).
+hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, bool sliced,
                       int group_lanes, int num_cus, hipStream_t s, LaunchInfo* info);
 
 // General positive metrics: buckets of width delta = min usable metric (Dial /
@@ -91,7 +111,7 @@ hipError_t launch_bucket(const DevGraph& g, const SolveArgs& a, uint32_t delta, 
                          int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
-uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode);
+uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool sliced);
 uint32_t bucket_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
 

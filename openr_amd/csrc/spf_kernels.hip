@@ -25,6 +25,7 @@
 // stream and the result write (DESIGN.md "Roofline").
 #include "spf_kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "spf_device.h"
@@ -237,6 +238,83 @@ uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus) {
 
 bool nh_mode_single(int mode) {
   return mode == kNhNibble || mode == kNhByte || mode == kNhHalf || mode == kNhW1;
+}
+
+int src_class_for_degree(uint32_t d) {
+  if (d <= 4) return kClsNibble;
+  if (d <= 8) return kClsByte;
+  if (d <= 16) return kClsHalf;
+  if (d <= 32) return kClsWord;
+  if (d <= 256) return kClsSliced;
+  return -1;
+}
+
+int nh_mode_of_class(int cls) {
+  switch (cls) {
+    case kClsNibble: return kNhNibble;
+    case kClsByte: return kNhByte;
+    case kClsHalf: return kNhHalf;
+    default: return kNhW1;  // kClsWord, and each 32-bit slice of kClsSliced
+  }
+}
+
+namespace {
+// Wave-aggregated class histogram / scatter of a source batch (one atomic per class
+// per wave). part = [counts | offsets | cursors], each kMaxClasses u32, zeroed by the
+// launcher.
+__global__ __launch_bounds__(256) void partition_count(const uint32_t* src, uint32_t n, const uint8_t* cls,
+                                                       uint32_t V, uint32_t* part) {
+  for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t u = i < n ? src[i] : V;
+    const uint32_t c = u < V ? cls[u] : 0u;
+    for (uint32_t k = 0; k < (uint32_t)kNumClasses; ++k) {
+      const unsigned long long m = __ballot(i < n && c == k);
+      if (m && __lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) atomicAdd(&part[k], (uint32_t)__popcll(m));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void partition_scatter(const uint32_t* src, uint32_t n, const uint8_t* cls,
+                                                         uint32_t V, uint32_t* part, uint32_t* perm) {
+  __shared__ uint32_t off[kMaxClasses];
+  if (threadIdx.x == 0) {
+    uint32_t o = 0;
+    for (uint32_t k = 0; k < kMaxClasses; ++k) {
+      off[k] = o;
+      o += part[k];
+      if (blockIdx.x == 0) part[kMaxClasses + k] = off[k];
+    }
+  }
+  __syncthreads();
+  const uint32_t lane = __lane_id();
+  for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t u = i < n ? src[i] : V;
+    const uint32_t c = u < V ? cls[u] : 0u;
+    for (uint32_t k = 0; k < (uint32_t)kNumClasses; ++k) {
+      const unsigned long long m = __ballot(i < n && c == k);
+      if (!m) continue;
+      const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+      uint32_t base = 0;
+      if (lane == leader) base = atomicAdd(&part[2u * kMaxClasses + k], (uint32_t)__popcll(m));
+      base = __shfl(base, (int)leader);
+      if (i < n && c == k) perm[off[k] + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+    }
+  }
+}
+}  // namespace
+
+hipError_t launch_partition(const uint32_t* d_sources, uint32_t n, const uint8_t* d_node_cls, uint32_t V,
+                            uint32_t* d_part, uint32_t* d_perm, hipStream_t s) {
+  hipError_t err = hipMemsetAsync(d_part, 0, 3u * kMaxClasses * sizeof(uint32_t), s);
+  if (err != hipSuccess || n == 0) return err;
+  const uint32_t grid = std::min<uint32_t>((n + 255u) / 256u, 1024u);
+  hipLaunchKernelGGL(partition_count, dim3(grid), dim3(256), 0, s, d_sources, n, d_node_cls, V, d_part);
+  err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(partition_scatter, dim3(grid), dim3(256), 0, s, d_sources, n, d_node_cls, V, d_part, d_perm);
+  return hipGetLastError();
 }
 
 int nh_mode_for_bits(uint32_t bits) {

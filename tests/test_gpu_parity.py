@@ -317,3 +317,56 @@ def test_spf_runs_counter(eng):
     before = eng.stats().spf_runs
     eng.solve(range(16), True)
     assert eng.stats().spf_runs - before == 16
+
+
+def hub_graph(seed, V=300, L=700, hub_deg=(40, 75, 130)):
+    """Random unit-metric graph plus hubs of distinct degree 40 / 75 / 130: every source
+    class (nibble .. 32-bit sliced next-hop sets, 2-5 slices) is present in one batch."""
+    g0 = random_graph(seed, V, L, 1, p_ovl=0.05, p_down=0.03, p_par=0.05)
+    rng = np.random.default_rng(seed + 1000)
+    links = []
+    src_of = g0.edge_owner()
+    for e in range(g0.num_dir_edges):  # keep the random graph's links (one direction each)
+        u, v = int(src_of[e]), int(g0.col[e])
+        if u < v:
+            links.append((u, v))
+    for h, d in enumerate(hub_deg):
+        for v in rng.choice(np.arange(len(hub_deg), V), d, replace=False):
+            links.append((h, int(v)))
+    links = np.array(links)
+    m = np.ones(len(links), dtype=np.uint64)
+    ovl = np.zeros(V, dtype=np.uint8)
+    ovl[rng.integers(len(hub_deg), V, 6)] = 1
+    names = [f"h{rng.integers(0, 10**6)}-{i}" for i in range(V)]
+    return T.csr_from_links(names, links, m, m, ovl)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_source_classes_and_sliced_next_hops(eng, seed):
+    g = hub_graph(seed)
+    assert g.max_distinct_degree() > 128  # 5 slices of 32 next-hop bits for the largest hub
+    srcs = list(range(g.num_nodes))
+    check_against_oracle(eng, g, srcs, True)
+    check_against_oracle(eng, g, srcs, False)
+    rng = np.random.default_rng(seed)
+    sub = [0, 1, 2] + rng.integers(3, g.num_nodes, 40).tolist()
+    ignore = [sorted(set(rng.integers(0, g.num_links, int(rng.integers(0, 20))).tolist())) for _ in sub]
+    check_against_oracle(eng, g, sub, True, ignore=ignore)
+
+
+def test_source_classes_device_partition(eng):
+    """solve_device partitions on the GPU: same results as the host-buffer solve."""
+    import torch
+
+    g = hub_graph(3)
+    eng.set_graph(g)
+    srcs = np.random.default_rng(3).permutation(g.num_nodes).astype(np.int32)
+    dist_h, nh_h, _ = eng.solve(srcs.astype(np.uint32), True)
+    dev = torch.device("cuda", 0)
+    d_src = torch.from_numpy(srcs).to(dev)
+    d_dist = torch.empty((len(srcs), g.num_nodes), dtype=torch.int64, device=dev)
+    d_nh = torch.empty((len(srcs), g.num_nodes, eng.nh_bytes), dtype=torch.uint8, device=dev)
+    eng.solve_device(d_src.data_ptr(), len(srcs), d_dist.data_ptr(), d_nh.data_ptr(), eng.nh_bytes, True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_dist.cpu().numpy().view(np.uint64), dist_h)
+    np.testing.assert_array_equal(d_nh.cpu().numpy(), nh_h)
