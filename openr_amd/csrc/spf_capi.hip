@@ -515,7 +515,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   // lanes per frontier node: enough that one pass of kBfsEdgesPerLane edges per lane
   // covers an average row (grid: 1 lane x 4 edges; fabric: 8 lanes x 4 edges)
   const uint32_t avg = V ? (E + V - 1) / V : 1;
-  const uint32_t per_lane = (avg + 4 * kBfsEdgesPerLane - 1) / (4 * kBfsEdgesPerLane);  // fabric: G=2 measured best
+  const uint32_t per_lane = (avg + 2 * kBfsEdgesPerLane - 1) / (2 * kBfsEdgesPerLane);  // fabric: G=4 measured best
   uint32_t gl = 1;
   while (gl < per_lane && gl < 64) gl <<= 1;
   ctx->group_lanes = gl;
