@@ -1,5 +1,7 @@
-// spf_bfs.hip — uniform-cost SPF kernel (every usable edge costs the same c: grids and
-// fabrics with unit metrics, and LinkState::runSpf(useLinkMetric=false) hop counts).
+// spf_bfs.hip — uniform-cost SPF kernel, "code" family (every usable edge costs the same
+// c: grids and fabrics with unit metrics, and runSpf(useLinkMetric=false) hop counts).
+// Chosen for shallow graphs (small diameter, wide frontiers: fabrics); deep graphs use
+// the exact-level family in spf_bfs_lvl.hip (spf_capi.hip picks per graph).
 //
 // Semantics (LinkState::runSpf, /root/reference/openr/decision/LinkState.cpp:808-882,
 // closed form for positive metrics): with uniform cost the
@@ -9,19 +11,34 @@
 // where u->v is tight iff it is usable, u is on level L, v on level L+1, and u may be
 // expanded (u == src or u not overloaded, LinkState.cpp:831-838).
 //
-// Shape: one 256-thread workgroup owns one solve (persistent, dynamically scheduled
-// over the batch). Per solve LDS holds level bytes, next-hop sets and a frontier ring;
-// the CSR mirror is streamed from L2/HBM and shared by every workgroup on the chip.
-// Level L expands ring slots [head, tail): G lanes per frontier node, K edges per lane
-// loaded ahead. An arrival on an edge u->v is tight iff lvl[v] > L; it ORs nh(u) into
-// nh(v) and stores lvl[v] = L+1 (idempotent). The arrival that appends v to the ring is
-// elected by the atomicOr on v's next-hop field (packed modes: the one that saw the
-// field empty) or by a visited bitmap (multi-dword modes). Appends are wave-aggregated
-// (3 ballots + one ds_add per wave per pass). One barrier per level.
+// Per-node state in LDS is ONE packed field: [next-hop bits | 3-bit level code].
+// code 0 = not reached, code (L % 3) + 1 = reached on level L, code | 4 = a sink
+// (overloaded, never expanded) already settled. With unit steps every EXPANDED
+// neighbour of a level-L node sits on level L-1, L or L+1, so the code alone tells a
+// tight arrival (v unreached, or reached on L+1 this level) from a stale one; a sink
+// can sit further back and is marked when popped so it never aliases. Levels are
+// never stored, so BFS depth is unbounded. One atomicOr per tight edge ORs nh(u)
+// and the code of L+1 into v's field; the arrival that saw code 0 appends v to the
+// frontier ring (no visited bitmap, no level array). dist(v) = c * L is stored to HBM
+// when v is expanded (scattered 8-byte stores, merged in L2); unreached nodes get
+// UINT64_MAX and every node its next-hop bytes in one coalesced pass at the end.
+//
+// Shape: one workgroup (128 or 256 threads) owns one solve at a time, dynamically
+// scheduled over the batch. Level L expands ring slots [head, tail): G lanes per
+// frontier node, K=4 edges per lane loaded ahead (one 16-byte ELL load when every row
+// has <= 4 edges); the K field reads and then the K atomics of a lane are issued
+// together; appends are wave-aggregated (3 ballots + one ds_add per wave). One LDS
+// barrier per level.
+//
+// Field widths by source class (distinct degree d of the source = next-hop set width):
+//   8 bits (d <= 5), 16 bits (d <= 13), 32 bits (d <= 24), and 32-bit fields holding
+//   24-bit slices of the set for d > 24 (one workgroup pass per (solve, slice)).
 //
 // No MFMA: min-plus relaxation is not a matrix contraction (DESIGN.md "Roofline").
+#include <algorithm>
 #include <cstdlib>
 
+#include "spf_bfs_common.h"
 #include "spf_device.h"
 #include "spf_kernels.h"
 
@@ -29,27 +46,44 @@ namespace openr_spf {
 
 namespace {
 using namespace dev;
+using namespace bfs;
 
-template <typename LT>
+// Packed node state: FB-bit fields, next-hop bits at kNhs, level code in bits [0, 3).
+template <int FB>
+struct State {
+  static constexpr uint32_t kPer = 32u / FB;
+  static constexpr uint32_t kFieldMask = FB == 32 ? 0xFFFFFFFFu : ((1u << (FB & 31)) - 1u);
+  static constexpr uint32_t kNhs = FB == 32 ? 8u : 3u;  // next-hop bits start here
+  static constexpr uint32_t kNhBits = FB - kNhs;         // 5 / 13 / 24
+  static constexpr uint32_t kNhMask = ((1u << kNhBits) - 1u) << kNhs;
+  static __host__ __device__ uint32_t words(uint32_t V) { return (V + kPer - 1u) / kPer; }
+  static __device__ __forceinline__ uint32_t word(uint32_t v) { return v / kPer; }
+  static __device__ __forceinline__ uint32_t shift(uint32_t v) { return (v % kPer) * FB; }
+  static __device__ __forceinline__ uint32_t field(const uint32_t* st, uint32_t v) {
+    return (st[word(v)] >> shift(v)) & kFieldMask;
+  }
+};
+
+__device__ __forceinline__ uint32_t level_code(uint32_t L) { return L % 3u + 1u; }
+constexpr uint32_t kCodeMask = 7u, kCodeSettledSink = 4u;
+
+
 struct BfsLayout {
-  uint32_t lvl, vis, nh, ring, ign, dummy, total;
+  uint32_t st, ring, ign, dummy, total;
 };
 
 // ring = frontier queue (power of two, wraps) in the fast path, or the full BFS-order
 // array (capacity V, never wraps) in the fallback path.
-template <typename LT>
-__host__ __device__ inline BfsLayout<LT> bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
-                                                    bool need_vis, uint32_t ring_cap) {
-  BfsLayout<LT> l;
-  uint32_t off = 16;  // control: append counters [0..2], overflow flag [3]
+__host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t fb, uint32_t ring_cap) {
+  BfsLayout l;
+  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4]
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
     return o;
   };
-  l.lvl = take((uint32_t)sizeof(LT) * (V + 4u));
-  l.vis = need_vis ? take(4u * ((V + 31u) / 32u)) : 0u;
-  l.nh = take(4u * nh_words);
+  const uint32_t per = 32u / fb;
+  l.st = take(4u * ((V + per - 1u) / per));
   l.ring = take(2u * ring_cap);
   l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
   l.dummy = take(4u * 64u);  // per-lane sink for the no-op atomics of non-tight edges
@@ -57,157 +91,109 @@ __host__ __device__ inline BfsLayout<LT> bfs_layout(uint32_t V, uint32_t L, bool
   return l;
 }
 
-template <typename LT>
-struct LvlOps;
-template <>
-struct LvlOps<uint8_t> {
-  static constexpr uint32_t kUnset = 0xFFu;
-};
-template <>
-struct LvlOps<uint16_t> {
-  static constexpr uint32_t kUnset = 0xFFFFu;
-};
-
-// Writes this solve's dist row (u64) and next-hop row from LDS, coalesced.
-template <typename T>
-__device__ __forceinline__ void store_row(T* p, const T& x, bool nt) {
-  if (nt)
-    __builtin_nontemporal_store(x, p);  // streamed result rows: keep the CSR resident in L2
-  else
-    *p = x;
-}
-
-// Sliced classes: slice s owns next-hop bytes [4s, 4s + 4); slice 0 also writes the
-// distance row and zero-fills the bytes past the last slice.
-template <int MODE, typename LT, bool SLICED>
-__device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
-                                           const LT* lvl, const uint32_t* nh, uint64_t cost, bool nt) {
-  using N = Nh<MODE>;
-  using O = LvlOps<LT>;
+// End of a solve: UINT64_MAX for unreached nodes (reached ones were stored when
+// expanded) and the next-hop bytes of every node, coalesced. Sliced classes: slice s
+// owns next-hop bytes [3s, 3s + 3); slice 0 also zero-fills the bytes past the last
+// slice.
+template <int FB, int BLOCK, bool SLICED>
+__device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
+                                          const uint32_t* st, bool nt) {
+  using S = State<FB>;
   const uint32_t tid = threadIdx.x;
-  if (SLICED) {
-    if (a.nh) {
-      const uint32_t nb = a.nh_bytes, j0 = 4u * slice, zero0 = 4u * a.nsl;
-      uint8_t* nrow = a.nh + (size_t)sid * V * nb;
-      for (uint32_t v = tid; v < V; v += kBlock) {
-        const uint32_t w = nh[v];
-        uint8_t* o = nrow + (size_t)v * nb;
-#pragma unroll
-        for (uint32_t jj = 0; jj < 4u; ++jj)
-          if (j0 + jj < nb) o[j0 + jj] = (uint8_t)(w >> (8u * jj));
-        if (slice == 0)
-          for (uint32_t j = zero0; j < nb; ++j) o[j] = 0;
-      }
-    }
-    if (slice != 0) return;
-  }
   uint64_t* drow = a.dist + (size_t)sid * V;
-  if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
-    // two nodes per lane: 16-byte stores
-    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
-    for (uint32_t i = tid; i < V / 2u; i += kBlock) {
-      const uint32_t l0 = lvl[2u * i], l1 = lvl[2u * i + 1u];
-      const uint64_t x0 = l0 != O::kUnset ? (uint64_t)l0 * cost : ~0ull;
-      const uint64_t x1 = l1 != O::kUnset ? (uint64_t)l1 * cost : ~0ull;
-      if (nt) {
-        __builtin_nontemporal_store(x0, &d2[i].x);
-        __builtin_nontemporal_store(x1, &d2[i].y);
-      } else {
-        d2[i] = make_ulonglong2(x0, x1);
-      }
-    }
-  } else {
-    for (uint32_t v = tid; v < V; v += kBlock) {
-      const uint32_t l = lvl[v];
-      store_row<uint64_t>(&drow[v], l != O::kUnset ? (uint64_t)l * cost : ~0ull, nt);
-    }
-  }
-  if (SLICED || !a.nh) return;
   const uint32_t nb = a.nh_bytes;
-  uint8_t* nrow = a.nh + (size_t)sid * V * nb;
-  const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
-  if (MODE == kNhNibble && nb == 1 && aligned4) {
-    // four nodes (four nibbles of one half-dword) per lane -> one u32 of four bytes
-    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
-    for (uint32_t i = tid; i < V / 4u; i += kBlock) {
-      const uint32_t h = (nh[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
-      store_row<uint32_t>(&nrow32[i], (h & 0xFu) | ((h & 0xF0u) << 4) | ((h & 0xF00u) << 8) | ((h & 0xF000u) << 12), nt);
+  uint8_t* nrow = a.nh ? a.nh + (size_t)sid * V * nb : nullptr;
+  if (!SLICED || slice == 0)
+    for (uint32_t v = tid; v < V; v += BLOCK)
+      if ((S::field(st, v) & kCodeMask) == 0u) drow[v] = ~0ull;
+  if (!nrow) return;
+  if (SLICED) {
+    const uint32_t j0 = 3u * slice, zero0 = 3u * a.nsl;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+      const uint32_t x = S::field(st, v) >> S::kNhs;
+      uint8_t* o = nrow + (size_t)v * nb;
+#pragma unroll
+      for (uint32_t jj = 0; jj < 3u; ++jj)
+        if (j0 + jj < nb) o[j0 + jj] = (uint8_t)(x >> (8u * jj));
+      if (slice == 0)
+        for (uint32_t j = zero0; j < nb; ++j) o[j] = 0;
     }
-  } else if (MODE == kNhByte && nb == 1 && aligned4) {
-    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
-    for (uint32_t i = tid; i < V / 4u; i += kBlock) store_row<uint32_t>(&nrow32[i], nh[i], nt);
-  } else {
-    const uint32_t total = V * nb;
-    for (uint32_t i = tid; i < total; i += kBlock) {
-      const uint32_t v = i / nb, j = i - v * nb;
-      nrow[i] = (uint8_t)N::byte(nh, v, j);
-    }
+    return;
+  }
+  if (FB == 8 && nb == 1 && ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0) {
+    // four nodes (one state dword) per lane -> one u32 of four next-hop bytes
+    uint32_t* n32 = reinterpret_cast<uint32_t*>(nrow);
+    for (uint32_t i = tid; i < V / 4u; i += BLOCK) store_row<uint32_t>(&n32[i], (st[i] >> 3) & 0x1F1F1F1Fu, nt);
+    return;
+  }
+  for (uint32_t i = tid; i < V * nb; i += BLOCK) {
+    const uint32_t v = i / nb, j = i - v * nb;
+    const uint32_t x = S::field(st, v) >> S::kNhs;
+    nrow[i] = j < 4u ? (uint8_t)(x >> (8u * j)) : (uint8_t)0;
   }
 }
 
 // ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
 // the rest from CSR (G == 1); 2 = ELL only (every row has <= 4 edges, no ignore set,
 // no tight-edge output).
-// RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent levels
-//               exceed the ring, or whose depth exceeds 253, sets ovf[sid] for a re-run.
-// RING = false: LT = u16, queue = full BFS order (capacity V).
+// RING = true : queue = power-of-two ring; a solve whose two adjacent levels exceed
+//               the ring gets ovf[sid] = rerun + 1 for the re-run, else ovf[sid] = 0.
+// RING = false: full BFS order (capacity V) — the re-run of flagged solves.
 // rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
-// SLICED: one unit = (solve, 32-bit slice of the next-hop set); arrivals are elected
-// by the visited bitmap (a slice of nh(u) may be empty).
-template <int MODE, int K, typename LT, bool RING, int ELLM, bool GENERIC, bool SLICED>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void bfs_kernel(
+// SLICED: one unit = (solve, 24-bit slice of the next-hop set).
+// GENERIC = false: no ignore set and no tight-edge output (compile time), the
+// all-sources / prefetch case; GENERIC = true handles both at run time.
+template <int FB, int BLOCK, bool RING, int ELLM, bool GENERIC, bool SLICED>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_code_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
-    uint32_t work_slot, uint32_t nt) {
-  // GENERIC = false: no ignore set and no tight-edge output (compile time), the
-  // all-sources / prefetch case; GENERIC = true handles both at run time.
-  constexpr bool ELECT = Nh<MODE>::kSingle && !SLICED;
+    uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+  using S = State<FB>;
+  constexpr int K = (int)kBfsEdgesPerLane;
   const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_next;
-  using N = Nh<MODE>;
-  using O = LvlOps<LT>;
-  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6;
-  const uint32_t nh_words = N::words(V);
-  const BfsLayout<LT> lay = bfs_layout<LT>(V, g.L, has_ign, nh_words, !ELECT, ring_cap);
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const BfsLayout lay = bfs_layout(V, g.L, has_ign, FB, ring_cap);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
-  LT* lvl = reinterpret_cast<LT*>(base + lay.lvl);
-  uint32_t* lvl_w = reinterpret_cast<uint32_t*>(base + lay.lvl);
-  uint32_t* vis = reinterpret_cast<uint32_t*>(base + lay.vis);
-  uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
+  uint32_t* st = reinterpret_cast<uint32_t*>(base + lay.st);
   uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
   uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
-  const uint32_t lane = __lane_id();
-  const uint32_t bit_words = (V + 31u) / 32u;
-  const uint32_t lvl_words = ((uint32_t)sizeof(LT) * (V + 4u)) / 4u;
+  const uint32_t st_words = S::words(V);
   const uint32_t ign_words = (g.L + 31u) / 32u;
-  const uint32_t G = 1u << glog, ngroups = kBlock >> glog, groups_per_wave = 64u >> glog;
+  const uint32_t G = 1u << glog, ngroups = BLOCK >> glog, groups_per_wave = 64u >> glog;
   const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
   const uint32_t tight_words = (g.E + 63u) / 64u;
   const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
-  uint32_t* work = a.work + work_slot;
   const uint32_t nsl = SLICED ? a.nsl : 1u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
-  const uint32_t units = count * nsl;
+  // a re-run launch with nothing flagged does no work
+  const uint32_t units = (rerun && RING == false && *ovf_count == 0u) ? 0u : count * nsl;
+#ifdef OPENR_SPF_PROFILE
+  // [0] load (ring + ELL/row), [1] field reads, [2] atomics, [3] append, [4] barrier,
+  // [5] init + level 0, [6] write out, [7] passes, [8] levels, [9] solves
+  uint64_t pc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+#endif
 
   for (uint32_t unit = blockIdx.x; unit < units;) {
     const uint32_t k = SLICED ? unit / nsl : unit, slice = SLICED ? unit - k * nsl : 0u;
     const uint32_t sid = a.perm ? a.perm[first + k] : k;
     const uint32_t src = a.sources[sid];
     if (src < V && !(rerun && a.ovf[sid] != rerun)) {  // block-uniform
-      for (uint32_t i = tid; i < lvl_words; i += kBlock) lvl_w[i] = 0xFFFFFFFFu;
-      if (!ELECT)
-        for (uint32_t i = tid; i < bit_words; i += kBlock) vis[i] = 0;
-      for (uint32_t i = tid; i < nh_words; i += kBlock) nh[i] = 0;
+      OPENR_PROF_STAMP(t0);
+      const bool own_dist = !SLICED || slice == 0;
+      uint64_t* drow = a.dist + (size_t)sid * V;
+      for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
       if (has_ign)
-        for (uint32_t i = tid; i < ign_words; i += kBlock) ign[i] = 0;
-      if (tid < 4) ctl[tid] = 0;
+        for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
+      if (tid < 8) ctl[tid] = 0;
       __syncthreads();
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
-        lvl[src] = 0;
-        if (!ELECT) vis[src >> 5] = 1u << (src & 31u);
+        atomicOr(&st[S::word(src)], level_code(0) << S::shift(src));
+        if (own_dist) drow[src] = 0;
       }
       __syncthreads();
       uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
@@ -216,7 +202,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
       // node's next hop is the node itself (LinkState.cpp:867-872)
       {
         const uint2 rs = g.row2[src];
-        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += kBlock) {
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
           const uint32_t e = e0 + tid;
           bool fresh = false;
           uint32_t v = 0;
@@ -224,54 +210,66 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
             const uint32_t av = g.adj[e];
             v = av & ~kEdgeDown;
             if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e])) && v != src) {
-              if constexpr (ELECT) {
-                fresh = N::fetch_or_bit(nh, v, g.nbr[e]) == 0u;
-              } else {
-                const uint32_t bit = 1u << (v & 31u);
-                fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
-                const uint32_t b = g.nbr[e];
-                if (!SLICED) N::or_bit(nh, v, b);
-                else if ((b >> 5) == slice) N::or_bit(nh, v, b & 31u);
-              }
-              lvl[v] = (LT)1;
+              const uint32_t b = g.nbr[e];
+              uint32_t nhb = 0;
+              if (!SLICED) nhb = 1u << b;
+              else if (b / S::kNhBits == slice) nhb = 1u << (b - slice * S::kNhBits);
+              const uint32_t x = (nhb << S::kNhs) | level_code(1);
+              fresh = ((atomicOr(&st[S::word(v)], x << S::shift(v)) >> S::shift(v)) & kCodeMask) == 0u;
               if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
             }
           }
-          // level-0 appends count in ctl[0]; level L >= 1 uses ctl[L % 3] (ctl[1] first)
+          // level-0 appends count in ctl[0]; level L >= 1 uses ctl[L & 3]
           const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
           if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap checked by the host
         }
       }
       __syncthreads();
+#ifdef OPENR_SPF_PROFILE
+      OPENR_PROF_STAMP(t1);
+      OPENR_PROF_ADD(5, t0, t1);
+      pc[9] += 1;
+#endif
 
-      uint32_t head = 1, tail = 1u + ctl[0], L = 1;
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2);
       bool overflow = false;  // block-uniform
       while (head < tail) {
-        if (RING && L + 1u >= O::kUnset) {  // next level not representable in u8
-          overflow = true;
-          break;
-        }
-        uint32_t* cnt = &ctl[L % 3u];
-        if (tid == 0) ctl[(L + 1u) % 3u] = 0;  // last read two barriers ago
+        uint32_t* cnt = &ctl[L & 3u];
+        if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
+        const uint64_t dL = (uint64_t)L * cost;
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
           if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
+          OPENR_PROF_STAMP(t0);
           const uint32_t idx = fb + group;
           const bool live = idx < tail;
           uint32_t u = 0, beg = 0, end = 0;
           uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
           if (live) {
             u = ring[RING ? (idx & rmask) : idx];
+            bool sink;
             if (ELLM == 2) {
               ell = g.ellt[u];
+              sink = (ell.x & kNodeSink) != 0u;
             } else {
-              const uint2 r = g.row2t[u];  // empty for overloaded nodes (sinks)
+              const uint2 r = g.row2t[u];  // empty (beg flagged kNodeSink) for overloaded nodes
               beg = r.x;
               end = r.y;
+              sink = (beg & kNodeSink) != 0u;
               if (ELLM == 1) ell = g.ellt[u];
+            }
+            if (lane_g == 0) {
+              if (own_dist) drow[u] = dL;  // u settled on level L
+              if (sink) atomicOr(&st[S::word(u)], kCodeSettledSink << S::shift(u));
             }
           }
           if (ELLM == 2 && live) end = 4;  // kEdgeDown-padded ELL slots stand for the row end
-          const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
+          // nh(u) (final: u was reached a level ago) + the code of level L+1
+          const uint32_t xu = (S::field(st, u) & S::kNhMask) | cnext;
+#ifdef OPENR_SPF_PROFILE
+          OPENR_PROF_STAMP(t1);
+          OPENR_PROF_ADD(0, t0, t1);
+          pc[7] += 1;
+#endif
           for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; __any(e0 < end); e0 += G * K) {
             uint32_t av[K], lv[K];
 #pragma unroll
@@ -286,48 +284,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
               }
               lv[j] = (has_ign && e < end) ? g.lid[e] : 0u;
             }
-            // (1) tight test: the K level reads are issued together (no branches)
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t1);
+#endif
+            // (1) tight test: the K field reads are issued together (every vv[j] is a
+            //     valid node id, padding included, so no address select is needed)
             bool tight[K];
             uint32_t vv[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j * G;
-              vv[j] = av[j] & ~kEdgeDown;
+              vv[j] = av[j] & ~(kEdgeDown | kNodeSink);  // always a valid node id
               const bool ok = !(av[j] & kEdgeDown) && (ELLM == 2 || e < end) && !(has_ign && test_bit(ign, lv[j]));
-              const uint32_t l = lvl[ok ? vv[j] : V];  // lvl[V] is padding
-              tight[j] = ok && l > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
+              const uint32_t c = S::field(st, vv[j]) & kCodeMask;
+              tight[j] = ok && (c == 0u || c == cnext);  // first or equal-cost arrival (LinkState.cpp:857-873)
             }
-            // (2) addNextHops(nh(u)) + election of the appending arrival: K atomics in
-            //     flight together; non-tight edges OR 0 into the lane's own dummy word
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t2);
+            OPENR_PROF_ADD(1, t1, t2);
+#endif
+            // (2) addNextHops(nh(u)) + level code + election of the appending arrival:
+            //     K atomics in flight together; non-tight edges OR 0 into the lane's
+            //     own dummy word
+            uint32_t old[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              old[j] = atomicOr(tight[j] ? &st[S::word(vv[j])] : &dummy[lane], tight[j] ? xu << S::shift(vv[j]) : 0u);
             uint32_t fresh_mask = 0;
-            if constexpr (ELECT) {
-              const uint32_t x = nhu.x;
-              uint32_t old[K];
-#pragma unroll
-              for (int j = 0; j < K; ++j)
-                old[j] = atomicOr(tight[j] ? &nh[N::word(vv[j])] : &dummy[lane], tight[j] ? x << N::shift(vv[j]) : 0u);
-#pragma unroll
-              for (int j = 0; j < K; ++j)
-                fresh_mask |= (tight[j] && ((old[j] >> N::shift(vv[j])) & N::kMask) == 0u) ? (1u << j) : 0u;
-            } else {
-              uint32_t old[K];
-#pragma unroll
-              for (int j = 0; j < K; ++j)
-                old[j] = atomicOr(tight[j] ? &vis[vv[j] >> 5] : &dummy[lane], tight[j] ? 1u << (vv[j] & 31u) : 0u);
-#pragma unroll
-              for (int j = 0; j < K; ++j) {
-                fresh_mask |= (tight[j] && !((old[j] >> (vv[j] & 31u)) & 1u)) ? (1u << j) : 0u;
-                if (tight[j]) N::or_val(nh, vv[j], nhu);
-              }
-            }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-              if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              fresh_mask |= (tight[j] && ((old[j] >> S::shift(vv[j])) & kCodeMask) == 0u) ? (1u << j) : 0u;
               if (trow && tight[j]) {
                 const uint32_t e = e0 + j * G;
                 atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
               }
             }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t3);
+            OPENR_PROF_ADD(2, t2, t3);
+#endif
             // (3) wave-aggregated append: 3 ballots + one ds_add per wave
             uint32_t total;
             uint32_t slot = wave_prefix_small((uint32_t)__popc(fresh_mask), &total);
@@ -350,138 +345,166 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                   ++slot;
                 }
               }
-              if (RING && __any(lost) && (int)lane == leader) ctl[3] = 1;
+              if (RING && __any(lost) && (int)lane == leader) ctl[4] = 1;
             }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t4);
+            OPENR_PROF_ADD(3, t3, t4);
+#endif
           }
         }
-        __syncthreads();
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t0);
+#endif
+        lds_barrier();
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t1);
+        OPENR_PROF_ADD(4, t0, t1);
+        pc[8] += 1;
+#endif
         head = tail;
         tail += *cnt;
         ++L;
-        if (RING && ctl[3]) {  // ring overflow; ctl[3] is uniform after the barrier
+        cnext = cnext == 3u ? 1u : cnext + 1u;
+        if (RING && ctl[4]) {  // ring overflow; ctl[4] is uniform after the barrier
           overflow = true;
           break;
         }
       }
-      if (RING && overflow) {  // re-run by the u16 / full-order variant
-        if (tid == 0) a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
+      if (RING && overflow) {  // re-run by the full-order variant
+        if (tid == 0) {
+          a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
+          if (!SLICED || slice == 0) atomicAdd(ovf_count, 1u);
+        }
       } else {
-        write_rows<MODE, LT, SLICED>(a, sid, slice, V, lvl, nh, cost, nt != 0);
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t0);
+#endif
+        if (RING && tid == 0 && (!SLICED || slice == 0)) a.ovf[sid] = 0;
+        write_out<FB, BLOCK, SLICED>(a, sid, slice, V, st, nt != 0);
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t1);
+        OPENR_PROF_ADD(6, t0, t1);
+#endif
       }
     }
     // next unit: dynamic scheduling (the first gridDim.x units are static)
     __syncthreads();  // every lane is done with this unit's LDS and s_next
-    if (tid == 0) s_next = gridDim.x + atomicAdd(work, 1u);
+    if (tid == 0) s_next = gridDim.x + atomicAdd(&ctr[0], 1u);
     __syncthreads();
     unit = s_next;
   }
+  // the re-run consumed the flags of its class: its last workgroup clears the count
+  retire_workgroup(ctr, (!RING && rerun) ? ovf_count : nullptr);
+#ifdef OPENR_SPF_PROFILE
+  if (lane == 0 && a.prof)
+    for (int i = 0; i < 10; ++i) atomicAdd(&a.prof[i], (unsigned long long)pc[i]);
+#endif
 }
 
-// Fast path: u8 levels + a ring sized so that target workgroups fit a CU.
-// It cannot be used when its ring would be smaller than 256 entries (or than a row);
-// then the full-order u16 variant runs directly.
-uint32_t target_wgs() {
-  if (const char* e = std::getenv("OPENR_SPF_BFS_WGS")) {  // tuning
-    const int v = std::atoi(e);
-    if (v >= 1 && v <= 16) return (uint32_t)v;
-  }
-  return kBfsTargetWgs;
-}
+struct BfsShape {
+  uint32_t block = 256, ring_cap = 0, per_cu = 1;
+};
 
-// Result rows are written once and read by the host / the next consumer, never by this
-// kernel: non-temporal stores keep them from evicting the CSR mirror out of L2.
-uint32_t nt_stores() {
-  if (const char* e = std::getenv("OPENR_SPF_NT")) return e[0] == '1' ? 1u : 0u;  // tuning
-  return 1u;
-}
-
-uint32_t fast_ring_cap(const DevGraph& g, bool has_ign, int mode, bool sliced) {
-  if (const char* e = std::getenv("OPENR_SPF_BFS_FULL"))  // tuning: force the full-order variant
-    if (e[0] == '1') return 0;
-  const bool vis = sliced || !nh_mode_single(mode);
-  const uint32_t fixed = bfs_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), vis, 0).total;
-  const uint32_t budget = kMaxLds / target_wgs();
-  if (fixed >= budget) {
-    // fewer workgroups per CU: the largest power-of-two ring that still fits one
+// Pick the block size and ring: as many solves per CU as LDS allows (<= 32 waves);
+// 128-thread workgroups when more than 8 solves fit. ring_cap == 0: no fast ring fits,
+// the full-order variant runs alone.
+BfsShape bfs_shape(const DevGraph& g, bool has_ign, uint32_t fb) {
+  BfsShape sh;
+  const uint32_t fixed = bfs_layout(g.V, g.L, has_ign, fb, 0).total;
+  const uint32_t min_cap = std::max<uint32_t>(256u, g.max_deg + 2u);
+  for (uint32_t want = env_u32("OPENR_SPF_BFS_WGS", 16u, 1u, 16u); want >= 1; --want) {
+    const uint32_t budget = kMaxLds / want;
+    if (budget <= fixed) continue;
     uint32_t cap = 1;
-    while (fixed + cap * 4u <= kMaxLds && cap < 4096u) cap *= 2u;
-    return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
+    while (cap * 2u <= (budget - fixed) / 2u && cap < 4096u) cap *= 2u;
+    if (cap >= min_cap) {
+      sh.ring_cap = cap;
+      sh.per_cu = want;
+      break;
+    }
   }
-  uint32_t cap = 1;
-  while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
-  return (cap >= 256u && cap > g.max_deg + 1u) ? cap : 0u;
+  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u)) sh.ring_cap = 0;
+  const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
+  sh.block = blk == 128u || blk == 256u ? blk : (sh.per_cu > 8u ? 128u : 256u);
+  return sh;
 }
 
-template <int MODE, typename LT, bool RING, int ELLM, bool SLICED>
+template <int FB, int BLOCK, bool RING, int ELLM, bool SLICED>
 hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                              uint32_t ring_cap, uint32_t rerun, uint32_t work_slot, int num_cus, hipStream_t s,
-                              LaunchInfo* info) {
-  constexpr int K = (int)kBfsEdgesPerLane;
-  const bool vis = SLICED || !Nh<MODE>::kSingle;
-  const uint32_t lds = bfs_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
-  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus);
+                              uint32_t ring_cap, uint32_t rerun, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
+                              hipStream_t s, LaunchInfo* info) {
+  const uint32_t lds = bfs_layout(g.V, g.L, has_ign, FB, ring_cap).total;
+  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
   const bool generic = has_ign || a.tight != nullptr;
-  auto k = generic ? bfs_kernel<MODE, K, LT, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
-                   : bfs_kernel<MODE, K, LT, RING, ELLM, false, SLICED>;
+  auto k = generic ? bfs_code_kernel<FB, BLOCK, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
+                   : bfs_code_kernel<FB, BLOCK, RING, ELLM, false, SLICED>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
   if (info && !rerun) {
     info->lds_bytes = lds;
     info->grid = grid;
-    info->kernel = RING ? "bfs_kernel<ring,u8>" : "bfs_kernel<full,u16>";
+    info->kernel = RING ? "bfs_code_kernel<ring>" : "bfs_code_kernel<full>";
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun,
-                     work_slot, nt_stores());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun, ctr,
+                     ovf_count, nt_stores());
   return hipGetLastError();
 }
 
-template <int MODE, int ELLM, bool SLICED>
-hipError_t launch_bfs_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                           uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
-  // ring/u8 variant first (or as the re-run of flagged multi-source batches); solves it
-  // flags are re-run by the full-order u16 variant on the same stream
-  const uint32_t slot = 2u * a.cls;
-  const uint32_t cap = fast_ring_cap(g, has_ign, MODE, SLICED);
-  if (!cap)
-    return launch_bfs_variant<MODE, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun, slot,
-                                                                   num_cus, s, info);
-  const bool may_overflow = g.V > cap || g.V > 254u;
-  hipError_t err = launch_bfs_variant<MODE, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, cap, first_rerun,
-                                                                         slot, num_cus, s, info);
-  if (err != hipSuccess || !may_overflow) return err;
-  return launch_bfs_variant<MODE, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u,
-                                                                 slot + 1u, num_cus, s, info);
+template <int FB, int BLOCK, int ELLM, bool SLICED>
+hipError_t launch_bfs_shape(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                            uint32_t ring_cap, uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // ring variant first; the solves it flags are re-run by the full-order variant.
+  // Counter block of the class: [0,1] fast launch, [2,3] re-run launch, [4] flagged.
+  uint32_t* blk = class_counters(a);
+  if (!ring_cap)
+    return launch_bfs_variant<FB, 256, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun, blk,
+                                                            blk + 4, num_cus, s, info);
+  hipError_t err = launch_bfs_variant<FB, BLOCK, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, first_rerun,
+                                                                     blk, blk + 4, num_cus, s, info);
+  if (err != hipSuccess || g.V <= ring_cap) return err;
+  return launch_bfs_variant<FB, 256, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u, blk + 2,
+                                                          blk + 4, num_cus, s, info);
 }
 
-template <int MODE, bool SLICED>
-hipError_t launch_bfs_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                          uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
-  if (ellm == 2) return launch_bfs_mode<MODE, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-  if (ellm == 1) return launch_bfs_mode<MODE, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-  return launch_bfs_mode<MODE, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+template <int FB, bool SLICED>
+hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                         uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
+  const BfsShape sh = bfs_shape(g, has_ign, FB);
+#define OPENR_BFS_SHAPE(BLK, E)                                                                                 \
+  return launch_bfs_shape<FB, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, first_rerun, num_cus, s, \
+                                              info)
+  if (sh.block == 128) {
+    if (ellm == 2) OPENR_BFS_SHAPE(128, 2);
+    if (ellm == 1) OPENR_BFS_SHAPE(128, 1);
+    OPENR_BFS_SHAPE(128, 0);
+  }
+  if (ellm == 2) OPENR_BFS_SHAPE(256, 2);
+  if (ellm == 1) OPENR_BFS_SHAPE(256, 1);
+  OPENR_BFS_SHAPE(256, 0);
+#undef OPENR_BFS_SHAPE
 }
+
+uint32_t field_bits(int cls) { return cls == kCls8 ? 8u : cls == kCls16 ? 16u : 32u; }
 }  // namespace
 
-uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool sliced) {
-  // the full-order u16 variant must fit (it re-runs solves the fast path flags)
-  if (V > 65535u) return 0;
-  const bool vis = sliced || !nh_mode_single(nh_mode);
-  uint32_t t = bfs_layout<uint16_t>(V, L, has_ignore, nh_words_for(nh_mode, V), vis, V).total;
+uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls) {
+  // the full-order variant must fit (it re-runs solves the fast path flags)
+  if (V > 65535u || cls < 0 || cls >= kNumClasses) return 0;
+  const uint32_t t = bfs_layout(V, L, has_ignore, field_bits(cls), V).total;
   return t <= kMaxLds ? t : 0;
 }
 
-hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, bool sliced,
-                      int group_lanes, int num_cus, hipStream_t s, LaunchInfo* info) {
+hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
+                           hipStream_t s, LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
-  if (!bfs_lds_bytes(g.V, g.L, has_ign, nh_mode, sliced)) return hipErrorInvalidValue;
-  if (sliced && (nh_mode != kNhW1 || a.nsl < 1u || a.nsl > 8u)) return hipErrorInvalidValue;
+  const int cls = (int)a.cls;
+  if (!bfs_code_lds_bytes(g.V, g.L, has_ign, cls)) return hipErrorInvalidValue;
+  const bool sliced = cls == kClsSliced;
+  if (sliced && (a.nsl < 1u || a.nsl > 11u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  if (!a.ovf || !a.work || a.cls >= kMaxClasses) return hipErrorInvalidValue;
-  hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
-  if (err != hipSuccess) return err;
-  err = hipMemsetAsync(a.work + 2u * a.cls, 0, 2u * sizeof(uint32_t), s);
-  if (err != hipSuccess) return err;
+  if (!a.ovf || !a.work) return hipErrorInvalidValue;
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
@@ -491,19 +514,20 @@ hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int 
   uint32_t first_rerun = 0;
   const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
   if (!a.perm && !sliced && ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
+    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
+    if (err != hipSuccess) return err;
     err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
                        info);
     if (err != hipSuccess) return err;
     first_rerun = 1;
   }
-  if (sliced) return launch_bfs_ell<kNhW1, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-  switch (nh_mode) {
-    case kNhNibble: return launch_bfs_ell<kNhNibble, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case kNhByte: return launch_bfs_ell<kNhByte, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case kNhHalf: return launch_bfs_ell<kNhHalf, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case kNhW1: return launch_bfs_ell<kNhW1, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+  switch (field_bits(cls)) {
+    case 8: return launch_bfs_fb<8, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    default:
+      if (sliced) return launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+      return launch_bfs_fb<32, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
   }
-  return hipErrorInvalidValue;
 }
 
 }  // namespace openr_spf

@@ -1,0 +1,77 @@
+// spf_bfs_common.h — helpers shared by the two uniform-cost BFS kernel families
+// (spf_bfs.hip: packed level-code state; spf_bfs_lvl.hip: exact level bytes).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdlib>
+
+#include "spf_kernels.h"
+
+// Profiling build (make prof): per-phase cycle counters of the level loop. Every stamp
+// drains outstanding memory ops first, so a phase is charged for what it waited on.
+#ifdef OPENR_SPF_PROFILE
+#define OPENR_PROF_STAMP(var)                                   \
+  do {                                                          \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    var = clock64();                                            \
+  } while (0)
+#define OPENR_PROF_ADD(i, a, b) pc[i] += (uint64_t)((b) - (a))
+#else
+#define OPENR_PROF_STAMP(var) \
+  do {                        \
+  } while (0)
+#define OPENR_PROF_ADD(i, a, b) \
+  do {                          \
+  } while (0)
+#endif
+
+namespace openr_spf {
+namespace bfs {
+
+template <typename T>
+__device__ __forceinline__ void store_row(T* p, const T& x, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(x, p);  // streamed result rows: keep the CSR resident in L2
+  else
+    *p = x;
+}
+
+// Workgroup barrier for LDS only: global stores issued during a level stay in flight
+// across it (__syncthreads()' release fence would drain them every level).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Per-launch device counters: [0] next unit (dynamic scheduling), [1] finished
+// workgroups. The last workgroup to finish zeroes both (and `also_zero`), so every
+// launch finds its counters zero without a memset.
+__device__ __forceinline__ void retire_workgroup(uint32_t* ctr, uint32_t* also_zero) {
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&ctr[1], 1u) == gridDim.x - 1u) {
+      ctr[0] = 0;
+      ctr[1] = 0;
+      if (also_zero) *also_zero = 0;
+      __threadfence();
+    }
+  }
+}
+
+inline uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+  if (const char* e = std::getenv(name)) {  // tuning knobs (benchmarks only)
+    const long v = std::atol(e);
+    if (v >= (long)lo && v <= (long)hi) return (uint32_t)v;
+  }
+  return dflt;
+}
+
+// Result rows are written once and read by the host / the next consumer, never by the
+// kernel: non-temporal stores keep them from evicting the CSR mirror out of L2.
+inline uint32_t nt_stores() { return env_u32("OPENR_SPF_NT", 1u, 0u, 1u); }
+
+// Counter block of a source class: [0,1] fast launch, [2,3] re-run launch, [4] solves
+// the fast launch flagged for the re-run (cleared by the re-run's last workgroup).
+inline uint32_t* class_counters(const SolveArgs& a) { return a.work + kCtrPerClass * a.cls; }
+
+}  // namespace bfs
+}  // namespace openr_spf

@@ -1,0 +1,549 @@
+// spf_bfs_lvl.hip — uniform-cost SPF kernel, "lvl" family: exact level bytes in LDS.
+//
+// Same semantics as spf_bfs.hip (LinkState::runSpf closed form for uniform cost,
+// /root/reference/openr/decision/LinkState.cpp:808-882): dist = c * level, next hops =
+// OR over tight in-edges. Chosen for DEEP graphs (grids: ~150 levels of ~70 nodes): the
+// per-solve LDS holds lvl[v] (u8) and the packed next-hop sets, and the u64 distance
+// row is written coalesced from lvl at the end — the code family's per-node scattered
+// distance stores cost more than they save there (G100: 1.42 vs 1.19 ms).
+//
+// Level L: an arrival on edge u->v is tight iff lvl[v] > L; it ORs nh(u) into nh(v)
+// and stores lvl[v] = L+1. The arrival whose atomicOr finds v's (single-dword) set empty
+// appends v (every reached node's set is non-empty); sliced classes (> 32 neighbours,
+// one 32-bit slice of the set per workgroup pass) elect by a visited bitmap instead.
+// One 256-thread workgroup per solve, persistent and dynamically scheduled; K=4 edges
+// per lane with their LDS reads, then their atomics, issued together.
+#include <algorithm>
+#include <cstdlib>
+
+#include "spf_bfs_common.h"
+#include "spf_device.h"
+#include "spf_kernels.h"
+
+namespace openr_spf {
+
+namespace {
+using namespace dev;
+using namespace bfs;
+
+template <typename LT>
+struct LvlLayout {
+  uint32_t lvl, vis, nh, ring, ign, dummy, total;
+};
+
+// ring = frontier queue (power of two, wraps) in the fast path, or the full BFS-order
+// array (capacity V, never wraps) in the fallback path.
+template <typename LT>
+__host__ __device__ inline LvlLayout<LT> lvl_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
+                                                    bool need_vis, uint32_t ring_cap) {
+  LvlLayout<LT> l;
+  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4]
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.lvl = take((uint32_t)sizeof(LT) * (V + 4u));
+  l.vis = need_vis ? take(4u * ((V + 31u) / 32u)) : 0u;
+  l.nh = take(4u * nh_words);
+  l.ring = take(2u * ring_cap);
+  l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
+  l.dummy = take(4u * 64u);  // per-lane sink for the no-op atomics of non-tight edges
+  l.total = off;
+  return l;
+}
+
+template <typename LT>
+struct LvlOps;
+template <>
+struct LvlOps<uint8_t> {
+  static constexpr uint32_t kUnset = 0xFFu;
+};
+template <>
+struct LvlOps<uint16_t> {
+  static constexpr uint32_t kUnset = 0xFFFFu;
+};
+
+int lvl_class_mode(int cls) {
+  switch (cls) {
+    case kLvl4: return kNhNibble;
+    case kLvl8: return kNhByte;
+    case kLvl16: return kNhHalf;
+    default: return kNhW1;  // kLvl32, and each 32-bit slice of kLvlSliced
+  }
+}
+
+// Writes this solve's dist row (u64) and next-hop row from LDS, coalesced.
+// Sliced classes: slice s owns next-hop bytes [4s, 4s + 4); slice 0 also writes the
+// distance row and zero-fills the bytes past the last slice.
+template <int MODE, typename LT, int BLOCK, bool SLICED>
+__device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
+                                           const LT* lvl, const uint32_t* nh, uint64_t cost, bool nt) {
+  using N = Nh<MODE>;
+  using O = LvlOps<LT>;
+  const uint32_t tid = threadIdx.x;
+  if (SLICED) {
+    if (a.nh) {
+      const uint32_t nb = a.nh_bytes, j0 = 4u * slice, zero0 = 4u * a.nsl;
+      uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+      for (uint32_t v = tid; v < V; v += BLOCK) {
+        const uint32_t w = nh[v];
+        uint8_t* o = nrow + (size_t)v * nb;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4u; ++jj)
+          if (j0 + jj < nb) o[j0 + jj] = (uint8_t)(w >> (8u * jj));
+        if (slice == 0)
+          for (uint32_t j = zero0; j < nb; ++j) o[j] = 0;
+      }
+    }
+    if (slice != 0) return;
+  }
+  uint64_t* drow = a.dist + (size_t)sid * V;
+  if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
+    // two nodes per lane: 16-byte stores
+    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
+    for (uint32_t i = tid; i < V / 2u; i += BLOCK) {
+      const uint32_t l0 = lvl[2u * i], l1 = lvl[2u * i + 1u];
+      const uint64_t x0 = l0 != O::kUnset ? (uint64_t)l0 * cost : ~0ull;
+      const uint64_t x1 = l1 != O::kUnset ? (uint64_t)l1 * cost : ~0ull;
+      if (nt) {
+        __builtin_nontemporal_store(x0, &d2[i].x);
+        __builtin_nontemporal_store(x1, &d2[i].y);
+      } else {
+        d2[i] = make_ulonglong2(x0, x1);
+      }
+    }
+  } else {
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+      const uint32_t l = lvl[v];
+      store_row<uint64_t>(&drow[v], l != O::kUnset ? (uint64_t)l * cost : ~0ull, nt);
+    }
+  }
+  if (SLICED || !a.nh) return;
+  const uint32_t nb = a.nh_bytes;
+  uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+  const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
+  if (MODE == kNhNibble && nb == 1 && aligned4) {
+    // four nodes (four nibbles of one half-dword) per lane -> one u32 of four bytes
+    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+    for (uint32_t i = tid; i < V / 4u; i += BLOCK) {
+      const uint32_t h = (nh[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
+      store_row<uint32_t>(&nrow32[i], (h & 0xFu) | ((h & 0xF0u) << 4) | ((h & 0xF00u) << 8) | ((h & 0xF000u) << 12),
+                          nt);
+    }
+  } else if (MODE == kNhByte && nb == 1 && aligned4) {
+    uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+    for (uint32_t i = tid; i < V / 4u; i += BLOCK) store_row<uint32_t>(&nrow32[i], nh[i], nt);
+  } else {
+    const uint32_t total = V * nb;
+    for (uint32_t i = tid; i < total; i += BLOCK) {
+      const uint32_t v = i / nb, j = i - v * nb;
+      nrow[i] = (uint8_t)N::byte(nh, v, j);
+    }
+  }
+}
+
+// ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
+// the rest from CSR (G == 1); 2 = ELL only (every row has <= 4 edges, no ignore set,
+// no tight-edge output).
+// RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent levels
+//               exceed the ring, or whose depth exceeds 253, gets ovf[sid] = rerun + 1
+//               (else 0). RING = false: LT = u16, full BFS order — the re-run.
+// rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
+// SLICED: one unit = (solve, 32-bit slice of the next-hop set).
+// GENERIC = false: no ignore set and no tight-edge output (compile time).
+template <int MODE, int BLOCK, typename LT, bool RING, int ELLM, bool GENERIC, bool SLICED>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_lvl_kernel(
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
+    uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+  constexpr int K = (int)kBfsEdgesPerLane;
+  constexpr bool ELECT = Nh<MODE>::kSingle && !SLICED;
+  const bool has_ign = GENERIC && has_ign_rt != 0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t s_next;
+  using N = Nh<MODE>;
+  using O = LvlOps<LT>;
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const uint32_t nh_words = N::words(V);
+  const LvlLayout<LT> lay = lvl_layout<LT>(V, g.L, has_ign, nh_words, !ELECT, ring_cap);
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  LT* lvl = reinterpret_cast<LT*>(base + lay.lvl);
+  uint32_t* lvl_w = reinterpret_cast<uint32_t*>(base + lay.lvl);
+  uint32_t* vis = reinterpret_cast<uint32_t*>(base + lay.vis);
+  uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
+  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
+  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
+  const uint32_t bit_words = (V + 31u) / 32u;
+  const uint32_t lvl_words = ((uint32_t)sizeof(LT) * (V + 4u)) / 4u;
+  const uint32_t ign_words = (g.L + 31u) / 32u;
+  const uint32_t G = 1u << glog, ngroups = BLOCK >> glog, groups_per_wave = 64u >> glog;
+  const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
+  const uint32_t tight_words = (g.E + 63u) / 64u;
+  const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
+  const uint32_t nsl = SLICED ? a.nsl : 1u;
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  // a re-run launch with nothing flagged does no work
+  const uint32_t units = (rerun && !RING && *ovf_count == 0u) ? 0u : count * nsl;
+#ifdef OPENR_SPF_PROFILE
+  // [0] load (ring + ELL/row), [1] level reads, [2] atomics, [3] append, [4] barrier,
+  // [5] init + level 0, [6] write rows, [7] passes, [8] levels, [9] solves
+  uint64_t pc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+#endif
+
+  for (uint32_t unit = blockIdx.x; unit < units;) {
+    const uint32_t k = SLICED ? unit / nsl : unit, slice = SLICED ? unit - k * nsl : 0u;
+    const uint32_t sid = a.perm ? a.perm[first + k] : k;
+    const uint32_t src = a.sources[sid];
+    if (src < V && !(rerun && a.ovf[sid] != rerun)) {  // block-uniform
+      OPENR_PROF_STAMP(t0);
+      for (uint32_t i = tid; i < lvl_words; i += BLOCK) lvl_w[i] = 0xFFFFFFFFu;
+      if (!ELECT)
+        for (uint32_t i = tid; i < bit_words; i += BLOCK) vis[i] = 0;
+      for (uint32_t i = tid; i < nh_words; i += BLOCK) nh[i] = 0;
+      if (has_ign)
+        for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
+      if (tid < 8) ctl[tid] = 0;
+      __syncthreads();
+      if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
+      if (tid == 0) {
+        lvl[src] = 0;
+        if (!ELECT) vis[src >> 5] = 1u << (src & 31u);
+      }
+      __syncthreads();
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+
+      // level 0: expand the source (even when overloaded); a directly connected
+      // node's next hop is the node itself (LinkState.cpp:867-872)
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
+          const uint32_t e = e0 + tid;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e])) && v != src) {
+              if constexpr (ELECT) {
+                fresh = N::fetch_or_bit(nh, v, g.nbr[e]) == 0u;
+              } else {
+                const uint32_t bit = 1u << (v & 31u);
+                fresh = !(atomicOr(&vis[v >> 5], bit) & bit);
+                const uint32_t b = g.nbr[e];
+                if (!SLICED) N::or_bit(nh, v, b);
+                else if ((b >> 5) == slice) N::or_bit(nh, v, b & 31u);
+              }
+              lvl[v] = (LT)1;
+              if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+            }
+          }
+          // level-0 appends count in ctl[0]; level L >= 1 uses ctl[L & 3]
+          const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
+          if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap checked by the host
+        }
+      }
+      __syncthreads();
+#ifdef OPENR_SPF_PROFILE
+      OPENR_PROF_STAMP(t1);
+      OPENR_PROF_ADD(5, t0, t1);
+      pc[9] += 1;
+#endif
+
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1;
+      bool overflow = false;  // block-uniform
+      while (head < tail) {
+        if (RING && L + 1u >= O::kUnset) {  // next level not representable in u8
+          overflow = true;
+          break;
+        }
+        uint32_t* cnt = &ctl[L & 3u];
+        if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
+        for (uint32_t fb = head; fb < tail; fb += ngroups) {
+          if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
+          OPENR_PROF_STAMP(t0);
+          const uint32_t idx = fb + group;
+          const bool live = idx < tail;
+          uint32_t u = 0, beg = 0, end = 0;
+          uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
+          if (live) {
+            u = ring[RING ? (idx & rmask) : idx];
+            if (ELLM == 2) {
+              ell = g.ellt[u];
+            } else {
+              const uint2 r = g.row2t[u];  // empty (begin flagged) for overloaded nodes (sinks)
+              beg = r.x;
+              end = r.y;
+              if (ELLM == 1) ell = g.ellt[u];
+            }
+          }
+          if (ELLM == 2 && live) end = 4;  // kEdgeDown-padded ELL slots stand for the row end
+          const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
+#ifdef OPENR_SPF_PROFILE
+          OPENR_PROF_STAMP(t1);
+          OPENR_PROF_ADD(0, t0, t1);
+          pc[7] += 1;
+#endif
+          for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; __any(e0 < end); e0 += G * K) {
+            uint32_t av[K], lv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j * G;
+              if (ELLM == 2) {
+                av[j] = j == 0 ? ell.x : j == 1 ? ell.y : j == 2 ? ell.z : ell.w;
+              } else if (ELLM == 1 && e0 == beg) {
+                av[j] = j == 0 ? ell.x : j == 1 ? ell.y : j == 2 ? ell.z : ell.w;
+              } else {
+                av[j] = e < end ? g.adj[e] : kEdgeDown;
+              }
+              lv[j] = (has_ign && e < end) ? g.lid[e] : 0u;
+            }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t1);
+#endif
+            // (1) tight test: the K level reads are issued together (no branches)
+            bool tight[K];
+            uint32_t vv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j * G;
+              vv[j] = av[j] & ~(kEdgeDown | kNodeSink);  // always a valid node id
+              const bool ok = !(av[j] & kEdgeDown) && (ELLM == 2 || e < end) && !(has_ign && test_bit(ign, lv[j]));
+              const uint32_t l = lvl[ok ? vv[j] : V];  // lvl[V] is padding
+              tight[j] = ok && l > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
+            }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t2);
+            OPENR_PROF_ADD(1, t1, t2);
+#endif
+            // (2) addNextHops(nh(u)) + election of the appending arrival: K atomics in
+            //     flight together; non-tight edges OR 0 into the lane's own dummy word
+            uint32_t fresh_mask = 0;
+            if constexpr (ELECT) {
+              const uint32_t x = nhu.x;
+              uint32_t old[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                old[j] = atomicOr(tight[j] ? &nh[N::word(vv[j])] : &dummy[lane], tight[j] ? x << N::shift(vv[j]) : 0u);
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                fresh_mask |= (tight[j] && ((old[j] >> N::shift(vv[j])) & N::kMask) == 0u) ? (1u << j) : 0u;
+            } else {
+              uint32_t old[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                old[j] = atomicOr(tight[j] ? &vis[vv[j] >> 5] : &dummy[lane], tight[j] ? 1u << (vv[j] & 31u) : 0u);
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                fresh_mask |= (tight[j] && !((old[j] >> (vv[j] & 31u)) & 1u)) ? (1u << j) : 0u;
+                if (tight[j]) N::or_val(nh, vv[j], nhu);
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              if (trow && tight[j]) {
+                const uint32_t e = e0 + j * G;
+                atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+              }
+            }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t3);
+            OPENR_PROF_ADD(2, t2, t3);
+#endif
+            // (3) wave-aggregated append: 3 ballots + one ds_add per wave
+            uint32_t total;
+            uint32_t slot = wave_prefix_small((uint32_t)__popc(fresh_mask), &total);
+            if (total) {  // wave-uniform
+              const int leader = __ffsll((long long)__ballot(1)) - 1;
+              uint32_t wbase = 0;
+              if ((int)lane == leader) wbase = atomicAdd(cnt, total);
+              slot += tail + __builtin_amdgcn_readfirstlane(wbase);
+              bool lost = false;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                if ((fresh_mask >> j) & 1u) {
+                  if (!RING) {
+                    ring[slot] = (uint16_t)vv[j];
+                  } else if (slot - head < ring_cap) {
+                    ring[slot & rmask] = (uint16_t)vv[j];
+                  } else {
+                    lost = true;  // two adjacent levels exceed the ring
+                  }
+                  ++slot;
+                }
+              }
+              if (RING && __any(lost) && (int)lane == leader) ctl[4] = 1;
+            }
+#ifdef OPENR_SPF_PROFILE
+            OPENR_PROF_STAMP(t4);
+            OPENR_PROF_ADD(3, t3, t4);
+#endif
+          }
+        }
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t0);
+#endif
+        lds_barrier();
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t1);
+        OPENR_PROF_ADD(4, t0, t1);
+        pc[8] += 1;
+#endif
+        head = tail;
+        tail += *cnt;
+        ++L;
+        if (RING && ctl[4]) {  // ring overflow; ctl[4] is uniform after the barrier
+          overflow = true;
+          break;
+        }
+      }
+      if (RING && overflow) {  // re-run by the u16 / full-order variant
+        if (tid == 0) {
+          a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
+          if (!SLICED || slice == 0) atomicAdd(ovf_count, 1u);
+        }
+      } else {
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t0);
+#endif
+        if (RING && tid == 0 && (!SLICED || slice == 0)) a.ovf[sid] = 0;
+        write_rows<MODE, LT, BLOCK, SLICED>(a, sid, slice, V, lvl, nh, cost, nt != 0);
+#ifdef OPENR_SPF_PROFILE
+        OPENR_PROF_STAMP(t1);
+        OPENR_PROF_ADD(6, t0, t1);
+#endif
+      }
+    }
+    // next unit: dynamic scheduling (the first gridDim.x units are static)
+    __syncthreads();  // every lane is done with this unit's LDS and s_next
+    if (tid == 0) s_next = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unit = s_next;
+  }
+  // the re-run consumed the flags of its class: its last workgroup clears the count
+  retire_workgroup(ctr, (!RING && rerun) ? ovf_count : nullptr);
+#ifdef OPENR_SPF_PROFILE
+  if (lane == 0 && a.prof)
+    for (int i = 0; i < 10; ++i) atomicAdd(&a.prof[i], (unsigned long long)pc[i]);
+#endif
+}
+
+// Fast path: u8 levels + a ring sized so that target workgroups fit a CU.
+uint32_t lvl_ring_cap(const DevGraph& g, bool has_ign, int mode, bool vis, uint32_t target) {
+  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u)) return 0;
+  const uint32_t fixed = lvl_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), vis, 0).total;
+  const uint32_t min_cap = std::max<uint32_t>(256u, g.max_deg + 2u);
+  for (uint32_t want = target; want >= 1; --want) {
+    const uint32_t budget = kMaxLds / want;
+    if (budget <= fixed) continue;
+    uint32_t cap = 1;
+    while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
+    if (cap >= min_cap) return cap;
+  }
+  return 0;
+}
+
+template <int MODE, int BLOCK, typename LT, bool RING, int ELLM, bool SLICED>
+hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                              uint32_t ring_cap, uint32_t rerun, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
+                              hipStream_t s, LaunchInfo* info) {
+  const bool vis = SLICED || !Nh<MODE>::kSingle;
+  const uint32_t lds = lvl_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
+  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
+  const bool generic = has_ign || a.tight != nullptr;
+  auto k = generic ? bfs_lvl_kernel<MODE, BLOCK, LT, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
+                   : bfs_lvl_kernel<MODE, BLOCK, LT, RING, ELLM, false, SLICED>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  if (info && !rerun) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = RING ? "bfs_lvl_kernel<ring,u8>" : "bfs_lvl_kernel<full,u16>";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun, ctr,
+                     ovf_count, nt_stores());
+  return hipGetLastError();
+}
+
+template <int MODE, int BLOCK, int ELLM, bool SLICED>
+hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                           uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // ring/u8 variant first; the solves it flags are re-run by the full-order u16 variant
+  uint32_t* blk = class_counters(a);
+  const bool vis = SLICED || !Nh<MODE>::kSingle;
+  const uint32_t target = env_u32("OPENR_SPF_BFS_WGS", kBfsTargetWgs, 1u, 16u);
+  const uint32_t cap = lvl_ring_cap(g, has_ign, MODE, vis, target);
+  if (!cap)
+    return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun,
+                                                                        blk, blk + 4, num_cus, s, info);
+  hipError_t err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, cap,
+                                                                                first_rerun, blk, blk + 4, num_cus, s,
+                                                                                info);
+  if (err != hipSuccess || (g.V <= cap && g.V <= 254u)) return err;
+  return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V,
+                                                                      first_rerun + 1u, blk + 2, blk + 4, num_cus, s,
+                                                                      info);
+}
+
+template <int MODE, bool SLICED>
+hipError_t launch_lvl_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
+                          uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
+  if (env_u32("OPENR_SPF_BFS_BLOCK", 256u, 128u, 256u) == 128u) {
+    if (ellm == 2) return launch_lvl_mode<MODE, 128, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+    if (ellm == 1) return launch_lvl_mode<MODE, 128, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+    return launch_lvl_mode<MODE, 128, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  }
+  if (ellm == 2) return launch_lvl_mode<MODE, 256, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  if (ellm == 1) return launch_lvl_mode<MODE, 256, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  return launch_lvl_mode<MODE, 256, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+}
+}  // namespace
+
+uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls) {
+  // the full-order u16 variant must fit (it re-runs solves the fast path flags)
+  if (V > 65535u || cls < 0 || cls >= kNumLvlClasses) return 0;
+  const int mode = lvl_class_mode(cls);
+  const bool vis = cls == kLvlSliced || !nh_mode_single(mode);
+  const uint32_t t = lvl_layout<uint16_t>(V, L, has_ignore, nh_words_for(mode, V), vis, V).total;
+  return t <= kMaxLds ? t : 0;
+}
+
+hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
+                          hipStream_t s, LaunchInfo* info) {
+  const bool has_ign = a.ign_ptr != nullptr;
+  const int cls = (int)a.cls;
+  if (!bfs_lvl_lds_bytes(g.V, g.L, has_ign, cls)) return hipErrorInvalidValue;
+  const bool sliced = cls == kLvlSliced;
+  if (sliced && (a.nsl < 1u || a.nsl > 8u)) return hipErrorInvalidValue;
+  if (a.n == 0) return hipSuccess;
+  if (!a.ovf || !a.work) return hipErrorInvalidValue;
+  uint32_t glog = 0;
+  while ((1 << glog) < group_lanes && glog < 6) ++glog;
+  // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
+  const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
+  // bit-parallel multi-source BFS when eligible (opt-in, single-class batches); its
+  // overflowing batches fall through to the per-source kernels
+  uint32_t first_rerun = 0;
+  const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
+  if (!a.perm && !sliced && ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
+    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
+    if (err != hipSuccess) return err;
+    err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
+                       info);
+    if (err != hipSuccess) return err;
+    first_rerun = 1;
+  }
+  if (sliced) return launch_lvl_ell<kNhW1, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+  switch (lvl_class_mode(cls)) {
+    case kNhNibble: return launch_lvl_ell<kNhNibble, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhByte: return launch_lvl_ell<kNhByte, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhHalf: return launch_lvl_ell<kNhHalf, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    default: return launch_lvl_ell<kNhW1, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+  }
+}
+
+}  // namespace openr_spf

@@ -77,8 +77,17 @@ struct Device {
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
 };
 
+// Launch counters live zeroed: each kernel's last workgroup resets what it used.
+hipError_t reserve_counters(Device& d) {
+  if (d.work.p) return hipSuccess;
+  hipError_t e = d.work.reserve(kWorkSlots);
+  if (e == hipSuccess) e = hipMemset(d.work.p, 0, kWorkSlots * sizeof(uint32_t));
+  return e;
+}
+
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj, g.w, g.win, g.rev, g.lid, g.nbr, g.ovl, g.cls};
+  void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj,    g.w,
+                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -95,20 +104,58 @@ struct openr_spf_ctx {
   uint32_t w_min = 0, w_max = 0;
   bool metric_ok = true;        // every usable metric in [1, 2^31-1]
   uint32_t group_lanes = 4;
-  uint32_t cls_mask = 0;        // source classes present among the nodes (SrcClass bits)
-  uint32_t nsl = 1;             // next-hop slices of the sliced class
+  int family = kFamCode;        // BFS kernel family picked for this graph (pick_family)
+  uint32_t cls_mask[kNumFamilies] = {0, 0};  // source classes present among the nodes, per family
+  uint32_t nsl[kNumFamilies] = {1, 1};       // next-hop slices of each family's sliced class
   openr_spf_stats_t stats{};
 };
 
 namespace {
 
+constexpr uint32_t kDeepGraphLevels = 24;
+
 struct Plan {
   bool bfs = true;
+  int family = kFamCode;
   uint64_t cost = 1;
   uint32_t delta = 1;
   bool dist64 = false;
   int nh_mode = kNhByte;
 };
+
+// Tuning / test override (benchmarks and parity tests only): OPENR_SPF_BFS_FAMILY=code|lvl.
+int family_override(int dflt) {
+  const char* e = std::getenv("OPENR_SPF_BFS_FAMILY");
+  if (!e) return dflt;
+  if (!std::strcmp(e, "code")) return kFamCode;
+  if (!std::strcmp(e, "lvl")) return kFamLvl;
+  return dflt;
+}
+
+// Family per graph: the lvl kernels win on deep graphs (grid G100: ~150 levels of ~70
+// nodes; 1.19 vs 1.42 ms), the code kernels on shallow ones (fabric: 5 levels; 1.45 vs
+// 1.89 ms). Depth = eccentricity of node 0 over up edges (host BFS, O(V + E)).
+int pick_family(uint32_t V, const uint32_t* row_ptr, const uint32_t* adj) {
+  if (V == 0) return kFamCode;
+  std::vector<uint32_t> lvl(V, UINT32_MAX), q;
+  q.reserve(V);
+  q.push_back(0);
+  lvl[0] = 0;
+  uint32_t depth = 0;
+  for (size_t i = 0; i < q.size(); ++i) {
+    const uint32_t u = q[i];
+    depth = lvl[u];
+    for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+      if (adj[e] & kEdgeDown) continue;
+      const uint32_t v = adj[e];
+      if (lvl[v] == UINT32_MAX) {
+        lvl[v] = lvl[u] + 1u;
+        q.push_back(v);
+      }
+    }
+  }
+  return depth >= kDeepGraphLevels ? kFamLvl : kFamCode;
+}
 
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   const bool use_metric = (flags & OPENR_SPF_USE_LINK_METRIC) != 0;
@@ -121,9 +168,10 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   if (!use_metric || ctx->w_min == ctx->w_max) {
     p->bfs = true;
     p->cost = use_metric ? std::max<uint32_t>(ctx->w_min, 1u) : 1u;
-    for (int c = 0; c < kNumClasses; ++c)
-      if ((ctx->cls_mask >> c) & 1u)
-        if (!bfs_lds_bytes(ctx->V, ctx->L, has_ign, nh_mode_of_class(c), c == kClsSliced))
+    p->family = family_override(ctx->family);
+    for (int c = 0; c < num_classes(p->family); ++c)
+      if ((ctx->cls_mask[p->family] >> c) & 1u)
+        if (!bfs_lds_bytes(p->family, ctx->V, ctx->L, has_ign, c))
           return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident BFS kernel", ctx->V);
   } else {
     p->bfs = false;
@@ -171,21 +219,24 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   const int gl = group_lanes_override((int)ctx->group_lanes);
   a.perm = nullptr;
   a.part = nullptr;
-  a.nsl = ctx->nsl;
-  if (__builtin_popcount(ctx->cls_mask) == 1) {
-    a.cls = (uint32_t)__builtin_ctz(ctx->cls_mask);
-    return launch_bfs(d.g, a, p.cost, nh_mode_of_class((int)a.cls), a.cls == kClsSliced, gl, d.num_cus, s, &info);
+  const int fam = p.family;
+  const uint32_t mask = ctx->cls_mask[fam];
+  a.nsl = ctx->nsl[fam];
+  if (__builtin_popcount(mask) == 1) {
+    a.cls = (uint32_t)__builtin_ctz(mask);
+    return launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
   }
   hipError_t err = d.perm.reserve(std::max<uint32_t>(a.n, 1u));
   if (err == hipSuccess) err = d.part.reserve(3u * kMaxClasses);
-  if (err == hipSuccess) err = launch_partition(a.sources, a.n, d.g.cls, d.g.V, d.part.p, d.perm.p, s);
+  if (err == hipSuccess) err = launch_partition(a.sources, a.n, fam == kFamLvl ? d.g.cls_lvl : d.g.cls, d.g.V, d.part.p,
+                                                 d.perm.p, s);
   if (err != hipSuccess) return err;
   a.perm = d.perm.p;
   a.part = d.part.p;
-  for (int c = kNumClasses - 1; c >= 0; --c) {
-    if (!((ctx->cls_mask >> c) & 1u)) continue;
+  for (int c = num_classes(fam) - 1; c >= 0; --c) {
+    if (!((mask >> c) & 1u)) continue;
     a.cls = (uint32_t)c;
-    err = launch_bfs(d.g, a, p.cost, nh_mode_of_class(c), c == kClsSliced, gl, d.num_cus, s, &info);
+    err = launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
     if (err != hipSuccess) return err;
   }
   return hipSuccess;
@@ -255,7 +306,7 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh_bits = ctx->nh_bits;
     HIP_TRY(d.ovf.reserve(m));
     a.ovf = d.ovf.p;
-    HIP_TRY(d.work.reserve(kWorkSlots));
+    HIP_TRY(reserve_counters(d));
     a.work = d.work.p;
     HIP_TRY(prepare_scratch(ctx, d, plan, a));
     HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
@@ -303,7 +354,7 @@ void openr_spf_limits(openr_spf_limits_t* out) {
   uint32_t lo = 1, hi = 65535;
   while (lo < hi) {
     uint32_t mid = (lo + hi + 1) / 2;
-    if (bfs_lds_bytes(mid, 0, false, kNhByte, false)) lo = mid;
+    if (bfs_lds_bytes(kFamCode, mid, 0, false, kCls8)) lo = mid;
     else hi = mid - 1;
   }
   out->max_nodes = lo;
@@ -379,7 +430,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   if (!gr->row_ptr || !gr->node_overloaded || !gr->name_rank || (E && (!gr->col || !gr->metric || !gr->link_id ||
                                                                       !gr->edge_up)))
     return fail(OPENR_SPF_EINVAL, "null graph array");
-  if (V >= kEdgeDown) return fail(OPENR_SPF_E2BIG, "too many nodes");
+  if (V >= kNodeSink || E >= kNodeSink) return fail(OPENR_SPF_E2BIG, "too many nodes or edges");
   if (gr->row_ptr[0] != 0 || gr->row_ptr[V] != E) return fail(OPENR_SPF_EINVAL, "row_ptr must span [0, E]");
   for (uint32_t u = 0; u < V; ++u)
     if (gr->row_ptr[u + 1] < gr->row_ptr[u]) return fail(OPENR_SPF_EINVAL, "row_ptr not monotone at %u", u);
@@ -443,27 +494,34 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     uint32_t x[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
     if (!ovl[u])
       for (uint32_t j = 0; j < 4 && gr->row_ptr[u] + j < gr->row_ptr[u + 1]; ++j) x[j] = adj[gr->row_ptr[u] + j];
+    else
+      x[0] |= kNodeSink;
     ellt[u] = make_uint4(x[0], x[1], x[2], x[3]);
   }
   std::vector<uint32_t> ovl_bits((V + 31) / 32 + 1, 0);
   for (uint32_t u = 0; u < V; ++u) {
     row2[u] = make_uint2(gr->row_ptr[u], gr->row_ptr[u + 1]);
-    row2t[u] = ovl[u] ? make_uint2(gr->row_ptr[u], gr->row_ptr[u]) : row2[u];
+    row2t[u] = ovl[u] ? make_uint2(gr->row_ptr[u] | kNodeSink, gr->row_ptr[u]) : row2[u];
     if (ovl[u]) ovl_bits[u >> 5] |= 1u << (u & 31u);
   }
   if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
   // source class of every node (distinct degree -> next-hop width)
-  std::vector<uint8_t> cls(V);
-  uint32_t cls_mask = 0, sliced_deg = 0;
+  std::vector<uint8_t> cls[kNumFamilies];
+  uint32_t cls_mask[kNumFamilies] = {0, 0}, sliced_deg[kNumFamilies] = {0, 0};
+  for (int f = 0; f < kNumFamilies; ++f) cls[f].resize(V);
   for (uint32_t u = 0; u < V; ++u) {
     uint32_t nd = 0;
     for (uint32_t e = gr->row_ptr[u]; e < gr->row_ptr[u + 1]; ++e) nd = std::max<uint32_t>(nd, nbr[e] + 1u);
-    const int c = src_class_for_degree(nd);
-    cls[u] = (uint8_t)c;
-    cls_mask |= 1u << c;
-    if (c == kClsSliced) sliced_deg = std::max(sliced_deg, nd);
+    for (int f = 0; f < kNumFamilies; ++f) {
+      const int c = src_class_for_degree(f, nd);
+      cls[f][u] = (uint8_t)c;
+      cls_mask[f] |= 1u << c;
+      if (c == sliced_class(f)) sliced_deg[f] = std::max(sliced_deg[f], nd);
+    }
   }
-  if (!cls_mask) cls_mask = 1u << kClsNibble;
+  for (int f = 0; f < kNumFamilies; ++f)
+    if (!cls_mask[f]) cls_mask[f] = 1u;  // no node: class 0
+  const int family = pick_family(V, gr->row_ptr, adj.data());
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
 
   for (Device& d : ctx->devs) {
@@ -494,7 +552,8 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.lid, lid.data(), E);
     if (err == hipSuccess) err = up(&g.nbr, nbr.data(), E);
     if (err == hipSuccess) err = up(&g.ovl, ovl.data(), V);
-    if (err == hipSuccess) err = up(&g.cls, cls.data(), V);
+    if (err == hipSuccess) err = up(&g.cls, cls[kFamCode].data(), V);
+    if (err == hipSuccess) err = up(&g.cls_lvl, cls[kFamLvl].data(), V);
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;
@@ -510,8 +569,11 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->w_min = w_min;
   ctx->w_max = w_max;
   ctx->metric_ok = metric_ok;
-  ctx->cls_mask = cls_mask;
-  ctx->nsl = std::max<uint32_t>(1u, (sliced_deg + 31u) / 32u);
+  ctx->family = family;
+  for (int f = 0; f < kNumFamilies; ++f) {
+    ctx->cls_mask[f] = cls_mask[f];
+    ctx->nsl[f] = std::max<uint32_t>(1u, (sliced_deg[f] + slice_bits(f) - 1u) / slice_bits(f));
+  }
   // lanes per frontier node: enough that one pass of kBfsEdgesPerLane edges per lane
   // covers an average row (grid: 1 lane x 4 edges; fabric: 8 lanes x 4 edges)
   const uint32_t avg = V ? (E + V - 1) / V : 1;
@@ -585,7 +647,7 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bits = ctx->nh_bits;
   HIP_TRY(d.ovf.reserve(n));
   a.ovf = d.ovf.p;
-  HIP_TRY(d.work.reserve(kWorkSlots));
+  HIP_TRY(reserve_counters(d));
   a.work = d.work.p;
   HIP_TRY(prepare_scratch(ctx, d, plan, a));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;

@@ -29,10 +29,14 @@ struct DevGraph {
   uint32_t* lid = nullptr;     // [E] undirected link id
   uint16_t* nbr = nullptr;     // [E] distinct-neighbour index of col within its row
   uint8_t* ovl = nullptr;      // [V] overloaded
-  uint8_t* cls = nullptr;      // [V] source class (SrcClass) of each node
+  uint8_t* cls = nullptr;      // [V] source class of each node, code family (SrcClass)
+  uint8_t* cls_lvl = nullptr;  // [V] source class of each node, lvl family (LvlClass)
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
+// Sink flag of a transit row: ellt[u].x and row2t[u].x carry it when u is overloaded.
+// (row2t of a sink is an empty range whose begin carries the flag, so it never loops.)
+constexpr uint32_t kNodeSink = 0x40000000u;
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
 constexpr uint32_t kBfsTargetWgs = 8;     // fast-path BFS sizes its LDS for this many workgroups per CU
@@ -43,8 +47,8 @@ int nh_mode_for_bits(uint32_t bits);            // -1 if > 256 bits
 uint32_t nh_mode_lds_bytes(int mode, uint32_t V);
 uint32_t nh_words_for(int mode, uint32_t V);     // LDS dwords of V next-hop sets
 bool nh_mode_single(int mode);                  // one node's set lives inside one dword
-// persistent grid: workgroups that fit a CU by LDS (<= 8 x 256 threads) x CUs, <= n
-uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus);
+// persistent grid: workgroups that fit a CU by LDS (<= 2048 threads) x CUs, <= n
+uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus, uint32_t block = 256);
 
 struct LaunchInfo {
   uint32_t lds_bytes = 0;
@@ -65,7 +69,7 @@ struct SolveArgs {
   uint8_t* ovf;               // [n] scratch: solves a faster variant could not finish (re-run flags)
   uint8_t* scratch;           // multi-source BFS level bytes ([grid][V][lanes]); nullable
   size_t scratch_bytes;
-  uint32_t* work;             // [kWorkSlots] dynamic-scheduling counters (zeroed by the launcher)
+  uint32_t* work;             // [kWorkSlots] per-class launch counters (zero at rest: kernels reset them)
   // Source classes (next-hop width): when perm != nullptr this launch solves only the
   // sources of class `cls`: solve k < part[cls] is sid = perm[part[kMaxClasses + cls] + k]
   // (part / perm in device memory, built by partition_sources or the host).
@@ -73,16 +77,31 @@ struct SolveArgs {
   const uint32_t* part;       // [2 * kMaxClasses]: counts, then offsets
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
+  unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
 };
-constexpr uint32_t kWorkSlots = 16;  // dynamic-scheduling counters: 2 per source class
 constexpr uint32_t kMaxClasses = 8;
+constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch, [4] flagged solves
+constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
 
-// Source classes by distinct degree (next-hop bitset width). Classes 0-3 keep a node's
-// set in one LDS dword; class 4 (> 32 neighbours) solves in ceil(deg / 32) slices of 32
-// next-hop bits each, one slice per workgroup pass.
-enum SrcClass : int { kClsNibble = 0, kClsByte = 1, kClsHalf = 2, kClsWord = 3, kClsSliced = 4, kNumClasses = 5 };
-int src_class_for_degree(uint32_t distinct_degree);  // -1 if > 256
-int nh_mode_of_class(int cls);
+// Uniform-cost BFS kernel families (spf_capi.hip picks one per graph):
+//  * code (spf_bfs.hip): one packed LDS field per node = [next-hop bits | 3-bit level
+//    code]; distances stored when a node is expanded. Smallest LDS footprint, best on
+//    shallow graphs with wide frontiers (fabrics).
+//  * lvl (spf_bfs_lvl.hip): exact u8/u16 level per node + packed next-hop sets; the
+//    distance row is written coalesced at the end. Best on deep graphs (grids).
+enum BfsFamily : int { kFamCode = 0, kFamLvl = 1, kNumFamilies = 2 };
+
+// Source classes by distinct degree (next-hop bitset width).
+// code family: the per-node field holds the set plus a 3-bit level code in 8 bits
+// (d <= 5), 16 bits (d <= 13) or 32 bits (d <= 24); d > 24 solves in ceil(d / 24)
+// slices of 24 next-hop bits, one workgroup pass per slice.
+enum SrcClass : int { kCls8 = 0, kCls16 = 1, kCls32 = 2, kClsSliced = 3, kNumClasses = 4 };
+// lvl family: next-hop sets of 4 / 8 / 16 / 32 bits; d > 32 in 32-bit slices.
+enum LvlClass : int { kLvl4 = 0, kLvl8 = 1, kLvl16 = 2, kLvl32 = 3, kLvlSliced = 4, kNumLvlClasses = 5 };
+int src_class_for_degree(int family, uint32_t distinct_degree);  // -1 if > 256
+int num_classes(int family);
+int sliced_class(int family);
+uint32_t slice_bits(int family);
 // Stable within a class is not required: perm maps class-local index -> sid.
 hipError_t launch_partition(const uint32_t* d_sources, uint32_t n, const uint8_t* d_node_cls, uint32_t V,
                             uint32_t* d_part, uint32_t* d_perm, hipStream_t s);
@@ -100,10 +119,14 @@ hipError_t launch_msbfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, ui
                         LaunchInfo* info);
 
 
-// Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels.
-// nh_mode = the class's storage (sliced classes: kNhW1 with a.nsl slices).
-hipError_t launch_bfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, int nh_mode, bool sliced,
-                      int group_lanes, int num_cus, hipStream_t s, LaunchInfo* info);
+// Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels,
+// sources of class a.cls of `family` (a.nsl slices for the sliced class).
+hipError_t launch_bfs(int family, const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
+                      int num_cus, hipStream_t s, LaunchInfo* info);
+hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
+                           hipStream_t s, LaunchInfo* info);
+hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
+                          hipStream_t s, LaunchInfo* info);
 
 // General positive metrics: buckets of width delta = min usable metric (Dial /
 // delta-stepping with settle-safe buckets) and a pull pass for next-hops.
@@ -111,7 +134,9 @@ hipError_t launch_bucket(const DevGraph& g, const SolveArgs& a, uint32_t delta, 
                          int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
-uint32_t bfs_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool sliced);
+uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);
+uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
+uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bucket_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
 

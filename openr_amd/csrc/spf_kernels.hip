@@ -227,9 +227,10 @@ uint32_t nh_words_for(int mode, uint32_t V) {
   return 0;
 }
 
-uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus) {
-  uint32_t per_cu = lds ? kMaxLds / lds : 8;
-  if (per_cu > 8) per_cu = 8;  // 8 x 256 threads = 2048 threads per CU
+uint32_t blocks_for(uint32_t n, uint32_t lds, int num_cus, uint32_t block) {
+  const uint32_t max_wg = 2048u / block;  // 2048 threads (32 waves) per CU
+  uint32_t per_cu = lds ? kMaxLds / lds : max_wg;
+  if (per_cu > max_wg) per_cu = max_wg;
   if (per_cu < 1) per_cu = 1;
   uint64_t g = (uint64_t)num_cus * per_cu;
   if (g > n) g = n;
@@ -240,22 +241,33 @@ bool nh_mode_single(int mode) {
   return mode == kNhNibble || mode == kNhByte || mode == kNhHalf || mode == kNhW1;
 }
 
-int src_class_for_degree(uint32_t d) {
-  if (d <= 4) return kClsNibble;
-  if (d <= 8) return kClsByte;
-  if (d <= 16) return kClsHalf;
-  if (d <= 32) return kClsWord;
-  if (d <= 256) return kClsSliced;
-  return -1;
+int src_class_for_degree(int family, uint32_t d) {
+  if (d > 256) return -1;
+  if (family == kFamLvl) {
+    if (d <= 4) return kLvl4;
+    if (d <= 8) return kLvl8;
+    if (d <= 16) return kLvl16;
+    if (d <= 32) return kLvl32;
+    return kLvlSliced;
+  }
+  if (d <= 5) return kCls8;
+  if (d <= 13) return kCls16;
+  if (d <= 24) return kCls32;
+  return kClsSliced;
 }
 
-int nh_mode_of_class(int cls) {
-  switch (cls) {
-    case kClsNibble: return kNhNibble;
-    case kClsByte: return kNhByte;
-    case kClsHalf: return kNhHalf;
-    default: return kNhW1;  // kClsWord, and each 32-bit slice of kClsSliced
-  }
+int num_classes(int family) { return family == kFamLvl ? kNumLvlClasses : kNumClasses; }
+int sliced_class(int family) { return family == kFamLvl ? kLvlSliced : kClsSliced; }
+uint32_t slice_bits(int family) { return family == kFamLvl ? 32u : 24u; }
+
+uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls) {
+  return family == kFamLvl ? bfs_lvl_lds_bytes(V, L, has_ignore, cls) : bfs_code_lds_bytes(V, L, has_ignore, cls);
+}
+
+hipError_t launch_bfs(int family, const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
+                      int num_cus, hipStream_t s, LaunchInfo* info) {
+  return family == kFamLvl ? launch_bfs_lvl(g, a, cost, group_lanes, num_cus, s, info)
+                           : launch_bfs_code(g, a, cost, group_lanes, num_cus, s, info);
 }
 
 namespace {
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(256) void partition_count(const uint32_t* src, uint
     const uint32_t i = i0 + threadIdx.x;
     const uint32_t u = i < n ? src[i] : V;
     const uint32_t c = u < V ? cls[u] : 0u;
-    for (uint32_t k = 0; k < (uint32_t)kNumClasses; ++k) {
+    for (uint32_t k = 0; k < kMaxClasses; ++k) {
       const unsigned long long m = __ballot(i < n && c == k);
       if (m && __lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) atomicAdd(&part[k], (uint32_t)__popcll(m));
     }
@@ -292,7 +304,7 @@ __global__ __launch_bounds__(256) void partition_scatter(const uint32_t* src, ui
     const uint32_t i = i0 + threadIdx.x;
     const uint32_t u = i < n ? src[i] : V;
     const uint32_t c = u < V ? cls[u] : 0u;
-    for (uint32_t k = 0; k < (uint32_t)kNumClasses; ++k) {
+    for (uint32_t k = 0; k < kMaxClasses; ++k) {
       const unsigned long long m = __ballot(i < n && c == k);
       if (!m) continue;
       const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);

@@ -18,6 +18,21 @@ from oracle import Oracle
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module", autouse=True, params=["code", "lvl"])
+def bfs_family(request):
+    """Every parity test runs on both uniform-cost kernel families (spf_bfs.hip and
+    spf_bfs_lvl.hip); production picks one per graph by depth (spf_capi.hip)."""
+    import os
+
+    old = os.environ.get("OPENR_SPF_BFS_FAMILY")
+    os.environ["OPENR_SPF_BFS_FAMILY"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("OPENR_SPF_BFS_FAMILY", None)
+    else:
+        os.environ["OPENR_SPF_BFS_FAMILY"] = old
+
+
 @pytest.fixture(scope="module")
 def eng():
     e = SpfEngine()
