@@ -136,16 +136,16 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
 // ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
 // the rest from CSR (G == 1); 2 = ELL only (every row has <= 4 edges, no ignore set,
 // no tight-edge output).
-// RING = true : queue = power-of-two ring; a solve whose two adjacent levels exceed
-//               the ring gets ovf[sid] = rerun + 1 for the re-run, else ovf[sid] = 0.
-// RING = false: full BFS order (capacity V) — the re-run of flagged solves.
-// rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
+// RING = true : queue = power-of-two ring; a (solve, slice) unit whose two adjacent
+//               levels exceed the ring is appended to a.ovf_list (count *ovf_count).
+// RING = false: full BFS order (capacity V, never overflows). from_list != 0: the
+//               units of a.ovf_list only (the re-run of what the ring variant flagged).
 // SLICED: one unit = (solve, 24-bit slice of the next-hop set).
 // GENERIC = false: no ignore set and no tight-edge output (compile time), the
 // all-sources / prefetch case; GENERIC = true handles both at run time.
 template <int FB, int BLOCK, bool RING, int ELLM, bool GENERIC, bool SLICED>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_code_kernel(
-    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t from_list,
     uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
   using S = State<FB>;
   constexpr int K = (int)kBfsEdgesPerLane;
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   const uint32_t nsl = SLICED ? a.nsl : 1u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   // a re-run launch with nothing flagged does no work
-  const uint32_t units = (rerun && RING == false && *ovf_count == 0u) ? 0u : count * nsl;
+  const uint32_t units = from_list ? *ovf_count : count * nsl;
 #ifdef OPENR_SPF_PROFILE
   // [0] load (ring + ELL/row), [1] field reads, [2] atomics, [3] append, [4] barrier,
   // [5] init + level 0, [6] write out, [7] passes, [8] levels, [9] solves
@@ -178,10 +178,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
 
   for (uint32_t unit = blockIdx.x; unit < units;) {
-    const uint32_t k = SLICED ? unit / nsl : unit, slice = SLICED ? unit - k * nsl : 0u;
+    const uint32_t uid = from_list ? a.ovf_list[unit] : unit;  // class-local (solve, slice) index
+    const uint32_t k = SLICED ? uid / nsl : uid, slice = SLICED ? uid - k * nsl : 0u;
     const uint32_t sid = a.perm ? a.perm[first + k] : k;
     const uint32_t src = a.sources[sid];
-    if (src < V && !(rerun && a.ovf[sid] != rerun)) {  // block-uniform
+    if (src < V) {  // block-uniform
       OPENR_PROF_STAMP(t0);
       const bool own_dist = !SLICED || slice == 0;
       uint64_t* drow = a.dist + (size_t)sid * V;
@@ -371,16 +372,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           break;
         }
       }
-      if (RING && overflow) {  // re-run by the full-order variant
-        if (tid == 0) {
-          a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
-          if (!SLICED || slice == 0) atomicAdd(ovf_count, 1u);
-        }
+      if (RING && overflow) {  // re-run by the full-order variant (from the list)
+        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = uid;
       } else {
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t0);
 #endif
-        if (RING && tid == 0 && (!SLICED || slice == 0)) a.ovf[sid] = 0;
         write_out<FB, BLOCK, SLICED>(a, sid, slice, V, st, nt != 0);
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t1);
@@ -395,7 +392,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
     unit = s_next;
   }
   // the re-run consumed the flags of its class: its last workgroup clears the count
-  retire_workgroup(ctr, (!RING && rerun) ? ovf_count : nullptr);
+  retire_workgroup(ctr, (!RING && from_list) ? ovf_count : nullptr);
 #ifdef OPENR_SPF_PROFILE
   if (lane == 0 && a.prof)
     for (int i = 0; i < 10; ++i) atomicAdd(&a.prof[i], (unsigned long long)pc[i]);
@@ -403,28 +400,40 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 }
 
 struct BfsShape {
-  uint32_t block = 256, ring_cap = 0, per_cu = 1;
+  uint32_t block = 256, ring_cap = 0, per_cu = 1;  // ring_cap == 0: full BFS order
 };
 
-// Pick the block size and ring: as many solves per CU as LDS allows (<= 32 waves);
-// 128-thread workgroups when more than 8 solves fit. ring_cap == 0: no fast ring fits,
-// the full-order variant runs alone.
+// As many solves per CU as LDS allows (<= 32 waves; 128-thread workgroups when more than
+// 8 fit). At each occupancy the full-order queue (never overflows) is preferred when it
+// fits, else a ring wide enough for the graph's estimated two-level frontier
+// (g.est_width2, sampled on the host) — a ring that overflows re-runs its solves, which
+// costs more than the occupancy it buys (fabric: levels of thousands of nodes).
 BfsShape bfs_shape(const DevGraph& g, bool has_ign, uint32_t fb) {
   BfsShape sh;
   const uint32_t fixed = bfs_layout(g.V, g.L, has_ign, fb, 0).total;
-  const uint32_t min_cap = std::max<uint32_t>(256u, g.max_deg + 2u);
+  const uint32_t full = bfs_layout(g.V, g.L, has_ign, fb, g.V).total;
+  const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
+  const bool force_full = env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u) != 0u;
   for (uint32_t want = env_u32("OPENR_SPF_BFS_WGS", 16u, 1u, 16u); want >= 1; --want) {
     const uint32_t budget = kMaxLds / want;
-    if (budget <= fixed) continue;
+    sh.per_cu = want;
+    if (full <= budget) {
+      sh.ring_cap = 0;
+      break;
+    }
+    if (force_full || budget <= fixed) continue;
     uint32_t cap = 1;
     while (cap * 2u <= (budget - fixed) / 2u && cap < 4096u) cap *= 2u;
-    if (cap >= min_cap) {
+    if (cap >= need) {
       sh.ring_cap = cap;
-      sh.per_cu = want;
       break;
     }
   }
-  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u)) sh.ring_cap = 0;
+  // test hook: force a (too small) ring so the overflow -> re-run-list path runs
+  const uint32_t forced = env_u32("OPENR_SPF_RING_CAP", 0u, 0u, 65536u);
+  if (forced && (forced & (forced - 1u)) == 0u && forced >= g.max_deg + 2u &&
+      fixed + 2u * forced <= kMaxLds / sh.per_cu)
+    sh.ring_cap = forced;
   const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
   sh.block = blk == 128u || blk == 256u ? blk : (sh.per_cu > 8u ? 128u : 256u);
   return sh;
@@ -432,7 +441,7 @@ BfsShape bfs_shape(const DevGraph& g, bool has_ign, uint32_t fb) {
 
 template <int FB, int BLOCK, bool RING, int ELLM, bool SLICED>
 hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                              uint32_t ring_cap, uint32_t rerun, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
+                              uint32_t ring_cap, bool from_list, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
                               hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = bfs_layout(g.V, g.L, has_ign, FB, ring_cap).total;
   const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
@@ -442,39 +451,37 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
-  if (info && !rerun) {
+  if (info && !from_list) {
     info->lds_bytes = lds;
     info->grid = grid;
     info->kernel = RING ? "bfs_code_kernel<ring>" : "bfs_code_kernel<full>";
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun, ctr,
-                     ovf_count, nt_stores());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
+                     (uint32_t)from_list, ctr, ovf_count, nt_stores());
   return hipGetLastError();
 }
 
 template <int FB, int BLOCK, int ELLM, bool SLICED>
 hipError_t launch_bfs_shape(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                            uint32_t ring_cap, uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
-  // ring variant first; the solves it flags are re-run by the full-order variant.
-  // Counter block of the class: [0,1] fast launch, [2,3] re-run launch, [4] flagged.
+                            uint32_t ring_cap, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // Counter block of the class: [0,1] first launch, [2,3] re-run launch, [4] listed units.
   uint32_t* blk = class_counters(a);
   if (!ring_cap)
-    return launch_bfs_variant<FB, 256, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun, blk,
-                                                            blk + 4, num_cus, s, info);
-  hipError_t err = launch_bfs_variant<FB, BLOCK, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, first_rerun,
-                                                                     blk, blk + 4, num_cus, s, info);
-  if (err != hipSuccess || g.V <= ring_cap) return err;
-  return launch_bfs_variant<FB, 256, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun + 1u, blk + 2,
-                                                          blk + 4, num_cus, s, info);
+    return launch_bfs_variant<FB, BLOCK, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, false, blk, blk + 4,
+                                                              num_cus, s, info);
+  hipError_t err = launch_bfs_variant<FB, BLOCK, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, false, blk,
+                                                                     blk + 4, num_cus, s, info);
+  if (err != hipSuccess || g.V <= ring_cap) return err;  // a ring of >= V slots never overflows
+  return launch_bfs_variant<FB, 256, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true, blk + 2, blk + 4,
+                                                          num_cus, s, info);
 }
 
 template <int FB, bool SLICED>
-hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                         uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
+hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign, int ellm,
+                         int num_cus, hipStream_t s, LaunchInfo* info) {
   const BfsShape sh = bfs_shape(g, has_ign, FB);
-#define OPENR_BFS_SHAPE(BLK, E)                                                                                 \
-  return launch_bfs_shape<FB, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, first_rerun, num_cus, s, \
-                                              info)
+#define OPENR_BFS_SHAPE(BLK, E) \
+  return launch_bfs_shape<FB, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, num_cus, s, info)
   if (sh.block == 128) {
     if (ellm == 2) OPENR_BFS_SHAPE(128, 2);
     if (ellm == 1) OPENR_BFS_SHAPE(128, 1);
@@ -504,29 +511,17 @@ hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   const bool sliced = cls == kClsSliced;
   if (sliced && (a.nsl < 1u || a.nsl > 11u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  if (!a.ovf || !a.work) return hipErrorInvalidValue;
+  if (!a.ovf_list || !a.work) return hipErrorInvalidValue;
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
   const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
-  // bit-parallel multi-source BFS when eligible (opt-in, single-class batches); its
-  // overflowing batches fall through to the per-source kernels
-  uint32_t first_rerun = 0;
-  const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
-  if (!a.perm && !sliced && ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
-    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
-    if (err != hipSuccess) return err;
-    err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
-                       info);
-    if (err != hipSuccess) return err;
-    first_rerun = 1;
-  }
   switch (field_bits(cls)) {
-    case 8: return launch_bfs_fb<8, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case 8: return launch_bfs_fb<8, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+    case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
     default:
-      if (sliced) return launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-      return launch_bfs_fb<32, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+      if (sliced) return launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+      return launch_bfs_fb<32, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   }
 }
 

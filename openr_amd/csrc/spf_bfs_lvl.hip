@@ -146,15 +146,16 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
 // ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
 // the rest from CSR (G == 1); 2 = ELL only (every row has <= 4 edges, no ignore set,
 // no tight-edge output).
-// RING = true : LT = u8, queue = power-of-two ring; a solve whose two adjacent levels
-//               exceed the ring, or whose depth exceeds 253, gets ovf[sid] = rerun + 1
-//               (else 0). RING = false: LT = u16, full BFS order — the re-run.
-// rerun != 0: only solves with ovf[sid] == rerun (flagged by the previous variant).
+// RING = true : LT = u8, queue = power-of-two ring; a (solve, slice) unit whose two
+//               adjacent levels exceed the ring, or whose depth exceeds 253, is appended
+//               to a.ovf_list (count *ovf_count).
+// RING = false: LT = u16, full BFS order (never overflows). from_list != 0: the units of
+//               a.ovf_list only (the re-run of what the ring variant flagged).
 // SLICED: one unit = (solve, 32-bit slice of the next-hop set).
 // GENERIC = false: no ignore set and no tight-edge output (compile time).
 template <int MODE, int BLOCK, typename LT, bool RING, int ELLM, bool GENERIC, bool SLICED>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_lvl_kernel(
-    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t rerun,
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t from_list,
     uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
   constexpr int K = (int)kBfsEdgesPerLane;
   constexpr bool ELECT = Nh<MODE>::kSingle && !SLICED;
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   const uint32_t nsl = SLICED ? a.nsl : 1u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   // a re-run launch with nothing flagged does no work
-  const uint32_t units = (rerun && !RING && *ovf_count == 0u) ? 0u : count * nsl;
+  const uint32_t units = from_list ? *ovf_count : count * nsl;
 #ifdef OPENR_SPF_PROFILE
   // [0] load (ring + ELL/row), [1] level reads, [2] atomics, [3] append, [4] barrier,
   // [5] init + level 0, [6] write rows, [7] passes, [8] levels, [9] solves
@@ -194,10 +195,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
 
   for (uint32_t unit = blockIdx.x; unit < units;) {
-    const uint32_t k = SLICED ? unit / nsl : unit, slice = SLICED ? unit - k * nsl : 0u;
+    const uint32_t uid = from_list ? a.ovf_list[unit] : unit;  // class-local (solve, slice) index
+    const uint32_t k = SLICED ? uid / nsl : uid, slice = SLICED ? uid - k * nsl : 0u;
     const uint32_t sid = a.perm ? a.perm[first + k] : k;
     const uint32_t src = a.sources[sid];
-    if (src < V && !(rerun && a.ovf[sid] != rerun)) {  // block-uniform
+    if (src < V) {  // block-uniform
       OPENR_PROF_STAMP(t0);
       for (uint32_t i = tid; i < lvl_words; i += BLOCK) lvl_w[i] = 0xFFFFFFFFu;
       if (!ELECT)
@@ -400,16 +402,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           break;
         }
       }
-      if (RING && overflow) {  // re-run by the u16 / full-order variant
-        if (tid == 0) {
-          a.ovf[sid] = (uint8_t)(rerun + 1u);  // any slice may set it (same value)
-          if (!SLICED || slice == 0) atomicAdd(ovf_count, 1u);
-        }
+      if (RING && overflow) {  // re-run by the full-order variant (from the list)
+        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = uid;
       } else {
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t0);
 #endif
-        if (RING && tid == 0 && (!SLICED || slice == 0)) a.ovf[sid] = 0;
         write_rows<MODE, LT, BLOCK, SLICED>(a, sid, slice, V, lvl, nh, cost, nt != 0);
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t1);
@@ -424,31 +422,53 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
     unit = s_next;
   }
   // the re-run consumed the flags of its class: its last workgroup clears the count
-  retire_workgroup(ctr, (!RING && rerun) ? ovf_count : nullptr);
+  retire_workgroup(ctr, (!RING && from_list) ? ovf_count : nullptr);
 #ifdef OPENR_SPF_PROFILE
   if (lane == 0 && a.prof)
     for (int i = 0; i < 10; ++i) atomicAdd(&a.prof[i], (unsigned long long)pc[i]);
 #endif
 }
 
-// Fast path: u8 levels + a ring sized so that target workgroups fit a CU.
-uint32_t lvl_ring_cap(const DevGraph& g, bool has_ign, int mode, bool vis, uint32_t target) {
-  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u)) return 0;
-  const uint32_t fixed = lvl_layout<uint8_t>(g.V, g.L, has_ign, nh_words_for(mode, g.V), vis, 0).total;
-  const uint32_t min_cap = std::max<uint32_t>(256u, g.max_deg + 2u);
+// Occupancy first (target workgroups per CU, 8 by default): the full-order u16 variant
+// when it fits the per-workgroup budget, else the u8 ring when a ring wide enough for the
+// estimated two-level frontier fits and the estimated depth stays under the u8 limit;
+// then lower occupancy.
+struct LvlShape {
+  uint32_t ring_cap = 0, per_cu = 1;  // ring_cap == 0: full order
+};
+LvlShape lvl_shape(const DevGraph& g, bool has_ign, int mode, bool vis, uint32_t target) {
+  LvlShape sh;
+  const uint32_t nw = nh_words_for(mode, g.V);
+  const uint32_t fixed = lvl_layout<uint8_t>(g.V, g.L, has_ign, nw, vis, 0).total;
+  const uint32_t full = lvl_layout<uint16_t>(g.V, g.L, has_ign, nw, vis, g.V).total;
+  const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
+  const bool ring_ok = !env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u) && g.est_depth + 8u < LvlOps<uint8_t>::kUnset;
   for (uint32_t want = target; want >= 1; --want) {
     const uint32_t budget = kMaxLds / want;
-    if (budget <= fixed) continue;
+    sh.per_cu = want;
+    if (full <= budget) {
+      sh.ring_cap = 0;
+      break;
+    }
+    if (!ring_ok || budget <= fixed) continue;
     uint32_t cap = 1;
     while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
-    if (cap >= min_cap) return cap;
+    if (cap >= need) {
+      sh.ring_cap = cap;
+      break;
+    }
   }
-  return 0;
+  // test hook: force a (too small) ring so the overflow -> re-run-list path runs
+  const uint32_t forced = env_u32("OPENR_SPF_RING_CAP", 0u, 0u, 65536u);
+  if (forced && (forced & (forced - 1u)) == 0u && forced >= g.max_deg + 2u &&
+      fixed + 2u * forced <= kMaxLds / sh.per_cu)
+    sh.ring_cap = forced;
+  return sh;
 }
 
 template <int MODE, int BLOCK, typename LT, bool RING, int ELLM, bool SLICED>
 hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                              uint32_t ring_cap, uint32_t rerun, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
+                              uint32_t ring_cap, bool from_list, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
                               hipStream_t s, LaunchInfo* info) {
   const bool vis = SLICED || !Nh<MODE>::kSingle;
   const uint32_t lds = lvl_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
@@ -459,47 +479,49 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
-  if (info && !rerun) {
+  if (info && !from_list) {
     info->lds_bytes = lds;
     info->grid = grid;
     info->kernel = RING ? "bfs_lvl_kernel<ring,u8>" : "bfs_lvl_kernel<full,u16>";
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap, rerun, ctr,
-                     ovf_count, nt_stores());
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
+                     (uint32_t)from_list, ctr, ovf_count, nt_stores());
   return hipGetLastError();
 }
 
 template <int MODE, int BLOCK, int ELLM, bool SLICED>
 hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                           uint32_t first_rerun, int num_cus, hipStream_t s, LaunchInfo* info) {
-  // ring/u8 variant first; the solves it flags are re-run by the full-order u16 variant
+                           uint32_t ring_cap, int num_cus, hipStream_t s, LaunchInfo* info) {
+  // Counter block of the class: [0,1] first launch, [2,3] re-run launch, [4] listed units.
   uint32_t* blk = class_counters(a);
-  const bool vis = SLICED || !Nh<MODE>::kSingle;
-  const uint32_t target = env_u32("OPENR_SPF_BFS_WGS", kBfsTargetWgs, 1u, 16u);
-  const uint32_t cap = lvl_ring_cap(g, has_ign, MODE, vis, target);
-  if (!cap)
-    return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, first_rerun,
-                                                                        blk, blk + 4, num_cus, s, info);
-  hipError_t err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, cap,
-                                                                                first_rerun, blk, blk + 4, num_cus, s,
-                                                                                info);
-  if (err != hipSuccess || (g.V <= cap && g.V <= 254u)) return err;
-  return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V,
-                                                                      first_rerun + 1u, blk + 2, blk + 4, num_cus, s,
-                                                                      info);
+  if (!ring_cap)
+    return launch_lvl_variant<MODE, BLOCK, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, false, blk,
+                                                                          blk + 4, num_cus, s, info);
+  hipError_t err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap,
+                                                                                false, blk, blk + 4, num_cus, s, info);
+  if (err != hipSuccess || (g.V <= ring_cap && g.V <= 254u)) return err;  // nothing can overflow
+  return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true, blk + 2,
+                                                                      blk + 4, num_cus, s, info);
 }
 
 template <int MODE, bool SLICED>
-hipError_t launch_lvl_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
-                          uint32_t first_rerun, int ellm, int num_cus, hipStream_t s, LaunchInfo* info) {
-  if (env_u32("OPENR_SPF_BFS_BLOCK", 256u, 128u, 256u) == 128u) {
-    if (ellm == 2) return launch_lvl_mode<MODE, 128, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-    if (ellm == 1) return launch_lvl_mode<MODE, 128, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-    return launch_lvl_mode<MODE, 128, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+hipError_t launch_lvl_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign, int ellm,
+                          int num_cus, hipStream_t s, LaunchInfo* info) {
+  const bool vis = SLICED || !Nh<MODE>::kSingle;
+  const LvlShape sh = lvl_shape(g, has_ign, MODE, vis, env_u32("OPENR_SPF_BFS_WGS", kBfsTargetWgs, 1u, 16u));
+  const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
+  const bool b128 = blk == 128u || (blk != 256u && sh.per_cu > 8u);
+#define OPENR_LVL_MODE(BLK, E) \
+  return launch_lvl_mode<MODE, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, num_cus, s, info)
+  if (b128) {
+    if (ellm == 2) OPENR_LVL_MODE(128, 2);
+    if (ellm == 1) OPENR_LVL_MODE(128, 1);
+    OPENR_LVL_MODE(128, 0);
   }
-  if (ellm == 2) return launch_lvl_mode<MODE, 256, 2, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-  if (ellm == 1) return launch_lvl_mode<MODE, 256, 1, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
-  return launch_lvl_mode<MODE, 256, 0, SLICED>(g, a, cost, glog, has_ign, first_rerun, num_cus, s, info);
+  if (ellm == 2) OPENR_LVL_MODE(256, 2);
+  if (ellm == 1) OPENR_LVL_MODE(256, 1);
+  OPENR_LVL_MODE(256, 0);
+#undef OPENR_LVL_MODE
 }
 }  // namespace
 
@@ -520,29 +542,17 @@ hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
   const bool sliced = cls == kLvlSliced;
   if (sliced && (a.nsl < 1u || a.nsl > 8u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  if (!a.ovf || !a.work) return hipErrorInvalidValue;
+  if (!a.ovf_list || !a.work) return hipErrorInvalidValue;
   uint32_t glog = 0;
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
   const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
-  // bit-parallel multi-source BFS when eligible (opt-in, single-class batches); its
-  // overflowing batches fall through to the per-source kernels
-  uint32_t first_rerun = 0;
-  const MsPlan ms = plan_msbfs(g, a.n, a.nh_bits, has_ign, a.tight != nullptr, num_cus);
-  if (!a.perm && !sliced && ms.use && a.scratch && a.scratch_bytes >= ms.scratch) {
-    hipError_t err = hipMemsetAsync(a.ovf, 0, a.n, s);
-    if (err != hipSuccess) return err;
-    err = launch_msbfs(g, a, cost, a.nh_bits ? a.nh_bits : 1u, ms.lanes, group_lanes, ms.cap, a.scratch, ms.grid, s,
-                       info);
-    if (err != hipSuccess) return err;
-    first_rerun = 1;
-  }
-  if (sliced) return launch_lvl_ell<kNhW1, true>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+  if (sliced) return launch_lvl_ell<kNhW1, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   switch (lvl_class_mode(cls)) {
-    case kNhNibble: return launch_lvl_ell<kNhNibble, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case kNhByte: return launch_lvl_ell<kNhByte, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    case kNhHalf: return launch_lvl_ell<kNhHalf, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
-    default: return launch_lvl_ell<kNhW1, false>(g, a, cost, glog, has_ign, first_rerun, ellm, num_cus, s, info);
+    case kNhNibble: return launch_lvl_ell<kNhNibble, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+    case kNhByte: return launch_lvl_ell<kNhByte, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+    case kNhHalf: return launch_lvl_ell<kNhHalf, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+    default: return launch_lvl_ell<kNhW1, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   }
 }
 

@@ -72,7 +72,8 @@ struct Device {
   // scratch for host-buffer solves
   DevBuf<uint32_t> src, ign_ptr, ign_links;
   DevBuf<uint64_t> dist, tight;
-  DevBuf<uint8_t> nh, ovf, scratch;
+  DevBuf<uint8_t> nh;
+  DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
 };
@@ -104,9 +105,10 @@ struct openr_spf_ctx {
   uint32_t w_min = 0, w_max = 0;
   bool metric_ok = true;        // every usable metric in [1, 2^31-1]
   uint32_t group_lanes = 4;
-  int family = kFamCode;        // BFS kernel family picked for this graph (pick_family)
+  int family = kFamCode;        // BFS kernel family picked for this graph (FrontierEstimate)
   uint32_t cls_mask[kNumFamilies] = {0, 0};  // source classes present among the nodes, per family
   uint32_t nsl[kNumFamilies] = {1, 1};       // next-hop slices of each family's sliced class
+  uint32_t nsl_max() const { return std::max(nsl[0], nsl[1]); }
   openr_spf_stats_t stats{};
 };
 
@@ -132,29 +134,52 @@ int family_override(int dflt) {
   return dflt;
 }
 
-// Family per graph: the lvl kernels win on deep graphs (grid G100: ~150 levels of ~70
-// nodes; 1.19 vs 1.42 ms), the code kernels on shallow ones (fabric: 5 levels; 1.45 vs
-// 1.89 ms). Depth = eccentricity of node 0 over up edges (host BFS, O(V + E)).
-int pick_family(uint32_t V, const uint32_t* row_ptr, const uint32_t* adj) {
-  if (V == 0) return kFamCode;
-  std::vector<uint32_t> lvl(V, UINT32_MAX), q;
+// Frontier shape of a graph, sampled on the host at set_graph (O(samples * (V + E))):
+// BFS from evenly spaced sources plus the widest row, overloaded nodes as sinks
+// (LinkState.cpp:831-838). depth picks the kernel family — the lvl kernels win on deep
+// graphs (grid G100: ~150 levels of ~70 nodes; 1.07 vs 1.92 ms), the code kernels on
+// shallow ones (fabric: 5 levels; 1.44 vs 1.95 ms) — and width2 (max |level L| +
+// |level L+1|) sizes the frontier ring.
+struct FrontierEstimate {
+  uint32_t depth = 0, width2 = 0;
+  int family() const { return depth >= kDeepGraphLevels ? kFamLvl : kFamCode; }
+};
+
+FrontierEstimate estimate_frontier(uint32_t V, const uint32_t* row_ptr, const uint32_t* adj, const uint8_t* ovl) {
+  FrontierEstimate est;
+  if (V == 0) return est;
+  std::vector<uint32_t> srcs;
+  const uint32_t ns = std::min<uint32_t>(V, 8u);
+  for (uint32_t i = 0; i < ns; ++i) srcs.push_back((uint32_t)((uint64_t)i * V / ns));
+  uint32_t widest = 0;
+  for (uint32_t u = 1; u < V; ++u)
+    if (row_ptr[u + 1] - row_ptr[u] > row_ptr[widest + 1] - row_ptr[widest]) widest = u;
+  srcs.push_back(widest);
+  std::vector<uint32_t> lvl(V), q, width;
   q.reserve(V);
-  q.push_back(0);
-  lvl[0] = 0;
-  uint32_t depth = 0;
-  for (size_t i = 0; i < q.size(); ++i) {
-    const uint32_t u = q[i];
-    depth = lvl[u];
-    for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
-      if (adj[e] & kEdgeDown) continue;
-      const uint32_t v = adj[e];
-      if (lvl[v] == UINT32_MAX) {
+  for (uint32_t src : srcs) {
+    std::fill(lvl.begin(), lvl.end(), UINT32_MAX);
+    q.clear();
+    width.assign(1, 1);
+    q.push_back(src);
+    lvl[src] = 0;
+    for (size_t i = 0; i < q.size(); ++i) {
+      const uint32_t u = q[i];
+      if (u != src && ovl[u]) continue;  // reached, never expanded
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+        if (adj[e] & kEdgeDown) continue;
+        const uint32_t v = adj[e];
+        if (lvl[v] != UINT32_MAX) continue;
         lvl[v] = lvl[u] + 1u;
+        if (lvl[v] >= width.size()) width.push_back(0);
+        ++width[lvl[v]];
         q.push_back(v);
       }
     }
+    est.depth = std::max<uint32_t>(est.depth, (uint32_t)width.size() - 1u);
+    for (size_t l = 0; l + 1 < width.size(); ++l) est.width2 = std::max<uint32_t>(est.width2, width[l] + width[l + 1]);
   }
-  return depth >= kDeepGraphLevels ? kFamLvl : kFamCode;
+  return est;
 }
 
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
@@ -192,19 +217,6 @@ int group_lanes_override(int dflt) {
   return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : dflt;
 }
 
-// Device scratch for the multi-source BFS (level bytes per lane); grown on demand.
-hipError_t prepare_scratch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs& a) {
-  a.scratch = nullptr;
-  a.scratch_bytes = 0;
-  if (!p.bfs) return hipSuccess;
-  const MsPlan ms = plan_msbfs(d.g, a.n, ctx->nh_bits, a.ign_ptr != nullptr, a.tight != nullptr, d.num_cus);
-  if (!ms.use) return hipSuccess;
-  hipError_t e = d.scratch.reserve(ms.scratch);
-  if (e != hipSuccess) return e;
-  a.scratch = d.scratch.p;
-  a.scratch_bytes = d.scratch.cap;
-  return hipSuccess;
-}
 
 // Uniform-cost solves run per source class (next-hop width): one class -> one launch;
 // several -> a device-side partition of the batch, then one launch per class, the
@@ -304,11 +316,10 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh_bytes = nh_bytes;
     a.tight = tight ? d.tight.p : nullptr;
     a.nh_bits = ctx->nh_bits;
-    HIP_TRY(d.ovf.reserve(m));
-    a.ovf = d.ovf.p;
+    HIP_TRY(d.ovf.reserve((size_t)m * ctx->nsl_max()));
+    a.ovf_list = d.ovf.p;
     HIP_TRY(reserve_counters(d));
     a.work = d.work.p;
-    HIP_TRY(prepare_scratch(ctx, d, plan, a));
     HIP_TRY(hipEventRecord(d.ev_begin, d.stream));
     HIP_TRY(launch(ctx, d, plan, a, d.stream));
     HIP_TRY(hipEventRecord(d.ev_end, d.stream));
@@ -413,7 +424,6 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.tight.release();
     d.nh.release();
     d.ovf.release();
-    d.scratch.release();
     d.work.release();
     d.perm.release();
     d.part.release();
@@ -521,7 +531,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   }
   for (int f = 0; f < kNumFamilies; ++f)
     if (!cls_mask[f]) cls_mask[f] = 1u;  // no node: class 0
-  const int family = pick_family(V, gr->row_ptr, adj.data());
+  const FrontierEstimate est = estimate_frontier(V, gr->row_ptr, adj.data(), ovl.data());
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
 
   for (Device& d : ctx->devs) {
@@ -533,6 +543,8 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     g.E = E;
     g.L = L;
     for (uint32_t u = 0; u < V; ++u) g.max_deg = std::max(g.max_deg, gr->row_ptr[u + 1] - gr->row_ptr[u]);
+    g.est_width2 = est.width2;
+    g.est_depth = est.depth;
     auto up = [&](auto** dst, const auto* srcp, size_t count) -> hipError_t {
       using T = std::remove_pointer_t<std::remove_pointer_t<decltype(dst)>>;
       hipError_t err = hipMalloc(reinterpret_cast<void**>(dst), std::max<size_t>(count, 1) * sizeof(T));
@@ -569,7 +581,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->w_min = w_min;
   ctx->w_max = w_max;
   ctx->metric_ok = metric_ok;
-  ctx->family = family;
+  ctx->family = est.family();
   for (int f = 0; f < kNumFamilies; ++f) {
     ctx->cls_mask[f] = cls_mask[f];
     ctx->nsl[f] = std::max<uint32_t>(1u, (sliced_deg[f] + slice_bits(f) - 1u) / slice_bits(f));
@@ -645,11 +657,10 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bytes = nh_bytes;
   a.tight = d_tight;
   a.nh_bits = ctx->nh_bits;
-  HIP_TRY(d.ovf.reserve(n));
-  a.ovf = d.ovf.p;
+  HIP_TRY(d.ovf.reserve((size_t)n * ctx->nsl_max()));
+  a.ovf_list = d.ovf.p;
   HIP_TRY(reserve_counters(d));
   a.work = d.work.p;
-  HIP_TRY(prepare_scratch(ctx, d, plan, a));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;

@@ -16,6 +16,8 @@ namespace openr_spf {
 struct DevGraph {
   uint32_t V = 0, E = 0, L = 0;
   uint32_t max_deg = 0;        // largest row (source expansion must fit the frontier queue)
+  uint32_t est_width2 = 0;     // sampled max |level L| + |level L+1| of a BFS (ring sizing)
+  uint32_t est_depth = 0;      // sampled max BFS depth (family choice, u8 level limit)
   uint32_t* row = nullptr;     // [V+1]
   uint2* row2 = nullptr;       // [V] (row[u], row[u+1]) in one 8-byte load
   uint2* row2t = nullptr;      // [V] transit row: row2[u], or an empty range when u is overloaded
@@ -66,9 +68,7 @@ struct SolveArgs {
   uint32_t nh_bytes;
   uint64_t* tight;            // nullable [n][ceil(E/64)] (zeroed by the launcher)
   uint32_t nh_bits;           // bits that are meaningful (max distinct degree)
-  uint8_t* ovf;               // [n] scratch: solves a faster variant could not finish (re-run flags)
-  uint8_t* scratch;           // multi-source BFS level bytes ([grid][V][lanes]); nullable
-  size_t scratch_bytes;
+  uint32_t* ovf_list;         // [n * nsl] scratch: units the ring variant could not finish (re-run list)
   uint32_t* work;             // [kWorkSlots] per-class launch counters (zero at rest: kernels reset them)
   // Source classes (next-hop width): when perm != nullptr this launch solves only the
   // sources of class `cls`: solve k < part[cls] is sid = perm[part[kMaxClasses + cls] + k]
@@ -105,19 +105,6 @@ uint32_t slice_bits(int family);
 // Stable within a class is not required: perm maps class-local index -> sid.
 hipError_t launch_partition(const uint32_t* d_sources, uint32_t n, const uint8_t* d_node_cls, uint32_t V,
                             uint32_t* d_part, uint32_t* d_perm, hipStream_t s);
-
-// Bit-parallel multi-source BFS plan (spf_msbfs.hip).
-struct MsPlan {
-  bool use = false;
-  int lanes = 16;
-  uint32_t cap = 0, lds = 0, grid = 0;
-  size_t scratch = 0;  // bytes of SolveArgs::scratch required
-};
-MsPlan plan_msbfs(const DevGraph& g, uint32_t n, uint32_t nh_bits, bool has_ign, bool tight, int num_cus);
-hipError_t launch_msbfs(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t D, int lanes,
-                        int group_lanes, uint32_t cap, uint8_t* scratch, uint32_t grid, hipStream_t s,
-                        LaunchInfo* info);
-
 
 // Uniform edge cost c (all usable edges cost c, or useLinkMetric=false): BFS levels,
 // sources of class a.cls of `family` (a.nsl slices for the sliced class).

@@ -56,7 +56,7 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 counts 128-B requests at 64 B); WRITE_SIZE as counted",
     })
     # n_sources of the launch: all V of the topology (bench default weak scaling, 1 rank)
-    res["n_sources"] = {"grid100": 10000}.get(topo)
+    res["n_sources"] = {"grid100": 10000, "fabric": 4992, "wan": 1000}.get(topo)
     print(json.dumps(res, indent=1))
 
 

@@ -18,8 +18,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"G": "OPENR_SPF_GROUP_LANES", "FULL": "OPENR_SPF_BFS_FULL", "MS": "OPENR_SPF_MSBFS",  # MS=1 enables
-        "LANES": "OPENR_SPF_MS_LANES", "WGS": "OPENR_SPF_BFS_WGS", "NT": "OPENR_SPF_NT", "BLK": "OPENR_SPF_BFS_BLOCK",
+KEYS = {"G": "OPENR_SPF_GROUP_LANES", "FULL": "OPENR_SPF_BFS_FULL",
+        "WGS": "OPENR_SPF_BFS_WGS", "NT": "OPENR_SPF_NT", "BLK": "OPENR_SPF_BFS_BLOCK",
         "FAM": "OPENR_SPF_BFS_FAMILY"}
 
 

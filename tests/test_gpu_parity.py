@@ -229,10 +229,11 @@ def test_large_metrics_use_u64_distances(eng):
     assert int(dist.max()) > 0xFFFFFFFF
 
 
-@pytest.mark.parametrize("ms", ["0", "1"])
-def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, ms):
-    """BFS deeper than 253 levels: the u8-level pass flags it, the u16 pass re-runs it."""
-    monkeypatch.setenv("OPENR_SPF_MSBFS", ms)
+@pytest.mark.parametrize("full", ["0", "1"])
+def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, full):
+    """BFS deeper than 253 levels: a u8-level ring pass flags it and the full-order pass
+    re-runs it from the list (or the full-order variant runs alone)."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FULL", full)
     V = 700
     names = [f"p{i:04d}" for i in range(V)]
     links = np.array([(i, i + 1) for i in range(V - 1)])
@@ -244,36 +245,19 @@ def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, ms):
     check_against_oracle(eng, g, srcs, True, ignore=ignore)
 
 
-@pytest.fixture
-def msbfs_on(monkeypatch):
-    monkeypatch.setenv("OPENR_SPF_MSBFS", "1")
-
-
-def test_msbfs_list_overflow_reruns(eng, monkeypatch, msbfs_on):
-    """A frontier larger than the multi-source kernel's list re-runs per source."""
-    monkeypatch.setenv("OPENR_SPF_MS_CAP", "16")
-    g = T.grid_fast(16)
-    dist, _ = check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
-    monkeypatch.setenv("OPENR_SPF_MS_LANES", "8")
-    check_against_oracle(eng, g, list(range(0, g.num_nodes, 3)), True, check_pathlinks=False)
-
-
-@pytest.mark.parametrize("lanes", ["8", "16"])
-def test_msbfs_lane_widths(eng, monkeypatch, lanes, msbfs_on):
-    monkeypatch.setenv("OPENR_SPF_MS_LANES", lanes)
-    for seed in range(3):
-        g = random_graph(200 + seed, 90, 200, 1)
-        check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
-        check_against_oracle(eng, g, list(range(g.num_nodes)), False, check_pathlinks=False)
-
-
-def test_msbfs_matches_per_source(eng, monkeypatch):
-    g = T.grid_fast(20)
+def test_ring_overflow_rerun_list(eng, monkeypatch):
+    """A ring too small for the frontier (forced: levels of ~1000 nodes on a random
+    expander) flags every solve; the full-order pass re-runs them from the list."""
+    g = random_graph(5, 3000, 6000, 1, p_ovl=0.02)
+    srcs = list(range(0, g.num_nodes, 11))
     eng.set_graph(g)
-    d1, n1, _ = eng.solve(range(400), True)
-    monkeypatch.setenv("OPENR_SPF_MSBFS", "1")
-    d2, n2, _ = eng.solve(range(400), True)
+    d1, n1, _ = eng.solve(srcs, True)
+    monkeypatch.setenv("OPENR_SPF_RING_CAP", "256")
+    check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
+    d2, n2, _ = eng.solve(srcs, True)
     assert np.array_equal(d1, d2) and np.array_equal(n1, n2)
+    hub = hub_graph(4)  # sliced classes: every (solve, slice) unit is listed on its own
+    check_against_oracle(eng, hub, list(range(hub.num_nodes)), True, check_pathlinks=False)
 
 
 # --- edge cases -------------------------------------------------------------
