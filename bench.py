@@ -166,10 +166,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from openr_amd.shard import max_over_ranks
+
+    elapsed = max_over_ranks(elapsed, dev)  # the slowest rank's clock
 
     # correctness spot check (grid: Manhattan distances) outside the timed region
     if args.topology == "grid100" and n_local:
@@ -190,11 +189,9 @@ def main():
         tg = time.perf_counter()
         allgather_results(d_dist, d_nh, V, world)
         torch.cuda.synchronize(dev)
-        gms = (time.perf_counter() - tg) * 1e3
-        t = torch.tensor([gms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        gather = {"ms": float(t.item()), "bytes": int(V * V * (8 + nb)),
-                  "gather_inclusive_value": V / (elapsed / args.steps + float(t.item()) / 1e3)}
+        gms = max_over_ranks((time.perf_counter() - tg) * 1e3, dev)
+        gather = {"ms": gms, "bytes": int(V * V * (8 + nb)),
+                  "gather_inclusive_value": V / (elapsed / args.steps + gms / 1e3)}
 
     solves_total = (V if args.scaling == "strong" else V * world) * args.steps
     value = solves_total / elapsed

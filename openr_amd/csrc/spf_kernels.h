@@ -41,7 +41,7 @@ constexpr uint32_t kEdgeDown = 0x80000000u;
 constexpr uint32_t kNodeSink = 0x40000000u;
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
-constexpr uint32_t kBfsTargetWgs = 8;     // fast-path BFS sizes its LDS for this many workgroups per CU
+constexpr uint32_t kBfsTargetWgs = 12;    // lvl BFS sizes its ring for this many workgroups per CU (G100: 8 -> 1.06 ms, 9..16 -> 1.02 ms)
 
 // Next-hop bitset storage classes in LDS (chosen from the max distinct degree).
 enum NhMode : int { kNhByte = 0, kNhHalf = 1, kNhW1 = 2, kNhW2 = 3, kNhW4 = 4, kNhW8 = 5, kNhNibble = 6 };

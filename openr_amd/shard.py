@@ -48,3 +48,16 @@ def allgather_results(dist_shard, nh_shard, n_units: int, world: int):
         parts = [full[r * m : r * m + sizes[r]] for r in range(world)]
         outs.append(torch.cat(parts, dim=0))
     return outs[0], outs[1]
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """MAX of a host scalar over all ranks (bench timing: the slowest rank's clock);
+    the identity without an initialised process group."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

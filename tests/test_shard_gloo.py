@@ -1,0 +1,68 @@
+"""Multi-rank sharding on CPU (gloo): contiguous source blocks per rank, the result
+all-gather of uneven shards (shard.py), and the max-over-ranks timing reduction the
+bench uses. The per-rank solve here is the CPU oracle standing in for the GPU engine
+(test infrastructure only); the GPU path runs the same shard.py code over RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from openr_amd import shard
+from openr_amd import topology as T
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, out_dir):
+    import torch.distributed as dist
+
+    from oracle import Oracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    g = T.grid_fast(n)
+    V = g.num_nodes
+    lo, hi = shard.shard_range(V, rank, world)
+    d, nh = Oracle(g).all_sources(np.arange(lo, hi, dtype=np.uint32))
+    d_t = torch.from_numpy(d.view(np.int64).copy())
+    nh_t = torch.from_numpy(nh.copy())
+    full_d, full_nh = shard.allgather_results(d_t, nh_t, V, world)
+    t = shard.max_over_ranks(float(rank + 1))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "dist.npy"), full_d.numpy())
+        np.save(os.path.join(out_dir, "nh.npy"), full_nh.numpy())
+        np.save(os.path.join(out_dir, "tmax.npy"), np.array([t]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 5), (3, 4), (2, 8)])
+def test_sharded_all_sources_allgather(tmp_path, world, n):
+    mp.start_processes(_worker, args=(world, _free_port(), n, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    from oracle import Oracle
+
+    g = T.grid_fast(n)
+    V = g.num_nodes
+    d, nh = Oracle(g).all_sources(np.arange(V, dtype=np.uint32))
+    np.testing.assert_array_equal(np.load(tmp_path / "dist.npy").view(np.uint64), d)
+    np.testing.assert_array_equal(np.load(tmp_path / "nh.npy"), nh)
+    assert float(np.load(tmp_path / "tmax.npy")[0]) == float(world)
+
+
+def test_shard_ranges_cover_exactly():
+    for n_units in (0, 1, 7, 10000):
+        for world in (1, 2, 3, 8):
+            rs = [shard.shard_range(n_units, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n_units
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            sizes = shard.shard_sizes(n_units, world)
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_range(10, 2, 2)
