@@ -98,6 +98,107 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
     }
 
 
+def whatif_cpu_baseline(g, seconds: float, use_metric: bool):
+    """The oracle on a bounded sample of what-if units: runSpf(src, {link}) per unit,
+    no skipping of unaffected units (the reference has no what-if path to skip with)."""
+    from oracle import Oracle
+
+    o = Oracle(g)
+    rng = np.random.default_rng(0)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(64):
+            o.run_spf(int(rng.integers(g.num_nodes)), use_metric, [int(rng.integers(g.num_links))])
+        n += 64
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "units/s", "cores": 1, "kind": "port",
+            "sample": f"{n} random (link, source) units, one oracle runSpf with a 1-link ignore set each, "
+                      f"dist+next-hops+pathLinks, 1 thread, {dt:.1f}s"}
+
+
+def whatif_main(args):
+    """BASELINE config 4: per-link-failure what-if sweep on the 1k-node WAN topology
+    (heterogeneous metrics U[1,64]); a step = every (failed link, source) unit, one
+    openr_spf_whatif_device call (base SPF, affected-unit filter, chunked solves,
+    row comparison). Per rank: its contiguous block of links (shard.py), weak scaling
+    is one WAN per GPU like the all-sources bench."""
+    import torch
+    import torch.distributed as dist
+
+    from openr_amd.engine import SpfEngine
+    from openr_amd.shard import max_over_ranks
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    g, cfg = build_topology("wan")
+    V, L = g.num_nodes, g.num_links
+    eng = SpfEngine([local_rank])
+    eng.set_graph(g)
+    use_metric = not args.no_metric
+    links = torch.arange(0, L, dtype=torch.int32, device=dev)
+    srcs = torch.arange(0, V, dtype=torch.int32, device=dev)
+    changed = torch.empty((L, V), dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    solved = [0]
+
+    def step():
+        solved[0] = eng.whatif_device(links.data_ptr(), L, srcs.data_ptr(), V, changed.data_ptr(), use_metric,
+                                      stream=stream.cuda_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    units = L * V
+    value = units * world * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    srcs_np = np.arange(V)
+    per_src = algorithmic_bytes(g, srcs_np) / V  # mean B(src)
+    bytes_step = per_src * units
+    bytes_solved = per_src * solved[0]
+    achieved = bytes_step / (elapsed / args.steps) / 1e9
+    if rank == 0:
+        out = {
+            "metric": "per-link-failure what-if SPF units/sec (link x source), 1k-node WAN, U[1,64] metrics",
+            "value": value, "unit": "units/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64", "data": "synthetic (seeded WAN generator, SURVEY.md Appendix B)",
+            "config": dict(cfg, workload="wan1k-whatif-all-links-x-all-sources", units_per_step=units,
+                           spf_solved_per_step=solved[0], use_link_metric=use_metric,
+                           parallelism=f"area-per-GPU x{world}"),
+            "solved_per_s": solved[0] * world * args.steps / elapsed,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_step": bytes_step,
+                         "note": "SURVEY.md 8d: B(src) per what-if unit, units resolved by the tight-edge "
+                                 "filter included; solved units only: "
+                                 f"{bytes_solved / (elapsed / args.steps) / 1e9:.1f} GB/s"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = whatif_cpu_baseline(g, min(args.cpu_seconds, 10.0), use_metric)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,7 +211,12 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
+    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif"],
+                    help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
+                         "(BASELINE config 4)")
     args = ap.parse_args()
+    if args.workload == "whatif":
+        return whatif_main(args)
 
     import torch
     import torch.distributed as dist

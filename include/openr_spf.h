@@ -18,6 +18,8 @@
  *                              what-if sweeps; one (source, ignore-set) pair per solve
  *   openr_spf_solve_device     the same on device-resident buffers and a caller stream
  *                              (batched prefetch / benchmarks / multi-GPU shards)
+ *   openr_spf_whatif           per-link-failure what-if sweep: runSpf(src, useLinkMetric, {link})
+ *                              for every (link, source), reduced to changed-node counts
  *   openr_spf_last_error       glog CHECK / exception text of the reference
  *
  * Conventions
@@ -144,6 +146,26 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index,
                            const uint32_t* d_ignore_ptr, const uint32_t* d_ignore_links,
                            uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes,
                            uint64_t* d_tight, void* stream);
+
+/* Per-link-failure what-if sweep (no reference API: the north-star what-if workload over
+   LinkState::runSpf(src, useLinkMetric, {link}), LinkState.cpp:808-882 with the
+   linksToIgnore argument getKthPaths uses at :769-779). Unit (i, j) fails links[i] for
+   sources[j]; changed[i * n_sources + j] = number of nodes whose distance or next-hop
+   set differs from the no-failure SPF of sources[j] (a node that becomes unreachable
+   counts). A link with no tight edge in the base SPF cannot change the result: such
+   units are 0 without a solve. *out_solved (nullable) = SPFs actually run (base solves
+   + affected units), also added to stats.spf_runs. Links are split across devices. */
+int openr_spf_whatif(openr_spf_ctx* ctx, const uint32_t* links, uint32_t n_links,
+                     const uint32_t* sources, uint32_t n_sources, uint32_t flags,
+                     uint32_t* changed, uint64_t* out_solved);
+
+/* Device-buffer form (pointers are device memory; d_changed [n_links][n_sources]).
+   Synchronizes `stream` once (the affected-unit count sizes the chunked solves).
+   Link ids >= L are never affected (0). */
+int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_links,
+                            uint32_t n_links, const uint32_t* d_sources, uint32_t n_sources,
+                            uint32_t flags, uint32_t* d_changed, void* stream,
+                            uint64_t* out_solved);
 
 int openr_spf_get_stats(const openr_spf_ctx* ctx, openr_spf_stats_t* out);
 

@@ -76,6 +76,10 @@ struct Device {
   DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
+  // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
+  DevBuf<uint64_t> base_dist, base_tight, wdist;
+  DevBuf<uint8_t> base_nh, wnh;
+  DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -88,7 +92,7 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj,    g.w,
-                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl};
+                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -351,6 +355,88 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
   return OPENR_SPF_OK;
 }
 
+// Bytes of chunk result rows a what-if sweep may hold on a device at once.
+constexpr size_t kWhatifChunkBytes = size_t(1) << 30;
+
+// Per-link-failure what-if sweep on one device (spf_sweep.hip has the unit semantics):
+// base SPF with tight edges -> filter of the affected units -> chunks of single-link
+// ignore-set solves through the ordinary launcher -> row comparison against the base.
+// Reads the affected-unit count back (one stream sync) to size the chunks.
+hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, const Plan& ign_plan,
+                            const uint32_t* d_links, uint32_t n_links, const uint32_t* d_sources, uint32_t n_src,
+                            uint32_t* d_changed, hipStream_t s, uint32_t* solved) {
+  const uint32_t V = ctx->V, tw = (ctx->E + 63u) / 64u;
+  const uint32_t nb = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
+  *solved = 0;
+  if (!n_src || !n_links) return hipSuccess;
+  hipError_t err;
+#define OPENR_TRY(x)              \
+  do {                            \
+    err = (x);                    \
+    if (err != hipSuccess) return err; \
+  } while (0)
+  OPENR_TRY(d.base_dist.reserve((size_t)n_src * V));
+  OPENR_TRY(d.base_nh.reserve((size_t)n_src * V * nb));
+  OPENR_TRY(d.base_tight.reserve((size_t)n_src * tw));
+  OPENR_TRY(reserve_counters(d));
+  SolveArgs a{};
+  a.sources = d_sources;
+  a.n = n_src;
+  a.dist = d.base_dist.p;
+  a.nh = d.base_nh.p;
+  a.nh_bytes = nb;
+  a.tight = d.base_tight.p;
+  a.nh_bits = ctx->nh_bits;
+  OPENR_TRY(d.ovf.reserve((size_t)n_src * ctx->nsl_max()));
+  a.ovf_list = d.ovf.p;
+  a.work = d.work.p;
+  OPENR_TRY(launch(ctx, d, base_plan, a, s));
+  const size_t units = (size_t)n_links * n_src;
+  OPENR_TRY(d.wsrc.reserve(units));
+  OPENR_TRY(d.wlink.reserve(units));
+  OPENR_TRY(d.wunit.reserve(units));
+  OPENR_TRY(d.wcount.reserve(1));
+  OPENR_TRY(launch_whatif_filter(d.g, d_links, n_links, d_sources, n_src, d.base_tight.p, d_changed, d.wsrc.p,
+                                 d.wlink.p, d.wunit.p, d.wcount.p, d.num_cus, s));
+  uint32_t count = 0;
+  OPENR_TRY(hipMemcpyAsync(&count, d.wcount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  OPENR_TRY(hipStreamSynchronize(s));
+  *solved = count;
+  if (!count) return hipSuccess;
+  const size_t row = (size_t)V * (8u + nb);
+  const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
+  OPENR_TRY(d.wdist.reserve((size_t)chunk * V));
+  OPENR_TRY(d.wnh.reserve((size_t)chunk * V * nb));
+  OPENR_TRY(d.wiota.reserve((size_t)chunk + 1u));
+  OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
+  OPENR_TRY(launch_iota(d.wiota.p, chunk + 1u, d.num_cus, s));
+  for (uint32_t off = 0; off < count; off += chunk) {
+    const uint32_t m = std::min(chunk, count - off);
+    SolveArgs b{};
+    b.sources = d.wsrc.p + off;
+    b.n = m;
+    b.ign_ptr = d.wiota.p;  // solve k ignores exactly wlink[off + k]
+    b.ign_links = d.wlink.p + off;
+    b.dist = d.wdist.p;
+    b.nh = d.wnh.p;
+    b.nh_bytes = nb;
+    b.nh_bits = ctx->nh_bits;
+    b.ovf_list = d.ovf.p;
+    b.work = d.work.p;
+    OPENR_TRY(launch(ctx, d, ign_plan, b, s));
+    OPENR_TRY(launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
+                                  d_changed, d.num_cus, s));
+  }
+#undef OPENR_TRY
+  return hipSuccess;
+}
+
+int whatif_plans(openr_spf_ctx* ctx, uint32_t flags, Plan* base_plan, Plan* ign_plan) {
+  int rc = make_plan(ctx, flags, false, base_plan);
+  if (rc) return rc;
+  return make_plan(ctx, flags, true, ign_plan);
+}
+
 }  // namespace
 
 extern "C" {
@@ -427,6 +513,10 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.work.release();
     d.perm.release();
     d.part.release();
+    void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
+                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p};
+    for (void* p : sweep)
+      if (p) (void)hipFree(p);
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -450,6 +540,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   std::vector<uint8_t> ovl(V);
   // link id -> its two directed edges
   std::vector<uint32_t> first(L, UINT32_MAX), second(L, UINT32_MAX);
+  std::vector<uint2> ledge(L);
   uint32_t nh_bits = 0, w_min = UINT32_MAX, w_max = 0;
   bool metric_ok = true;
   std::vector<uint32_t> seen_stamp(V, UINT32_MAX), seen_idx(V, 0);
@@ -494,8 +585,11 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
       return fail(OPENR_SPF_EINVAL, "link %u edge_up differs by direction (Link::isUp is per link)", l);
     rev[a] = b;
     rev[b] = a;
+    ledge[l] = make_uint2(a, b);
   }
   for (uint32_t e = 0; e < E; ++e) win[e] = w[rev[e]];
+  for (uint32_t l = 0; l < L; ++l)
+    if (first[l] == UINT32_MAX) ledge[l] = make_uint2(UINT32_MAX, UINT32_MAX);  // unused id: never affected
   // transit views: an overloaded node is reached but never expanded unless it is the
   // source (LinkState.cpp:831-838), so its transit row is empty / all-down
   std::vector<uint2> row2(V), row2t(V);
@@ -566,6 +660,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.ovl, ovl.data(), V);
     if (err == hipSuccess) err = up(&g.cls, cls[kFamCode].data(), V);
     if (err == hipSuccess) err = up(&g.cls_lvl, cls[kFamLvl].data(), V);
+    if (err == hipSuccess) err = up(&g.ledge, ledge.data(), L);
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;
@@ -665,6 +760,74 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;
   ctx->stats.batches += 1;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_whatif(openr_spf_ctx* ctx, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                     uint32_t n_sources, uint32_t flags, uint32_t* changed, uint64_t* out_solved) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if ((n_links && !links) || (n_sources && !sources) || (n_links && n_sources && !changed))
+    return fail(OPENR_SPF_EINVAL, "null links, sources or changed");
+  for (uint32_t i = 0; i < n_sources; ++i)
+    if (sources[i] >= ctx->V) return fail(OPENR_SPF_EINVAL, "source %u out of range (V=%u)", sources[i], ctx->V);
+  for (uint32_t i = 0; i < n_links; ++i)
+    if (links[i] >= ctx->L) return fail(OPENR_SPF_EINVAL, "link %u out of range (L=%u)", links[i], ctx->L);
+  Plan bp, ip;
+  int rc = whatif_plans(ctx, flags, &bp, &ip);
+  if (rc) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  // links are split in contiguous blocks across the context's devices
+  const uint32_t nd = (uint32_t)ctx->devs.size();
+  const uint32_t per = (n_links + nd - 1) / std::max<uint32_t>(nd, 1);
+  uint64_t solved_total = 0;
+  for (uint32_t di = 0; di < nd; ++di) {
+    Device& d = ctx->devs[di];
+    const uint32_t b = std::min(n_links, di * per), e = std::min(n_links, b + per), m = e - b;
+    if (!m || !n_sources) continue;
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(d.win_links.reserve(m));
+    HIP_TRY(d.win_src.reserve(n_sources));
+    HIP_TRY(d.wchanged.reserve((size_t)m * n_sources));
+    HIP_TRY(hipMemcpyAsync(d.win_links.p, links + b, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.win_src.p, sources, n_sources * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    uint32_t solved = 0;
+    HIP_TRY(whatif_on_device(ctx, d, bp, ip, d.win_links.p, m, d.win_src.p, n_sources, d.wchanged.p, d.stream,
+                             &solved));
+    HIP_TRY(hipMemcpyAsync(changed + (size_t)b * n_sources, d.wchanged.p, (size_t)m * n_sources * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    solved_total += solved + n_sources;
+  }
+  ctx->stats.spf_runs += solved_total;
+  ctx->stats.batches += 1;
+  ctx->stats.last_batch_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (out_solved) *out_solved = solved_total;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_links, uint32_t n_links,
+                            const uint32_t* d_sources, uint32_t n_sources, uint32_t flags, uint32_t* d_changed,
+                            void* stream, uint64_t* out_solved) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  if ((n_links && !d_links) || (n_sources && !d_sources) || (n_links && n_sources && !d_changed))
+    return fail(OPENR_SPF_EINVAL, "null links, sources or changed");
+  Plan bp, ip;
+  int rc = whatif_plans(ctx, flags, &bp, &ip);
+  if (rc) return rc;
+  Device& d = ctx->devs[device_index];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  uint32_t solved = 0;
+  HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_sources, d_changed, s, &solved));
+  const uint64_t total = n_links && n_sources ? (uint64_t)solved + n_sources : 0u;
+  ctx->stats.spf_runs += total;
+  ctx->stats.batches += 1;
+  if (out_solved) *out_solved = total;
   return OPENR_SPF_OK;
 }
 

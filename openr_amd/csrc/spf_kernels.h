@@ -33,6 +33,7 @@ struct DevGraph {
   uint8_t* ovl = nullptr;      // [V] overloaded
   uint8_t* cls = nullptr;      // [V] source class of each node, code family (SrcClass)
   uint8_t* cls_lvl = nullptr;  // [V] source class of each node, lvl family (LvlClass)
+  uint2* ledge = nullptr;      // [L] the two directed edges of each link (UINT32_MAX if unused)
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
@@ -119,6 +120,18 @@ hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
 // delta-stepping with settle-safe buckets) and a pull pass for next-hops.
 hipError_t launch_bucket(const DevGraph& g, const SolveArgs& a, uint32_t delta, bool dist64,
                          int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
+
+// What-if sweep (spf_sweep.hip): unit u = i * n_src + j (links[i] failed, sources[j]).
+// Filter: changed[u] = 0 for every unit; units whose link has a tight edge in
+// base_tight[j] are appended to (wsrc, wlink, wunit), *wcount of them.
+hipError_t launch_whatif_filter(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                                uint32_t n_src, const uint64_t* base_tight, uint32_t* changed, uint32_t* wsrc,
+                                uint32_t* wlink, uint32_t* wunit, uint32_t* wcount, int num_cus, hipStream_t s);
+// changed[wunit[k]] = nodes whose dist / next-hop bytes differ from base row wunit[k] % n_src.
+hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64_t* dist, const uint8_t* nh,
+                               const uint64_t* base_dist, const uint8_t* base_nh, const uint32_t* wunit,
+                               uint32_t n_src, uint32_t* changed, int num_cus, hipStream_t s);
+hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);

@@ -33,6 +33,8 @@ EXPORTS = (
     "openr_spf_solve",
     "openr_spf_solve_ignore",
     "openr_spf_solve_device",
+    "openr_spf_whatif",
+    "openr_spf_whatif_device",
     "openr_spf_get_stats",
 )
 
@@ -98,6 +100,8 @@ def load_library():
     l.openr_spf_solve.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp]
     l.openr_spf_solve_ignore.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, u32, vp]
     l.openr_spf_solve_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
+    l.openr_spf_whatif.argtypes = [vp, vp, u32, vp, u32, u32, vp, P(ctypes.c_uint64)]
+    l.openr_spf_whatif_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, P(ctypes.c_uint64)]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
     for name in EXPORTS:
         if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy"):
@@ -193,6 +197,29 @@ class SpfEngine:
                                                 vp(d_ignore_ptr or None), vp(d_ignore_links or None), vp(d_dist),
                                                 vp(d_nh or None), nh_bytes or self.nh_bytes, vp(d_tight or None),
                                                 vp(stream or None)))
+
+    def whatif(self, links: Sequence[int], sources: Sequence[int], use_link_metric: bool = True
+               ) -> Tuple[np.ndarray, int]:
+        """Per-link-failure sweep: (changed[n_links, n_sources] u32, SPFs run)."""
+        lk = np.ascontiguousarray(links, dtype=np.uint32)
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        changed = np.zeros((lk.shape[0], src.shape[0]), dtype=np.uint32)
+        solved = ctypes.c_uint64()
+        flags = USE_LINK_METRIC if use_link_metric else 0
+        _check(self._lib.openr_spf_whatif(self._ctx, _p(lk), lk.shape[0], _p(src), src.shape[0], flags,
+                                          _p(changed), ctypes.byref(solved)))
+        return changed, int(solved.value)
+
+    def whatif_device(self, d_links: int, n_links: int, d_sources: int, n_sources: int, d_changed: int,
+                      use_link_metric: bool = True, stream: int = 0, device_index: int = 0) -> int:
+        """Device-pointer form; returns the number of SPFs run."""
+        vp = ctypes.c_void_p
+        solved = ctypes.c_uint64()
+        flags = USE_LINK_METRIC if use_link_metric else 0
+        _check(self._lib.openr_spf_whatif_device(self._ctx, device_index, vp(d_links), n_links, vp(d_sources),
+                                                 n_sources, flags, vp(d_changed), vp(stream or None),
+                                                 ctypes.byref(solved)))
+        return int(solved.value)
 
     def stats(self) -> SpfStats:
         s = SpfStats()

@@ -369,3 +369,71 @@ def test_source_classes_device_partition(eng):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d_dist.cpu().numpy().view(np.uint64), dist_h)
     np.testing.assert_array_equal(d_nh.cpu().numpy(), nh_h)
+
+
+# --- per-link-failure what-if sweep (openr_spf_whatif) -----------------------
+def whatif_oracle(g, links, sources, use_metric=True):
+    """changed[i, j] = nodes whose dist or next-hop set differ between runSpf(s) and
+    runSpf(s, {links[i]}) on the oracle."""
+    o = Oracle(g)
+    base = {s: o.run_spf(int(s), use_metric) for s in sources}
+    out = np.zeros((len(links), len(sources)), dtype=np.uint32)
+    for i, l in enumerate(links):
+        for j, s in enumerate(sources):
+            r = o.run_spf(int(s), use_metric, [int(l)])
+            b = base[s]
+            out[i, j] = int(np.count_nonzero((r.dist != b.dist) | np.any(r.nh != b.nh, axis=1)))
+    return out
+
+
+@pytest.mark.parametrize("seed,max_metric", [(0, 64), (1, 1), (2, 7)])
+def test_whatif_sweep_matches_oracle(eng, seed, max_metric):
+    g = random_graph(300 + seed, 120, 300, max_metric, p_ovl=0.05, p_down=0.05, p_par=0.1)
+    eng.set_graph(g)
+    links = list(range(g.num_links))
+    sources = list(range(0, g.num_nodes, 3))
+    changed, solved = eng.whatif(links, sources, True)
+    want = whatif_oracle(g, links, sources, True)
+    np.testing.assert_array_equal(changed, want)
+    # only units whose link is on a shortest path are solved, plus the base solves
+    assert len(sources) <= solved < len(links) * len(sources) + len(sources)
+    c2, _ = eng.whatif(links[::5], sources[:7], False)
+    np.testing.assert_array_equal(c2, whatif_oracle(g, links[::5], sources[:7], False))
+
+
+def test_whatif_wan_sample_and_device_form(eng):
+    import torch
+
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    rng = np.random.default_rng(11)
+    links = np.sort(rng.choice(g.num_links, 40, replace=False)).astype(np.uint32)
+    sources = np.sort(rng.choice(g.num_nodes, 12, replace=False)).astype(np.uint32)
+    changed, _ = eng.whatif(links, sources, True)
+    np.testing.assert_array_equal(changed, whatif_oracle(g, links, sources, True))
+    dev = torch.device("cuda", 0)
+    d_l = torch.from_numpy(links.astype(np.int32)).to(dev)
+    d_s = torch.from_numpy(sources.astype(np.int32)).to(dev)
+    d_c = torch.full((len(links), len(sources)), -1, dtype=torch.int32, device=dev)
+    eng.whatif_device(d_l.data_ptr(), len(links), d_s.data_ptr(), len(sources), d_c.data_ptr(), True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_c.cpu().numpy().view(np.uint32), changed)
+
+
+def test_whatif_edge_cases(eng):
+    g = T.grid_fast(6)
+    eng.set_graph(g)
+    c, solved = eng.whatif([], [0, 1], True)
+    assert c.shape == (0, 2) and solved == 0
+    c, solved = eng.whatif([0, 1], [], True)
+    assert c.shape == (2, 0)
+    with pytest.raises(SpfError) as ei:
+        eng.whatif([g.num_links], [0], True)
+    assert ei.value.code == EINVAL
+    with pytest.raises(SpfError):
+        eng.whatif([0], [g.num_nodes], True)
+    # a grid edge failure: exact counts against the oracle, all links x all sources
+    links = list(range(g.num_links))
+    srcs = list(range(g.num_nodes))
+    c, _ = eng.whatif(links, srcs, True)
+    np.testing.assert_array_equal(c, whatif_oracle(g, links, srcs, True))
