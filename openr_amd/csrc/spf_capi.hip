@@ -206,8 +206,8 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
     p->bfs = false;
     p->delta = ctx->w_min;
     p->dist64 = (uint64_t)ctx->V * ctx->w_max >= 0xFFFFFFFFull;
-    if (!bucket_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64))
-      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident bucket kernel", ctx->V);
+    if (!fringe_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64))
+      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident general-metric kernel", ctx->V);
   }
   return OPENR_SPF_OK;
 }
@@ -231,7 +231,7 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((d.g.E + 63u) / 64u) * 8u, s);
     if (err != hipSuccess) return err;
   }
-  if (!p.bfs) return launch_bucket(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+  if (!p.bfs) return launch_fringe(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
   const int gl = group_lanes_override((int)ctx->group_lanes);
   a.perm = nullptr;
   a.part = nullptr;

@@ -107,7 +107,7 @@ __device__ __forceinline__ uint32_t wave_append(bool fresh, uint32_t* counter) {
 __device__ __forceinline__ void load_ignore(uint32_t* ign, uint32_t words, const SolveArgs& a,
                                             uint32_t sid, uint32_t L) {
   const uint32_t b = a.ign_ptr[sid], e = a.ign_ptr[sid + 1];
-  for (uint32_t k = b + threadIdx.x; k < e; k += kBlock) {
+  for (uint32_t k = b + threadIdx.x; k < e; k += blockDim.x) {  // any workgroup size
     const uint32_t l = a.ign_links[k];
     if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
   }

@@ -83,6 +83,7 @@ struct SolveArgs {
 constexpr uint32_t kMaxClasses = 8;
 constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch, [4] flagged solves
 constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
+constexpr uint32_t kFringeCtr = kCtrPerClass * (kMaxClasses - 1);  // BFS classes use < 7 blocks
 
 // Uniform-cost BFS kernel families (spf_capi.hip picks one per graph):
 //  * code (spf_bfs.hip): one packed LDS field per node = [next-hop bits | 3-bit level
@@ -116,9 +117,10 @@ hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost,
 hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
                           hipStream_t s, LaunchInfo* info);
 
-// General positive metrics: buckets of width delta = min usable metric (Dial /
-// delta-stepping with settle-safe buckets) and a pull pass for next-hops.
-hipError_t launch_bucket(const DevGraph& g, const SolveArgs& a, uint32_t delta, bool dist64,
+// General positive metrics (spf_fringe.hip): one wavefront per solve, settle-safe
+// buckets of width delta = min usable metric over a fringe list, next hops pulled over
+// tight in-edges. Uses a.work[kFringeCtr, +2) for dynamic scheduling.
+hipError_t launch_fringe(const DevGraph& g, const SolveArgs& a, uint32_t delta, bool dist64,
                          int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
 
 // What-if sweep (spf_sweep.hip): unit u = i * n_src + j (links[i] failed, sources[j]).
@@ -137,7 +139,7 @@ hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
-uint32_t bucket_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
+uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
 
 }  // namespace openr_spf
