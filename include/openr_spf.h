@@ -20,6 +20,8 @@
  *                              (batched prefetch / benchmarks / multi-GPU shards)
  *   openr_spf_whatif           per-link-failure what-if sweep: runSpf(src, useLinkMetric, {link})
  *                              for every (link, source), reduced to changed-node counts
+ *   openr_spf_ksp2             LinkState::getKthPaths(src, dst, 1 and 2) (LinkState.cpp:762-791)
+ *                              for a batch of pairs, paths traced on the device
  *   openr_spf_last_error       glog CHECK / exception text of the reference
  *
  * Conventions
@@ -166,6 +168,24 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
                             uint32_t n_links, const uint32_t* d_sources, uint32_t n_sources,
                             uint32_t flags, uint32_t* d_changed, void* stream,
                             uint64_t* out_solved);
+
+/* LinkState::getKthPaths(src[i], dst[i], 1) and (.., 2) (LinkState.cpp:762-791, with
+   traceOnePath :398-419) for a batch of pairs, traced on the device. Per pair, tok1 /
+   tok2 [n_pairs][tok_cap] hold [n_paths, len_0, e.., len_1, e.., ...]: every path as
+   its directed edge ids in src -> dest order (link = link_id[e]), paths in the
+   reference's order; tokens past a row's used prefix are left unspecified. k = 2 ignores the links of the k = 1 paths. Link metrics are
+   used (getKthPaths calls getSpfResult(src, true) / runSpf(src, true, ignore)). A pair
+   whose paths exceed tok_cap tokens (or 255 hops) gets n_paths = 0xFFFFFFFF and the
+   call returns OPENR_SPF_E2BIG after filling the others. */
+int openr_spf_ksp2(openr_spf_ctx* ctx, const uint32_t* src, const uint32_t* dst, uint32_t n_pairs,
+                   uint32_t tok_cap, uint32_t* tok1, uint32_t* tok2);
+
+/* Device-buffer form: pair i = (d_sources[d_pair_row[i]], d_pair_dst[i]); the base SPF
+   is solved once per listed source. Synchronizes `stream` once at the end. */
+int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources,
+                          uint32_t n_sources, const uint32_t* d_pair_row,
+                          const uint32_t* d_pair_dst, uint32_t n_pairs, uint32_t tok_cap,
+                          uint32_t* d_tok1, uint32_t* d_tok2, void* stream);
 
 int openr_spf_get_stats(const openr_spf_ctx* ctx, openr_spf_stats_t* out);
 

@@ -80,6 +80,9 @@ struct Device {
   DevBuf<uint64_t> base_dist, base_tight, wdist;
   DevBuf<uint8_t> base_nh, wnh;
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
+  // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
+  DevBuf<uint64_t> kbase, krows;
+  DevBuf<uint32_t> kign, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -92,7 +95,7 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj,    g.w,
-                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge};
+                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge, g.rank};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -431,6 +434,75 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   return hipSuccess;
 }
 
+// Bytes of second-SPF distance rows a KSP2 batch may hold on a device at once.
+constexpr size_t kKspChunkBytes = size_t(2) << 30;
+
+// getKthPaths(src, dest, 1) and (.., 2) for a batch of pairs on one device: the base SPF
+// of every listed source (the reference's memoized getSpfResult), then per chunk of
+// pairs: k = 1 trace on the base rows (its links become the pair's ignore set), the
+// second SPF with that ignore set (runSpf(src, true, ignore)), the k = 2 trace.
+// Sets *overflow when a pair's paths exceed tok_cap tokens or kKspMaxDepth hops.
+hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, const Plan& ign_plan,
+                          const uint32_t* d_sources, uint32_t n_src, const uint32_t* d_prow, const uint32_t* d_pdst,
+                          uint32_t n_pairs, uint32_t tok_cap, uint32_t* d_tok1, uint32_t* d_tok2, hipStream_t s,
+                          bool* overflow) {
+  const uint32_t V = ctx->V;
+  *overflow = false;
+  if (!n_pairs) return hipSuccess;
+  hipError_t err;
+#define OPENR_TRY(x)                   \
+  do {                                 \
+    err = (x);                         \
+    if (err != hipSuccess) return err; \
+  } while (0)
+  OPENR_TRY(reserve_counters(d));
+  OPENR_TRY(d.kbase.reserve((size_t)n_src * V));
+  OPENR_TRY(d.kstatus.reserve(1));
+  OPENR_TRY(hipMemsetAsync(d.kstatus.p, 0, sizeof(uint32_t), s));
+  SolveArgs a{};
+  a.sources = d_sources;
+  a.n = n_src;
+  a.dist = d.kbase.p;
+  a.nh_bits = ctx->nh_bits;
+  OPENR_TRY(d.ovf.reserve((size_t)n_src * ctx->nsl_max()));
+  a.ovf_list = d.ovf.p;
+  a.work = d.work.p;
+  OPENR_TRY(launch(ctx, d, base_plan, a, s));
+  const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens
+  const uint32_t chunk =
+      (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / ((size_t)V * 8u + 4u * ign_cap)));
+  OPENR_TRY(d.krows.reserve((size_t)chunk * V));
+  OPENR_TRY(d.kign.reserve((size_t)chunk * ign_cap));
+  OPENR_TRY(d.ksrc.reserve(chunk));
+  OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
+  OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
+  OPENR_TRY(launch_strided_iota(d.kptr.p, chunk + 1u, ign_cap, d.num_cus, s));
+  for (uint32_t first = 0; first < n_pairs; first += chunk) {
+    const uint32_t m = std::min(chunk, n_pairs - first);
+    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, ign_cap, d_tok1,
+                               tok_cap, d.kstatus.p, d.num_cus, s));
+    OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
+    SolveArgs b{};
+    b.sources = d.ksrc.p;
+    b.n = m;
+    b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, +ign_cap) (0xFFFFFFFF-padded)
+    b.ign_links = d.kign.p;
+    b.dist = d.krows.p;
+    b.nh_bits = ctx->nh_bits;
+    b.ovf_list = d.ovf.p;
+    b.work = d.work.p;
+    OPENR_TRY(launch(ctx, d, ign_plan, b, s));
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, ign_cap, d_tok2,
+                               tok_cap, d.kstatus.p, d.num_cus, s));
+  }
+  uint32_t status = 0;
+  OPENR_TRY(hipMemcpyAsync(&status, d.kstatus.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  OPENR_TRY(hipStreamSynchronize(s));
+  *overflow = status != 0;
+#undef OPENR_TRY
+  return hipSuccess;
+}
+
 int whatif_plans(openr_spf_ctx* ctx, uint32_t flags, Plan* base_plan, Plan* ign_plan) {
   int rc = make_plan(ctx, flags, false, base_plan);
   if (rc) return rc;
@@ -514,7 +586,9 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.perm.release();
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
-                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p};
+                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
+                     d.kbase.p,     d.krows.p,      d.kign.p,  d.ksrc.p,      d.kptr.p,    d.kstatus.p,
+                     d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
@@ -661,6 +735,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.cls, cls[kFamCode].data(), V);
     if (err == hipSuccess) err = up(&g.cls_lvl, cls[kFamLvl].data(), V);
     if (err == hipSuccess) err = up(&g.ledge, ledge.data(), L);
+    if (err == hipSuccess) err = up(&g.rank, gr->name_rank, V);
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;
@@ -828,6 +903,82 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
   ctx->stats.spf_runs += total;
   ctx->stats.batches += 1;
   if (out_solved) *out_solved = total;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_ksp2(openr_spf_ctx* ctx, const uint32_t* src, const uint32_t* dst, uint32_t n_pairs,
+                   uint32_t tok_cap, uint32_t* tok1, uint32_t* tok2) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (n_pairs && (!src || !dst || !tok1 || !tok2)) return fail(OPENR_SPF_EINVAL, "null argument");
+  if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
+  if (!ksp_lds_bytes(ctx->L, true)) return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  // distinct sources (the memoized SPF of each), pair -> base row
+  std::vector<uint32_t> srcs, prow(n_pairs), row_of(ctx->V, UINT32_MAX);
+  for (uint32_t i = 0; i < n_pairs; ++i) {
+    if (src[i] >= ctx->V || dst[i] >= ctx->V) return fail(OPENR_SPF_EINVAL, "pair %u out of range", i);
+    if (row_of[src[i]] == UINT32_MAX) {
+      row_of[src[i]] = (uint32_t)srcs.size();
+      srcs.push_back(src[i]);
+    }
+    prow[i] = row_of[src[i]];
+  }
+  Plan bp, ip;
+  int rc = whatif_plans(ctx, OPENR_SPF_USE_LINK_METRIC, &bp, &ip);  // getKthPaths uses link metrics
+  if (rc) return rc;
+  if (!n_pairs) return OPENR_SPF_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  Device& d = ctx->devs[0];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  HIP_TRY(d.kin_src.reserve(srcs.size()));
+  HIP_TRY(d.kin_row.reserve(n_pairs));
+  HIP_TRY(d.kin_dst.reserve(n_pairs));
+  HIP_TRY(d.ktok1.reserve((size_t)n_pairs * tok_cap));
+  HIP_TRY(d.ktok2.reserve((size_t)n_pairs * tok_cap));
+  HIP_TRY(hipMemcpyAsync(d.kin_src.p, srcs.data(), srcs.size() * 4u, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(d.kin_row.p, prow.data(), (size_t)n_pairs * 4u, hipMemcpyHostToDevice, d.stream));
+  HIP_TRY(hipMemcpyAsync(d.kin_dst.p, dst, (size_t)n_pairs * 4u, hipMemcpyHostToDevice, d.stream));
+  bool overflow = false;
+  HIP_TRY(ksp2_on_device(ctx, d, bp, ip, d.kin_src.p, (uint32_t)srcs.size(), d.kin_row.p, d.kin_dst.p, n_pairs,
+                         tok_cap, d.ktok1.p, d.ktok2.p, d.stream, &overflow));
+  HIP_TRY(hipMemcpyAsync(tok1, d.ktok1.p, (size_t)n_pairs * tok_cap * 4u, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipMemcpyAsync(tok2, d.ktok2.p, (size_t)n_pairs * tok_cap * 4u, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  ctx->stats.spf_runs += srcs.size() + n_pairs;
+  ctx->stats.batches += 1;
+  ctx->stats.last_batch_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (overflow)
+    return fail(OPENR_SPF_E2BIG, "a pair's paths exceed tok_cap=%u tokens or %u hops (marked 0xFFFFFFFF)", tok_cap,
+                kKspMaxDepth - 1u);
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n_sources,
+                          const uint32_t* d_pair_row, const uint32_t* d_pair_dst, uint32_t n_pairs, uint32_t tok_cap,
+                          uint32_t* d_tok1, uint32_t* d_tok2, void* stream) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  if (n_pairs && (!d_sources || !d_pair_row || !d_pair_dst || !d_tok1 || !d_tok2))
+    return fail(OPENR_SPF_EINVAL, "null argument");
+  if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
+  if (!ksp_lds_bytes(ctx->L, true)) return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  Plan bp, ip;
+  int rc = whatif_plans(ctx, OPENR_SPF_USE_LINK_METRIC, &bp, &ip);
+  if (rc) return rc;
+  Device& d = ctx->devs[device_index];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  bool overflow = false;
+  HIP_TRY(ksp2_on_device(ctx, d, bp, ip, d_sources, n_sources, d_pair_row, d_pair_dst, n_pairs, tok_cap, d_tok1,
+                         d_tok2, s, &overflow));
+  ctx->stats.spf_runs += (uint64_t)n_sources + n_pairs;
+  ctx->stats.batches += 1;
+  if (overflow)
+    return fail(OPENR_SPF_E2BIG, "a pair's paths exceed tok_cap=%u tokens or %u hops (marked 0xFFFFFFFF)", tok_cap,
+                kKspMaxDepth - 1u);
   return OPENR_SPF_OK;
 }
 

@@ -34,6 +34,7 @@ struct DevGraph {
   uint8_t* cls = nullptr;      // [V] source class of each node, code family (SrcClass)
   uint8_t* cls_lvl = nullptr;  // [V] source class of each node, lvl family (LvlClass)
   uint2* ledge = nullptr;      // [L] the two directed edges of each link (UINT32_MAX if unused)
+  uint32_t* rank = nullptr;    // [V] name rank (pathLinks / pop-order tie-break)
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
@@ -134,6 +135,17 @@ hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64
                                const uint64_t* base_dist, const uint8_t* base_nh, const uint32_t* wunit,
                                uint32_t n_src, uint32_t* changed, int num_cus, hipStream_t s);
 hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
+
+// KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
+constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)
+hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
+                            const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
+                            uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status, int num_cus,
+                            hipStream_t s);
+hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
+hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
+                                 uint32_t* out, int num_cus, hipStream_t s);
+uint32_t ksp_lds_bytes(uint32_t L, bool ign);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);

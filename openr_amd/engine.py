@@ -35,6 +35,8 @@ EXPORTS = (
     "openr_spf_solve_device",
     "openr_spf_whatif",
     "openr_spf_whatif_device",
+    "openr_spf_ksp2",
+    "openr_spf_ksp2_device",
     "openr_spf_get_stats",
 )
 
@@ -102,6 +104,8 @@ def load_library():
     l.openr_spf_solve_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
     l.openr_spf_whatif.argtypes = [vp, vp, u32, vp, u32, u32, vp, P(ctypes.c_uint64)]
     l.openr_spf_whatif_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, P(ctypes.c_uint64)]
+    l.openr_spf_ksp2.argtypes = [vp, vp, vp, u32, u32, vp, vp]
+    l.openr_spf_ksp2_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, vp, u32, u32, vp, vp, vp]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
     for name in EXPORTS:
         if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy"):
@@ -221,10 +225,48 @@ class SpfEngine:
                                                  ctypes.byref(solved)))
         return int(solved.value)
 
+    def ksp2_tokens(self, src: Sequence[int], dst: Sequence[int], tok_cap: int = 256,
+                    allow_overflow: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+        """getKthPaths(s, d, 1) and (.., 2) per pair as raw token rows [n, tok_cap] u32."""
+        s_ = np.ascontiguousarray(src, dtype=np.uint32)
+        d_ = np.ascontiguousarray(dst, dtype=np.uint32)
+        n = int(s_.shape[0])
+        t1 = np.zeros((n, tok_cap), dtype=np.uint32)
+        t2 = np.zeros((n, tok_cap), dtype=np.uint32)
+        rc = self._lib.openr_spf_ksp2(self._ctx, _p(s_), _p(d_), n, tok_cap, _p(t1), _p(t2))
+        if not (allow_overflow and rc == E2BIG):
+            _check(rc)
+        return t1, t2
+
+    def ksp2(self, src: Sequence[int], dst: Sequence[int], tok_cap: int = 256):
+        """[(paths_k1, paths_k2)] per pair; a path = list of directed edge ids, src -> dest."""
+        t1, t2 = self.ksp2_tokens(src, dst, tok_cap)
+        return [(decode_paths(t1[i]), decode_paths(t2[i])) for i in range(t1.shape[0])]
+
+    def ksp2_device(self, d_sources: int, n_sources: int, d_pair_row: int, d_pair_dst: int, n_pairs: int,
+                    tok_cap: int, d_tok1: int, d_tok2: int, stream: int = 0, device_index: int = 0) -> None:
+        vp = ctypes.c_void_p
+        _check(self._lib.openr_spf_ksp2_device(self._ctx, device_index, vp(d_sources), n_sources, vp(d_pair_row),
+                                               vp(d_pair_dst), n_pairs, tok_cap, vp(d_tok1), vp(d_tok2),
+                                               vp(stream or None)))
+
     def stats(self) -> SpfStats:
         s = SpfStats()
         _check(self._lib.openr_spf_get_stats(self._ctx, ctypes.byref(s)))
         return s
+
+
+def decode_paths(tok: np.ndarray):
+    """Token row [n_paths, len_0, e.., len_1, e.., ...] -> list of edge-id lists."""
+    n = int(tok[0])
+    if n == 0xFFFFFFFF:
+        raise SpfError(E2BIG, "pair overflowed its token row")
+    out, pos = [], 1
+    for _ in range(n):
+        ln = int(tok[pos])
+        out.append(tok[pos + 1 : pos + 1 + ln].astype(np.int64).tolist())
+        pos += 1 + ln
+    return out
 
 
 def limits() -> SpfLimits:

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "openr_spf.h")
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(openr_spf_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(openr_spf_[a-z_0-9]+)\s*\(", text)))
 
 
 def test_header_declares_binding_exports():

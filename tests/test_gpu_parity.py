@@ -11,7 +11,7 @@ import pytest
 
 import golden_cases as G
 from openr_amd import topology as T
-from openr_amd.engine import EINVAL, ENOTSUP, SpfEngine, SpfError
+from openr_amd.engine import E2BIG, EINVAL, ENOTSUP, SpfEngine, SpfError
 from openr_amd.spf_result import get_kth_paths, materialize, tight_in_edges
 from oracle import Oracle
 
@@ -437,3 +437,74 @@ def test_whatif_edge_cases(eng):
     srcs = list(range(g.num_nodes))
     c, _ = eng.whatif(links, srcs, True)
     np.testing.assert_array_equal(c, whatif_oracle(g, links, srcs, True))
+
+
+# --- KSP2 traced on the device (openr_spf_ksp2) ------------------------------
+def check_ksp2_against_oracle(eng, g, pairs):
+    eng.set_graph(g)
+    o = Oracle(g)
+    src = [p[0] for p in pairs]
+    dst = [p[1] for p in pairs]
+    got = eng.ksp2(src, dst)
+    for (s, d), (k1, k2) in zip(pairs, got):
+        assert k1 == o.kth_paths(s, d, 1), ("k1", s, d)
+        assert k2 == o.kth_paths(s, d, 2), ("k2", s, d)
+    return got
+
+
+@pytest.mark.parametrize("case", G.load()["cases"], ids=lambda c: c["name"])
+def test_ksp2_device_reference_cases_all_pairs(eng, case):
+    g = G.build(case)
+    pairs = [(s, d) for s in range(g.num_nodes) for d in range(g.num_nodes)]
+    got = check_ksp2_against_oracle(eng, g, pairs)
+    for exp in case.get("kth", []):  # the reference tests' own expectations
+        s, d = g.id(exp["src"]), g.id(exp["dst"])
+        if exp["k"] in (1, 2):
+            assert len(got[pairs.index((s, d))][exp["k"] - 1]) == exp["num_paths"]
+
+
+@pytest.mark.parametrize("seed,max_metric", [(0, 1), (1, 9), (2, 1)])
+def test_ksp2_device_random_graphs(eng, seed, max_metric):
+    g = random_graph(400 + seed, 70, 160, max_metric, p_ovl=0.08, p_down=0.05, p_par=0.15)
+    rng = np.random.default_rng(seed)
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (400, 2))] + [(3, 3)]
+    check_ksp2_against_oracle(eng, g, pairs)
+
+
+def test_ksp2_device_fabric_sample(eng):
+    g = T.fabric(288 + 56)
+    rng = np.random.default_rng(5)
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))]
+    got = check_ksp2_against_oracle(eng, g, pairs)
+    assert any(len(k1) > 1 for k1, _ in got)  # ECMP: several edge-disjoint first paths
+
+
+def test_ksp2_device_form_and_overflow(eng):
+    import torch
+
+    g = T.grid_fast(9)
+    eng.set_graph(g)
+    V = g.num_nodes
+    srcs = np.array([0, 40, 80], dtype=np.uint32)
+    prow = np.repeat(np.arange(3, dtype=np.uint32), V)
+    pdst = np.tile(np.arange(V, dtype=np.uint32), 3)
+    t1h, t2h = eng.ksp2_tokens(srcs[prow], pdst, 128)
+    dev = torch.device("cuda", 0)
+    to = lambda a: torch.from_numpy(a.astype(np.int32)).to(dev)
+    d1 = torch.zeros((len(pdst), 128), dtype=torch.int32, device=dev)
+    d2 = torch.zeros_like(d1)
+    keep = [to(srcs), to(prow), to(pdst)]  # alive until the stream is synchronized
+    eng.ksp2_device(keep[0].data_ptr(), 3, keep[1].data_ptr(), keep[2].data_ptr(), len(pdst), 128, d1.data_ptr(),
+                    d2.data_ptr())
+    torch.cuda.synchronize()
+    from openr_amd.engine import decode_paths
+
+    for dev_t, host_t in ((d1, t1h), (d2, t2h)):  # tokens past a row's used prefix are unspecified
+        dt = dev_t.cpu().numpy().view(np.uint32)
+        assert [decode_paths(r) for r in dt] == [decode_paths(r) for r in host_t]
+    # a token row too small for the corner-to-corner paths: flagged, the call fails loudly
+    with pytest.raises(SpfError) as ei:
+        eng.ksp2_tokens([0], [V - 1], 8)
+    assert ei.value.code == E2BIG
+    t1, _ = eng.ksp2_tokens([0, 0], [V - 1, 1], 8, allow_overflow=True)
+    assert t1[0, 0] == 0xFFFFFFFF and t1[1, 0] == 1
