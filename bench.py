@@ -199,6 +199,126 @@ def whatif_main(args):
     eng.close()
 
 
+def ksp2_cpu_baseline(g, seconds: float):
+    """The oracle's getKthPaths(s, d, 2) (k = 1 SPF + trace, second SPF + trace) on random
+    pairs, 1 thread, for about `seconds`."""
+    from oracle import Oracle
+
+    o = Oracle(g)
+    rng = np.random.default_rng(0)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(8):
+            o.kth_paths(int(rng.integers(g.num_nodes)), int(rng.integers(g.num_nodes)), 2)
+        n += 8
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"{n} random (src, dst) pairs, oracle getKthPaths(k=2) each (2 SPFs + traces), 1 thread, "
+                      f"{dt:.1f}s"}
+
+
+def ksp2_main(args):
+    """BASELINE config 5: KSP2 edge-disjoint second paths (getKthPaths k=1 and k=2) for
+    all (src, dst) pairs of the fabric topology. A step = every pair of this rank's
+    contiguous block of sources (shard.py; strong scaling: the ranks split ONE
+    fabric's all-pairs job, no collective on the data path), one
+    openr_spf_ksp2_device call: base SPF per source, device traces, one second SPF per
+    pair with its k=1 links ignored."""
+    import torch
+    import torch.distributed as dist
+
+    from openr_amd.engine import SpfEngine
+    from openr_amd.shard import max_over_ranks, shard_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    g, cfg = build_topology("fabric")
+    V = g.num_nodes
+    eng = SpfEngine([local_rank])
+    eng.set_graph(g)
+    n_src_total = args.ksp_sources or V
+    lo, hi = shard_range(n_src_total, rank, world)
+    nsrc = hi - lo
+    tok_cap = 1024  # FSW -> FSW k=2: 48 edge-disjoint 6-hop paths = 337 tokens
+    srcs = (torch.arange(lo, hi, dtype=torch.int64, device=dev) * V // n_src_total).to(torch.int32)  # spread
+    blk = max(1, min(args.ksp_block, nsrc))
+    prow = torch.arange(blk, dtype=torch.int32, device=dev).repeat_interleave(V)
+    pdst = torch.arange(V, dtype=torch.int32, device=dev).repeat(blk)
+    n_pairs = nsrc * V
+    tok1 = torch.empty((blk * V, tok_cap), dtype=torch.int32, device=dev)
+    tok2 = torch.empty((blk * V, tok_cap), dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+
+    def step():
+        for b in range(0, nsrc, blk):  # a block of sources x all destinations per call
+            m = min(blk, nsrc - b)
+            eng.ksp2_device(srcs[b:].data_ptr(), m, prow.data_ptr(), pdst.data_ptr(), m * V, tok_cap,
+                            tok1.data_ptr(), tok2.data_ptr(), stream=stream.cuda_stream)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    pairs_total = n_src_total * V * args.steps
+    value = pairs_total / elapsed
+    # spot check against the oracle outside the timed region (a few pairs)
+    from openr_amd.engine import decode_paths
+    from oracle import Oracle
+
+    o = Oracle(g)
+    last_b = ((nsrc - 1) // blk) * blk  # the token rows hold the last block's pairs
+    m_last = nsrc - last_b
+    idx = list(range(0, m_last * V, max(1, m_last * V // 7)))
+    t1 = tok1[idx].cpu().numpy().view(np.uint32)
+    t2 = tok2[idx].cpu().numpy().view(np.uint32)
+    s_np, d_np = srcs.cpu().numpy(), pdst.cpu().numpy()
+    p_np = prow.cpu().numpy()
+    for r, i in enumerate(idx):
+        s, d = int(s_np[last_b + p_np[i]]), int(d_np[i])
+        assert decode_paths(t1[r]) == o.kth_paths(s, d, 1) and decode_paths(t2[r]) == o.kth_paths(s, d, 2), \
+            "ksp2 bench result check failed"
+    srcs_np = np.asarray(s_np, dtype=np.int64)
+    per_pair = algorithmic_bytes(g, srcs_np) / max(nsrc, 1)  # B(src) per second SPF (SURVEY 8d)
+    achieved = per_pair * n_pairs * world / (elapsed / args.steps) / 1e9
+    if rank == 0:
+        out = {
+            "metric": "KSP2 (getKthPaths k=1,2) all-pairs throughput, pairs/sec, fabric ~5k nodes",
+            "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic (fabric generator, unit metrics)",
+            "config": dict(cfg, workload="fabric5000-ksp2-all-pairs" if not args.ksp_sources else
+                           f"fabric5000-ksp2-{n_src_total}-sources-x-all-dests", pairs_per_step=n_src_total * V,
+                           tok_cap=tok_cap, sources_per_call=blk, parallelism=f"source-sharded x{world}"),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "note": "SURVEY.md 8d: B(src) per second SPF (one per pair); k=1 base SPFs and "
+                                 "traces not credited"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = ksp2_cpu_baseline(g, min(args.cpu_seconds, 10.0))
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,12 +331,18 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
-    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif"],
+    ap.add_argument("--ksp-sources", type=int, default=0,
+                    help="ksp2: sources per step (0 = all; each source pairs with every node)")
+    ap.add_argument("--ksp-block", type=int, default=256,
+                    help="ksp2: sources per device call within a step (token rows are reused)")
+    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif", "ksp2"],
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
                          "(BASELINE config 4)")
     args = ap.parse_args()
     if args.workload == "whatif":
         return whatif_main(args)
+    if args.workload == "ksp2":
+        return ksp2_main(args)
 
     import torch
     import torch.distributed as dist

@@ -82,7 +82,7 @@ struct Device {
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
-  DevBuf<uint32_t> kign, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2;
+  DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -468,32 +468,34 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   a.ovf_list = d.ovf.p;
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
-  const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens
+  const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
   const uint32_t chunk =
       (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / ((size_t)V * 8u + 4u * ign_cap)));
   OPENR_TRY(d.krows.reserve((size_t)chunk * V));
   OPENR_TRY(d.kign.reserve((size_t)chunk * ign_cap));
+  OPENR_TRY(d.kend.reserve(chunk));
   OPENR_TRY(d.ksrc.reserve(chunk));
   OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
   OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
   OPENR_TRY(launch_strided_iota(d.kptr.p, chunk + 1u, ign_cap, d.num_cus, s));
   for (uint32_t first = 0; first < n_pairs; first += chunk) {
     const uint32_t m = std::min(chunk, n_pairs - first);
-    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, ign_cap, d_tok1,
-                               tok_cap, d.kstatus.p, d.num_cus, s));
+    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok1, tok_cap, d.kstatus.p, d.num_cus, s));
     OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
     SolveArgs b{};
     b.sources = d.ksrc.p;
     b.n = m;
-    b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, +ign_cap) (0xFFFFFFFF-padded)
+    b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, kend[k])
+    b.ign_end = d.kend.p;
     b.ign_links = d.kign.p;
     b.dist = d.krows.p;
     b.nh_bits = ctx->nh_bits;
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
-    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, ign_cap, d_tok2,
-                               tok_cap, d.kstatus.p, d.num_cus, s));
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok2, tok_cap, d.kstatus.p, d.num_cus, s));
   }
   uint32_t status = 0;
   OPENR_TRY(hipMemcpyAsync(&status, d.kstatus.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -587,7 +589,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
-                     d.kbase.p,     d.krows.p,      d.kign.p,  d.ksrc.p,      d.kptr.p,    d.kstatus.p,
+                     d.kbase.p,     d.krows.p,      d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
@@ -912,7 +914,8 @@ int openr_spf_ksp2(openr_spf_ctx* ctx, const uint32_t* src, const uint32_t* dst,
   if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
   if (n_pairs && (!src || !dst || !tok1 || !tok2)) return fail(OPENR_SPF_EINVAL, "null argument");
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
-  if (!ksp_lds_bytes(ctx->L, true)) return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  if (!ksp_lds_bytes(ctx->V, ctx->L))
+    return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
   // distinct sources (the memoized SPF of each), pair -> base row
   std::vector<uint32_t> srcs, prow(n_pairs), row_of(ctx->V, UINT32_MAX);
   for (uint32_t i = 0; i < n_pairs; ++i) {
@@ -964,7 +967,8 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
   if (n_pairs && (!d_sources || !d_pair_row || !d_pair_dst || !d_tok1 || !d_tok2))
     return fail(OPENR_SPF_EINVAL, "null argument");
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
-  if (!ksp_lds_bytes(ctx->L, true)) return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  if (!ksp_lds_bytes(ctx->V, ctx->L))
+    return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
   Plan bp, ip;
   int rc = whatif_plans(ctx, OPENR_SPF_USE_LINK_METRIC, &bp, &ip);
   if (rc) return rc;

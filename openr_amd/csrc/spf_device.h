@@ -106,7 +106,7 @@ __device__ __forceinline__ uint32_t wave_append(bool fresh, uint32_t* counter) {
 // Build the per-solve ignore mask (linksToIgnore) in LDS.
 __device__ __forceinline__ void load_ignore(uint32_t* ign, uint32_t words, const SolveArgs& a,
                                             uint32_t sid, uint32_t L) {
-  const uint32_t b = a.ign_ptr[sid], e = a.ign_ptr[sid + 1];
+  const uint32_t b = a.ign_ptr[sid], e = a.ign_end ? a.ign_end[sid] : a.ign_ptr[sid + 1];
   for (uint32_t k = b + threadIdx.x; k < e; k += blockDim.x) {  // any workgroup size
     const uint32_t l = a.ign_links[k];
     if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));

@@ -63,8 +63,9 @@ struct LaunchInfo {
 struct SolveArgs {
   const uint32_t* sources;
   uint32_t n;
-  const uint32_t* ign_ptr;    // nullable
+  const uint32_t* ign_ptr;    // nullable: solve i ignores ign_links[ign_ptr[i], end_i)
   const uint32_t* ign_links;
+  const uint32_t* ign_end;    // nullable: end_i = ign_end[i], else ign_ptr[i + 1]
   uint64_t* dist;             // [n][V]
   uint8_t* nh;                // nullable [n][V][nh_bytes]
   uint32_t nh_bytes;
@@ -138,14 +139,15 @@ hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
 
 // KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
 constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)
+// kind 1 writes the k = 1 links to ign_io[k * ign_cap, ign_end[k]); kind 2 ignores them.
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
-                            uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status, int num_cus,
-                            hipStream_t s);
+                            uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
+                            int num_cus, hipStream_t s);
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);
-uint32_t ksp_lds_bytes(uint32_t L, bool ign);
+uint32_t ksp_lds_bytes(uint32_t V, uint32_t L);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);
