@@ -13,14 +13,15 @@ ENGINE_HDRS := $(CSRC)/spf_kernels.h $(CSRC)/spf_device.h $(CSRC)/spf_bfs_common
 ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_bfs.o $(LIBDIR)/spf_bfs_lvl.o $(LIBDIR)/spf_sweep.o $(LIBDIR)/spf_fringe.o $(LIBDIR)/spf_ksp.o $(LIBDIR)/spf_capi.o
 
 HOST := $(LIBDIR)/libopenr_decision.so
-HOST_SRCS := $(CSRC)/host/LinkState.cpp
-HOST_HDRS := $(CSRC)/host/LinkState.h include/openr_spf.h
+HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp
+HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h include/openr_spf.h
 CXX ?= g++
 CC ?= gcc
 CXXFLAGS ?= -O2 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 CPPTEST := tests/cpp/build/linkstate_test
+DECTEST := tests/cpp/build/decision_test
 
-all: $(ENGINE) $(HOST) oracle $(CPPTEST)
+all: $(ENGINE) $(HOST) oracle $(CPPTEST) $(DECTEST)
 
 $(LIBDIR):
 	mkdir -p $@
@@ -36,10 +37,16 @@ $(HOST): $(HOST_SRCS) $(HOST_HDRS) $(ENGINE)
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) -L$(LIBDIR) -lopenr_spf -Wl,-rpath,'$$ORIGIN'
 
 # C++ tests of the host mirror (oracle linked as the checker)
-$(CPPTEST): tests/cpp/linkstate_test.cpp $(HOST) oracle/spf_oracle.c oracle/spf_oracle.h
+$(CPPTEST): tests/cpp/linkstate_test.cpp tests/cpp/harness.h $(HOST) oracle/spf_oracle.c oracle/spf_oracle.h
 	mkdir -p tests/cpp/build
 	$(CC) -O2 -g -std=c11 -c oracle/spf_oracle.c -o tests/cpp/build/spf_oracle.o
 	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/linkstate_test.cpp tests/cpp/build/spf_oracle.o \
+	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
+
+# C++ tests of the SpfSolver / RibPolicy mirror
+$(DECTEST): tests/cpp/decision_test.cpp tests/cpp/harness.h $(HOST)
+	mkdir -p tests/cpp/build
+	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/decision_test.cpp \
 	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 
 oracle:

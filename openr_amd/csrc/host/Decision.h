@@ -1,0 +1,262 @@
+// Decision.h — host mirror of openr::SpfSolver (route build) and openr::RibPolicy.
+//
+// Reference: /root/reference/openr/decision/Decision.{h,cpp} (SpfSolver::SpfSolverImpl,
+// :401-1317), RibEntry.h, RibPolicy.{h,cpp}, common/Util.{h,cpp} (route helpers).
+// Same names, argument meaning and results for the SP_ECMP and KSP2_ED_ECMP algorithms
+// with IP and SR_MPLS forwarding, LFA, node- and adjacency-label MPLS routes, static
+// MPLS routes, min-nexthop and best-route selection by PrefixMetrics.
+//
+// What changes is where the SPF results come from: every getSpfResult here is served by
+// the engine (LinkState.cpp over the C-ABI), and buildRouteDb first prefetches the SPFs
+// it will read — this node plus, with LFA, every up neighbour — in ONE batched device
+// launch (LinkState::prefetchSpfResults) instead of one Dijkstra per call.
+// buildRouteDbs() does the same for a list of nodes (the getRouteMap /
+// GridTopologyFixture workload: all nodes' route DBs from one all-sources batch).
+//
+// Not mirrored: BGP metric-vector best path selection (runBestPathSelectionBgp; a BGP
+// prefix without enableBestRouteSelection is skipped with an error counter), ordered-FIB
+// hold timers (Decision event plumbing), thrift serialization.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <map>
+#include <optional>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "LinkState.h"
+
+namespace openr {
+
+using Metric = LinkStateMetric;
+using NodeAndArea = std::pair<std::string, std::string>;
+
+namespace thrift {
+
+enum class PrefixType : int32_t { LOOPBACK = 1, DEFAULT = 2, BGP = 3, PREFIX_ALLOCATOR = 4, BREEZE = 5, RIB = 6 };
+enum class PrefixForwardingType : int32_t { IP = 0, SR_MPLS = 1 };
+enum class PrefixForwardingAlgorithm : int32_t { SP_ECMP = 0, KSP2_ED_ECMP = 1 };
+enum class MplsActionCode : int32_t { PUSH = 0, SWAP = 1, PHP = 2, POP_AND_LOOKUP = 3, NOOP = 4 };
+
+// Network.thrift IpPrefix: `addr` is the textual address ("10.0.0.1", "fc00::1");
+// an address with a '.' and no ':' is IPv4 (the reference tests the binary size).
+struct IpPrefix {
+  std::string addr;
+  int16_t prefixLength = 0;
+  bool isV4() const { return addr.find(':') == std::string::npos; }
+  bool operator<(const IpPrefix& o) const { return std::tie(addr, prefixLength) < std::tie(o.addr, o.prefixLength); }
+  bool operator==(const IpPrefix& o) const { return addr == o.addr && prefixLength == o.prefixLength; }
+  std::string toString() const { return addr + "/" + std::to_string(prefixLength); }
+};
+
+struct PrefixMetrics {  // Lsdb.thrift:228 (defaults 1, 0, 0, 0)
+  int32_t version = 1;
+  int32_t path_preference = 0;
+  int32_t source_preference = 0;
+  int32_t distance = 0;
+};
+
+struct PrefixEntry {  // Lsdb.thrift:269
+  IpPrefix prefix;
+  PrefixType type = PrefixType::LOOPBACK;
+  PrefixForwardingType forwardingType = PrefixForwardingType::IP;
+  PrefixForwardingAlgorithm forwardingAlgorithm = PrefixForwardingAlgorithm::SP_ECMP;
+  bool hasMv = false;  // deprecated BGP metric vector present
+  std::optional<int64_t> minNexthop;
+  std::optional<int32_t> prependLabel;
+  PrefixMetrics metrics;
+};
+
+struct MplsAction {  // Network.thrift MplsAction
+  MplsActionCode action = MplsActionCode::NOOP;
+  std::optional<int32_t> swapLabel;
+  std::optional<std::vector<int32_t>> pushLabels;
+  bool operator<(const MplsAction& o) const {
+    return std::tie(action, swapLabel, pushLabels) < std::tie(o.action, o.swapLabel, o.pushLabels);
+  }
+  bool operator==(const MplsAction& o) const {
+    return action == o.action && swapLabel == o.swapLabel && pushLabels == o.pushLabels;
+  }
+};
+
+struct NextHopThrift {  // Network.thrift NextHopThrift
+  BinaryAddress address;
+  int32_t weight = 0;
+  std::optional<MplsAction> mplsAction;
+  int32_t metric = 0;
+  std::optional<std::string> area;
+  std::optional<std::string> neighborNodeName;
+  bool operator<(const NextHopThrift& o) const {
+    return std::tie(address.addr, address.ifName, weight, mplsAction, metric, area, neighborNodeName) <
+           std::tie(o.address.addr, o.address.ifName, o.weight, o.mplsAction, o.metric, o.area, o.neighborNodeName);
+  }
+  bool operator==(const NextHopThrift& o) const { return !(*this < o) && !(o < *this); }
+};
+
+}  // namespace thrift
+
+// Set semantics of the reference's unordered_set<NextHopThrift>, ordered for tests.
+using NextHopSet = std::set<thrift::NextHopThrift>;
+using PrefixEntries = std::unordered_map<NodeAndArea, thrift::PrefixEntry>;
+
+struct RibUnicastEntry {  // RibEntry.h:37
+  thrift::IpPrefix prefix;
+  NextHopSet nexthops;
+  thrift::PrefixEntry bestPrefixEntry;
+  std::string bestArea;
+  bool doNotInstall = false;
+};
+
+struct RibMplsEntry {  // RibEntry.h:92
+  int32_t label = 0;
+  NextHopSet nexthops;
+};
+
+struct DecisionRouteDb {  // Decision.h:80
+  std::map<thrift::IpPrefix, RibUnicastEntry> unicastRoutes;
+  std::map<int32_t, RibMplsEntry> mplsRoutes;
+  void addUnicastRoute(RibUnicastEntry&& e) { unicastRoutes.insert_or_assign(e.prefix, std::move(e)); }
+  void addMplsRoute(RibMplsEntry&& e) { mplsRoutes.insert_or_assign(e.label, std::move(e)); }
+};
+
+// PrefixState (decision/PrefixState.h): prefix -> (node, area) -> PrefixEntry.
+class PrefixState {
+ public:
+  using Entries = std::map<thrift::IpPrefix, PrefixEntries>;
+  void updatePrefix(const std::string& node, const std::string& area, const thrift::PrefixEntry& entry);
+  void deletePrefix(const std::string& node, const std::string& area, const thrift::IpPrefix& prefix);
+  Entries const& prefixes() const { return prefixes_; }
+
+ private:
+  Entries prefixes_;
+};
+
+struct BestRouteSelectionResult {  // Decision.h
+  bool success = false;
+  std::set<NodeAndArea> allNodeAreas;
+  NodeAndArea bestNodeArea;
+  bool hasNode(const std::string& node) const {
+    for (auto const& na : allNodeAreas)
+      if (na.first == node) return true;
+    return false;
+  }
+};
+
+struct DecisionCounters {  // fb303 decision.* counters the route build bumps
+  uint64_t route_build_runs = 0, get_route_for_prefix = 0, no_route_to_prefix = 0, skipped_unicast_route = 0,
+           skipped_mpls_route = 0, duplicate_node_label = 0, no_route_to_label = 0,
+           incompatible_forwarding_type = 0;
+};
+
+// Util.h helpers
+bool isMplsLabelValid(int32_t mplsLabel);
+thrift::NextHopThrift createNextHop(thrift::BinaryAddress addr, std::optional<std::string> ifName, int32_t metric,
+                                    std::optional<thrift::MplsAction> mplsAction,
+                                    const std::optional<std::string>& area = std::nullopt,
+                                    const std::optional<std::string>& neighborNodeName = std::nullopt);
+thrift::MplsAction createMplsAction(thrift::MplsActionCode code, std::optional<int32_t> swapLabel = std::nullopt,
+                                    std::optional<std::vector<int32_t>> pushLabels = std::nullopt);
+std::set<NodeAndArea> selectBestPrefixMetrics(PrefixEntries const& prefixes);
+NodeAndArea selectBestNodeArea(std::set<NodeAndArea> const& allNodeAreas, std::string const& myNodeName);
+std::pair<thrift::PrefixForwardingType, thrift::PrefixForwardingAlgorithm> getPrefixForwardingTypeAndAlgorithm(
+    const PrefixEntries& prefixEntries, const std::set<NodeAndArea>& bestNodeAreas);
+
+class SpfSolver {
+ public:
+  SpfSolver(const std::string& myNodeName, bool enableV4, bool computeLfaPaths, bool enableOrderedFib = false,
+            bool bgpDryRun = false, bool enableBestRouteSelection = false);
+
+  // static MPLS routes (updateStaticRoutes): label -> next-hops
+  void updateStaticMplsRoutes(const std::unordered_map<int32_t, std::vector<thrift::NextHopThrift>>& add,
+                              const std::vector<int32_t>& del);
+
+  std::optional<DecisionRouteDb> buildRouteDb(const std::string& myNodeName,
+                                              std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                                              PrefixState const& prefixState);
+
+  // Batched: the route DBs of many nodes (getRouteMap), after one all-sources prefetch
+  // per area. Entry i is buildRouteDb(nodes[i], ...).
+  std::vector<std::optional<DecisionRouteDb>> buildRouteDbs(
+      const std::vector<std::string>& nodes, std::unordered_map<std::string, LinkState> const& areaLinkStates,
+      PrefixState const& prefixState);
+
+  std::optional<RibUnicastEntry> createRouteForPrefix(const std::string& myNodeName,
+                                                      std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                                                      PrefixState const& prefixState, thrift::IpPrefix const& prefix);
+
+  std::map<thrift::IpPrefix, BestRouteSelectionResult> const& getBestRoutesCache() const { return bestRoutesCache_; }
+  DecisionCounters const& counters() const { return counters_; }
+
+ private:
+  BestRouteSelectionResult selectBestRoutes(std::string const& myNodeName, thrift::IpPrefix const& prefix,
+                                            PrefixEntries const& prefixEntries, bool isBgp,
+                                            std::unordered_map<std::string, LinkState> const& areaLinkStates);
+  BestRouteSelectionResult maybeFilterDrainedNodes(
+      BestRouteSelectionResult&& result, std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
+  std::optional<int64_t> getMinNextHopThreshold(BestRouteSelectionResult const& nodes,
+                                                PrefixEntries const& prefixEntries) const;
+  std::optional<RibUnicastEntry> selectBestPathsSpf(std::string const& myNodeName, thrift::IpPrefix const& prefix,
+                                                    BestRouteSelectionResult const& best,
+                                                    PrefixEntries const& prefixEntries, bool isBgp,
+                                                    thrift::PrefixForwardingType forwardingType,
+                                                    std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                                                    PrefixState const& prefixState);
+  std::optional<RibUnicastEntry> selectBestPathsKsp2(std::string const& myNodeName, thrift::IpPrefix const& prefix,
+                                                     BestRouteSelectionResult const& best,
+                                                     PrefixEntries const& prefixEntries, bool isBgp,
+                                                     thrift::PrefixForwardingType forwardingType,
+                                                     std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                                                     PrefixState const& prefixState);
+  std::optional<RibUnicastEntry> addBestPaths(std::string const& myNodeName, thrift::IpPrefix const& prefix,
+                                              BestRouteSelectionResult const& best, PrefixEntries const& prefixEntries,
+                                              PrefixState const& prefixState, bool isBgp, NextHopSet&& nextHops);
+  std::pair<Metric, std::unordered_set<std::string>> getMinCostNodes(
+      const LinkState::SpfResult& spfResult, const std::set<NodeAndArea>& dstNodeAreas) const;
+  std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric>> getNextHopsWithMetric(
+      const std::string& myNodeName, const std::set<NodeAndArea>& dstNodeAreas, bool perDestination,
+      std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
+  NextHopSet getNextHopsThrift(const std::string& myNodeName, const std::set<NodeAndArea>& dstNodeAreas, bool isV4,
+                               bool perDestination, Metric minMetric,
+                               std::unordered_map<std::pair<std::string, std::string>, Metric> nextHopNodes,
+                               std::optional<int32_t> swapLabel,
+                               std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                               PrefixEntries const& prefixEntries = {});
+  void prefetch(const std::string& myNodeName, std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
+
+  const std::string myNodeName_;
+  const bool enableV4_, computeLfaPaths_, enableOrderedFib_, bgpDryRun_, enableBestRouteSelection_;
+  std::unordered_map<int32_t, std::vector<thrift::NextHopThrift>> staticMplsRoutes_;
+  std::map<thrift::IpPrefix, BestRouteSelectionResult> bestRoutesCache_;
+  DecisionCounters counters_;
+};
+
+// RibPolicy (RibPolicy.{h,cpp}): statements matching prefixes; action set_weight with
+// neighbor > area > default precedence; weight 0 drops a next-hop; a route whose every
+// next-hop would be dropped is kept unchanged.
+struct RibPolicyStatement {
+  std::string name;
+  std::set<thrift::IpPrefix> prefixes;  // matcher.prefixes (required)
+  int32_t defaultWeight = 0;            // action.set_weight
+  std::unordered_map<std::string, int32_t> areaToWeight, neighborToWeight;
+  bool match(const RibUnicastEntry& route) const { return prefixes.count(route.prefix) > 0; }
+  bool applyAction(RibUnicastEntry& route) const;
+};
+
+class RibPolicy {
+ public:
+  explicit RibPolicy(std::vector<RibPolicyStatement> statements, int64_t ttlSecs = 3600);
+  bool isActive() const;
+  bool applyAction(RibUnicastEntry& route) const;  // first matching statement wins
+  // prefixes of the routes the policy transformed
+  std::vector<thrift::IpPrefix> applyPolicy(std::map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries) const;
+
+ private:
+  std::vector<RibPolicyStatement> statements_;
+  std::chrono::steady_clock::time_point validUntil_;
+};
+
+}  // namespace openr

@@ -1,4 +1,4 @@
-"""Runs the C++ host-mirror tests (tests/cpp/linkstate_test.cpp).
+"""Runs the C++ host-mirror tests (tests/cpp/linkstate_test.cpp, decision_test.cpp).
 
 cpu group: HoldableValue / Link / LinkState topology semantics and the CSR mirror
 (LinkStateTest.cpp:22-242); gpu group: SPF, KSP, hop counts, spf_runs counters and
@@ -11,11 +11,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tests", "cpp", "build", "linkstate_test")
+DEC_BIN = os.path.join(ROOT, "tests", "cpp", "build", "decision_test")
 
 
-def run(group):
-    assert os.path.exists(BIN), "build first: make"
-    p = subprocess.run([BIN, group], capture_output=True, text=True, timeout=600)
+def run(group, binary=BIN):
+    assert os.path.exists(binary), "build first: make"
+    p = subprocess.run([binary, group], capture_output=True, text=True, timeout=600)
     print(p.stdout)
     print(p.stderr)
     assert p.returncode == 0, p.stdout + p.stderr
@@ -35,3 +36,16 @@ def test_host_mirror_cpu():
 def test_host_mirror_gpu():
     out = run("gpu")
     assert "0 failures" in out
+
+
+def test_decision_mirror_cpu():
+    """SpfSolver / RibPolicy host logic without SPF (best-route selection, RibPolicy,
+    unknown node)."""
+    assert "0 failures" in run("cpu", DEC_BIN)
+
+
+@pytest.mark.gpu
+def test_decision_mirror_gpu():
+    """Route builds transcribed from DecisionTest.cpp (ring SP / LFA / KSP2, MPLS label
+    routes, grid route counts 2n^4 + 3n^2 - 4n) over engine SPF results."""
+    assert "0 failures" in run("gpu", DEC_BIN)
