@@ -330,7 +330,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r01/pmc_traffic_<topology>.json")
     ap.add_argument("--ksp-sources", type=int, default=0,
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
@@ -433,6 +434,8 @@ def main():
     mean_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = bytes_launch / mean_kernel_s / 1e9 if mean_kernel_s > 0 else 0.0
     traffic = None
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, "profiles", "r01", f"pmc_traffic_{args.topology}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))

@@ -444,7 +444,10 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
                               uint32_t ring_cap, bool from_list, uint32_t* ctr, uint32_t* ovf_count, int num_cus,
                               hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = bfs_layout(g.V, g.L, has_ign, FB, ring_cap).total;
-  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
+  // a re-run covers only the listed units (usually none): one workgroup per CU is plenty
+  const uint32_t grid = from_list ? std::min<uint32_t>(blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK),
+                                                       (uint32_t)num_cus)
+                                  : blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
   const bool generic = has_ign || a.tight != nullptr;
   auto k = generic ? bfs_code_kernel<FB, BLOCK, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
                    : bfs_code_kernel<FB, BLOCK, RING, ELLM, false, SLICED>;

@@ -472,7 +472,10 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
                               hipStream_t s, LaunchInfo* info) {
   const bool vis = SLICED || !Nh<MODE>::kSingle;
   const uint32_t lds = lvl_layout<LT>(g.V, g.L, has_ign, nh_words_for(MODE, g.V), vis, ring_cap).total;
-  const uint32_t grid = blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
+  // a re-run covers only the listed units (usually none): one workgroup per CU is plenty
+  const uint32_t grid = from_list ? std::min<uint32_t>(blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK),
+                                                       (uint32_t)num_cus)
+                                  : blocks_for(a.n * (SLICED ? a.nsl : 1u), lds, num_cus, BLOCK);
   const bool generic = has_ign || a.tight != nullptr;
   auto k = generic ? bfs_lvl_kernel<MODE, BLOCK, LT, RING, ELLM == 2 ? 1 : ELLM, true, SLICED>
                    : bfs_lvl_kernel<MODE, BLOCK, LT, RING, ELLM, false, SLICED>;
