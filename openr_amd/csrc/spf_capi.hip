@@ -914,7 +914,7 @@ int openr_spf_ksp2(openr_spf_ctx* ctx, const uint32_t* src, const uint32_t* dst,
   if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
   if (n_pairs && (!src || !dst || !tok1 || !tok2)) return fail(OPENR_SPF_EINVAL, "null argument");
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
-  if (!ksp_lds_bytes(ctx->V, ctx->L))
+  if (!ksp_lds_bytes(ctx->V, ctx->L, ctx->devs[0].g.max_deg))
     return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
   // distinct sources (the memoized SPF of each), pair -> base row
   std::vector<uint32_t> srcs, prow(n_pairs), row_of(ctx->V, UINT32_MAX);
@@ -967,7 +967,7 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
   if (n_pairs && (!d_sources || !d_pair_row || !d_pair_dst || !d_tok1 || !d_tok2))
     return fail(OPENR_SPF_EINVAL, "null argument");
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
-  if (!ksp_lds_bytes(ctx->V, ctx->L))
+  if (!ksp_lds_bytes(ctx->V, ctx->L, ctx->devs[0].g.max_deg))
     return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
   Plan bp, ip;
   int rc = whatif_plans(ctx, OPENR_SPF_USE_LINK_METRIC, &bp, &ip);

@@ -139,6 +139,7 @@ hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
 
 // KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
 constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)
+constexpr uint32_t kKspArena = 1024;    // sorted pathLinks of the frames on the DFS stack
 // kind 1 writes the k = 1 links to ign_io[k * ign_cap, ign_end[k]); kind 2 ignores them.
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
@@ -147,7 +148,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);
-uint32_t ksp_lds_bytes(uint32_t V, uint32_t L);
+uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);

@@ -17,12 +17,11 @@
 // u->v is tight iff the edge is up, its link is not ignored, u may expand (u == src
 // or not overloaded, LinkState.cpp:831-838) and dist[u] + w(u->v) == dist[v].
 //
-// Shape: one wavefront per (src, dest) pair. Instead of the reference's backtracking
-// DFS, the kernel keeps the exact set of nodes that can still be reached from src over
-// unused tight edges ("dead" = not), so each traceOnePath is a straight descent from
-// dest (see descend()); after a path is found its links are used and the nodes that
-// lose their last live pathLink are killed by a decremental sweep down the tight DAG
-// (kill_unreachable). Visited links and dead nodes are LDS bitmaps.
+// Shape: one wavefront per (src, dest) pair. Entering a DFS frame gathers v's live
+// pathLinks with all 64 lanes and ranks them into the frame's slice of an LDS arena, so
+// each later step of the frame is a few LDS reads. A frame that fails marks its node
+// dead for the rest of the pair (trace_one), which bounds a pair's DFS work by the nodes
+// it can kill plus the paths it finds. Visited links and dead nodes are LDS bitmaps.
 //
 // Output tokens per pair (ReadMe: include/openr_spf.h openr_spf_ksp2): [n_paths,
 // len_0, edges_0..., len_1, edges_1..., ...], directed edge ids in src -> dest order.
@@ -40,12 +39,13 @@ constexpr uint32_t kWave = 64;
 constexpr uint64_t kNoKey = ~0ull;
 
 struct KspLayout {
-  uint32_t vis, dead, path, work, total;
+  uint32_t vis, dead, fr_node, fr_edge, fr_beg, fr_cnt, fr_idx, ar_e, ar_l, ar_u, skd, skr, sidx, total;
 };
 
-__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L) {
+// deg = largest row (candidate scratch of one frame).
+__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg) {
   KspLayout l;
-  uint32_t off = 16;  // control: [0] worklist tail
+  uint32_t off = 16;  // control: [0] candidate count
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
@@ -53,162 +53,149 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L) {
   };
   l.vis = take(4u * ((L + 31u) / 32u));
   l.dead = take(4u * ((V + 31u) / 32u));
-  l.path = take(4u * kKspMaxDepth);
-  l.work = take(2u * V);
+  l.fr_node = take(4u * kKspMaxDepth);
+  l.fr_edge = take(4u * kKspMaxDepth);
+  l.fr_beg = take(4u * kKspMaxDepth);
+  l.fr_cnt = take(4u * kKspMaxDepth);
+  l.fr_idx = take(4u * kKspMaxDepth);
+  l.ar_e = take(4u * kKspArena);
+  l.ar_l = take(4u * kKspArena);
+  l.ar_u = take(4u * kKspArena);
+  l.skd = take(8u * deg);
+  l.skr = take(8u * deg);
+  l.sidx = take(4u * deg);
   l.total = off;
   return l;
 }
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t y = __shfl_xor(x, o);
-    x = y < x ? y : x;
-  }
-  return x;
-}
-
 struct KspState {
   const DevGraph* g;
   uint32_t src;
   const uint64_t* drow;
   uint32_t* ctl;
-  uint32_t* vis;   // used links: visited by found paths (+ the k = 1 links for k = 2)
-  uint32_t* dead;  // nodes that can no longer be reached from src over unused tight edges
-  uint32_t* path;
-  uint16_t* work;
+  uint32_t* vis;   // visited links (linksToIgnore of traceOnePath; + the k = 1 links for k = 2)
+  uint32_t* dead;  // nodes whose DFS subtree failed: they can never reach src again
+  uint32_t *fr_node, *fr_edge, *fr_beg, *fr_cnt, *fr_idx;  // DFS frames
+  uint32_t *ar_e, *ar_l, *ar_u;                            // per-frame sorted pathLinks
+  uint64_t *skd, *skr;
+  uint32_t* sidx;
 };
 
-// Tight in-edge u->v (e = v's row entry for v->u, re = rev[e] = u->v) usable as a
-// pathLink now: edge up, link unused, u may expand, dist[u] + w(u->v) == dist[v], u alive.
-__device__ __forceinline__ bool live_pred(const KspState& st, uint32_t e, uint64_t dv, uint32_t* u_out,
-                                          uint64_t* du_out) {
+// pathLinks(v) still worth trying -> arena[beg, beg + count) as (edge u->v, link, u):
+// tight in-edges (edge up, u may expand, dist[u] + w(u->v) == dist[v]) whose link is
+// unvisited and whose tail is not dead, in the reference's order (dist[u], name rank of
+// u, position in u's row). Gathered with one wave-aggregated append per 64 in-edges,
+// ranked by counting (keys are distinct). UINT32_MAX when the arena is full.
+__device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg) {
   const DevGraph& g = *st.g;
-  const uint32_t av = g.adj[e];
-  const uint32_t u = av & ~kEdgeDown;
-  *u_out = u;
-  if ((av & kEdgeDown) || test_bit(st.vis, g.lid[e]) || (u != st.src && g.ovl[u]) || test_bit(st.dead, u))
-    return false;
-  const uint64_t du = st.drow[u];
-  *du_out = du;
-  return du != kNoKey && du + g.win[e] == dv;
-}
-
-// Does v keep a live pathLink? (lanes over v's in-edges; wave-uniform result)
-__device__ bool has_live_pred(const KspState& st, uint32_t v) {
-  const DevGraph& g = *st.g;
+  const uint32_t lane = threadIdx.x;
   const uint64_t dv = st.drow[v];
   const uint2 r = g.row2[v];
-  for (uint32_t e = r.x + threadIdx.x; __any(e < r.y); e += kWave) {
-    uint32_t u;
-    uint64_t du;
-    const bool ok = e < r.y && live_pred(st, e, dv, &u, &du);
-    if (__any(ok)) return true;
-  }
-  return false;
-}
-
-// The links of a found path are now used: nodes left without a live pathLink die, and
-// their death is pushed down their tight out-edges (decremental reachability from src
-// over the tight DAG). Keeps `dead` exact, so the next descent never backtracks.
-__device__ void kill_unreachable(const KspState& st, uint32_t len) {
-  const DevGraph& g = *st.g;
-  const uint32_t lane = threadIdx.x;
-  uint32_t head = 0, tail = 0;
-  // heads of the path's edges lost an in-edge (path[i] = edge u->v, src side first)
-  for (uint32_t i = 0; i < len; ++i) {
-    const uint32_t v = g.adj[st.path[i]] & ~kEdgeDown;  // head of u->v
-    if (v == st.src || test_bit(st.dead, v) || has_live_pred(st, v)) continue;
-    if (lane == 0) {
-      st.dead[v >> 5] |= 1u << (v & 31u);
-      st.work[tail] = (uint16_t)v;
-    }
-    lds_fence();
-    ++tail;
-  }
-  while (head < tail) {
-    const uint32_t b = st.work[head++];
-    if (b != st.src && g.ovl[b]) continue;  // a sink never expanded: no tight out-edges
-    const uint64_t db = st.drow[b];
-    const uint2 r = g.row2[b];
-    for (uint32_t e0 = r.x; e0 < r.y; e0 += kWave) {
-      const uint32_t e = e0 + lane;
-      uint32_t c = 0;
-      bool cand = false;
-      if (e < r.y) {
-        const uint32_t av = g.adj[e];
-        c = av & ~kEdgeDown;
-        cand = !(av & kEdgeDown) && !test_bit(st.vis, g.lid[e]) && c != st.src && !test_bit(st.dead, c) &&
-               st.drow[c] != kNoKey && db + g.w[e] == st.drow[c];
-      }
-      unsigned long long m = __ballot(cand);
-      while (m) {  // re-check each tight successor, one at a time (all lanes help)
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1ull;
-        const uint32_t cc = __shfl(c, l);
-        if (test_bit(st.dead, cc) || has_live_pred(st, cc)) continue;
-        if (lane == 0) {
-          st.dead[cc >> 5] |= 1u << (cc & 31u);
-          st.work[tail] = (uint16_t)cc;
-        }
-        lds_fence();
-        ++tail;
+  if (lane == 0) st.ctl[0] = 0;
+  lds_fence();
+  for (uint32_t e0 = r.x; e0 < r.y; e0 += kWave) {
+    const uint32_t e = e0 + lane;
+    bool cand = false;
+    uint64_t du = 0;
+    uint32_t u = 0;
+    if (e < r.y) {
+      const uint32_t av = g.adj[e];
+      u = av & ~kEdgeDown;
+      if (!(av & kEdgeDown) && !test_bit(st.vis, g.lid[e]) && !test_bit(st.dead, u) && (u == st.src || !g.ovl[u])) {
+        du = st.drow[u];
+        cand = du != kNoKey && du + g.win[e] == dv;
       }
     }
-  }
-}
-
-// One traceOnePath (LinkState.cpp:398-419) given exact liveness: from dest, take the
-// first pathLink in the reference's order whose link is unused and whose tail is live,
-// down to src. The reference's DFS would also try (and mark) links into dead tails and
-// backtrack out of them; such links lead to nodes that can never reach src again, so
-// skipping them finds the same path and leaves every later trace unchanged.
-// Returns the path length (edges in path[0..len), src side first), 0 for no path,
-// -1 when the path is longer than kKspMaxDepth (or liveness was inconsistent).
-__device__ int descend(const KspState& st, uint32_t dst) {
-  const DevGraph& g = *st.g;
-  const uint32_t lane = threadIdx.x;
-  uint32_t v = dst, len = 0;
-  while (v != st.src) {
-    const uint64_t dv = st.drow[v];
-    const uint2 r = g.row2[v];
-    uint64_t best_d = kNoKey, best_r = kNoKey;
-    for (uint32_t e = r.x + lane; __any(e < r.y); e += kWave) {
-      uint64_t kd = kNoKey, kr = kNoKey;
-      uint32_t u;
-      uint64_t du;
-      if (e < r.y && live_pred(st, e, dv, &u, &du)) {
-        kd = du;  // pathLinks order: pop order of u = (dist, name), then u's row order
-        kr = ((uint64_t)g.rank[u] << 32) | g.rev[e];
-      }
-      const uint64_t md = wave_min_u64(kd);
-      const uint64_t mr = wave_min_u64(kd == md ? kr : kNoKey);
-      if (md < best_d || (md == best_d && mr < best_r)) {
-        best_d = md;
-        best_r = mr;
-      }
+    const uint32_t slot = wave_append(cand, &st.ctl[0]);
+    if (cand) {
+      const uint32_t re = g.rev[e];
+      st.skd[slot] = du;
+      st.skr[slot] = ((uint64_t)g.rank[u] << 32) | re;
+      st.sidx[slot] = e;  // v's row entry v->u: lid[e] is the link, rev[e] the pathLink edge
     }
-    if (best_d == kNoKey) return v == dst ? 0 : -1;  // a live node always has a live pathLink
-    if (len >= kKspMaxDepth) return -1;
-    const uint32_t re = (uint32_t)best_r;
-    const uint32_t link = g.lid[re];
-    if (lane == 0) {
-      st.vis[link >> 5] |= 1u << (link & 31u);
-      st.path[kKspMaxDepth - 1u - len] = re;  // filled dest side first
-    }
-    lds_fence();
-    ++len;
-    v = g.adj[g.rev[re]] & ~kEdgeDown;  // pathLink.prevNode = tail of re
-  }
-  // move to path[0..len), src side first
-  for (uint32_t i = lane; i < len; i += kWave) {
-    const uint32_t x = st.path[kKspMaxDepth - len + i];
-    st.path[i] = x;  // i < kKspMaxDepth - len + i: reads stay ahead of writes within a chunk
   }
   lds_fence();
-  return (int)len;
+  const uint32_t cnt = __builtin_amdgcn_readfirstlane(st.ctl[0]);
+  if (beg + cnt > kKspArena) return UINT32_MAX;
+  for (uint32_t i = lane; i < cnt; i += kWave) {
+    const uint64_t kd = st.skd[i], kr = st.skr[i];
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      const uint64_t od = st.skd[j], orr = st.skr[j];
+      rank += (od < kd || (od == kd && orr < kr)) ? 1u : 0u;
+    }
+    const uint32_t e = st.sidx[i];
+    st.ar_e[beg + rank] = (uint32_t)kr;  // re
+    st.ar_l[beg + rank] = g.lid[e];
+    st.ar_u[beg + rank] = g.adj[e] & ~kEdgeDown;
+  }
+  lds_fence();
+  return cnt;
+}
+
+// One traceOnePath (LinkState.cpp:398-419): DFS from dest over pathLinks in the
+// reference's order, inserting each tried link into the visited set. A frame whose
+// candidates are exhausted failed: its node can no longer reach src (the visited set only
+// grows), so it is marked dead and never entered again within this pair — the reference
+// would re-enter it, skip or fail every candidate again and return nullopt, so the paths
+// found are the same. Returns the path length (edges in fr_edge[1..len], dest side
+// first), 0 for src == dest, -1 for no path, -2 when the DFS outgrows its frames/arena.
+__device__ int trace_one(const KspState& st, uint32_t dst) {
+  if (st.src == dst) return 0;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t c0 = load_path_links(st, dst, 0);
+  if (c0 == UINT32_MAX) return -2;
+  if (lane == 0) {
+    st.fr_node[0] = dst;
+    st.fr_beg[0] = 0;
+    st.fr_cnt[0] = c0;
+    st.fr_idx[0] = 0;
+  }
+  lds_fence();
+  uint32_t sp = 1, top = c0;
+  while (sp > 0) {
+    const uint32_t f = sp - 1;
+    const uint32_t idx = st.fr_idx[f], cnt = st.fr_cnt[f], beg = st.fr_beg[f];
+    if (idx >= cnt) {  // exhausted: std::nullopt back to the caller frame
+      const uint32_t v = st.fr_node[f];
+      if (lane == 0) st.dead[v >> 5] |= 1u << (v & 31u);
+      lds_fence();
+      top -= cnt;
+      --sp;
+      continue;
+    }
+    const uint32_t link = st.ar_l[beg + idx], u = st.ar_u[beg + idx];
+    const bool fresh = !test_bit(st.vis, link);
+    const bool live = !test_bit(st.dead, u);
+    if (lane == 0) {
+      st.fr_idx[f] = idx + 1u;
+      if (fresh && live) st.vis[link >> 5] |= 1u << (link & 31u);
+    }
+    lds_fence();
+    if (!fresh || !live) continue;  // insert() failed, or a subtree known to fail
+    if (sp >= kKspMaxDepth) return -2;
+    const uint32_t re = st.ar_e[beg + idx];
+    if (u == st.src) {
+      if (lane == 0) st.fr_edge[sp] = re;
+      lds_fence();
+      return (int)sp;
+    }
+    const uint32_t c = load_path_links(st, u, top);
+    if (c == UINT32_MAX) return -2;
+    if (lane == 0) {
+      st.fr_edge[sp] = re;
+      st.fr_node[sp] = u;
+      st.fr_beg[sp] = top;
+      st.fr_cnt[sp] = c;
+      st.fr_idx[sp] = 0;
+    }
+    lds_fence();
+    top += c;
+    ++sp;
+  }
+  return -1;
 }
 
 // Pairs [first, first + n) of a chunk; k = pair - first.
@@ -224,15 +211,24 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t* status) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L);
+  const KspLayout lay = ksp_layout(V, g.L, g.max_deg);
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
   st.g = &g;
   st.ctl = smem;
   st.vis = reinterpret_cast<uint32_t*>(base + lay.vis);
   st.dead = reinterpret_cast<uint32_t*>(base + lay.dead);
-  st.path = reinterpret_cast<uint32_t*>(base + lay.path);
-  st.work = reinterpret_cast<uint16_t*>(base + lay.work);
+  st.fr_node = reinterpret_cast<uint32_t*>(base + lay.fr_node);
+  st.fr_edge = reinterpret_cast<uint32_t*>(base + lay.fr_edge);
+  st.fr_beg = reinterpret_cast<uint32_t*>(base + lay.fr_beg);
+  st.fr_cnt = reinterpret_cast<uint32_t*>(base + lay.fr_cnt);
+  st.fr_idx = reinterpret_cast<uint32_t*>(base + lay.fr_idx);
+  st.ar_e = reinterpret_cast<uint32_t*>(base + lay.ar_e);
+  st.ar_l = reinterpret_cast<uint32_t*>(base + lay.ar_l);
+  st.ar_u = reinterpret_cast<uint32_t*>(base + lay.ar_u);
+  st.skd = reinterpret_cast<uint64_t*>(base + lay.skd);
+  st.skr = reinterpret_cast<uint64_t*>(base + lay.skr);
+  st.sidx = reinterpret_cast<uint32_t*>(base + lay.sidx);
   const uint32_t lane = threadIdx.x, lw = (g.L + 31u) / 32u, vw = (V + 31u) / 32u;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t pair = first + k;
@@ -258,18 +254,18 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     // res.count(dest); src == dest traces an empty path, which ends the loop at once
     if (!bad && src != dst && st.drow[dst] != kNoKey) {
       for (;;) {
-        const int len = descend(st, dst);
-        if (len < 0) {
+        const int len = trace_one(st, dst);
+        if (len == -2) {
           bad = true;
           break;
         }
-        if (len == 0) break;
+        if (len <= 0) break;  // while (path && !path->empty())
         if (pos + 1u + (uint32_t)len > tok_cap || (KIND == 1 && nign + (uint32_t)len > ign_cap)) {
           bad = true;
           break;
         }
         for (uint32_t i = lane; i < (uint32_t)len; i += kWave) {
-          const uint32_t e = st.path[i];
+          const uint32_t e = st.fr_edge[(uint32_t)len - i];  // dest side first -> src -> dest
           out[pos + 1u + i] = e;
           if (KIND == 1) ig[nign + i] = g.lid[e];
         }
@@ -277,7 +273,6 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
         pos += 1u + (uint32_t)len;
         nign += (uint32_t)len;
         ++npaths;
-        kill_unreachable(st, (uint32_t)len);
       }
     }
     if (lane == 0) {
@@ -300,9 +295,8 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 
 }  // namespace
 
-uint32_t ksp_lds_bytes(uint32_t V, uint32_t L) {
-  if (V > 65535u) return 0;
-  const uint32_t t = ksp_layout(V, L).total;
+uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
+  const uint32_t t = ksp_layout(V, L, max_deg).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -311,7 +305,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
                             int num_cus, hipStream_t s) {
   if (!n) return hipSuccess;
-  const uint32_t lds = ksp_lds_bytes(g.V, g.L);
+  const uint32_t lds = ksp_lds_bytes(g.V, g.L, g.max_deg);
   if (!lds) return hipErrorInvalidValue;
   const uint32_t grid = blocks_for(n, lds, num_cus, kWave);
   auto k = kind == 1 ? ksp_trace_kernel<1> : ksp_trace_kernel<2>;
