@@ -82,7 +82,7 @@ struct Device {
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
-  DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2;
+  DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -95,7 +95,7 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj,    g.w,
-                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge, g.rank};
+                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge, g.rank, g.erec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -474,6 +474,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   OPENR_TRY(d.krows.reserve((size_t)chunk * V));
   OPENR_TRY(d.kign.reserve((size_t)chunk * ign_cap));
   OPENR_TRY(d.kend.reserve(chunk));
+  OPENR_TRY(d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V));
   OPENR_TRY(d.ksrc.reserve(chunk));
   OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
   OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
@@ -481,7 +482,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   for (uint32_t first = 0; first < n_pairs; first += chunk) {
     const uint32_t m = std::min(chunk, n_pairs - first);
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok1, tok_cap, d.kstatus.p, d.num_cus, s));
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s));
     OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
     SolveArgs b{};
     b.sources = d.ksrc.p;
@@ -495,7 +496,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.work = d.work.p;
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok2, tok_cap, d.kstatus.p, d.num_cus, s));
+                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s));
   }
   uint32_t status = 0;
   OPENR_TRY(hipMemcpyAsync(&status, d.kstatus.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -590,7 +591,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
                      d.kbase.p,     d.krows.p,      d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
-                     d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p};
+                     d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
@@ -669,7 +670,9 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   // transit views: an overloaded node is reached but never expanded unless it is the
   // source (LinkState.cpp:831-838), so its transit row is empty / all-down
   std::vector<uint2> row2(V), row2t(V);
-  std::vector<uint4> ellt(V);
+  std::vector<uint4> ellt(V), erec(E);
+  for (uint32_t e = 0; e < E; ++e)
+    erec[e] = make_uint4(adj[e] | (ovl[gr->col[e]] ? kNodeSink : 0u), win[e], lid[e], rev[e]);
   for (uint32_t u = 0; u < V; ++u) {
     uint32_t x[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
     if (!ovl[u])
@@ -727,6 +730,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.row2t, row2t.data(), V);
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
     if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
+    if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
     if (err == hipSuccess) err = up(&g.win, win.data(), E);

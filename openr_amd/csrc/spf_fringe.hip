@@ -144,28 +144,31 @@ __global__ __launch_bounds__(kWave) void fringe_kernel(DevGraph g, SolveArgs a, 
           const bool expand = v == src || !g.ovl[v];
           typename N::Val acc{};
           for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
-            uint32_t av[K], wo[K], wi[K];
-            bool ok[K];
+            uint4 rec[K];  // v->u: {u | down | sink(u), w(u->v), link, rev = u->v}
+            uint32_t wo[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j;
-              av[j] = e < r.y ? g.adj[e] : kEdgeDown;
+              rec[j] = e < r.y ? g.erec[e] : make_uint4(kEdgeDown, 0u, 0u, 0u);
               wo[j] = e < r.y ? g.w[e] : 0u;
-              wi[j] = e < r.y ? g.win[e] : 0u;
             }
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-              ok[j] = !(av[j] & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e0 + j]));
+            bool ok[K];
+            uint32_t uu[K];
             D du[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) du[j] = ok[j] ? dist[av[j]] : INF;
+            for (int j = 0; j < K; ++j) {
+              uu[j] = rec[j].x & ~(kEdgeDown | kNodeSink);
+              ok[j] = !(rec[j].x & kEdgeDown) && !(has_ign && test_bit(ign, rec[j].z));
+              du[j] = ok[j] ? dist[uu[j]] : INF;
+            }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               if (!ok[j]) continue;
-              const uint32_t u = av[j], e = e0 + j;
+              const uint32_t u = uu[j];
               // pull: in-edge u->v (metric win) is tight (LinkState.cpp:857-873)
-              if (v != src && du[j] != INF && (uint64_t)du[j] + wi[j] == (uint64_t)dv && (u == src || !g.ovl[u])) {
-                const uint32_t re = g.rev[e];
+              if (v != src && du[j] != INF && (uint64_t)du[j] + rec[j].y == (uint64_t)dv &&
+                  (u == src || !(rec[j].x & kNodeSink))) {
+                const uint32_t re = rec[j].w;
                 if (u == src) {
                   const uint32_t b = g.nbr[re];
                   if constexpr (N::kSingle) {

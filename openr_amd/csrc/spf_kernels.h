@@ -35,6 +35,8 @@ struct DevGraph {
   uint8_t* cls_lvl = nullptr;  // [V] source class of each node, lvl family (LvlClass)
   uint2* ledge = nullptr;      // [L] the two directed edges of each link (UINT32_MAX if unused)
   uint32_t* rank = nullptr;    // [V] name rank (pathLinks / pop-order tie-break)
+  uint4* erec = nullptr;       // [E] packed edge e = u->col: {col | kEdgeDown | kNodeSink if col is
+                               //     overloaded, win[e], lid[e], rev[e]} (one 16-byte load per edge)
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
@@ -144,7 +146,8 @@ constexpr uint32_t kKspArena = 1024;    // sorted pathLinks of the frames on the
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            int num_cus, hipStream_t s);
+                            uint32_t* qbuf, int num_cus, hipStream_t s);
+uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);

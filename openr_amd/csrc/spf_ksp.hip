@@ -27,6 +27,7 @@
 // len_0, edges_0..., len_1, edges_1..., ...], directed edge ids in src -> dest order.
 #include <algorithm>
 
+#include "spf_bfs_common.h"
 #include "spf_device.h"
 #include "spf_kernels.h"
 
@@ -36,10 +37,12 @@ namespace {
 using namespace dev;
 
 constexpr uint32_t kWave = 64;
+constexpr uint32_t kKspProbeAfter = 256;  // DFS frame entries of one trace before the reachability probe
+                                         // (OPENR_SPF_KSP_PROBE overrides: tests force 0)
 constexpr uint64_t kNoKey = ~0ull;
 
 struct KspLayout {
-  uint32_t vis, dead, fr_node, fr_edge, fr_beg, fr_cnt, fr_idx, ar_e, ar_l, ar_u, skd, skr, sidx, total;
+  uint32_t vis, dead, fr_node, fr_edge, fr_beg, fr_cnt, fr_idx, ar_e, ar_l, ar_u, skd, skr, sl, su, seen, total;
 };
 
 // deg = largest row (candidate scratch of one frame).
@@ -63,7 +66,9 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.ar_u = take(4u * kKspArena);
   l.skd = take(8u * deg);
   l.skr = take(8u * deg);
-  l.sidx = take(4u * deg);
+  l.sl = take(4u * deg);
+  l.su = take(4u * deg);
+  l.seen = take(4u * ((V + 31u) / 32u));
   l.total = off;
   return l;
 }
@@ -80,7 +85,10 @@ struct KspState {
   uint32_t *fr_node, *fr_edge, *fr_beg, *fr_cnt, *fr_idx;  // DFS frames
   uint32_t *ar_e, *ar_l, *ar_u;                            // per-frame sorted pathLinks
   uint64_t *skd, *skr;
-  uint32_t* sidx;
+  uint32_t *sl, *su;  // candidate scratch: link, tail
+  uint32_t* seen;  // reachability probe: visited nodes (V bits)
+  uint32_t* q;     // reachability probe queue (global, V entries per wavefront)
+  uint32_t probe_after;
 };
 
 // pathLinks(v) still worth trying -> arena[beg, beg + count) as (edge u->v, link, u):
@@ -99,21 +107,24 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
     const uint32_t e = e0 + lane;
     bool cand = false;
     uint64_t du = 0;
-    uint32_t u = 0;
+    uint32_t u = 0, rk = 0;
+    uint4 rec = make_uint4(kEdgeDown, 0u, 0u, 0u);
     if (e < r.y) {
-      const uint32_t av = g.adj[e];
-      u = av & ~kEdgeDown;
-      if (!(av & kEdgeDown) && !test_bit(st.vis, g.lid[e]) && !test_bit(st.dead, u) && (u == st.src || !g.ovl[u])) {
+      rec = g.erec[e];  // v->u: {u | flags, w(u->v), link, rev = u->v}
+      u = rec.x & ~(kEdgeDown | kNodeSink);
+      if (!(rec.x & kEdgeDown) && !test_bit(st.vis, rec.z) && !test_bit(st.dead, u) &&
+          (u == st.src || !(rec.x & kNodeSink))) {
         du = st.drow[u];
-        cand = du != kNoKey && du + g.win[e] == dv;
+        rk = g.rank[u];
+        cand = du != kNoKey && du + rec.y == dv;
       }
     }
     const uint32_t slot = wave_append(cand, &st.ctl[0]);
     if (cand) {
-      const uint32_t re = g.rev[e];
       st.skd[slot] = du;
-      st.skr[slot] = ((uint64_t)g.rank[u] << 32) | re;
-      st.sidx[slot] = e;  // v's row entry v->u: lid[e] is the link, rev[e] the pathLink edge
+      st.skr[slot] = ((uint64_t)rk << 32) | rec.w;
+      st.sl[slot] = rec.z;
+      st.su[slot] = u;
     }
   }
   lds_fence();
@@ -126,13 +137,76 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
       const uint64_t od = st.skd[j], orr = st.skr[j];
       rank += (od < kd || (od == kd && orr < kr)) ? 1u : 0u;
     }
-    const uint32_t e = st.sidx[i];
     st.ar_e[beg + rank] = (uint32_t)kr;  // re
-    st.ar_l[beg + rank] = g.lid[e];
-    st.ar_u[beg + rank] = g.adj[e] & ~kEdgeDown;
+    st.ar_l[beg + rank] = st.sl[i];
+    st.ar_u[beg + rank] = st.su[i];
   }
   lds_fence();
   return cnt;
+}
+
+// Will the running DFS still find a path? It keeps the prefix dest -> ... -> x on its
+// stack and, after deeper frames fail, tries the remaining pathLinks of every stack node
+// in turn, each link at most once: it succeeds iff some stack node (or `next`, the node
+// it is about to enter) reaches src over live pathLinks (unvisited link, tail not dead).
+// Checked by a backward BFS over the tight DAG from those seeds, one lane per frontier
+// node (its in-edges in a sequential loop, 4 loads in flight), queue in global scratch.
+// A negative answer ends the trace (and the pair's traces) without the rest of the DFS.
+// Wave-uniform result.
+__device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
+  const DevGraph& g = *st.g;
+  const uint32_t lane = threadIdx.x, vw = (g.V + 31u) / 32u;
+  for (uint32_t i = lane; i < vw; i += kWave) st.seen[i] = 0;
+  lds_fence();
+  if (lane == 0) {
+    uint32_t t = 0;
+    for (uint32_t i = 0; i <= sp; ++i) {
+      const uint32_t x = i < sp ? st.fr_node[i] : next;
+      if (!(st.seen[x >> 5] & (1u << (x & 31u)))) {
+        st.seen[x >> 5] |= 1u << (x & 31u);
+        st.q[t++] = x;
+      }
+    }
+    st.ctl[1] = t;
+  }
+  lds_fence();
+  __threadfence_block();
+  uint32_t head = 0, tail = __builtin_amdgcn_readfirstlane(st.ctl[1]);
+  bool found = false;
+  while (head < tail && !found) {
+    const uint32_t i = head + lane;
+    bool hit = false;
+    if (i < tail) {
+      const uint32_t v = st.q[i];
+      const uint64_t dv = st.drow[v];
+      const uint2 r = g.row2[v];
+      for (uint32_t e0 = r.x; e0 < r.y && !hit; e0 += 4u) {
+        uint4 rec[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rec[j] = e0 + j < r.y ? g.erec[e0 + j] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t u = rec[j].x & ~(kEdgeDown | kNodeSink);
+          if ((rec[j].x & kEdgeDown) || test_bit(st.vis, rec[j].z) || test_bit(st.dead, u)) continue;
+          if (u != st.src && (rec[j].x & kNodeSink)) continue;
+          const uint64_t du = st.drow[u];
+          if (du == kNoKey || du + rec[j].y != dv) continue;
+          if (u == st.src) {
+            hit = true;
+            break;
+          }
+          const uint32_t bit = 1u << (u & 31u);
+          if (!(atomicOr(&st.seen[u >> 5], bit) & bit)) st.q[atomicAdd(&st.ctl[1], 1u)] = u;
+        }
+      }
+    }
+    found = __any(hit);
+    __threadfence_block();
+    lds_fence();
+    head = std::min(tail, head + kWave);
+    tail = __builtin_amdgcn_readfirstlane(st.ctl[1]);
+  }
+  return found;
 }
 
 // One traceOnePath (LinkState.cpp:398-419): DFS from dest over pathLinks in the
@@ -154,7 +228,8 @@ __device__ int trace_one(const KspState& st, uint32_t dst) {
     st.fr_idx[0] = 0;
   }
   lds_fence();
-  uint32_t sp = 1, top = c0;
+  uint32_t sp = 1, top = c0, entries = 0;
+  bool probed = false;
   while (sp > 0) {
     const uint32_t f = sp - 1;
     const uint32_t idx = st.fr_idx[f], cnt = st.fr_cnt[f], beg = st.fr_beg[f];
@@ -182,6 +257,10 @@ __device__ int trace_one(const KspState& st, uint32_t dst) {
       lds_fence();
       return (int)sp;
     }
+    if (!probed && ++entries > st.probe_after) {  // a long search: is there a path at all?
+      probed = true;
+      if (!reachable(st, sp, u)) return -1;
+    }
     const uint32_t c = load_path_links(st, u, top);
     if (c == UINT32_MAX) return -2;
     if (lane == 0) {
@@ -208,7 +287,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           const uint32_t* pdst, uint32_t first, uint32_t n,
                                                           const uint64_t* rows, uint32_t* ign_io, uint32_t* ign_end,
                                                           uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap,
-                                                          uint32_t* status) {
+                                                          uint32_t* status, uint32_t* qbuf, uint32_t probe_after) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay = ksp_layout(V, g.L, g.max_deg);
@@ -228,7 +307,11 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
   st.ar_u = reinterpret_cast<uint32_t*>(base + lay.ar_u);
   st.skd = reinterpret_cast<uint64_t*>(base + lay.skd);
   st.skr = reinterpret_cast<uint64_t*>(base + lay.skr);
-  st.sidx = reinterpret_cast<uint32_t*>(base + lay.sidx);
+  st.sl = reinterpret_cast<uint32_t*>(base + lay.sl);
+  st.su = reinterpret_cast<uint32_t*>(base + lay.su);
+  st.seen = reinterpret_cast<uint32_t*>(base + lay.seen);
+  st.q = qbuf + (size_t)blockIdx.x * V;
+  st.probe_after = probe_after;
   const uint32_t lane = threadIdx.x, lw = (g.L + 31u) / 32u, vw = (V + 31u) / 32u;
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t pair = first + k;
@@ -295,6 +378,10 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 
 }  // namespace
 
+uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
+  return blocks_for(UINT32_MAX, ksp_lds_bytes(g.V, g.L, g.max_deg), num_cus, kWave);
+}
+
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
   const uint32_t t = ksp_layout(V, L, max_deg).total;
   return t <= kMaxLds ? t : 0;
@@ -303,17 +390,18 @@ uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            int num_cus, hipStream_t s) {
+                            uint32_t* qbuf, int num_cus, hipStream_t s) {
   if (!n) return hipSuccess;
   const uint32_t lds = ksp_lds_bytes(g.V, g.L, g.max_deg);
-  if (!lds) return hipErrorInvalidValue;
-  const uint32_t grid = blocks_for(n, lds, num_cus, kWave);
+  if (!lds || !qbuf) return hipErrorInvalidValue;
+  const uint32_t grid = blocks_for(n, lds, num_cus, kWave);  // <= ksp_max_grid: qbuf holds grid * V
   auto k = kind == 1 ? ksp_trace_kernel<1> : ksp_trace_kernel<2>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
-                     ign_cap, tok, tok_cap, status);
+                     ign_cap, tok, tok_cap, status, qbuf,
+                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30));
   return hipGetLastError();
 }
 

@@ -452,8 +452,16 @@ def check_ksp2_against_oracle(eng, g, pairs):
     return got
 
 
+@pytest.fixture(params=["default", "0", "3"])
+def ksp_probe(request, monkeypatch):
+    """KSP DFS reachability probe: default threshold, before every frame, after 3."""
+    if request.param != "default":
+        monkeypatch.setenv("OPENR_SPF_KSP_PROBE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("case", G.load()["cases"], ids=lambda c: c["name"])
-def test_ksp2_device_reference_cases_all_pairs(eng, case):
+def test_ksp2_device_reference_cases_all_pairs(eng, case, ksp_probe):
     g = G.build(case)
     pairs = [(s, d) for s in range(g.num_nodes) for d in range(g.num_nodes)]
     got = check_ksp2_against_oracle(eng, g, pairs)
@@ -464,14 +472,14 @@ def test_ksp2_device_reference_cases_all_pairs(eng, case):
 
 
 @pytest.mark.parametrize("seed,max_metric", [(0, 1), (1, 9), (2, 1)])
-def test_ksp2_device_random_graphs(eng, seed, max_metric):
+def test_ksp2_device_random_graphs(eng, seed, max_metric, ksp_probe):
     g = random_graph(400 + seed, 70, 160, max_metric, p_ovl=0.08, p_down=0.05, p_par=0.15)
     rng = np.random.default_rng(seed)
     pairs = [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (400, 2))] + [(3, 3)]
     check_ksp2_against_oracle(eng, g, pairs)
 
 
-def test_ksp2_device_fabric_sample(eng):
+def test_ksp2_device_fabric_sample(eng, ksp_probe):
     g = T.fabric(288 + 56)
     rng = np.random.default_rng(5)
     pairs = [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))]
