@@ -113,6 +113,7 @@ struct openr_spf_ctx {
   bool metric_ok = true;        // every usable metric in [1, 2^31-1]
   uint32_t group_lanes = 4;
   int family = kFamCode;        // BFS kernel family picked for this graph (FrontierEstimate)
+  uint32_t est_depth = 0;       // sampled BFS hop depth (general-metric kernel choice)
   uint32_t cls_mask[kNumFamilies] = {0, 0};  // source classes present among the nodes, per family
   uint32_t nsl[kNumFamilies] = {1, 1};       // next-hop slices of each family's sliced class
   uint32_t nsl_max() const { return std::max(nsl[0], nsl[1]); }
@@ -122,9 +123,11 @@ struct openr_spf_ctx {
 namespace {
 
 constexpr uint32_t kDeepGraphLevels = 24;
+constexpr uint32_t kRoundsMaxDepth = 48;  // hop depth below which general metrics use the rounds kernel
 
 struct Plan {
   bool bfs = true;
+  bool rounds = false;  // general metrics: distance rounds + Kahn (shallow graphs), else fringe
   int family = kFamCode;
   uint64_t cost = 1;
   uint32_t delta = 1;
@@ -209,6 +212,14 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
     p->bfs = false;
     p->delta = ctx->w_min;
     p->dist64 = (uint64_t)ctx->V * ctx->w_max >= 0xFFFFFFFFull;
+    // shallow graphs (sampled hop depth): rounds scale with hops, the fringe with distinct
+    // distances (OPENR_SPF_GENERAL=fringe|rounds overrides)
+    p->rounds = ctx->est_depth < kRoundsMaxDepth && ctx->devs[0].g.max_deg < 65535u;  // u16 in-degrees
+    if (const char* e = std::getenv("OPENR_SPF_GENERAL")) {
+      if (!std::strcmp(e, "fringe")) p->rounds = false;
+      if (!std::strcmp(e, "rounds")) p->rounds = ctx->devs[0].g.max_deg < 65535u;
+    }
+    if (p->rounds && !rounds_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64)) p->rounds = false;
     if (!fringe_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64))
       return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident general-metric kernel", ctx->V);
   }
@@ -234,7 +245,10 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((d.g.E + 63u) / 64u) * 8u, s);
     if (err != hipSuccess) return err;
   }
-  if (!p.bfs) return launch_fringe(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+  if (!p.bfs) {
+    if (p.rounds) return launch_rounds(d.g, a, p.dist64, p.nh_mode, d.num_cus, s, &info);
+    return launch_fringe(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
+  }
   const int gl = group_lanes_override((int)ctx->group_lanes);
   a.perm = nullptr;
   a.part = nullptr;
@@ -758,6 +772,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->w_max = w_max;
   ctx->metric_ok = metric_ok;
   ctx->family = est.family();
+  ctx->est_depth = est.depth;
   for (int f = 0; f < kNumFamilies; ++f) {
     ctx->cls_mask[f] = cls_mask[f];
     ctx->nsl[f] = std::max<uint32_t>(1u, (sliced_deg[f] + slice_bits(f) - 1u) / slice_bits(f));

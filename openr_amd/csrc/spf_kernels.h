@@ -126,6 +126,11 @@ hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
 // tight in-edges. Uses a.work[kFringeCtr, +2) for dynamic scheduling.
 hipError_t launch_fringe(const DevGraph& g, const SolveArgs& a, uint32_t delta, bool dist64,
                          int nh_mode, int num_cus, hipStream_t s, LaunchInfo* info);
+// General positive metrics on shallow graphs (spf_rounds.hip): Bellman-Ford distance
+// rounds, then next hops in Kahn order of the tight DAG. Same counters as the fringe.
+hipError_t launch_rounds(const DevGraph& g, const SolveArgs& a, bool dist64, int nh_mode, int num_cus,
+                         hipStream_t s, LaunchInfo* info);
+uint32_t rounds_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 
 // What-if sweep (spf_sweep.hip): unit u = i * n_src + j (links[i] failed, sources[j]).
 // Filter: changed[u] = 0 for every unit; units whose link has a tight edge in

@@ -1,0 +1,289 @@
+// spf_rounds.hip — general-metric SPF kernel for shallow graphs: distance rounds, then
+// next hops in topological order of the shortest-path DAG. One wavefront per solve.
+//
+// Semantics: LinkState::runSpf (/root/reference/openr/decision/LinkState.cpp:808-882)
+// in closed form for strictly positive metrics:
+//   dist(v) = shortest distance over usable edges; overloaded nodes other than the
+//             source are reached but never expanded (:831-838);
+//   nh(v)   = OR over tight in-edges u->v of (u == src ? {v} : nh(u))  (:857-873),
+//   u->v tight iff usable, u may expand and dist[u] + w(u->v) == dist[v].
+//
+// The fringe kernel (spf_fringe.hip) settles one bucket of width w_min per step, so a
+// solve costs one dependent chain of L2 loads per DISTINCT distance (~150-200 on the
+// 1k-node WAN with metrics U[1,64]). Here the sequential steps scale with the HOP depth
+// instead (~10 on the WAN):
+//   1. distance rounds (Bellman-Ford over a frontier): every node whose distance dropped
+//      in the last round relaxes its out-edges with LDS atomicMin; a node re-enters the
+//      next frontier at most once per round (an LDS bitmap dedups);
+//   2. tight in-degree of every reached node (lane per node over its in-edges);
+//   3. Kahn rounds over the tight DAG: a node whose tight in-degree reached 0 has its
+//      final next-hop set; it ORs it into its tight successors and decrements them.
+// Chosen per graph when the sampled hop depth is small (spf_capi.hip); the fringe kernel
+// keeps deep or chain-like graphs. Integer work only, no MFMA.
+#include <algorithm>
+
+#include "spf_bfs_common.h"
+#include "spf_device.h"
+#include "spf_kernels.h"
+
+namespace openr_spf {
+
+namespace {
+using namespace dev;
+using namespace bfs;
+
+constexpr uint32_t kWave = 64;
+
+struct RoundsLayout {
+  uint32_t dist, nh, cnt, fa, fb, inq, ign, total;
+};
+
+__host__ __device__ inline RoundsLayout rounds_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
+                                                      uint32_t dist_bytes) {
+  RoundsLayout l;
+  uint32_t off = 16;  // control: [0] next-frontier append counter
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.dist = take(dist_bytes * V);
+  l.nh = take(4u * nh_words);
+  l.cnt = take(2u * V);
+  l.fa = take(2u * V);
+  l.fb = take(2u * V);
+  l.inq = take(4u * ((V + 31u) / 32u));
+  l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
+  l.total = off;
+  return l;
+}
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int MODE, typename D, bool GENERIC>
+__global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, uint32_t has_ign_rt, uint32_t* ctr) {
+  using N = Nh<MODE>;
+  constexpr D INF = (D)~(D)0;
+  constexpr int K = 4;
+  const bool has_ign = GENERIC && has_ign_rt != 0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t V = g.V, lane = threadIdx.x;
+  const uint32_t nh_words = N::words(V);
+  const RoundsLayout lay = rounds_layout(V, g.L, has_ign, nh_words, sizeof(D));
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  D* dist = reinterpret_cast<D*>(base + lay.dist);
+  uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(base + lay.cnt);
+  uint16_t* fa = reinterpret_cast<uint16_t*>(base + lay.fa);
+  uint16_t* fb = reinterpret_cast<uint16_t*>(base + lay.fb);
+  uint32_t* inq = reinterpret_cast<uint32_t*>(base + lay.inq);
+  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
+  const uint32_t vw = (V + 31u) / 32u, ign_words = (g.L + 31u) / 32u;
+  const uint32_t tight_words = (g.E + 63u) / 64u;
+
+  for (uint32_t sid = blockIdx.x; sid < a.n;) {
+    const uint32_t src = a.sources[sid];
+    if (src < V) {
+      for (uint32_t v = lane; v < V; v += kWave) dist[v] = INF;
+      for (uint32_t i = lane; i < nh_words; i += kWave) nh[i] = 0;
+      for (uint32_t i = lane; i < vw; i += kWave) inq[i] = 0;
+      if (has_ign) {
+        for (uint32_t i = lane; i < ign_words; i += kWave) ign[i] = 0;
+        lds_fence();
+        load_ignore(ign, ign_words, a, sid, g.L);
+      }
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+      lds_fence();
+      if (lane == 0) {
+        dist[src] = 0;
+        fa[0] = (uint16_t)src;
+      }
+      lds_fence();
+
+      // (1) distance rounds over the frontier of nodes whose distance dropped
+      uint16_t *cur = fa, *nxt = fb;
+      uint32_t n = 1;
+      while (n) {
+        if (lane == 0) ctl[0] = 0;
+        lds_fence();
+        for (uint32_t i = lane; i < n; i += kWave) {
+          const uint32_t u = cur[i];
+          atomicAnd(&inq[u >> 5], ~(1u << (u & 31u)));  // may re-enter the next frontier
+          if (u != src && g.ovl[u]) continue;           // reached, never expanded
+          const D du = dist[u];
+          const uint2 r = g.row2[u];
+          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+            uint32_t av[K], wo[K], lv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j;
+              av[j] = e < r.y ? g.adj[e] : kEdgeDown;
+              wo[j] = e < r.y ? g.w[e] : 0u;
+              lv[j] = (has_ign && e < r.y) ? g.lid[e] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              if ((av[j] & kEdgeDown) || (has_ign && test_bit(ign, lv[j]))) continue;
+              const uint32_t v = av[j];
+              const D cand = du + (D)wo[j];
+              if (cand < dist[v]) {
+                const D old = atomicMin(&dist[v], cand);
+                if (cand < old) {
+                  const uint32_t bit = 1u << (v & 31u);
+                  if (!(atomicOr(&inq[v >> 5], bit) & bit)) nxt[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+                }
+              }
+            }
+          }
+        }
+        lds_fence();
+        n = __builtin_amdgcn_readfirstlane(ctl[0]);
+        uint16_t* t = cur;
+        cur = nxt;
+        nxt = t;
+      }
+
+      // (2) tight in-degree of every reached node; the source (and nodes with no tight
+      //     in-edge) start the topological rounds
+      if (lane == 0) ctl[0] = 0;
+      lds_fence();
+      for (uint32_t v = lane; v < V; v += kWave) {
+        const D dv = dist[v];
+        uint32_t c = 0;
+        if (dv != INF && v != src) {
+          const uint2 r = g.row2[v];
+          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+            uint4 rec[K];  // v->u: {u | down | sink(u), w(u->v), link, rev}
+#pragma unroll
+            for (int j = 0; j < K; ++j) rec[j] = e0 + j < r.y ? g.erec[e0 + j] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t u = rec[j].x & ~(kEdgeDown | kNodeSink);
+              if ((rec[j].x & kEdgeDown) || (has_ign && test_bit(ign, rec[j].z))) continue;
+              if (u != src && (rec[j].x & kNodeSink)) continue;
+              const D du = dist[u];
+              c += (du != INF && (uint64_t)du + rec[j].y == (uint64_t)dv) ? 1u : 0u;
+            }
+          }
+        }
+        cnt[v] = (uint16_t)c;
+        if (v == src) cur[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+      }
+      lds_fence();
+      n = __builtin_amdgcn_readfirstlane(ctl[0]);
+
+      // (3) Kahn rounds: a finished node pushes its set down its tight out-edges; the
+      //     decrement that empties a successor's count makes it finished next round
+      while (n) {
+        if (lane == 0) ctl[0] = 0;
+        lds_fence();
+        for (uint32_t i = lane; i < n; i += kWave) {
+          const uint32_t u = cur[i];
+          if (u != src && g.ovl[u]) continue;  // a sink has no tight out-edges
+          const D du = dist[u];
+          const typename N::Val xu = N::load(nh, u);
+          const uint2 r = g.row2[u];
+          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+            uint32_t av[K], wo[K], lv[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j;
+              av[j] = e < r.y ? g.adj[e] : kEdgeDown;
+              wo[j] = e < r.y ? g.w[e] : 0u;
+              lv[j] = (has_ign && e < r.y) ? g.lid[e] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              if ((av[j] & kEdgeDown) || (has_ign && test_bit(ign, lv[j]))) continue;
+              const uint32_t v = av[j], e = e0 + j;
+              const D dv = dist[v];
+              if (dv == INF || (uint64_t)du + wo[j] != (uint64_t)dv) continue;  // not tight
+              if (u == src) N::or_bit(nh, v, g.nbr[e]);
+              else N::or_val(nh, v, xu);
+              if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
+              const uint32_t sh = 16u * (v & 1u);
+              const uint32_t old = atomicSub(reinterpret_cast<uint32_t*>(cnt) + (v >> 1), 1u << sh);
+              if (((old >> sh) & 0xFFFFu) == 1u) nxt[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+            }
+          }
+        }
+        lds_fence();
+        n = __builtin_amdgcn_readfirstlane(ctl[0]);
+        uint16_t* t = cur;
+        cur = nxt;
+        nxt = t;
+      }
+      // (result rows, coalesced; unreached nodes keep UINT64_MAX)
+      uint64_t* drow = a.dist + (size_t)sid * V;
+      for (uint32_t v = lane; v < V; v += kWave) {
+        const D d = dist[v];
+        store_row<uint64_t>(&drow[v], d == INF ? ~0ull : (uint64_t)d, true);
+      }
+      if (a.nh) {
+        const uint32_t nb = a.nh_bytes;
+        uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+        for (uint32_t i = lane; i < V * nb; i += kWave) {
+          const uint32_t v = i / nb, j = i - v * nb;
+          nrow[i] = (uint8_t)N::byte(nh, v, j);
+        }
+      }
+    }
+    uint32_t nxt_sid = 0;
+    if (lane == 0) nxt_sid = gridDim.x + atomicAdd(&ctr[0], 1u);
+    sid = __builtin_amdgcn_readfirstlane(__shfl(nxt_sid, 0));
+  }
+  retire_workgroup(ctr, nullptr);
+}
+
+template <int MODE, typename D>
+hipError_t launch_rounds_t(const DevGraph& g, const SolveArgs& a, uint32_t lds, uint32_t grid, uint32_t* ctr,
+                           hipStream_t s) {
+  const bool has_ign = a.ign_ptr != nullptr;
+  const bool generic = has_ign || a.tight != nullptr;
+  auto k = generic ? rounds_kernel<MODE, D, true> : rounds_kernel<MODE, D, false>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, a, (uint32_t)has_ign, ctr);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+uint32_t rounds_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64) {
+  if (V > 65535u) return 0;
+  const uint32_t t = rounds_layout(V, L, has_ignore, nh_words_for(nh_mode, V), dist64 ? 8u : 4u).total;
+  return t <= kMaxLds ? t : 0;
+}
+
+hipError_t launch_rounds(const DevGraph& g, const SolveArgs& a, bool dist64, int nh_mode, int num_cus, hipStream_t s,
+                         LaunchInfo* info) {
+  const bool has_ign = a.ign_ptr != nullptr;
+  const uint32_t lds = rounds_lds_bytes(g.V, g.L, has_ign, nh_mode, dist64);
+  if (!lds || !a.work) return hipErrorInvalidValue;
+  if (a.n == 0) return hipSuccess;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus, kWave);
+  if (info) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = dist64 ? "rounds_kernel<u64>" : "rounds_kernel<u32>";
+  }
+  uint32_t* ctr = a.work + kFringeCtr;
+#define OPENR_ROUNDS_CASE(M) \
+  case M: return dist64 ? launch_rounds_t<M, unsigned long long>(g, a, lds, grid, ctr, s) \
+                        : launch_rounds_t<M, uint32_t>(g, a, lds, grid, ctr, s);
+  switch (nh_mode) {
+    OPENR_ROUNDS_CASE(kNhNibble)
+    OPENR_ROUNDS_CASE(kNhByte)
+    OPENR_ROUNDS_CASE(kNhHalf)
+    OPENR_ROUNDS_CASE(kNhW1)
+    OPENR_ROUNDS_CASE(kNhW2)
+    OPENR_ROUNDS_CASE(kNhW4)
+    OPENR_ROUNDS_CASE(kNhW8)
+  }
+#undef OPENR_ROUNDS_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace openr_spf

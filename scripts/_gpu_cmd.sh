@@ -3,6 +3,6 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --workload whatif --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/whatif.log 2>&1; rc=$?
-grep -v amdgpu.ids gpurun_out/whatif.log | tail -1 | cut -c1-400; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --workload ksp2 --ksp-sources 512 --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/ksp2.log 2>&1; rc=$?
-grep -v amdgpu.ids gpurun_out/ksp2.log | tail -1 | cut -c1-300; exit $rc
+grep -v amdgpu.ids gpurun_out/whatif.log | tail -1 | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u scripts/sweep.py --topology wan --variants "GEN=rounds;GEN=fringe" --rounds 3 > gpurun_out/sweepw.log 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/sweepw.log; exit $rc

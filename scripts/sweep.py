@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 
 KEYS = {"G": "OPENR_SPF_GROUP_LANES", "FULL": "OPENR_SPF_BFS_FULL",
         "WGS": "OPENR_SPF_BFS_WGS", "NT": "OPENR_SPF_NT", "BLK": "OPENR_SPF_BFS_BLOCK",
-        "FAM": "OPENR_SPF_BFS_FAMILY"}
+        "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL"}
 
 
 def parse(v):

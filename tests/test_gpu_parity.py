@@ -18,19 +18,24 @@ from oracle import Oracle
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", autouse=True, params=["code", "lvl"])
+@pytest.fixture(scope="module", autouse=True, params=[("code", "fringe"), ("lvl", "rounds")],
+                ids=["code-fringe", "lvl-rounds"])
 def bfs_family(request):
     """Every parity test runs on both uniform-cost kernel families (spf_bfs.hip and
-    spf_bfs_lvl.hip); production picks one per graph by depth (spf_capi.hip)."""
+    spf_bfs_lvl.hip) and both general-metric kernels (spf_fringe.hip, spf_rounds.hip);
+    production picks per graph by sampled depth (spf_capi.hip)."""
     import os
 
-    old = os.environ.get("OPENR_SPF_BFS_FAMILY")
-    os.environ["OPENR_SPF_BFS_FAMILY"] = request.param
+    keys = ("OPENR_SPF_BFS_FAMILY", "OPENR_SPF_GENERAL")
+    old = {k: os.environ.get(k) for k in keys}
+    for k, v in zip(keys, request.param):
+        os.environ[k] = v
     yield request.param
-    if old is None:
-        os.environ.pop("OPENR_SPF_BFS_FAMILY", None)
-    else:
-        os.environ["OPENR_SPF_BFS_FAMILY"] = old
+    for k in keys:
+        if old[k] is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = old[k]
 
 
 @pytest.fixture(scope="module")
