@@ -381,7 +381,7 @@ constexpr size_t kWhatifChunkBytes = size_t(1) << 30;
 // Reads the affected-unit count back (one stream sync) to size the chunks.
 hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, const Plan& ign_plan,
                             const uint32_t* d_links, uint32_t n_links, const uint32_t* d_sources, uint32_t n_src,
-                            uint32_t* d_changed, hipStream_t s, uint32_t* solved) {
+                            uint32_t* d_changed, hipStream_t s, uint32_t* solved, bool use_link_metric) {
   const uint32_t V = ctx->V, tw = (ctx->E + 63u) / 64u;
   const uint32_t nb = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
   *solved = 0;
@@ -420,6 +420,14 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(hipStreamSynchronize(s));
   *solved = count;
   if (!count) return hipSuccess;
+  // incremental by default: each affected unit is repaired from the base rows (A set,
+  // distances inside A, dirty next hops); OPENR_SPF_WHATIF=solve re-solves every unit
+  const char* mode = std::getenv("OPENR_SPF_WHATIF");
+  const bool dist64 = use_link_metric && (uint64_t)V * ctx->w_max >= 0xFFFFFFFFull;
+  if (!(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
+    return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
+                              !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);
+  }
   const size_t row = (size_t)V * (8u + nb);
   const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
   OPENR_TRY(d.wdist.reserve((size_t)chunk * V));
@@ -889,7 +897,7 @@ int openr_spf_whatif(openr_spf_ctx* ctx, const uint32_t* links, uint32_t n_links
     HIP_TRY(hipMemcpyAsync(d.win_src.p, sources, n_sources * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
     uint32_t solved = 0;
     HIP_TRY(whatif_on_device(ctx, d, bp, ip, d.win_links.p, m, d.win_src.p, n_sources, d.wchanged.p, d.stream,
-                             &solved));
+                             &solved, (flags & OPENR_SPF_USE_LINK_METRIC) != 0));
     HIP_TRY(hipMemcpyAsync(changed + (size_t)b * n_sources, d.wchanged.p, (size_t)m * n_sources * sizeof(uint32_t),
                            hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -919,7 +927,8 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   uint32_t solved = 0;
-  HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_sources, d_changed, s, &solved));
+  HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_sources, d_changed, s, &solved,
+                           (flags & OPENR_SPF_USE_LINK_METRIC) != 0));
   const uint64_t total = n_links && n_sources ? (uint64_t)solved + n_sources : 0u;
   ctx->stats.spf_runs += total;
   ctx->stats.batches += 1;

@@ -88,6 +88,7 @@ constexpr uint32_t kMaxClasses = 8;
 constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch, [4] flagged solves
 constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
 constexpr uint32_t kFringeCtr = kCtrPerClass * (kMaxClasses - 1);  // BFS classes use < 7 blocks
+constexpr uint32_t kIncrCtr = kFringeCtr + 2;                        // incremental what-if
 
 // Uniform-cost BFS kernel families (spf_capi.hip picks one per graph):
 //  * code (spf_bfs.hip): one packed LDS field per node = [next-hop bits | 3-bit level
@@ -143,6 +144,13 @@ hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64
                                const uint64_t* base_dist, const uint8_t* base_nh, const uint32_t* wunit,
                                uint32_t n_src, uint32_t* changed, int num_cus, hipStream_t s);
 hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
+// Incremental what-if (spf_sweep.hip): changed[wunit[k]] for every listed unit from the
+// base rows alone (no full re-solve). Uses a.work-style counters `ctr` (2 slots).
+hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uint32_t* wlink, const uint32_t* wunit,
+                              uint32_t count, uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
+                              uint32_t nb, bool unit_cost, bool dist64, uint32_t* changed, uint32_t* ctr,
+                              int num_cus, hipStream_t s);
+uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
 
 // KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
 constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)

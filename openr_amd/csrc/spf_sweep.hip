@@ -10,6 +10,7 @@
 // The rest are solved in chunks by the ordinary batched kernels (one (source,
 // {link}) ignore set per solve) and reduced against the base rows by rows_compare.
 // Integer / byte work only: HBM-bound, coalesced row reads, one workgroup per unit.
+#include "spf_bfs_common.h"
 #include "spf_kernels.h"
 
 namespace openr_spf {
@@ -84,6 +85,341 @@ __global__ __launch_bounds__(256) void rows_compare(uint32_t n, uint32_t V, uint
   }
 }
 
+// --- incremental what-if (one wavefront per affected unit) ---------------------------
+//
+// Removing link l from the SPF of s changes only part of the result. With (a->b) the
+// tight direction of l in the base SPF (dist D, next hops H):
+//   A = nodes whose distance grows: b if it has no other live tight in-edge, then every
+//       tight successor of an A node whose tight in-edges all come from A (decremental
+//       propagation over the base tight DAG). Every A node's distance strictly grows, and
+//       no A node can become a tight predecessor of a node outside A.
+//   D'  = D outside A; inside A: the best entry from outside A, then relaxation within A.
+//   nh' = recomputed in increasing D' for the dirty nodes: A, b, the non-A tight
+//         successors of A nodes, and the tight successors of every non-A node whose set
+//         changed (pulled over the new tight in-edges; clean nodes keep H).
+// changed = |A| + non-A nodes whose set changed — the same count rows_compare gets from a
+// full re-solve (the parity tests check both against oracle re-solves).
+struct IncrLayout {
+  uint32_t dist, nh, ina, dq, alist, dlist, total;
+};
+
+__host__ __device__ inline IncrLayout incr_layout(uint32_t V, uint32_t nb, uint32_t dist_bytes) {
+  IncrLayout l;
+  uint32_t off = 16;  // control: [0] A count, [1] dirty count, [2] flag
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.dist = take(dist_bytes * V);
+  l.nh = take(nb * V);
+  l.ina = take(4u * ((V + 31u) / 32u));
+  l.dq = take(4u * ((V + 31u) / 32u));
+  l.alist = take(2u * V);
+  l.dlist = take(2u * V);
+  l.total = off;
+  return l;
+}
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ bool bit_of(const uint32_t* b, uint32_t i) { return (b[i >> 5] >> (i & 31u)) & 1u; }
+
+template <typename D>
+__device__ __forceinline__ D wave_min_t(D x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const D y = __shfl_xor(x, o);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+template <typename D>
+struct IncrCtx {
+  const DevGraph* g;
+  uint32_t src, link, nb;
+  bool unit;
+  D* dist;
+  uint8_t* nh;
+  uint32_t *ina, *dq, *ctl;
+  uint16_t *alist, *dlist;
+  __device__ uint32_t wout(uint32_t e) const { return unit ? 1u : g->w[e]; }
+  __device__ bool expands(uint32_t x) const { return x == src || !g->ovl[x]; }
+};
+
+// Does v keep a tight in-edge from a node outside A (other than link l)? Lanes over v's
+// in-edges; wave-uniform.
+template <typename D>
+__device__ bool live_pred(const IncrCtx<D>& c, uint32_t v) {
+  const DevGraph& g = *c.g;
+  constexpr D INF = (D)~(D)0;
+  const D dv = c.dist[v];
+  const uint2 r = g.row2[v];
+  for (uint32_t e = r.x + threadIdx.x; __any(e < r.y); e += 64u) {
+    bool ok = false;
+    if (e < r.y) {
+      const uint4 rec = g.erec[e];  // v->u: {u | down | sink(u), w(u->v), link, rev}
+      const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+      if (!(rec.x & kEdgeDown) && rec.z != c.link && (u == c.src || !(rec.x & kNodeSink)) && !bit_of(c.ina, u)) {
+        const D du = c.dist[u];
+        ok = du != INF && (uint64_t)du + (c.unit ? 1u : rec.y) == (uint64_t)dv;
+      }
+    }
+    if (__any(ok)) return true;
+  }
+  return false;
+}
+
+template <typename D>
+__device__ void push_dirty(const IncrCtx<D>& c, uint32_t y) {  // lane 0 only
+  if (!bit_of(c.dq, y)) {
+    c.dq[y >> 5] |= 1u << (y & 31u);
+    c.dlist[c.ctl[1]++] = (uint16_t)y;
+  }
+}
+
+template <typename D>
+__global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint32_t* wsrc, const uint32_t* wlink,
+                                                         const uint32_t* wunit, uint32_t count, uint32_t n_src,
+                                                         const uint64_t* base_dist, const uint8_t* base_nh,
+                                                         uint32_t nb, uint32_t unit, uint32_t* changed,
+                                                         uint32_t* ctr) {
+  constexpr D INF = (D)~(D)0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t V = g.V, lane = threadIdx.x, vw = (V + 31u) / 32u;
+  const IncrLayout lay = incr_layout(V, nb, sizeof(D));
+  char* base = reinterpret_cast<char*>(smem);
+  IncrCtx<D> c;
+  c.g = &g;
+  c.nb = nb;
+  c.unit = unit != 0;
+  c.ctl = smem;
+  c.dist = reinterpret_cast<D*>(base + lay.dist);
+  c.nh = reinterpret_cast<uint8_t*>(base + lay.nh);
+  c.ina = reinterpret_cast<uint32_t*>(base + lay.ina);
+  c.dq = reinterpret_cast<uint32_t*>(base + lay.dq);
+  c.alist = reinterpret_cast<uint16_t*>(base + lay.alist);
+  c.dlist = reinterpret_cast<uint16_t*>(base + lay.dlist);
+  for (uint32_t k = blockIdx.x; k < count;) {
+    const uint32_t unit_id = wunit[k], j = unit_id % n_src;
+    c.src = wsrc[k];
+    c.link = wlink[k];
+    const uint64_t* drow = base_dist + (size_t)j * V;
+    const uint8_t* hrow = base_nh + (size_t)j * V * nb;
+    for (uint32_t v = lane; v < V; v += 64u) {
+      const uint64_t d = drow[v];
+      c.dist[v] = d == ~0ull ? INF : (D)d;
+    }
+    for (uint32_t i = lane; i < V * nb; i += 64u) c.nh[i] = hrow[i];
+    for (uint32_t i = lane; i < vw; i += 64u) {
+      c.ina[i] = 0;
+      c.dq[i] = 0;
+    }
+    if (lane == 0) c.ctl[0] = c.ctl[1] = 0;
+    lds_fence();
+    // the tight direction a->b of link l (the filter guarantees one)
+    const uint2 ee = g.ledge[c.link];
+    uint32_t bnode = UINT32_MAX;
+    for (int t = 0; t < 2; ++t) {
+      const uint32_t e = t ? ee.y : ee.x;
+      const uint32_t av = g.adj[e];
+      const uint32_t head = av & ~kEdgeDown, tail = g.adj[g.rev[e]] & ~kEdgeDown;
+      if ((av & kEdgeDown) || !c.expands(tail)) continue;
+      const D dt = c.dist[tail], dh = c.dist[head];
+      if (dt != INF && dh != INF && (uint64_t)dt + c.wout(e) == (uint64_t)dh) bnode = head;
+    }
+    uint32_t nchanged = 0;
+    if (bnode != UINT32_MAX) {
+      // (1) A by decremental propagation over the base tight DAG
+      if (!live_pred(c, bnode)) {
+        if (lane == 0) {
+          c.ina[bnode >> 5] |= 1u << (bnode & 31u);
+          c.alist[c.ctl[0]++] = (uint16_t)bnode;
+        }
+      }
+      if (lane == 0) push_dirty(c, bnode);
+      lds_fence();
+      for (uint32_t idx = 0; idx < __builtin_amdgcn_readfirstlane(c.ctl[0]); ++idx) {
+        const uint32_t x = c.alist[idx];
+        if (!c.expands(x)) continue;
+        const D dx = c.dist[x];
+        const uint2 r = g.row2[x];
+        for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+          const uint32_t e = e0 + lane;
+          uint32_t y = 0;
+          bool cand = false;
+          if (e < r.y) {
+            const uint32_t av = g.adj[e];
+            y = av & ~kEdgeDown;
+            cand = !(av & kEdgeDown) && g.lid[e] != c.link && !bit_of(c.ina, y) && c.dist[y] != INF &&
+                   (uint64_t)dx + c.wout(e) == (uint64_t)c.dist[y];
+          }
+          unsigned long long m = __ballot(cand);
+          while (m) {  // each base-tight successor outside A: does it keep a live pred?
+            const int ln = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const uint32_t yy = __shfl(y, ln);
+            if (bit_of(c.ina, yy)) continue;
+            const bool keep = live_pred(c, yy);
+            if (lane == 0) {
+              if (!keep) {
+                c.ina[yy >> 5] |= 1u << (yy & 31u);
+                c.alist[c.ctl[0]++] = (uint16_t)yy;
+              }
+              push_dirty(c, yy);  // A or not, its set must be recomputed
+            }
+            lds_fence();
+          }
+        }
+      }
+      const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
+      // (2) new distances inside A: best entry from outside A, then relaxation within A
+      for (uint32_t i = lane; i < na; i += 64u) {
+        const uint32_t x = c.alist[i];
+        const uint2 r = g.row2[x];
+        D best = INF;
+        for (uint32_t e = r.x; e < r.y; ++e) {
+          const uint4 rec = g.erec[e];
+          const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+          if ((rec.x & kEdgeDown) || rec.z == c.link || bit_of(c.ina, u)) continue;
+          if (u != c.src && (rec.x & kNodeSink)) continue;
+          const D du = c.dist[u];
+          if (du == INF) continue;
+          const D cand = du + (D)(c.unit ? 1u : rec.y);
+          best = cand < best ? cand : best;
+        }
+        c.dist[x] = best;  // only non-A distances are read above
+      }
+      lds_fence();
+      for (;;) {
+        if (lane == 0) c.ctl[2] = 0;
+        lds_fence();
+        for (uint32_t i = lane; i < na; i += 64u) {
+          const uint32_t x = c.alist[i];
+          const D dx = c.dist[x];
+          if (dx == INF || !c.expands(x)) continue;
+          const uint2 r = g.row2[x];
+          for (uint32_t e = r.x; e < r.y; ++e) {
+            const uint32_t av = g.adj[e];
+            const uint32_t y = av & ~kEdgeDown;
+            if ((av & kEdgeDown) || g.lid[e] == c.link || !bit_of(c.ina, y)) continue;
+            const D cand = dx + (D)c.wout(e);
+            if (cand < c.dist[y]) {
+              atomicMin(&c.dist[y], cand);
+              c.ctl[2] = 1;
+            }
+          }
+        }
+        lds_fence();
+        if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
+      }
+      // (3) next hops in increasing new distance over the dirty set
+      uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
+      while (done < nd) {
+        D mn = INF;
+        for (uint32_t i = done + lane; i < nd; i += 64u) {
+          const D d = c.dist[c.dlist[i]];
+          mn = d < mn ? d : mn;
+        }
+        mn = wave_min_t(mn);
+        // move this bucket's members to [done, done + nm) (order within the list is free)
+        uint32_t nm = 0;
+        if (lane == 0) {
+          for (uint32_t i = done; i < nd; ++i) {
+            const uint32_t v = c.dlist[i];
+            if (c.dist[v] == mn) {
+              c.dlist[i] = c.dlist[done + nm];
+              c.dlist[done + nm] = (uint16_t)v;
+              ++nm;
+            }
+          }
+          c.ctl[3] = nm;
+        }
+        lds_fence();
+        nm = __builtin_amdgcn_readfirstlane(c.ctl[3]);
+        for (uint32_t i = lane; i < nm; i += 64u) {
+          const uint32_t v = c.dlist[done + i];
+          uint8_t acc[32];
+          uint32_t acc1 = 0;  // nb == 1 (<= 8 next hops): register accumulator
+          if (nb > 1)
+            for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
+          const D dv = c.dist[v];
+          const uint2 r = g.row2[v];
+          if (dv != INF)
+            for (uint32_t e = r.x; e < r.y; ++e) {
+              const uint4 rec = g.erec[e];
+              const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+              if ((rec.x & kEdgeDown) || rec.z == c.link) continue;
+              if (u != c.src && (rec.x & kNodeSink)) continue;
+              const D du = c.dist[u];
+              if (du == INF || (uint64_t)du + (c.unit ? 1u : rec.y) != (uint64_t)dv) continue;
+              if (u == c.src) {
+                const uint32_t bit = g.nbr[rec.w];
+                if (nb == 1) acc1 |= 1u << bit;
+                else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
+              } else if (nb == 1) {
+                acc1 |= c.nh[u];
+              } else {
+                for (uint32_t b = 0; b < nb; ++b) acc[b] |= c.nh[(size_t)u * nb + b];
+              }
+            }
+          bool diff = false;
+          if (nb == 1) {
+            diff = (uint8_t)acc1 != c.nh[v];
+            if (diff) c.nh[v] = (uint8_t)acc1;
+          } else {
+            for (uint32_t b = 0; b < nb; ++b) diff |= acc[b] != c.nh[(size_t)v * nb + b];
+            if (diff)
+              for (uint32_t b = 0; b < nb; ++b) c.nh[(size_t)v * nb + b] = acc[b];
+          }
+          const bool in_a = bit_of(c.ina, v);
+          // alist is free after (2): per-member flags, 1 = push successors, 2 = in A
+          c.alist[i] = (uint16_t)(((diff && !in_a) ? 1u : 0u) | (in_a ? 2u : 0u));
+        }
+        lds_fence();
+        // count and push successors of the non-A nodes whose set changed (lane 0 loops)
+        for (uint32_t i = 0; i < nm; ++i) {
+          const uint32_t fl = c.alist[i];
+          const uint32_t v = c.dlist[done + i];
+          if (fl & 2u) ++nchanged;
+          if (!(fl & 1u)) continue;
+          ++nchanged;
+          if (!c.expands(v)) continue;
+          const D dv = c.dist[v];
+          const uint2 r = g.row2[v];
+          for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+            const uint32_t e = e0 + lane;
+            uint32_t y = 0;
+            bool cand = false;
+            if (e < r.y) {
+              const uint32_t av = g.adj[e];
+              y = av & ~kEdgeDown;
+              cand = !(av & kEdgeDown) && g.lid[e] != c.link && y != c.src && c.dist[y] != INF &&
+                     (uint64_t)dv + c.wout(e) == (uint64_t)c.dist[y];
+            }
+            unsigned long long m = __ballot(cand);
+            while (m) {
+              const int ln = __ffsll((long long)m) - 1;
+              m &= m - 1ull;
+              const uint32_t yy = __shfl(y, ln);
+              if (lane == 0) push_dirty(c, yy);
+            }
+            lds_fence();
+          }
+        }
+        done += nm;
+        nd = __builtin_amdgcn_readfirstlane(c.ctl[1]);
+      }
+    }
+    if (lane == 0) changed[unit_id] = nchanged;
+    uint32_t nxt = 0;
+    if (lane == 0) nxt = gridDim.x + atomicAdd(&ctr[0], 1u);
+    k = __builtin_amdgcn_readfirstlane(__shfl(nxt, 0));
+    lds_fence();
+  }
+  bfs::retire_workgroup(ctr, nullptr);
+}
+
 __global__ __launch_bounds__(256) void iota_u32(uint32_t* p, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) p[i] = i;
 }
@@ -115,6 +451,29 @@ hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(rows_compare, dim3(grid_for(n, 1u, num_cus)), dim3(256), 0, s, n, V, nb, dist, nh, base_dist,
                      base_nh, wunit, n_src, changed);
+  return hipGetLastError();
+}
+
+uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64) {
+  if (V > 65535u || nb > 32u) return 0;
+  const uint32_t t = incr_layout(V, nb, dist64 ? 8u : 4u).total;
+  return t <= kMaxLds ? t : 0;
+}
+
+hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uint32_t* wlink, const uint32_t* wunit,
+                              uint32_t count, uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
+                              uint32_t nb, bool unit_cost, bool dist64, uint32_t* changed, uint32_t* ctr,
+                              int num_cus, hipStream_t s) {
+  if (!count) return hipSuccess;
+  const uint32_t lds = whatif_incr_lds_bytes(g.V, nb, dist64);
+  if (!lds) return hipErrorInvalidValue;
+  const uint32_t grid = blocks_for(count, lds, num_cus, 64u);
+  auto k = dist64 ? whatif_incr_kernel<unsigned long long> : whatif_incr_kernel<uint32_t>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, s, g, wsrc, wlink, wunit, count, n_src, base_dist, base_nh, nb,
+                     (uint32_t)unit_cost, changed, ctr);
   return hipGetLastError();
 }
 

@@ -391,8 +391,15 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
+@pytest.fixture(params=["incr", "solve"])
+def whatif_mode(request, monkeypatch):
+    """What-if units repaired incrementally from the base rows (default) or re-solved."""
+    monkeypatch.setenv("OPENR_SPF_WHATIF", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("seed,max_metric", [(0, 64), (1, 1), (2, 7)])
-def test_whatif_sweep_matches_oracle(eng, seed, max_metric):
+def test_whatif_sweep_matches_oracle(eng, seed, max_metric, whatif_mode):
     g = random_graph(300 + seed, 120, 300, max_metric, p_ovl=0.05, p_down=0.05, p_par=0.1)
     eng.set_graph(g)
     links = list(range(g.num_links))
@@ -406,7 +413,7 @@ def test_whatif_sweep_matches_oracle(eng, seed, max_metric):
     np.testing.assert_array_equal(c2, whatif_oracle(g, links[::5], sources[:7], False))
 
 
-def test_whatif_wan_sample_and_device_form(eng):
+def test_whatif_wan_sample_and_device_form(eng, whatif_mode):
     import torch
 
     g = T.wan(1000, 3000, 64, seed=1)
@@ -425,7 +432,7 @@ def test_whatif_wan_sample_and_device_form(eng):
     np.testing.assert_array_equal(d_c.cpu().numpy().view(np.uint32), changed)
 
 
-def test_whatif_edge_cases(eng):
+def test_whatif_edge_cases(eng, whatif_mode):
     g = T.grid_fast(6)
     eng.set_graph(g)
     c, solved = eng.whatif([], [0, 1], True)
@@ -521,3 +528,15 @@ def test_ksp2_device_form_and_overflow(eng):
     assert ei.value.code == E2BIG
     t1, _ = eng.ksp2_tokens([0, 0], [V - 1, 1], 8, allow_overflow=True)
     assert t1[0, 0] == 0xFFFFFFFF and t1[1, 0] == 1
+
+
+def test_whatif_overloads_parallel_links_hubs(eng, whatif_mode):
+    """What-if on graphs with overloaded nodes, down links, parallel links and wide
+    next-hop sets (multi-byte rows), all links x all sources."""
+    g = hub_graph(7, V=160, L=320, hub_deg=(30, 45))
+    eng.set_graph(g)
+    links = list(range(g.num_links))
+    srcs = list(range(0, g.num_nodes, 4))
+    for use_metric in (True, False):
+        changed, _ = eng.whatif(links, srcs, use_metric)
+        np.testing.assert_array_equal(changed, whatif_oracle(g, links, srcs, use_metric))
