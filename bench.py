@@ -187,8 +187,10 @@ def whatif_main(args):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "bytes_per_step": bytes_step,
-                         "note": "SURVEY.md 8d: B(src) per what-if unit, units resolved by the tight-edge "
-                                 "filter included; solved units only: "
+                         "note": "SURVEY.md 8d: B(src) credited per what-if unit (the formula is applied even "
+                                 "when the kernel exits early); units resolved by the tight-edge filter included. "
+                                 "Affected units are repaired incrementally from the base rows "
+                                 f"(openr_spf_whatif); affected units only: "
                                  f"{bytes_solved / (elapsed / args.steps) / 1e9:.1f} GB/s"},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -115,7 +115,7 @@ __host__ __device__ inline IncrLayout incr_layout(uint32_t V, uint32_t nb, uint3
   l.nh = take(nb * V);
   l.ina = take(4u * ((V + 31u) / 32u));
   l.dq = take(4u * ((V + 31u) / 32u));
-  l.alist = take(2u * V);
+  l.alist = take(2u * V);  // A list; in (3) split scratch: members from the front, rest from the back
   l.dlist = take(2u * V);
   l.total = off;
   return l;
@@ -166,6 +166,28 @@ __device__ bool live_pred(const IncrCtx<D>& c, uint32_t v) {
       }
     }
     if (__any(ok)) return true;
+  }
+  return false;
+}
+
+// Same test by a single lane (sequential in-edge loop, 4 records in flight).
+template <typename D>
+__device__ bool live_pred_lane(const IncrCtx<D>& c, uint32_t v, D INF) {
+  const DevGraph& g = *c.g;
+  const D dv = c.dist[v];
+  const uint2 r = g.row2[v];
+  for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+    uint4 rec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+      if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
+      if (u != c.src && (rec[q].x & kNodeSink)) continue;
+      const D du = c.dist[u];
+      if (du != INF && (uint64_t)du + (c.unit ? 1u : rec[q].y) == (uint64_t)dv) return true;
+    }
   }
   return false;
 }
@@ -231,13 +253,11 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
     uint32_t nchanged = 0;
     if (bnode != UINT32_MAX) {
       // (1) A by decremental propagation over the base tight DAG
-      if (!live_pred(c, bnode)) {
-        if (lane == 0) {
-          c.ina[bnode >> 5] |= 1u << (bnode & 31u);
-          c.alist[c.ctl[0]++] = (uint16_t)bnode;
-        }
-      }
       if (lane == 0) push_dirty(c, bnode);
+      if (!live_pred(c, bnode) && lane == 0) {
+        c.ina[bnode >> 5] |= 1u << (bnode & 31u);
+        c.alist[c.ctl[0]++] = (uint16_t)bnode;
+      }
       lds_fence();
       for (uint32_t idx = 0; idx < __builtin_amdgcn_readfirstlane(c.ctl[0]); ++idx) {
         const uint32_t x = c.alist[idx];
@@ -245,31 +265,22 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
         const D dx = c.dist[x];
         const uint2 r = g.row2[x];
         for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+          // lane per out-edge: a base-tight successor y outside A either keeps a live
+          // pred or joins A (checked in parallel; a pred that joins A later re-checks y)
           const uint32_t e = e0 + lane;
-          uint32_t y = 0;
-          bool cand = false;
           if (e < r.y) {
             const uint32_t av = g.adj[e];
-            y = av & ~kEdgeDown;
-            cand = !(av & kEdgeDown) && g.lid[e] != c.link && !bit_of(c.ina, y) && c.dist[y] != INF &&
-                   (uint64_t)dx + c.wout(e) == (uint64_t)c.dist[y];
-          }
-          unsigned long long m = __ballot(cand);
-          while (m) {  // each base-tight successor outside A: does it keep a live pred?
-            const int ln = __ffsll((long long)m) - 1;
-            m &= m - 1ull;
-            const uint32_t yy = __shfl(y, ln);
-            if (bit_of(c.ina, yy)) continue;
-            const bool keep = live_pred(c, yy);
-            if (lane == 0) {
-              if (!keep) {
-                c.ina[yy >> 5] |= 1u << (yy & 31u);
-                c.alist[c.ctl[0]++] = (uint16_t)yy;
+            const uint32_t y = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && g.lid[e] != c.link && !bit_of(c.ina, y) && c.dist[y] != INF &&
+                (uint64_t)dx + c.wout(e) == (uint64_t)c.dist[y]) {
+              const uint32_t bit = 1u << (y & 31u);
+              if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
+              if (!live_pred_lane(c, y, INF)) {
+                if (!(atomicOr(&c.ina[y >> 5], bit) & bit)) c.alist[atomicAdd(&c.ctl[0], 1u)] = (uint16_t)y;
               }
-              push_dirty(c, yy);  // A or not, its set must be recomputed
             }
-            lds_fence();
           }
+          lds_fence();
         }
       }
       const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
@@ -278,15 +289,20 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
         const uint32_t x = c.alist[i];
         const uint2 r = g.row2[x];
         D best = INF;
-        for (uint32_t e = r.x; e < r.y; ++e) {
-          const uint4 rec = g.erec[e];
-          const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-          if ((rec.x & kEdgeDown) || rec.z == c.link || bit_of(c.ina, u)) continue;
-          if (u != c.src && (rec.x & kNodeSink)) continue;
-          const D du = c.dist[u];
-          if (du == INF) continue;
-          const D cand = du + (D)(c.unit ? 1u : rec.y);
-          best = cand < best ? cand : best;
+        for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+          uint4 rec[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+            if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
+            if (u != c.src && (rec[q].x & kNodeSink)) continue;
+            const D du = c.dist[u];
+            if (du == INF) continue;
+            const D cand = du + (D)(c.unit ? 1u : rec[q].y);
+            best = cand < best ? cand : best;
+          }
         }
         c.dist[x] = best;  // only non-A distances are read above
       }
@@ -313,7 +329,8 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
         lds_fence();
         if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
       }
-      // (3) next hops in increasing new distance over the dirty set
+      // (3) next hops in increasing new distance over the dirty set; bucket members are
+      //     independent (positive metrics), one lane per member
       uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
       while (done < nd) {
         D mn = INF;
@@ -322,91 +339,90 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
           mn = d < mn ? d : mn;
         }
         mn = wave_min_t(mn);
-        // move this bucket's members to [done, done + nm) (order within the list is free)
-        uint32_t nm = 0;
-        if (lane == 0) {
-          for (uint32_t i = done; i < nd; ++i) {
-            const uint32_t v = c.dlist[i];
-            if (c.dist[v] == mn) {
-              c.dlist[i] = c.dlist[done + nm];
-              c.dlist[done + nm] = (uint16_t)v;
-              ++nm;
-            }
-          }
-          c.ctl[3] = nm;
+        // split [done, nd): members first (alist is free after (2): scratch)
+        uint32_t nm = 0, nr = 0;
+        for (uint32_t i0 = done; i0 < nd; i0 += 64u) {
+          const uint32_t i = i0 + lane;
+          const bool live = i < nd;
+          const uint32_t v = live ? c.dlist[i] : 0u;
+          const bool in = live && c.dist[v] == mn;
+          const unsigned long long mi = __ballot(in), mr = __ballot(live && !in);
+          const unsigned long long lt = (1ull << lane) - 1ull;
+          if (in) c.alist[nm + (uint32_t)__popcll(mi & lt)] = (uint16_t)v;
+          if (live && !in) c.alist[V - 1u - (nr + (uint32_t)__popcll(mr & lt))] = (uint16_t)v;
+          nm += (uint32_t)__popcll(mi);
+          nr += (uint32_t)__popcll(mr);
         }
         lds_fence();
-        nm = __builtin_amdgcn_readfirstlane(c.ctl[3]);
-        for (uint32_t i = lane; i < nm; i += 64u) {
-          const uint32_t v = c.dlist[done + i];
-          uint8_t acc[32];
-          uint32_t acc1 = 0;  // nb == 1 (<= 8 next hops): register accumulator
-          if (nb > 1)
-            for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
-          const D dv = c.dist[v];
-          const uint2 r = g.row2[v];
-          if (dv != INF)
-            for (uint32_t e = r.x; e < r.y; ++e) {
-              const uint4 rec = g.erec[e];
-              const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-              if ((rec.x & kEdgeDown) || rec.z == c.link) continue;
-              if (u != c.src && (rec.x & kNodeSink)) continue;
-              const D du = c.dist[u];
-              if (du == INF || (uint64_t)du + (c.unit ? 1u : rec.y) != (uint64_t)dv) continue;
-              if (u == c.src) {
-                const uint32_t bit = g.nbr[rec.w];
-                if (nb == 1) acc1 |= 1u << bit;
-                else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
-              } else if (nb == 1) {
-                acc1 |= c.nh[u];
-              } else {
-                for (uint32_t b = 0; b < nb; ++b) acc[b] |= c.nh[(size_t)u * nb + b];
+        for (uint32_t i = lane; i < nm + nr; i += 64u)
+          c.dlist[done + i] = i < nm ? c.alist[i] : c.alist[V - 1u - (i - nm)];
+        if (lane == 0) c.ctl[1] = nd;  // appends of this bucket go after the list
+        lds_fence();
+        uint32_t cnt_changed = 0;
+        for (uint32_t i0 = 0; i0 < nm; i0 += 64u) {
+          const uint32_t i = i0 + lane;
+          bool counted = false;
+          if (i < nm) {
+            const uint32_t v = c.dlist[done + i];
+            uint8_t acc[32];
+            uint32_t acc1 = 0;  // nb == 1 (<= 8 next hops): register accumulator
+            if (nb > 1)
+              for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
+            const D dv = c.dist[v];
+            const uint2 r = g.row2[v];
+            if (dv != INF)
+              for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+                uint4 rec[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+                  if ((rec[q].x & kEdgeDown) || rec[q].z == c.link) continue;
+                  if (u != c.src && (rec[q].x & kNodeSink)) continue;
+                  const D du = c.dist[u];
+                  if (du == INF || (uint64_t)du + (c.unit ? 1u : rec[q].y) != (uint64_t)dv) continue;
+                  if (u == c.src) {
+                    const uint32_t bit = g.nbr[rec[q].w];
+                    if (nb == 1) acc1 |= 1u << bit;
+                    else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
+                  } else if (nb == 1) {
+                    acc1 |= c.nh[u];
+                  } else {
+                    for (uint32_t b = 0; b < nb; ++b) acc[b] |= c.nh[(size_t)u * nb + b];
+                  }
+                }
+              }
+            bool diff = false;
+            if (nb == 1) {
+              diff = (uint8_t)acc1 != c.nh[v];
+              if (diff) c.nh[v] = (uint8_t)acc1;
+            } else {
+              for (uint32_t b = 0; b < nb; ++b) diff |= acc[b] != c.nh[(size_t)v * nb + b];
+              if (diff)
+                for (uint32_t b = 0; b < nb; ++b) c.nh[(size_t)v * nb + b] = acc[b];
+            }
+            const bool in_a = bit_of(c.ina, v);
+            counted = in_a || diff;
+            // a non-A node whose set changed dirties its tight successors (an A node's new
+            // tight successors are A nodes, already dirty)
+            if (diff && !in_a && c.expands(v)) {
+              const uint2 ro = g.row2[v];
+              for (uint32_t e = ro.x; e < ro.y; ++e) {
+                const uint32_t av = g.adj[e];
+                const uint32_t y = av & ~kEdgeDown;
+                if ((av & kEdgeDown) || g.lid[e] == c.link || y == c.src || c.dist[y] == INF) continue;
+                if ((uint64_t)dv + c.wout(e) != (uint64_t)c.dist[y]) continue;
+                const uint32_t bit = 1u << (y & 31u);
+                if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
               }
             }
-          bool diff = false;
-          if (nb == 1) {
-            diff = (uint8_t)acc1 != c.nh[v];
-            if (diff) c.nh[v] = (uint8_t)acc1;
-          } else {
-            for (uint32_t b = 0; b < nb; ++b) diff |= acc[b] != c.nh[(size_t)v * nb + b];
-            if (diff)
-              for (uint32_t b = 0; b < nb; ++b) c.nh[(size_t)v * nb + b] = acc[b];
           }
-          const bool in_a = bit_of(c.ina, v);
-          // alist is free after (2): per-member flags, 1 = push successors, 2 = in A
-          c.alist[i] = (uint16_t)(((diff && !in_a) ? 1u : 0u) | (in_a ? 2u : 0u));
+          cnt_changed += (uint32_t)__popcll(__ballot(counted));
         }
+        nchanged += cnt_changed;
         lds_fence();
-        // count and push successors of the non-A nodes whose set changed (lane 0 loops)
-        for (uint32_t i = 0; i < nm; ++i) {
-          const uint32_t fl = c.alist[i];
-          const uint32_t v = c.dlist[done + i];
-          if (fl & 2u) ++nchanged;
-          if (!(fl & 1u)) continue;
-          ++nchanged;
-          if (!c.expands(v)) continue;
-          const D dv = c.dist[v];
-          const uint2 r = g.row2[v];
-          for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
-            const uint32_t e = e0 + lane;
-            uint32_t y = 0;
-            bool cand = false;
-            if (e < r.y) {
-              const uint32_t av = g.adj[e];
-              y = av & ~kEdgeDown;
-              cand = !(av & kEdgeDown) && g.lid[e] != c.link && y != c.src && c.dist[y] != INF &&
-                     (uint64_t)dv + c.wout(e) == (uint64_t)c.dist[y];
-            }
-            unsigned long long m = __ballot(cand);
-            while (m) {
-              const int ln = __ffsll((long long)m) - 1;
-              m &= m - 1ull;
-              const uint32_t yy = __shfl(y, ln);
-              if (lane == 0) push_dirty(c, yy);
-            }
-            lds_fence();
-          }
-        }
         done += nm;
         nd = __builtin_amdgcn_readfirstlane(c.ctl[1]);
       }
