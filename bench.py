@@ -174,6 +174,17 @@ def whatif_main(args):
     bytes_step = per_src * units
     bytes_solved = per_src * solved[0]
     achieved = bytes_step / (elapsed / args.steps) / 1e9
+    traffic = None  # PMC HBM bytes per step of the dominant kernel (scripts: whatif profile in profiles/r01b)
+    tj_path = os.path.join(ROOT, "profiles", "r01b", "whatif_pmc_traffic.json")
+    if os.path.exists(tj_path):
+        try:
+            traffic = json.load(open(tj_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    physical = {"traffic_bytes": traffic,
+                "achieved_gbs": traffic / (elapsed / args.steps) / 1e9 if traffic else None}
+    if traffic:
+        physical["frac"] = physical["achieved_gbs"] / HBM_PEAK_GBS
     if rank == 0:
         out = {
             "metric": "per-link-failure what-if SPF units/sec (link x source), 1k-node WAN, U[1,64] metrics",
@@ -185,13 +196,15 @@ def whatif_main(args):
                            parallelism=f"area-per-GPU x{world}"),
             "solved_per_s": solved[0] * world * args.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_step": bytes_step,
                          "note": "SURVEY.md 8d: B(src) credited per what-if unit (the formula is applied even "
                                  "when the kernel exits early); units resolved by the tight-edge filter included. "
                                  "Affected units are repaired incrementally from the base rows "
                                  f"(openr_spf_whatif); affected units only: "
-                                 f"{bytes_solved / (elapsed / args.steps) / 1e9:.1f} GB/s"},
+                                 f"{bytes_solved / (elapsed / args.steps) / 1e9:.1f} GB/s. frac can exceed 1 because "
+                                 "the repair reads ~V*(8+nb) B per unit instead of solving; see physical",
+                         "physical": physical},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = whatif_cpu_baseline(g, min(args.cpu_seconds, 10.0), use_metric)
