@@ -213,7 +213,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             if (!(av & kEdgeDown) && !(has_ign && test_bit(ign, g.lid[e])) && v != src) {
               const uint32_t b = g.nbr[e];
               uint32_t nhb = 0;
-              if (!SLICED) nhb = 1u << b;
+              if (!SLICED) nhb = a.dist_only ? 0u : 1u << b;
               else if (b / S::kNhBits == slice) nhb = 1u << (b - slice * S::kNhBits);
               const uint32_t x = (nhb << S::kNhs) | level_code(1);
               fresh = ((atomicOr(&st[S::word(v)], x << S::shift(v)) >> S::shift(v)) & kCodeMask) == 0u;

@@ -253,8 +253,14 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   a.perm = nullptr;
   a.part = nullptr;
   const int fam = p.family;
-  const uint32_t mask = ctx->cls_mask[fam];
+  uint32_t mask = ctx->cls_mask[fam];
   a.nsl = ctx->nsl[fam];
+  a.dist_only = 0;
+  if (fam == kFamCode && !a.nh && !a.tight) {  // distances only (KSP2 SPFs): 8-bit fields, no slices
+    a.dist_only = 1;
+    a.nsl = 1;
+    mask = 1u << kCls8;
+  }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
     return launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
@@ -501,10 +507,17 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
   OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
   OPENR_TRY(launch_strided_iota(d.kptr.p, chunk + 1u, ign_cap, d.num_cus, s));
+  // OPENR_SPF_KSP_STATS=1: per-kind trace counters printed to stderr (tuning only)
+  const uint32_t nst = ksp_stats_count();
+  unsigned long long* kst = nullptr;
+  if (const char* e = std::getenv("OPENR_SPF_KSP_STATS"); e && std::atoi(e) == 1) {
+    OPENR_TRY(hipMallocAsync(reinterpret_cast<void**>(&kst), 2 * nst * sizeof(unsigned long long), s));
+    OPENR_TRY(hipMemsetAsync(kst, 0, 2 * nst * sizeof(unsigned long long), s));
+  }
   for (uint32_t first = 0; first < n_pairs; first += chunk) {
     const uint32_t m = std::min(chunk, n_pairs - first);
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s));
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst));
     OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
     SolveArgs b{};
     b.sources = d.ksrc.p;
@@ -518,7 +531,18 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.work = d.work.p;
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s));
+                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr));
+  }
+  if (kst) {
+    std::vector<unsigned long long> h(2 * nst);
+    OPENR_TRY(hipMemcpyAsync(h.data(), kst, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    OPENR_TRY(hipStreamSynchronize(s));
+    OPENR_TRY(hipFree(kst));
+    for (int k = 0; k < 2; ++k) {
+      std::fprintf(stderr, "ksp_stats k=%d", k + 1);
+      for (uint32_t i = 0; i < nst; ++i) std::fprintf(stderr, " %llu", h[k * nst + i]);
+      std::fprintf(stderr, "\n");
+    }
   }
   uint32_t status = 0;
   OPENR_TRY(hipMemcpyAsync(&status, d.kstatus.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));

@@ -82,6 +82,7 @@ struct SolveArgs {
   const uint32_t* part;       // [2 * kMaxClasses]: counts, then offsets
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
+  uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class)
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
 };
 constexpr uint32_t kMaxClasses = 8;
@@ -159,7 +160,8 @@ constexpr uint32_t kKspArena = 1024;    // sorted pathLinks of the frames on the
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            uint32_t* qbuf, int num_cus, hipStream_t s);
+                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats = nullptr);
+uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,

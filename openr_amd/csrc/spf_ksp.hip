@@ -37,16 +37,23 @@ namespace {
 using namespace dev;
 
 constexpr uint32_t kWave = 64;
-constexpr uint32_t kKspProbeAfter = 256;  // DFS frame entries of one trace before the reachability probe
+constexpr uint32_t kKspProbeAfter = 64;   // DFS frame entries of one trace before the reachability probe
                                          // (OPENR_SPF_KSP_PROBE overrides: tests force 0)
 constexpr uint64_t kNoKey = ~0ull;
-
-struct KspLayout {
-  uint32_t vis, dead, fr_node, fr_edge, fr_beg, fr_cnt, fr_idx, ar_e, ar_l, ar_u, skd, skr, sl, su, seen, total;
+// Optional per-launch counters (OPENR_SPF_KSP_STATS=1; tuning only), indices into KspState::stats
+enum : uint32_t {
+  kStPairs, kStTraces, kStPaths, kStEntries, kStCands, kStProbes, kStProbeNeg, kStCyc, kStCycLoad, kStCycProbe,
+  kStProbeNodes, kStSteps, kStCycFail, kStEntFail, kStCycInit, kStCycRank, kKspStats
 };
 
+struct KspLayout {
+  uint32_t vis, dead, fr_node, fr_edge, fr_beg, fr_cnt, fr_idx, ar_e, ar_l, ar_u, skd, skr, sl, su, seen, stats, d16, total;
+};
+
+constexpr uint32_t kD16Budget = 64u * 1024u;  // LDS per wavefront up to which the u16 distance copy is kept
+
 // deg = largest row (candidate scratch of one frame).
-__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg) {
+__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg, bool want_d16) {
   KspLayout l;
   uint32_t off = 16;  // control: [0] candidate count
   auto take = [&](uint32_t bytes) {
@@ -69,6 +76,9 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.sl = take(4u * deg);
   l.su = take(4u * deg);
   l.seen = take(4u * ((V + 31u) / 32u));
+  l.stats = take(8u * kKspStats);
+  l.d16 = 0;
+  if (want_d16 && off + 2u * V + 16u <= kD16Budget) l.d16 = take(2u * V);
   l.total = off;
   return l;
 }
@@ -89,18 +99,146 @@ struct KspState {
   uint32_t* seen;  // reachability probe: visited nodes (V bits)
   uint32_t* q;     // reachability probe queue (global, V entries per wavefront)
   uint32_t probe_after;
+  uint64_t* stats;  // LDS counters (lane 0 updates), null unless enabled
+  const uint16_t* d16;  // LDS copy of drow saturated at 0xFFFF, valid when use16
+  bool use16;
 };
+
+// dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
+// reads as unreached: such a u has dist[u] > dist[dest] and can never be the tail of a
+// pathLink on the way to dest (tight means dist[u] + w == dist[v] <= dist[dest], w >= 1).
+__device__ __forceinline__ uint64_t dist_of(const KspState& st, uint32_t u) {
+  if (st.use16) {
+    const uint32_t d = st.d16[u];
+    return d == 0xFFFFu ? kNoKey : (uint64_t)d;
+  }
+  return st.drow[u];
+}
+
+// LDS copy of a distance row (u16, saturated), 8 row loads in flight per lane.
+__device__ void copy_row16(uint16_t* d16, const uint64_t* drow, uint32_t V) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i0 = 0; i0 < V; i0 += 8u * kWave) {
+    uint64_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + j * kWave + lane;
+      x[j] = i < V ? drow[i] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + j * kWave + lane;
+      if (i < V) d16[i] = x[j] < 0xFFFFull ? (uint16_t)x[j] : (uint16_t)0xFFFFu;
+    }
+  }
+}
+
+__device__ __forceinline__ void stat_add(const KspState& st, uint32_t i, uint64_t v) {
+  if (st.stats && threadIdx.x == 0) st.stats[i] += v;
+}
 
 // pathLinks(v) still worth trying -> arena[beg, beg + count) as (edge u->v, link, u):
 // tight in-edges (edge up, u may expand, dist[u] + w(u->v) == dist[v]) whose link is
 // unvisited and whose tail is not dead, in the reference's order (dist[u], name rank of
-// u, position in u's row). Gathered with one wave-aggregated append per 64 in-edges,
-// ranked by counting (keys are distinct). UINT32_MAX when the arena is full.
+// u, position in u's row). UINT32_MAX when the arena is full.
+//
+// Rows of up to 128 in-edges (every benchmark topology) are ranked from registers: each
+// lane holds the keys of in-edges lane and lane + 64, and counts the smaller keys by
+// walking the candidate ballot with v_readlane (no LDS round trips; keys are distinct).
+// Longer rows go through an LDS append + counting rank (load_path_links_long).
+struct PathCand {
+  bool ok;
+  uint64_t kd, kr;  // (dist[u]) and (name rank of u << 32 | u->v edge)
+  uint32_t link, u;
+};
+
+__device__ __forceinline__ PathCand gather_cand(const KspState& st, uint32_t e, uint32_t end, uint64_t dv) {
+  PathCand c{false, 0, 0, 0, 0};
+  if (e < end) {
+    const uint4 rec = st.g->erec[e];  // v->u: {u | flags, w(u->v), link, rev = u->v}
+    const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+    if (!(rec.x & kEdgeDown) && !test_bit(st.vis, rec.z) && !test_bit(st.dead, u) &&
+        (u == st.src || !(rec.x & kNodeSink))) {
+      const uint64_t du = dist_of(st, u);
+      const uint32_t rk = st.g->rank[u];
+      c.ok = du != kNoKey && du + rec.y == dv;
+      c.kd = du;
+      c.kr = ((uint64_t)rk << 32) | rec.w;
+      c.link = rec.z;
+      c.u = u;
+    }
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)j);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t key_less(uint64_t od, uint64_t orr, const PathCand& c) {
+  return (od < c.kd || (od == c.kd && orr < c.kr)) ? 1u : 0u;
+}
+
+// rank of c.kd/kr among the candidates of ballot m held by (kd, kr) registers
+__device__ __forceinline__ void rank_against(uint64_t m, const PathCand& src, const PathCand& a, const PathCand& b,
+                                             uint32_t& ra, uint32_t& rb) {
+  while (m) {
+    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t od = readlane64(src.kd, j), orr = readlane64(src.kr, j);
+    ra += key_less(od, orr, a);
+    rb += key_less(od, orr, b);
+  }
+}
+
+__device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_t beg);
+
 __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg) {
+  const uint2 r = st.g->row2[v];
+  if (r.y - r.x > 2u * kWave) return load_path_links_long(st, v, beg);
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t0 = st.stats ? clock64() : 0;
+  const uint64_t dv = dist_of(st, v);
+  const PathCand c0 = gather_cand(st, r.x + lane, r.y, dv);
+  const PathCand c1 = gather_cand(st, r.x + kWave + lane, r.y, dv);
+  const uint64_t m0 = __ballot(c0.ok), m1 = __ballot(c1.ok);
+  const uint64_t t1 = st.stats ? clock64() : 0;
+  const uint32_t cnt = (uint32_t)(__popcll(m0) + __popcll(m1));
+  if (beg + cnt > kKspArena) return UINT32_MAX;
+  uint32_t r0 = 0, r1 = 0;
+  rank_against(m0, c0, c0, c1, r0, r1);
+  rank_against(m1, c1, c0, c1, r0, r1);
+  if (c0.ok) {
+    st.ar_e[beg + r0] = (uint32_t)c0.kr;
+    st.ar_l[beg + r0] = c0.link;
+    st.ar_u[beg + r0] = c0.u;
+  }
+  if (c1.ok) {
+    st.ar_e[beg + r1] = (uint32_t)c1.kr;
+    st.ar_l[beg + r1] = c1.link;
+    st.ar_u[beg + r1] = c1.u;
+  }
+  lds_fence();
+  if (st.stats) {
+    const uint64_t t2 = clock64();
+    stat_add(st, kStEntries, 1);
+    stat_add(st, kStCands, cnt);
+    stat_add(st, kStCycLoad, t2 - t0);
+    stat_add(st, kStCycRank, t2 - t1);
+  }
+  return cnt;
+}
+
+// Rows longer than 128 in-edges: wave-aggregated LDS append per 64 in-edges, ranked by
+// counting over the LDS copy of the keys.
+__device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_t beg) {
   const DevGraph& g = *st.g;
   const uint32_t lane = threadIdx.x;
-  const uint64_t dv = st.drow[v];
+  const uint64_t dv = dist_of(st, v);
   const uint2 r = g.row2[v];
+  const uint64_t t0 = st.stats ? clock64() : 0;
   if (lane == 0) st.ctl[0] = 0;
   lds_fence();
   for (uint32_t e0 = r.x; e0 < r.y; e0 += kWave) {
@@ -114,7 +252,7 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
       u = rec.x & ~(kEdgeDown | kNodeSink);
       if (!(rec.x & kEdgeDown) && !test_bit(st.vis, rec.z) && !test_bit(st.dead, u) &&
           (u == st.src || !(rec.x & kNodeSink))) {
-        du = st.drow[u];
+        du = dist_of(st, u);
         rk = g.rank[u];
         cand = du != kNoKey && du + rec.y == dv;
       }
@@ -128,6 +266,7 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
     }
   }
   lds_fence();
+  const uint64_t t1 = st.stats ? clock64() : 0;
   const uint32_t cnt = __builtin_amdgcn_readfirstlane(st.ctl[0]);
   if (beg + cnt > kKspArena) return UINT32_MAX;
   for (uint32_t i = lane; i < cnt; i += kWave) {
@@ -142,6 +281,13 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
     st.ar_u[beg + rank] = st.su[i];
   }
   lds_fence();
+  if (st.stats) {
+    stat_add(st, kStEntries, 1);
+    stat_add(st, kStCands, cnt);
+    const uint64_t t2 = clock64();
+    stat_add(st, kStCycLoad, t2 - t0);
+    stat_add(st, kStCycRank, t2 - t1);
+  }
   return cnt;
 }
 
@@ -150,12 +296,15 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
 // in turn, each link at most once: it succeeds iff some stack node (or `next`, the node
 // it is about to enter) reaches src over live pathLinks (unvisited link, tail not dead).
 // Checked by a backward BFS over the tight DAG from those seeds, one lane per frontier
-// node (its in-edges in a sequential loop, 4 loads in flight), queue in global scratch.
+// node (its in-edges in a sequential loop, 4 loads in flight), queue in global scratch
+// (an edge-parallel variant — rows flattened by a wave scan — measured slower: the
+// binary search per edge costs more than the idle lanes of short frontiers).
 // A negative answer ends the trace (and the pair's traces) without the rest of the DFS.
 // Wave-uniform result.
 __device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
   const DevGraph& g = *st.g;
   const uint32_t lane = threadIdx.x, vw = (g.V + 31u) / 32u;
+  const uint64_t t0 = st.stats ? clock64() : 0;
   for (uint32_t i = lane; i < vw; i += kWave) st.seen[i] = 0;
   lds_fence();
   if (lane == 0) {
@@ -178,7 +327,7 @@ __device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
     bool hit = false;
     if (i < tail) {
       const uint32_t v = st.q[i];
-      const uint64_t dv = st.drow[v];
+      const uint64_t dv = dist_of(st, v);
       const uint2 r = g.row2[v];
       for (uint32_t e0 = r.x; e0 < r.y && !hit; e0 += 4u) {
         uint4 rec[4];
@@ -189,7 +338,7 @@ __device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
           const uint32_t u = rec[j].x & ~(kEdgeDown | kNodeSink);
           if ((rec[j].x & kEdgeDown) || test_bit(st.vis, rec[j].z) || test_bit(st.dead, u)) continue;
           if (u != st.src && (rec[j].x & kNodeSink)) continue;
-          const uint64_t du = st.drow[u];
+          const uint64_t du = dist_of(st, u);
           if (du == kNoKey || du + rec[j].y != dv) continue;
           if (u == st.src) {
             hit = true;
@@ -206,7 +355,40 @@ __device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
     head = std::min(tail, head + kWave);
     tail = __builtin_amdgcn_readfirstlane(st.ctl[1]);
   }
+  if (st.stats) {
+    stat_add(st, kStProbes, 1);
+    stat_add(st, kStProbeNeg, found ? 0 : 1);
+    stat_add(st, kStProbeNodes, tail);
+    stat_add(st, kStCycProbe, clock64() - t0);
+  }
   return found;
+}
+
+// Live first links of a path: src -> x tight in the pair's row (link unvisited,
+// dist[src] + w(src->x) == dist[x]), x not dead and able to expand (or x == dest). Every
+// traced path starts with one of them and the visited / dead sets only grow, so after
+// this many more paths the next trace must fail: the pair loop stops without it.
+__device__ uint32_t live_src_links(const KspState& st, uint32_t dst) {
+  const DevGraph& g = *st.g;
+  const uint32_t lane = threadIdx.x;
+  const uint2 r = g.row2[st.src];
+  const uint64_t ds = dist_of(st, st.src);
+  uint32_t n = 0;
+  for (uint32_t e0 = r.x; e0 < r.y; e0 += kWave) {
+    const uint32_t e = e0 + lane;
+    bool live = false;
+    if (e < r.y) {
+      const uint4 rec = g.erec[e];  // src->x: {x | flags, w(x->src), link, rev}
+      const uint32_t x = rec.x & ~(kEdgeDown | kNodeSink);
+      // (no edge-up test: the tracer reads x's copy of the flag; counting more is safe)
+      if (!test_bit(st.vis, rec.z) && !test_bit(st.dead, x) && (x == dst || !(rec.x & kNodeSink))) {
+        const uint64_t dx = dist_of(st, x);
+        live = dx != kNoKey && ds + g.w[e] == dx;
+      }
+    }
+    n += (uint32_t)__popcll(__ballot(live));
+  }
+  return n;
 }
 
 // One traceOnePath (LinkState.cpp:398-419): DFS from dest over pathLinks in the
@@ -232,6 +414,7 @@ __device__ int trace_one(const KspState& st, uint32_t dst) {
   bool probed = false;
   while (sp > 0) {
     const uint32_t f = sp - 1;
+    stat_add(st, kStSteps, 1);
     const uint32_t idx = st.fr_idx[f], cnt = st.fr_cnt[f], beg = st.fr_beg[f];
     if (idx >= cnt) {  // exhausted: std::nullopt back to the caller frame
       const uint32_t v = st.fr_node[f];
@@ -287,10 +470,11 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           const uint32_t* pdst, uint32_t first, uint32_t n,
                                                           const uint64_t* rows, uint32_t* ign_io, uint32_t* ign_end,
                                                           uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap,
-                                                          uint32_t* status, uint32_t* qbuf, uint32_t probe_after) {
+                                                          uint32_t* status, uint32_t* qbuf, uint32_t probe_after,
+                                                          uint32_t use_d16, unsigned long long* gstats) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L, g.max_deg);
+  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, use_d16 != 0);
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
   st.g = &g;
@@ -312,13 +496,26 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
   st.seen = reinterpret_cast<uint32_t*>(base + lay.seen);
   st.q = qbuf + (size_t)blockIdx.x * V;
   st.probe_after = probe_after;
+  st.stats = gstats ? reinterpret_cast<uint64_t*>(base + lay.stats) : nullptr;
   const uint32_t lane = threadIdx.x, lw = (g.L + 31u) / 32u, vw = (V + 31u) / 32u;
+  if (st.stats && lane < kKspStats) st.stats[lane] = 0;
+  uint16_t* d16 = lay.d16 ? reinterpret_cast<uint16_t*>(base + lay.d16) : nullptr;
+  st.d16 = d16;
+  uint32_t d16_row = UINT32_MAX;  // KIND 1: the base row already in d16
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint64_t tp = st.stats ? clock64() : 0;
     const uint32_t pair = first + k;
     const uint32_t row = prow[pair];
     const uint32_t src = sources[row], dst = pdst[pair];
     st.src = src;
     st.drow = rows + (size_t)(KIND == 1 ? row : k) * V;
+    st.use16 = false;
+    const uint64_t ddst = dst < V ? st.drow[dst] : kNoKey;
+    if (d16 && ddst < 0xFFFFull) {
+      if (KIND == 2 || row != d16_row) copy_row16(d16, st.drow, V);
+      d16_row = KIND == 1 ? row : UINT32_MAX;
+      st.use16 = true;
+    }
     uint32_t* out = tok + (size_t)pair * tok_cap;
     uint32_t* ig = ign_io + (size_t)k * ign_cap;  // chunk-local ignore slot
     for (uint32_t i = lane; i < lw; i += kWave) st.vis[i] = 0;
@@ -335,9 +532,20 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     uint32_t npaths = 0, pos = 1, nign = 0;
     bool bad = src >= V || dst >= V;
     // res.count(dest); src == dest traces an empty path, which ends the loop at once
-    if (!bad && src != dst && st.drow[dst] != kNoKey) {
-      for (;;) {
+    stat_add(st, kStPairs, 1);
+    if (st.stats) stat_add(st, kStCycInit, clock64() - tp);
+    if (!bad && src != dst && ddst != kNoKey) {
+      uint32_t src_live = live_src_links(st, dst);
+      while (src_live) {
+        const uint64_t tt = st.stats ? clock64() : 0, e0 = st.stats ? st.stats[kStEntries] : 0;
         const int len = trace_one(st, dst);
+        if (st.stats) {
+          stat_add(st, kStTraces, 1);
+          if (len <= 0) {
+            stat_add(st, kStCycFail, clock64() - tt);
+            stat_add(st, kStEntFail, st.stats[kStEntries] - e0);
+          }
+        }
         if (len == -2) {
           bad = true;
           break;
@@ -356,6 +564,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
         pos += 1u + (uint32_t)len;
         nign += (uint32_t)len;
         ++npaths;
+        --src_live;
       }
     }
     if (lane == 0) {
@@ -363,6 +572,14 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
       out[0] = bad ? 0xFFFFFFFFu : npaths;
       if (bad) atomicOr(status, 1u);
     }
+    if (st.stats) {
+      stat_add(st, kStPaths, npaths);
+      stat_add(st, kStCyc, clock64() - tp);
+    }
+  }
+  if (st.stats) {
+    lds_fence();
+    if (lane < kKspStats) atomicAdd(&gstats[lane], (unsigned long long)st.stats[lane]);
   }
 }
 
@@ -378,19 +595,25 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 
 }  // namespace
 
+// OPENR_SPF_KSP_D16=1: keep a u16 copy of the pair's distance row in LDS (fewer
+// wavefronts per CU; measured slower on the fabric, kept as a tuning knob)
+bool ksp_use_d16() { return bfs::env_u32("OPENR_SPF_KSP_D16", 0u, 0u, 1u) != 0; }
+
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
   return blocks_for(UINT32_MAX, ksp_lds_bytes(g.V, g.L, g.max_deg), num_cus, kWave);
 }
 
+uint32_t ksp_stats_count() { return kKspStats; }
+
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
-  const uint32_t t = ksp_layout(V, L, max_deg).total;
+  const uint32_t t = ksp_layout(V, L, max_deg, ksp_use_d16()).total;
   return t <= kMaxLds ? t : 0;
 }
 
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            uint32_t* qbuf, int num_cus, hipStream_t s) {
+                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats) {
   if (!n) return hipSuccess;
   const uint32_t lds = ksp_lds_bytes(g.V, g.L, g.max_deg);
   if (!lds || !qbuf) return hipErrorInvalidValue;
@@ -401,7 +624,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
-                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30));
+                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16() ? 1u : 0u,
+                     stats);
   return hipGetLastError();
 }
 

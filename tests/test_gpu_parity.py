@@ -499,6 +499,38 @@ def test_ksp2_device_fabric_sample(eng, ksp_probe):
     assert any(len(k1) > 1 for k1, _ in got)  # ECMP: several edge-disjoint first paths
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_distance_only_solves(eng, seed):
+    """No next-hop output: the code family solves every source in one 8-bit-field class
+    without next-hop bits (no slices). Distances must match the full solve and the
+    oracle, with and without ignore sets, for sources of every degree."""
+    for g in (hub_graph(30 + seed, V=220, L=500), T.fabric(288 + 56)):
+        eng.set_graph(g)
+        o = Oracle(g)
+        rng = np.random.default_rng(seed)
+        srcs = list(range(3)) + rng.integers(0, g.num_nodes, 60).tolist()
+        ignore = [sorted(set(rng.integers(0, g.num_links, int(rng.integers(0, 16))).tolist())) for _ in srcs]
+        for ig in (None, ignore):
+            d_only, nh, _ = eng.solve(srcs, True, want_nh=False, ignore=ig)
+            assert nh is None
+            d_full, _, _ = eng.solve(srcs, True, want_nh=True, ignore=ig)
+            np.testing.assert_array_equal(d_only, d_full)
+            for i, s in enumerate(srcs):
+                np.testing.assert_array_equal(d_only[i], o.run_spf(int(s), True, ig[i] if ig else None).dist)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_ksp2_device_hub_graphs(eng, seed, ksp_probe):
+    """Rows of 40 / 75 / 130 in-edges: the register rank (<= 64, <= 128 in-edges) and the
+    LDS rank (> 128) of pathLinks, with the hubs as sources, destinations and transit."""
+    g = hub_graph(20 + seed, V=220, L=500)
+    rng = np.random.default_rng(seed)
+    pairs = [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 40)]
+    pairs += [(int(s), h) for h in range(3) for s in rng.integers(0, g.num_nodes, 40)]
+    pairs += [(int(a), int(b)) for a, b in rng.integers(3, g.num_nodes, (200, 2))]
+    check_ksp2_against_oracle(eng, g, pairs)
+
+
 def test_ksp2_device_form_and_overflow(eng):
     import torch
 
