@@ -371,6 +371,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           overflow = true;
           break;
         }
+        if (!SLICED && a.target && a.dist_only) {
+          // the target is settled: every node nearer than it has its distance; the
+          // target's level [head, tail) gets its distances here instead of on expansion
+          const uint32_t t = a.target[sid];
+          if (t < V && (S::field(st, t) & kCodeMask) != 0u) {
+            const uint64_t dT = (uint64_t)L * cost;
+            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dT;
+            break;
+          }
+        }
       }
       if (RING && overflow) {  // re-run by the full-order variant (from the list)
         if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = uid;

@@ -529,6 +529,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.nh_bits = ctx->nh_bits;
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
+    b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr));

@@ -83,6 +83,10 @@ struct SolveArgs {
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
   uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class)
+  // nullable, honoured by dist_only code-family solves: solve sid may stop at the level of
+  // target[sid]; nodes farther than the target then read UINT64_MAX (a KSP trace to the
+  // target only reads nodes no farther than it)
+  const uint32_t* target;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
 };
 constexpr uint32_t kMaxClasses = 8;
