@@ -8,9 +8,9 @@ LIBDIR := openr_amd/lib
 CSRC := openr_amd/csrc
 
 ENGINE := $(LIBDIR)/libopenr_spf.so
-ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_bfs.hip $(CSRC)/spf_bfs_lvl.hip $(CSRC)/spf_sweep.hip $(CSRC)/spf_fringe.hip $(CSRC)/spf_rounds.hip $(CSRC)/spf_ksp.hip $(CSRC)/spf_capi.hip
+ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_bfs.hip $(CSRC)/spf_bfs_lvl.hip $(CSRC)/spf_sweep.hip $(CSRC)/spf_fringe.hip $(CSRC)/spf_rounds.hip $(CSRC)/spf_ksp.hip $(CSRC)/spf_update.hip $(CSRC)/spf_capi.hip
 ENGINE_HDRS := $(CSRC)/spf_kernels.h $(CSRC)/spf_device.h $(CSRC)/spf_bfs_common.h include/openr_spf.h
-ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_bfs.o $(LIBDIR)/spf_bfs_lvl.o $(LIBDIR)/spf_sweep.o $(LIBDIR)/spf_fringe.o $(LIBDIR)/spf_rounds.o $(LIBDIR)/spf_ksp.o $(LIBDIR)/spf_capi.o
+ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_bfs.o $(LIBDIR)/spf_bfs_lvl.o $(LIBDIR)/spf_sweep.o $(LIBDIR)/spf_fringe.o $(LIBDIR)/spf_rounds.o $(LIBDIR)/spf_ksp.o $(LIBDIR)/spf_update.o $(LIBDIR)/spf_capi.o
 
 HOST := $(LIBDIR)/libopenr_decision.so
 HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp

@@ -334,6 +334,118 @@ def ksp2_main(args):
     eng.close()
 
 
+def update_main(args):
+    """Convergence after an attribute change: the BM_DecisionGrid /
+    BM_DecisionFabric update loop of the reference benchmark (RoutingBenchmarkUtils.cpp:
+    407-479) toggles the overload bit of a random node (grid: any node; fabric: an RSW),
+    then reverts it on the next update. A step = one such update applied to the resident
+    mirror (openr_spf_patch_graph) + every source's dist / next-hop row brought up to date
+    (openr_spf_refresh_device: affected-row filter, re-solve of the affected rows in
+    place). The reference clears its memo and re-runs Dijkstra per source instead
+    (LinkState.cpp:714-717), so cpu_baseline = the oracle's all-sources pass / V, i.e.
+    full re-solves per second divided by the sources one update invalidates."""
+    import torch
+    import torch.distributed as dist
+
+    from openr_amd.engine import SpfEngine
+    from openr_amd.shard import max_over_ranks
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    g, cfg = build_topology(args.topology)
+    V = g.num_nodes
+    eng = SpfEngine([local_rank])
+    eng.set_graph(g)
+    nb = eng.nh_bytes
+    use_metric = not args.no_metric
+    src = torch.arange(0, V, dtype=torch.int32, device=dev)
+    d_dist = torch.empty((V, V), dtype=torch.int64, device=dev)
+    d_nh = torch.empty((V, V, nb), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    # candidates: the reference's toggled node kinds (fabric: RSWs, marker 3)
+    cand = [i for i, nm in enumerate(g.names) if nm.startswith("3-")] if args.topology == "fabric" else list(range(V))
+    rng = np.random.default_rng(1 + rank)
+    sel = [None]
+    resolved = []
+
+    def step():
+        if sel[0] is None:
+            sel[0] = int(cand[int(rng.integers(len(cand)))])
+            flag = 1
+        else:
+            flag = 0
+        eng.patch(nodes=[sel[0]], node_overloaded=[flag], track=False)
+        if flag == 0:
+            sel[0] = None
+        resolved.append(eng.refresh_device(src.data_ptr(), V, d_dist.data_ptr(), d_nh.data_ptr(), nb, use_metric,
+                                           stream=stream.cuda_stream))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    # resident rows of the unpatched graph, and the full re-solve time for comparison
+    eng.solve_device(src.data_ptr(), V, d_dist.data_ptr(), d_nh.data_ptr(), nb, use_metric, stream=stream.cuda_stream)
+    barrier()
+    tf = time.perf_counter()
+    for _ in range(3):
+        eng.solve_device(src.data_ptr(), V, d_dist.data_ptr(), d_nh.data_ptr(), nb, use_metric,
+                         stream=stream.cuda_stream)
+    barrier()
+    full_ms = (time.perf_counter() - tf) / 3 * 1e3
+    steps = args.steps + (args.steps % 2)  # whole set/revert pairs
+    for _ in range(args.warmup + (args.warmup % 2)):
+        step()
+    barrier()
+    resolved.clear()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    # the rows must equal a fresh solve of the final (reverted) graph
+    chk = torch.empty((2, V), dtype=torch.int64, device=dev)
+    eng.solve_device(src.data_ptr(), 2, chk.data_ptr(), 0, nb, use_metric, stream=stream.cuda_stream)
+    barrier()
+    assert torch.equal(chk, d_dist[:2]), "refreshed rows differ from a fresh solve"
+    value = steps * world / elapsed
+    per_src = algorithmic_bytes(g, np.arange(V)) / V
+    mean_resolved = float(np.mean(resolved)) if resolved else 0.0
+    achieved = per_src * mean_resolved / (elapsed / steps) / 1e9
+    if rank == 0:
+        out = {
+            "metric": "node-overload updates/sec with all-sources SPF rows kept current (BM_Decision update loop)",
+            "value": value, "unit": "updates/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic (reference benchmark generators, unit metrics)",
+            "config": dict(cfg, workload=cfg["workload"].replace("all-sources", "overload-toggle-refresh"),
+                           rows=V, mean_rows_resolved=mean_resolved, full_resolve_ms=full_ms,
+                           use_link_metric=use_metric, parallelism=f"area-per-GPU x{world}"),
+            "speedup_vs_full_resolve": full_ms / (elapsed / steps * 1e3),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "note": "SURVEY.md 8d B(src) per re-solved row / step time (host patch, filter and the "
+                                 "count read-back included)"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(g, args.cpu_seconds, use_metric)
+            cb = dict(cb, value=cb["value"] / V, unit="updates/s",
+                      sample=cb["sample"] + f"; updates/s = solves/s / {V} (the reference re-solves every source)")
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -351,7 +463,7 @@ def main():
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
                     help="ksp2: sources per device call within a step (token rows are reused)")
-    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif", "ksp2"],
+    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif", "ksp2", "update"],
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
                          "(BASELINE config 4)")
     args = ap.parse_args()
@@ -359,6 +471,8 @@ def main():
         return whatif_main(args)
     if args.workload == "ksp2":
         return ksp2_main(args)
+    if args.workload == "update":
+        return update_main(args)
 
     import torch
     import torch.distributed as dist

@@ -22,6 +22,10 @@
  *                              for every (link, source), reduced to changed-node counts
  *   openr_spf_ksp2             LinkState::getKthPaths(src, dst, 1 and 2) (LinkState.cpp:762-791)
  *                              for a batch of pairs, paths traced on the device
+ *   openr_spf_patch_graph      attribute-only mirror updates (metric, Link::isUp, node
+ *                              overload) at the same memo-clearing points, without a rebuild
+ *   openr_spf_refresh          incremental re-SPF of resident rows after a patch: only the
+ *                              rows the change can touch are re-solved
  *   openr_spf_last_error       glog CHECK / exception text of the reference
  *
  * Conventions
@@ -186,6 +190,45 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
                           uint32_t n_sources, const uint32_t* d_pair_row,
                           const uint32_t* d_pair_dst, uint32_t n_pairs, uint32_t tok_cap,
                           uint32_t* d_tok1, uint32_t* d_tok2, void* stream);
+
+/* In-place attribute patch of the mirror: the link structure —
+   rows, columns, link ids — is unchanged; only attributes the reference changes on an
+   existing Link / node move. Replaces a full openr_spf_set_graph at the reference's
+   memo-clearing points when updateAdjacencyDatabase (LinkState.cpp:564-719) or
+   decrementHolds (:500-514) changed nothing but:
+     metric of directed edge e         Link::setMetricFromNode   (LinkState.cpp:195-204 getter)
+     usability of link l (both edges)  Link::isUp: holds / adjacency overload (:233-236)
+     overload of node x                LinkState::updateNodeOverloaded / isNodeOverloaded
+   The patch is also recorded as a delta for openr_spf_refresh (each call replaces the
+   previous delta). No solve may be in flight on the context's devices. */
+typedef struct {
+  uint32_t n_edges;
+  const uint32_t* edge_ids;         /* [n_edges] directed edge ids */
+  const uint64_t* metric;           /* [n_edges] new Link::getMetricFromNode(owner) */
+  uint32_t n_links;
+  const uint32_t* link_ids;         /* [n_links] */
+  const uint8_t* link_up;           /* [n_links] new Link::isUp() */
+  uint32_t n_nodes;
+  const uint32_t* node_ids;         /* [n_nodes] */
+  const uint8_t* node_overloaded;   /* [n_nodes] new isNodeOverloaded() */
+} openr_spf_patch;
+
+int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* patch);
+
+/* Incremental re-SPF after the most recent openr_spf_patch_graph: rows [n] (dist, and nh
+   / tight when non-NULL, laid out as openr_spf_solve writes them) hold the results of
+   sources[0..n) on the graph BEFORE that patch; on return they hold the results on the
+   patched graph, bit-exact with a fresh solve. Only rows the patch can change are
+   re-solved: row s is affected iff some changed directed edge u->v was tight for s
+   before, or is usable with d_s(u) + w_new <= d_s(v) after (u expanding for s);
+   *out_resolved (nullable) = rows re-solved (added to stats.spf_runs). Fails with
+   OPENR_SPF_EINVAL when no patch followed the last set_graph. The host form splits the
+   rows across devices like openr_spf_solve; the device form synchronizes `stream` once. */
+int openr_spf_refresh(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags, uint64_t* dist,
+                      uint8_t* nh, uint32_t nh_bytes, uint64_t* tight, uint32_t* out_resolved);
+int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n,
+                             uint32_t flags, uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes,
+                             uint64_t* d_tight, void* stream, uint32_t* out_resolved);
 
 int openr_spf_get_stats(const openr_spf_ctx* ctx, openr_spf_stats_t* out);
 

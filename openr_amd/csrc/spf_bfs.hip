@@ -100,9 +100,9 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
                                           const uint32_t* st, bool nt) {
   using S = State<FB>;
   const uint32_t tid = threadIdx.x;
-  uint64_t* drow = a.dist + (size_t)sid * V;
+  uint64_t* drow = a.dist + out_row_of(a, sid) * V;
   const uint32_t nb = a.nh_bytes;
-  uint8_t* nrow = a.nh ? a.nh + (size_t)sid * V * nb : nullptr;
+  uint8_t* nrow = a.nh ? a.nh + out_row_of(a, sid) * V * nb : nullptr;
   if (!SLICED || slice == 0)
     for (uint32_t v = tid; v < V; v += BLOCK)
       if ((S::field(st, v) & kCodeMask) == 0u) drow[v] = ~0ull;
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
     if (src < V) {  // block-uniform
       OPENR_PROF_STAMP(t0);
       const bool own_dist = !SLICED || slice == 0;
-      uint64_t* drow = a.dist + (size_t)sid * V;
+      uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
       if (has_ign)
         for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         if (own_dist) drow[src] = 0;
       }
       __syncthreads();
-      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
 
       // level 0: expand the source (even when overloaded); a directly connected
       // node's next hop is the node itself (LinkState.cpp:867-872)

@@ -85,7 +85,7 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
   if (SLICED) {
     if (a.nh) {
       const uint32_t nb = a.nh_bytes, j0 = 4u * slice, zero0 = 4u * a.nsl;
-      uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+      uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
       for (uint32_t v = tid; v < V; v += BLOCK) {
         const uint32_t w = nh[v];
         uint8_t* o = nrow + (size_t)v * nb;
@@ -98,7 +98,7 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
     }
     if (slice != 0) return;
   }
-  uint64_t* drow = a.dist + (size_t)sid * V;
+  uint64_t* drow = a.dist + out_row_of(a, sid) * V;
   if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
     // two nodes per lane: 16-byte stores
     ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
@@ -121,7 +121,7 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
   }
   if (SLICED || !a.nh) return;
   const uint32_t nb = a.nh_bytes;
-  uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+  uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
   const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
   if (MODE == kNhNibble && nb == 1 && aligned4) {
     // four nodes (four nibbles of one half-dword) per lane -> one u32 of four bytes
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         if (!ELECT) vis[src >> 5] = 1u << (src & 31u);
       }
       __syncthreads();
-      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
 
       // level 0: expand the source (even when overloaded); a directly connected
       // node's next hop is the node itself (LinkState.cpp:867-872)

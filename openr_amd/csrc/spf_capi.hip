@@ -83,6 +83,11 @@ struct Device {
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
+  // incremental updates: patch records, the last patch's delta edges, refresh work list,
+  // host-form refresh rows
+  DevBuf<PatchRec> precs;
+  DevBuf<DeltaEdge> delta;
+  DevBuf<uint32_t> alist, asrc, acount;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -118,6 +123,16 @@ struct openr_spf_ctx {
   uint32_t nsl[kNumFamilies] = {1, 1};       // next-hop slices of each family's sliced class
   uint32_t nsl_max() const { return std::max(nsl[0], nsl[1]); }
   openr_spf_stats_t stats{};
+  // host copy of the mutable attributes and of the device arrays derived from them, so
+  // openr_spf_patch_graph can recompute and re-upload single elements
+  std::vector<uint64_t> metric;
+  std::vector<uint8_t> edge_up, ovl;
+  std::vector<uint32_t> adj, w, win, rev, lid, owner, ovl_bits;
+  std::vector<uint2> ledge, row2t;
+  std::vector<uint4> erec, ellt;
+  // delta edges of the most recent patch (openr_spf_refresh); invalid after set_graph
+  std::vector<DeltaEdge> delta;
+  bool delta_valid = false;
 };
 
 namespace {
@@ -241,7 +256,7 @@ int group_lanes_override(int dflt) {
 // widest first.
 hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs a, hipStream_t s) {
   LaunchInfo info;
-  if (a.tight) {
+  if (a.tight && !a.out_row) {
     hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((d.g.E + 63u) / 64u) * 8u, s);
     if (err != hipSuccess) return err;
   }
@@ -641,6 +656,11 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
+    d.precs.release();
+    d.delta.release();
+    d.alist.release();
+    d.asrc.release();
+    d.acount.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -817,7 +837,269 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   uint32_t gl = 1;
   while (gl < per_lane && gl < 64) gl <<= 1;
   ctx->group_lanes = gl;
+  ctx->metric.assign(gr->metric, gr->metric + E);
+  ctx->edge_up.assign(gr->edge_up, gr->edge_up + E);
+  ctx->ovl = std::move(ovl);
+  ctx->adj = std::move(adj);
+  ctx->w = std::move(w);
+  ctx->win = std::move(win);
+  ctx->rev = std::move(rev);
+  ctx->lid = std::move(lid);
+  ctx->owner = std::move(owner);
+  ctx->ovl_bits = std::move(ovl_bits);
+  ctx->ledge = std::move(ledge);
+  ctx->row2t = std::move(row2t);
+  ctx->erec = std::move(erec);
+  ctx->ellt = std::move(ellt);
+  ctx->delta.clear();
+  ctx->delta_valid = false;
   ctx->has_graph = true;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
+  if (!ctx || !p) return fail(OPENR_SPF_EINVAL, "null argument");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if ((p->n_edges && (!p->edge_ids || !p->metric)) || (p->n_links && (!p->link_ids || !p->link_up)) ||
+      (p->n_nodes && (!p->node_ids || !p->node_overloaded)))
+    return fail(OPENR_SPF_EINVAL, "null patch array");
+  const uint32_t V = ctx->V, E = ctx->E, L = ctx->L;
+  for (uint32_t i = 0; i < p->n_edges; ++i)
+    if (p->edge_ids[i] >= E) return fail(OPENR_SPF_EINVAL, "edge id %u out of range (E=%u)", p->edge_ids[i], E);
+  for (uint32_t i = 0; i < p->n_links; ++i)
+    if (p->link_ids[i] >= L || ctx->ledge[p->link_ids[i]].x == UINT32_MAX)
+      return fail(OPENR_SPF_EINVAL, "link id %u is not a link of the graph", p->link_ids[i]);
+  for (uint32_t i = 0; i < p->n_nodes; ++i)
+    if (p->node_ids[i] >= V) return fail(OPENR_SPF_EINVAL, "node id %u out of range (V=%u)", p->node_ids[i], V);
+
+  // 1) every directed edge whose (usable, weight, tail overload) may change, old state
+  std::vector<uint32_t> cand;
+  std::vector<uint8_t> seen(E, 0);
+  auto add = [&](uint32_t e) {
+    if (!seen[e]) {
+      seen[e] = 1;
+      cand.push_back(e);
+    }
+  };
+  for (uint32_t i = 0; i < p->n_edges; ++i) add(p->edge_ids[i]);
+  for (uint32_t i = 0; i < p->n_links; ++i) {
+    add(ctx->ledge[p->link_ids[i]].x);
+    add(ctx->ledge[p->link_ids[i]].y);
+  }
+  for (uint32_t i = 0; i < p->n_nodes; ++i)
+    for (uint32_t e = ctx->row_ptr[p->node_ids[i]]; e < ctx->row_ptr[p->node_ids[i] + 1]; ++e) add(e);
+  auto state = [&](uint32_t e, uint32_t* wout) {
+    *wout = ctx->w[e];
+    return ((ctx->adj[e] & kEdgeDown) ? 0u : 1u) | (ctx->ovl[ctx->owner[e]] ? 2u : 0u);
+  };
+  std::vector<uint32_t> w0(cand.size()), f0(cand.size());
+  for (size_t k = 0; k < cand.size(); ++k) f0[k] = state(cand[k], &w0[k]);
+
+  // 2) apply to the host attributes; collect dirty device elements
+  std::vector<uint8_t> dirty_e(E, 0), dirty_v(V, 0);
+  for (uint32_t i = 0; i < p->n_edges; ++i) {  // Link::setMetricFromNode (LinkState.cpp:195-204)
+    const uint32_t e = p->edge_ids[i];
+    ctx->metric[e] = p->metric[i];
+    ctx->w[e] = (uint32_t)std::min<uint64_t>(p->metric[i], 0xFFFFFFFFull);
+    ctx->win[ctx->rev[e]] = ctx->w[e];
+    dirty_e[e] = dirty_e[ctx->rev[e]] = 1;
+  }
+  for (uint32_t i = 0; i < p->n_links; ++i) {  // Link::isUp (LinkState.cpp:233-236), per link
+    const uint2 ab = ctx->ledge[p->link_ids[i]];
+    for (uint32_t e : {ab.x, ab.y}) {
+      ctx->edge_up[e] = p->link_up[i] ? 1 : 0;
+      ctx->adj[e] = ctx->col[e] | (p->link_up[i] ? 0u : kEdgeDown);
+      dirty_e[e] = 1;
+      dirty_v[ctx->owner[e]] = 1;  // ellt
+    }
+  }
+  for (uint32_t i = 0; i < p->n_nodes; ++i) {  // LinkState::updateNodeOverloaded / isNodeOverloaded
+    const uint32_t x = p->node_ids[i];
+    ctx->ovl[x] = p->node_overloaded[i] ? 1 : 0;
+    dirty_v[x] = 1;
+    for (uint32_t e = ctx->row_ptr[x]; e < ctx->row_ptr[x + 1]; ++e) dirty_e[ctx->rev[e]] = 1;  // erec sink flag
+  }
+
+  // 3) recompute the dirty device elements exactly as set_graph derives them
+  std::vector<PatchRec> recs;
+  auto rec = [&](uint32_t arr, uint32_t idx, uint4 val) { recs.push_back(PatchRec{arr, idx, 0u, 0u, val}); };
+  for (uint32_t e = 0; e < E; ++e) {
+    if (!dirty_e[e]) continue;
+    ctx->erec[e] = make_uint4(ctx->adj[e] | (ctx->ovl[ctx->col[e]] ? kNodeSink : 0u), ctx->win[e], ctx->lid[e],
+                              ctx->rev[e]);
+    rec(kPatchAdj, e, make_uint4(ctx->adj[e], 0, 0, 0));
+    rec(kPatchW, e, make_uint4(ctx->w[e], 0, 0, 0));
+    rec(kPatchWin, e, make_uint4(ctx->win[e], 0, 0, 0));
+    rec(kPatchErec, e, ctx->erec[e]);
+  }
+  std::vector<uint8_t> dirty_bits((V + 31) / 32 + 1, 0);
+  for (uint32_t u = 0; u < V; ++u) {
+    if (!dirty_v[u]) continue;
+    const uint32_t rb = ctx->row_ptr[u], re = ctx->row_ptr[u + 1];
+    uint32_t x4[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
+    if (!ctx->ovl[u])
+      for (uint32_t j = 0; j < 4 && rb + j < re; ++j) x4[j] = ctx->adj[rb + j];
+    else
+      x4[0] |= kNodeSink;
+    ctx->ellt[u] = make_uint4(x4[0], x4[1], x4[2], x4[3]);
+    ctx->row2t[u] = ctx->ovl[u] ? make_uint2(rb | kNodeSink, rb) : make_uint2(rb, re);
+    if (ctx->ovl[u]) ctx->ovl_bits[u >> 5] |= 1u << (u & 31u);
+    else ctx->ovl_bits[u >> 5] &= ~(1u << (u & 31u));
+    dirty_bits[u >> 5] = 1;
+    rec(kPatchEllt, u, ctx->ellt[u]);
+    rec(kPatchRow2t, u, make_uint4(ctx->row2t[u].x, ctx->row2t[u].y, 0, 0));
+    rec(kPatchOvl, u, make_uint4(ctx->ovl[u], 0, 0, 0));
+  }
+  for (uint32_t k = 0; k < dirty_bits.size(); ++k)
+    if (dirty_bits[k]) rec(kPatchOvlBits, k, make_uint4(ctx->ovl_bits[k], 0, 0, 0));
+
+  // 4) graph-wide metric facts (kernel choice / ENOTSUP) over the usable edges
+  uint32_t w_min = UINT32_MAX, w_max = 0;
+  bool metric_ok = true;
+  for (uint32_t e = 0; e < E; ++e) {
+    if (ctx->adj[e] & kEdgeDown) continue;
+    const uint64_t m = ctx->metric[e];
+    if (m == 0 || m > 0x7FFFFFFFull) metric_ok = false;
+    else {
+      w_min = std::min<uint32_t>(w_min, (uint32_t)m);
+      w_max = std::max<uint32_t>(w_max, (uint32_t)m);
+    }
+  }
+  if (w_min == UINT32_MAX) w_min = w_max = 1;
+
+  // 5) the delta edges of this patch (openr_spf_refresh)
+  ctx->delta.clear();
+  for (size_t k = 0; k < cand.size(); ++k) {
+    uint32_t w1 = 0;
+    const uint32_t f1 = state(cand[k], &w1);
+    if (f1 == f0[k] && w1 == w0[k]) continue;
+    const uint32_t e = cand[k];
+    DeltaEdge de{};
+    de.u = ctx->owner[e];
+    de.v = ctx->col[e];
+    de.w0 = w0[k];
+    de.w1 = w1;
+    de.flags = ((f0[k] & 1u) ? kDeltaUp0 : 0u) | ((f1 & 1u) ? kDeltaUp1 : 0u) | ((f0[k] & 2u) ? kDeltaOvl0 : 0u) |
+               ((f1 & 2u) ? kDeltaOvl1 : 0u);
+    ctx->delta.push_back(de);
+  }
+
+  // 6) upload: one record list + one scatter kernel per replica
+  for (Device& d : ctx->devs) {
+    HIP_TRY(hipSetDevice(d.ordinal));
+    if (recs.empty()) continue;
+    HIP_TRY(d.precs.reserve(recs.size()));
+    HIP_TRY(hipMemcpyAsync(d.precs.p, recs.data(), recs.size() * sizeof(PatchRec), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(launch_patch_apply(d.g, d.precs.p, (uint32_t)recs.size(), d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // recs is host memory of this call
+  }
+  ctx->w_min = w_min;
+  ctx->w_max = w_max;
+  ctx->metric_ok = metric_ok;
+  ctx->delta_valid = true;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n,
+                             uint32_t flags, uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes, uint64_t* d_tight,
+                             void* stream, uint32_t* out_resolved) {
+  int rc = check_solve_args(ctx, d_sources, n, d_dist, d_nh, nh_bytes);
+  if (rc) return rc;
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  if (!ctx->delta_valid)
+    return fail(OPENR_SPF_EINVAL, "no patch since the last openr_spf_set_graph: rows must be re-solved");
+  Plan plan;
+  rc = make_plan(ctx, flags, false, &plan);
+  if (rc) return rc;
+  Device& d = ctx->devs[device_index];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  const uint32_t nd = (uint32_t)ctx->delta.size();
+  uint32_t count = 0;
+  if (nd && n) {
+    HIP_TRY(d.delta.reserve(nd));
+    HIP_TRY(d.alist.reserve(n));
+    HIP_TRY(d.asrc.reserve(n));
+    HIP_TRY(d.acount.reserve(1));
+    HIP_TRY(hipMemcpyAsync(d.delta.p, ctx->delta.data(), nd * sizeof(DeltaEdge), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(d.acount.p, 0, sizeof(uint32_t), s));
+    HIP_TRY(launch_refresh_filter(d.delta.p, nd, d_sources, n, ctx->V, d_dist,
+                                  (flags & OPENR_SPF_USE_LINK_METRIC) == 0, d.alist.p, d.asrc.p, d.acount.p,
+                                  d.num_cus, s));
+    HIP_TRY(hipMemcpyAsync(&count, d.acount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the affected-row count sizes the re-solve
+  }
+  if (count) {
+    if (d_tight) HIP_TRY(launch_zero_rows(d_tight, (ctx->E + 63u) / 64u, d.alist.p, count, d.num_cus, s));
+    SolveArgs a{};
+    a.sources = d.asrc.p;
+    a.n = count;
+    a.out_row = d.alist.p;
+    a.dist = d_dist;
+    a.nh = d_nh;
+    a.nh_bytes = nh_bytes;
+    a.tight = d_tight;
+    a.nh_bits = ctx->nh_bits;
+    HIP_TRY(d.ovf.reserve((size_t)count * ctx->nsl_max()));
+    a.ovf_list = d.ovf.p;
+    HIP_TRY(reserve_counters(d));
+    a.work = d.work.p;
+    HIP_TRY(launch(ctx, d, plan, a, s));
+    ctx->stats.spf_runs += count;
+    ctx->stats.batches += 1;
+  }
+  if (out_resolved) *out_resolved = count;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_refresh(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags, uint64_t* dist,
+                      uint8_t* nh, uint32_t nh_bytes, uint64_t* tight, uint32_t* out_resolved) {
+  int rc = check_solve_args(ctx, sources, n, dist, nh, nh_bytes);
+  if (rc) return rc;
+  for (uint32_t i = 0; i < n; ++i)
+    if (sources[i] >= ctx->V) return fail(OPENR_SPF_EINVAL, "source %u out of range (V=%u)", sources[i], ctx->V);
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t V = ctx->V, tw = (ctx->E + 63u) / 64u;
+  const uint32_t ndev = (uint32_t)ctx->devs.size();
+  const uint32_t per = (n + ndev - 1) / std::max<uint32_t>(ndev, 1);
+  uint32_t total = 0;
+  for (uint32_t di = 0; di < ndev; ++di) {
+    Device& d = ctx->devs[di];
+    const uint32_t b = std::min(n, di * per), e = std::min(n, b + per), m = e - b;
+    if (!m) continue;
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(d.src.reserve(m));
+    HIP_TRY(d.dist.reserve((size_t)m * V));
+    if (nh) HIP_TRY(d.nh.reserve((size_t)m * V * nh_bytes));
+    if (tight) HIP_TRY(d.tight.reserve((size_t)m * tw));
+    HIP_TRY(hipMemcpyAsync(d.src.p, sources + b, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.dist.p, dist + (size_t)b * V, (size_t)m * V * 8u, hipMemcpyHostToDevice, d.stream));
+    if (nh)
+      HIP_TRY(hipMemcpyAsync(d.nh.p, nh + (size_t)b * V * nh_bytes, (size_t)m * V * nh_bytes, hipMemcpyHostToDevice,
+                             d.stream));
+    if (tight)
+      HIP_TRY(hipMemcpyAsync(d.tight.p, tight + (size_t)b * tw, (size_t)m * tw * 8u, hipMemcpyHostToDevice,
+                             d.stream));
+    uint32_t c = 0;
+    rc = openr_spf_refresh_device(ctx, (int)di, d.src.p, m, flags, d.dist.p, nh ? d.nh.p : nullptr, nh_bytes,
+                                  tight ? d.tight.p : nullptr, nullptr, &c);
+    if (rc) return rc;
+    total += c;
+    HIP_TRY(hipMemcpyAsync(dist + (size_t)b * V, d.dist.p, (size_t)m * V * 8u, hipMemcpyDeviceToHost, d.stream));
+    if (nh)
+      HIP_TRY(hipMemcpyAsync(nh + (size_t)b * V * nh_bytes, d.nh.p, (size_t)m * V * nh_bytes, hipMemcpyDeviceToHost,
+                             d.stream));
+    if (tight)
+      HIP_TRY(hipMemcpyAsync(tight + (size_t)b * tw, d.tight.p, (size_t)m * tw * 8u, hipMemcpyDeviceToHost,
+                             d.stream));
+  }
+  for (Device& d : ctx->devs) {
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+  }
+  ctx->stats.last_batch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (out_resolved) *out_resolved = total;
   return OPENR_SPF_OK;
 }
 

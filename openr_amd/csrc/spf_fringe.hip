@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kWave) void fringe_kernel(DevGraph g, SolveArgs a, 
         lds_fence();
         load_ignore(ign, ign_words, a, sid, g.L);
       }
-      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
       lds_fence();
       if (lane == 0) {
         dist[src] = 0;
@@ -202,14 +202,14 @@ __global__ __launch_bounds__(kWave) void fringe_kernel(DevGraph g, SolveArgs a, 
         nf = __builtin_amdgcn_readfirstlane(ctl[0]);
       }
       // result rows, coalesced; unreached nodes keep UINT64_MAX
-      uint64_t* drow = a.dist + (size_t)sid * V;
+      uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       for (uint32_t v = lane; v < V; v += kWave) {
         const D d = dist[v];
         store_row<uint64_t>(&drow[v], d == INF ? ~0ull : (uint64_t)d, true);
       }
       if (a.nh) {
         const uint32_t nb = a.nh_bytes;
-        uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+        uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
         const uint32_t total = V * nb;
         for (uint32_t i = lane; i < total; i += kWave) {
           const uint32_t v = i / nb, j = i - v * nb;

@@ -87,8 +87,16 @@ struct SolveArgs {
   // target[sid]; nodes farther than the target then read UINT64_MAX (a KSP trace to the
   // target only reads nodes no farther than it)
   const uint32_t* target;
+  // nullable: solve sid writes its dist / nh / tight rows at row out_row[sid] instead of
+  // sid (openr_spf_refresh re-solves a scattered subset of resident rows in place; the
+  // launcher then leaves zeroing those tight rows to the caller)
+  const uint32_t* out_row;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
 };
+// output row of solve sid (SolveArgs::out_row)
+__host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
+  return a.out_row ? (size_t)a.out_row[sid] : (size_t)sid;
+}
 constexpr uint32_t kMaxClasses = 8;
 constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch, [4] flagged solves
 constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
@@ -156,6 +164,33 @@ hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uin
                               uint32_t nb, bool unit_cost, bool dist64, uint32_t* changed, uint32_t* ctr,
                               int num_cus, hipStream_t s);
 uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
+
+// Incremental mirror updates (spf_update.hip).
+// In-place attribute patch of the device mirror: each record overwrites one element of
+// one DevGraph array (structure — rows, columns, link ids — never changes).
+enum PatchArray : uint32_t {
+  kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kNumPatchArrays
+};
+struct PatchRec {
+  uint32_t arr, idx, pad0, pad1;
+  uint4 val;  // x (u32 / u8 arrays), xy (uint2), xyzw (uint4)
+};
+hipError_t launch_patch_apply(const DevGraph& g, const PatchRec* recs, uint32_t n, hipStream_t s);
+// One directed edge u->v whose usability / weight / tail overload changed in a patch.
+struct DeltaEdge {
+  uint32_t u, v, w0, w1;  // weight before / after (u32; usable metrics are i32-positive)
+  uint32_t flags, pad0, pad1, pad2;
+};
+constexpr uint32_t kDeltaUp0 = 1u, kDeltaUp1 = 2u, kDeltaOvl0 = 4u, kDeltaOvl1 = 8u;
+// Refresh filter: row i (source sources[i], distances dist[i][V] of the graph before the
+// patch) is affected iff some delta edge was tight for it or may now be tight / shorter;
+// affected rows are appended to alist (row index) / asrc (source), *count of them.
+hipError_t launch_refresh_filter(const DeltaEdge* delta, uint32_t n_delta, const uint32_t* sources, uint32_t n,
+                                 uint32_t V, const uint64_t* dist, bool unit_cost, uint32_t* alist, uint32_t* asrc,
+                                 uint32_t* count, int num_cus, hipStream_t s);
+// rows[alist[k]][0 .. words) = 0 for k < n
+hipError_t launch_zero_rows(uint64_t* rows, uint32_t words, const uint32_t* alist, uint32_t n, int num_cus,
+                            hipStream_t s);
 
 // KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
 constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)

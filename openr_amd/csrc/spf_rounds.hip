@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
         lds_fence();
         load_ignore(ign, ign_words, a, sid, g.L);
       }
-      uint64_t* trow = (GENERIC && a.tight) ? a.tight + (size_t)sid * tight_words : nullptr;
+      uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
       lds_fence();
       if (lane == 0) {
         dist[src] = 0;
@@ -215,14 +215,14 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
         nxt = t;
       }
       // (result rows, coalesced; unreached nodes keep UINT64_MAX)
-      uint64_t* drow = a.dist + (size_t)sid * V;
+      uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       for (uint32_t v = lane; v < V; v += kWave) {
         const D d = dist[v];
         store_row<uint64_t>(&drow[v], d == INF ? ~0ull : (uint64_t)d, true);
       }
       if (a.nh) {
         const uint32_t nb = a.nh_bytes;
-        uint8_t* nrow = a.nh + (size_t)sid * V * nb;
+        uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
         for (uint32_t i = lane; i < V * nb; i += kWave) {
           const uint32_t v = i / nb, j = i - v * nb;
           nrow[i] = (uint8_t)N::byte(nh, v, j);

@@ -37,6 +37,9 @@ EXPORTS = (
     "openr_spf_whatif_device",
     "openr_spf_ksp2",
     "openr_spf_ksp2_device",
+    "openr_spf_patch_graph",
+    "openr_spf_refresh",
+    "openr_spf_refresh_device",
     "openr_spf_get_stats",
 )
 
@@ -59,6 +62,20 @@ class SpfGraph(ctypes.Structure):
         ("edge_up", ctypes.POINTER(ctypes.c_uint8)),
         ("node_overloaded", ctypes.POINTER(ctypes.c_uint8)),
         ("name_rank", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+class SpfPatch(ctypes.Structure):
+    _fields_ = [
+        ("n_edges", ctypes.c_uint32),
+        ("edge_ids", ctypes.c_void_p),
+        ("metric", ctypes.c_void_p),
+        ("n_links", ctypes.c_uint32),
+        ("link_ids", ctypes.c_void_p),
+        ("link_up", ctypes.c_void_p),
+        ("n_nodes", ctypes.c_uint32),
+        ("node_ids", ctypes.c_void_p),
+        ("node_overloaded", ctypes.c_void_p),
     ]
 
 
@@ -106,6 +123,9 @@ def load_library():
     l.openr_spf_whatif_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, P(ctypes.c_uint64)]
     l.openr_spf_ksp2.argtypes = [vp, vp, vp, u32, u32, vp, vp]
     l.openr_spf_ksp2_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, vp, u32, u32, vp, vp, vp]
+    l.openr_spf_patch_graph.argtypes = [vp, P(SpfPatch)]
+    l.openr_spf_refresh.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, P(u32)]
+    l.openr_spf_refresh_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, u32, vp, vp, P(u32)]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
     for name in EXPORTS:
         if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy"):
@@ -249,6 +269,50 @@ class SpfEngine:
         _check(self._lib.openr_spf_ksp2_device(self._ctx, device_index, vp(d_sources), n_sources, vp(d_pair_row),
                                                vp(d_pair_dst), n_pairs, tok_cap, vp(d_tok1), vp(d_tok2),
                                                vp(stream or None)))
+
+    def patch(self, edges: Sequence[int] = (), metrics: Sequence[int] = (), links: Sequence[int] = (),
+              link_up: Sequence[int] = (), nodes: Sequence[int] = (), node_overloaded: Sequence[int] = (),
+              track: bool = True) -> None:
+        """Attribute-only mirror update (openr_spf_patch_graph); with ``track`` also applies it
+        to ``self.g`` (a patched copy of the host graph)."""
+        e = np.ascontiguousarray(edges, dtype=np.uint32)
+        m = np.ascontiguousarray(metrics, dtype=np.uint64)
+        lk = np.ascontiguousarray(links, dtype=np.uint32)
+        lu = np.ascontiguousarray(link_up, dtype=np.uint8)
+        nd = np.ascontiguousarray(nodes, dtype=np.uint32)
+        no = np.ascontiguousarray(node_overloaded, dtype=np.uint8)
+        if e.shape != m.shape or lk.shape != lu.shape or nd.shape != no.shape:
+            raise ValueError("patch id / value arrays differ in length")
+        p = SpfPatch(int(e.shape[0]), _p(e), _p(m), int(lk.shape[0]), _p(lk), _p(lu), int(nd.shape[0]), _p(nd),
+                     _p(no))
+        _check(self._lib.openr_spf_patch_graph(self._ctx, ctypes.byref(p)))
+        if track:
+            self.g = self.g.patched(e, m, lk, lu, nd, no)
+
+    def refresh(self, sources: Sequence[int], dist: np.ndarray, nh: Optional[np.ndarray] = None,
+                tight: Optional[np.ndarray] = None, use_link_metric: bool = True) -> int:
+        """Bring rows solved before the last patch up to date in place; returns rows re-solved."""
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        for a in (dist, nh, tight):
+            if a is not None and not a.flags.c_contiguous:
+                raise ValueError("rows must be C-contiguous")
+        nb = nh.shape[2] if nh is not None else self.nh_bytes
+        flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if tight is not None else 0)
+        out = ctypes.c_uint32()
+        _check(self._lib.openr_spf_refresh(self._ctx, _p(src), int(src.shape[0]), flags, _p(dist), _p(nh), nb,
+                                           _p(tight), ctypes.byref(out)))
+        return int(out.value)
+
+    def refresh_device(self, d_sources: int, n: int, d_dist: int, d_nh: int = 0, nh_bytes: int = 0,
+                       use_link_metric: bool = True, stream: int = 0, device_index: int = 0,
+                       d_tight: int = 0) -> int:
+        vp = ctypes.c_void_p
+        flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if d_tight else 0)
+        out = ctypes.c_uint32()
+        _check(self._lib.openr_spf_refresh_device(self._ctx, device_index, vp(d_sources), n, flags, vp(d_dist),
+                                                  vp(d_nh or None), nh_bytes or self.nh_bytes, vp(d_tight or None),
+                                                  vp(stream or None), ctypes.byref(out)))
+        return int(out.value)
 
     def stats(self) -> SpfStats:
         s = SpfStats()

@@ -106,6 +106,21 @@ class CsrGraph:
     def edge_owner(self) -> np.ndarray:
         return np.repeat(np.arange(self.num_nodes, dtype=np.uint32), np.diff(self.row_ptr))
 
+    def patched(self, edges, metrics, links, link_up, nodes, node_overloaded) -> "CsrGraph":
+        """Copy with the attributes of ``openr_spf_patch_graph`` applied (same structure)."""
+        metric = self.metric.copy()
+        up = self.edge_up.copy()
+        ovl = self.node_overloaded.copy()
+        metric[np.asarray(edges, dtype=np.int64)] = np.asarray(metrics, dtype=np.uint64)
+        if len(links):
+            lk = set(int(x) for x in links)
+            want = dict(zip((int(x) for x in links), (1 if x else 0 for x in link_up)))
+            for e in np.nonzero(np.isin(self.link_id, list(lk)))[0]:
+                up[e] = want[int(self.link_id[e])]
+        ovl[np.asarray(nodes, dtype=np.int64)] = np.asarray(node_overloaded, dtype=np.uint8) != 0
+        return CsrGraph(self.names, self.row_ptr, self.col, metric, self.link_id, up, ovl, self.name_rank,
+                        self.num_links, self.link_ends, self.index)
+
     def ctypes_struct(self, struct_type):
         """Fill a ctypes mirror of ``openr_spf_graph``/``oracle_graph``; keeps refs alive."""
         arrs = [

@@ -1,9 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "ksp or kth or distance_only" > gpurun_out/ksp_tests.log 2>&1 || { tail -30 gpurun_out/ksp_tests.log; exit 1; }
-tail -2 gpurun_out/ksp_tests.log
-for p in 64; do
-  echo "== probe $p"
-  OPENR_SPF_KSP_STATS=1 OPENR_SPF_KSP_PROBE=$p timeout -k 10 200 python -u bench.py --workload ksp2 --ksp-sources 256 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ksp_st_$p.log 2>&1 || exit $?
-  grep -E "ksp_stats|^\{" gpurun_out/ksp_st_$p.log | tail -3 | cut -c1-300
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_update.py -m gpu > gpurun_out/update_tests.log 2>&1 || { tail -40 gpurun_out/update_tests.log; exit 1; }
+tail -3 gpurun_out/update_tests.log
+for t in grid100 fabric; do
+  timeout -k 10 200 python -u bench.py --workload update --topology $t --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/update_$t.log 2>&1 || { tail -20 gpurun_out/update_$t.log; exit 1; }
+  grep '^{' gpurun_out/update_$t.log | cut -c1-900
 done
