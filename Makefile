@@ -13,8 +13,8 @@ ENGINE_HDRS := $(CSRC)/spf_kernels.h $(CSRC)/spf_device.h $(CSRC)/spf_bfs_common
 ENGINE_OBJS := $(LIBDIR)/spf_kernels.o $(LIBDIR)/spf_bfs.o $(LIBDIR)/spf_bfs_lvl.o $(LIBDIR)/spf_sweep.o $(LIBDIR)/spf_fringe.o $(LIBDIR)/spf_rounds.o $(LIBDIR)/spf_ksp.o $(LIBDIR)/spf_update.o $(LIBDIR)/spf_capi.o
 
 HOST := $(LIBDIR)/libopenr_decision.so
-HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp
-HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h include/openr_spf.h
+HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp $(CSRC)/host/AdjDbCodec.cpp $(CSRC)/host/adjdb_capi.cpp
+HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h $(CSRC)/host/AdjDbCodec.h include/openr_spf.h include/openr_adjdb.h
 CXX ?= g++
 CC ?= gcc
 CXXFLAGS ?= -O2 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter

@@ -92,11 +92,22 @@ struct Adjacency {
   std::string otherIfName;
 };
 
+// Lsdb.thrift:24-32
+struct PerfEvent {
+  std::string nodeName;
+  std::string eventDescr;
+  int64_t unixTs = 0;
+};
+struct PerfEvents {
+  std::vector<PerfEvent> events;
+};
+
 struct AdjacencyDatabase {
   std::string thisNodeName;
   bool isOverloaded = false;
   std::vector<Adjacency> adjacencies;
   int32_t nodeLabel = 0;
+  std::optional<PerfEvents> perfEvents;
   std::string area;
 };
 }  // namespace thrift

@@ -16,6 +16,7 @@
 #include "../../oracle/spf_oracle.h"
 #include "harness.h"
 #include "../../openr_amd/csrc/host/LinkState.h"
+#include "../../openr_amd/csrc/host/AdjDbCodec.h"
 
 using namespace openr;
 
@@ -216,6 +217,60 @@ TEST_CPU(LinkStateTest_BasicOperation) {
   EXPECT_TRUE(state.linksFromNode(n1).empty());
   EXPECT_TRUE(sameLinks(state.linksFromNode(n2), {l2}));
   EXPECT_TRUE(sameLinks(state.linksFromNode(n3), {l2}));
+}
+
+// Bulk adjacency publication (Decision.cpp:1737-1782 through AdjDbCodec): encoded
+// "adj:" values applied in one call give the same LinkState and CSR mirror as direct
+// updateAdjacencyDatabase calls; other keys are ignored; a key/node mismatch throws.
+TEST_CPU(AdjDbCodec_PublicationMatchesDirectUpdates) {
+  std::string n1 = "node1", n2 = "node2", n3 = "node3";
+  auto db1 = createAdjDb(n1, {createAdjacency(n2, "if2", "if1", 3, 1), createAdjacency(n3, "if3", "if1", 1, 1)}, 1);
+  auto db2 = createAdjDb(n2, {createAdjacency(n1, "if1", "if2", 5, 1), createAdjacency(n3, "if3", "if2", 1, 1)}, 2);
+  auto db3 = createAdjDb(n3, {createAdjacency(n1, "if1", "if3", 1, 1), createAdjacency(n2, "if2", "if3", 7, 1)}, 3);
+  db2.isOverloaded = true;
+  db3.adjacencies[1].isOverloaded = true;
+  db1.perfEvents = thrift::PerfEvents{{{n1, "ADJ_DB_UPDATED", 42}}};
+  LinkState direct{kArea};
+  for (auto const* db : {&db1, &db2, &db3}) direct.updateAdjacencyDatabase(*db, 0, 0);
+
+  std::vector<std::pair<std::string, std::string>> kv;
+  for (auto db : {db1, db2, db3}) {
+    db.area = "stale";  // Decision stamps the area of the LinkState (Decision.cpp:1762)
+    kv.emplace_back("adj:" + db.thisNodeName, serializer::writeAdjacencyDatabase(db));
+  }
+  kv.emplace_back("prefix:node1:0:[10.0.0.0/8]", "not an adjacency db");
+  LinkState bulk{kArea};
+  auto res = applyAdjacencyPublication(bulk, kv, 2);
+  EXPECT_EQ(res.adjDbsApplied, 3u);
+  EXPECT_TRUE(res.topologyChanged);
+  EXPECT_EQ(bulk.numLinks(), direct.numLinks());
+  EXPECT_EQ(bulk.getAdjacencyDatabases().at(n3).area, kArea);
+  auto const& a = direct.csrMirror();
+  auto const& b = bulk.csrMirror();
+  EXPECT_TRUE(a.names == b.names);
+  EXPECT_TRUE(a.rowPtr == b.rowPtr);
+  EXPECT_TRUE(a.col == b.col);
+  EXPECT_TRUE(a.metric == b.metric);
+  EXPECT_TRUE(a.edgeUp == b.edgeUp);
+  EXPECT_TRUE(a.overloaded == b.overloaded);
+  // decoded struct equals the original, perf events included
+  auto rt = serializer::readAdjacencyDatabase(serializer::writeAdjacencyDatabase(db1));
+  EXPECT_TRUE(rt.perfEvents.has_value() && rt.perfEvents->events.size() == 1 &&
+              rt.perfEvents->events[0].unixTs == 42);
+  EXPECT_EQ(rt.adjacencies[0].nextHopV6.addr, db1.adjacencies[0].nextHopV6.addr);
+  // key/node mismatch: CHECK_EQ in the reference
+  std::vector<std::pair<std::string, std::string>> wrong{{"adj:node9", serializer::writeAdjacencyDatabase(db1)}};
+  LinkState other{kArea};
+  EXPECT_THROW(applyAdjacencyPublication(other, wrong));
+  // a malformed value names its index
+  std::vector<std::pair<std::string, std::string>> broken{kv[0], {"adj:node2", kv[1].second.substr(0, 9)}};
+  bool named = false;
+  try {
+    applyAdjacencyPublication(other, broken);
+  } catch (const CompactProtocolError& e) {
+    named = std::string(e.what()).rfind("value 1:", 0) == 0;
+  }
+  EXPECT_TRUE(named);
 }
 
 // LinkStateTest.cpp:202-242

@@ -53,3 +53,18 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(engine.SpfError) as ei:
         engine.SpfEngine()
     assert ei.value.code == engine.ENODEV
+
+
+def test_adjdb_library_exports_every_declared_symbol():
+    """include/openr_adjdb.h (bulk AdjacencyDatabase decode) is exported by libopenr_decision.so."""
+    from openr_amd import adjdb
+
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "openr_adjdb.h")).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(openr_adjdb_[a-z_0-9]+)\s*\(", text)))
+    assert len(declared) >= 12
+    lib = adjdb.load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", adjdb.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (openr_adjdb_\w+)", out.stdout))
+    for name in declared:
+        assert name in exported, name
+        assert hasattr(lib, name)
