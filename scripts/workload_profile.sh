@@ -16,6 +16,8 @@ for W in $WORKLOADS; do
     ksp2)   ARGS="--workload ksp2 --steps 2 --warmup 1" ;;       # all 24.9 M fabric pairs per step
     whatif) ARGS="--workload whatif --steps 5 --warmup 1" ;;     # all 3 M WAN (link, source) units
     update) ARGS="--workload update --topology fabric --steps 20 --warmup 2" ;;
+    adjdb)  ARGS="--workload adjdb --steps 5 --warmup 1" ;;                    # G100 full adj: sync
+    adjdb_fabric) ARGS="--workload adjdb --topology fabric --steps 5 --warmup 1" ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
   cd "$R" && timeout -k 10 400 python3 -u bench.py $ARGS > "$OUT/bench.log" 2>&1; stop $?
