@@ -83,6 +83,7 @@ struct Device {
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
+  DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
@@ -522,6 +523,11 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
   OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
   OPENR_TRY(launch_strided_iota(d.kptr.p, chunk + 1u, ign_cap, d.num_cus, s));
+  OPENR_TRY(d.kretry.reserve(8u + 2u * (size_t)chunk));
+  uint32_t* rcount = d.kretry.p;  // [0] k = 1, [1] k = 2; [2..5] work counters of the 4 launches
+  uint32_t* wctr = d.kretry.p + 2;
+  uint32_t* rlist1 = d.kretry.p + 8;
+  uint32_t* rlist2 = rlist1 + chunk;
   // OPENR_SPF_KSP_STATS=1: per-kind trace counters printed to stderr (tuning only)
   const uint32_t nst = ksp_stats_count();
   unsigned long long* kst = nullptr;
@@ -531,8 +537,14 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   }
   for (uint32_t first = 0; first < n_pairs; first += chunk) {
     const uint32_t m = std::min(chunk, n_pairs - first);
+    OPENR_TRY(hipMemsetAsync(rcount, 0, 8u * sizeof(uint32_t), s));
+    // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst));
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst, nullptr, nullptr, rlist1,
+                               rcount, wctr));
+    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst, rlist1, rcount, nullptr,
+                               nullptr, wctr + 1));
     OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
     SolveArgs b{};
     b.sources = d.ksrc.p;
@@ -547,7 +559,11 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr));
+                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, nullptr,
+                               nullptr, rlist2, rcount + 1, wctr + 2));
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, rlist2,
+                               rcount + 1, nullptr, nullptr, wctr + 3));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);
@@ -653,7 +669,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
                      d.kbase.p,     d.krows.p,      d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
-                     d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p};
+                     d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
     d.precs.release();

@@ -195,11 +195,21 @@ hipError_t launch_zero_rows(uint64_t* rows, uint32_t words, const uint32_t* alis
 // KSP2 tracing (spf_ksp.hip), one wavefront per (src, dest) pair of a chunk.
 constexpr uint32_t kKspMaxDepth = 256;  // DFS frames (hops of a traced shortest path)
 constexpr uint32_t kKspArena = 1024;    // sorted pathLinks of the frames on the DFS stack
+struct KspCaps {
+  uint32_t frames, arena;
+};
+KspCaps ksp_caps(const DevGraph& g, bool full);  // small tier (occupancy) or full tier
 // kind 1 writes the k = 1 links to ign_io[k * ign_cap, ign_end[k]); kind 2 ignores them.
+// Small tier: retry_list != null; pairs that outgrow it are appended there (count in
+// *retry_count). Full tier: retry_list == null; with `list` it traces only the chunk-local
+// pairs list[0 .. *list_count).
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats = nullptr);
+                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats = nullptr,
+                            const uint32_t* list = nullptr, const uint32_t* list_count = nullptr,
+                            uint32_t* retry_list = nullptr, uint32_t* retry_count = nullptr,
+                            uint32_t* work_ctr = nullptr);  // zeroed dynamic-scheduling counter (required)
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);

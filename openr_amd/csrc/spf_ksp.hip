@@ -52,8 +52,11 @@ struct KspLayout {
 
 constexpr uint32_t kD16Budget = 64u * 1024u;  // LDS per wavefront up to which the u16 distance copy is kept
 
-// deg = largest row (candidate scratch of one frame).
-__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg, bool want_d16) {
+// deg = largest row (candidate scratch of one frame); frames / arena = DFS capacity
+// (KspCaps: a small tier sized from the graph's depth for occupancy, and the full tier
+// that re-runs the pairs the small one could not hold).
+__host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg, uint32_t frames, uint32_t arena,
+                                                bool want_d16) {
   KspLayout l;
   uint32_t off = 16;  // control: [0] candidate count
   auto take = [&](uint32_t bytes) {
@@ -63,14 +66,14 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   };
   l.vis = take(4u * ((L + 31u) / 32u));
   l.dead = take(4u * ((V + 31u) / 32u));
-  l.fr_node = take(4u * kKspMaxDepth);
-  l.fr_edge = take(4u * kKspMaxDepth);
-  l.fr_beg = take(4u * kKspMaxDepth);
-  l.fr_cnt = take(4u * kKspMaxDepth);
-  l.fr_idx = take(4u * kKspMaxDepth);
-  l.ar_e = take(4u * kKspArena);
-  l.ar_l = take(4u * kKspArena);
-  l.ar_u = take(4u * kKspArena);
+  l.fr_node = take(4u * frames);
+  l.fr_edge = take(4u * frames);
+  l.fr_beg = take(4u * frames);
+  l.fr_cnt = take(4u * frames);
+  l.fr_idx = take(4u * frames);
+  l.ar_e = take(4u * arena);
+  l.ar_l = take(4u * arena);
+  l.ar_u = take(4u * arena);
   l.skd = take(8u * deg);
   l.skr = take(8u * deg);
   l.sl = take(4u * deg);
@@ -99,6 +102,7 @@ struct KspState {
   uint32_t* seen;  // reachability probe: visited nodes (V bits)
   uint32_t* q;     // reachability probe queue (global, V entries per wavefront)
   uint32_t probe_after;
+  uint32_t max_depth, arena_cap;  // DFS frames / arena entries of this launch's tier
   uint64_t* stats;  // LDS counters (lane 0 updates), null unless enabled
   const uint16_t* d16;  // LDS copy of drow saturated at 0xFFFF, valid when use16
   bool use16;
@@ -206,7 +210,7 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
   const uint64_t m0 = __ballot(c0.ok), m1 = __ballot(c1.ok);
   const uint64_t t1 = st.stats ? clock64() : 0;
   const uint32_t cnt = (uint32_t)(__popcll(m0) + __popcll(m1));
-  if (beg + cnt > kKspArena) return UINT32_MAX;
+  if (beg + cnt > st.arena_cap) return UINT32_MAX;
   uint32_t r0 = 0, r1 = 0;
   rank_against(m0, c0, c0, c1, r0, r1);
   rank_against(m1, c1, c0, c1, r0, r1);
@@ -268,7 +272,7 @@ __device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_
   lds_fence();
   const uint64_t t1 = st.stats ? clock64() : 0;
   const uint32_t cnt = __builtin_amdgcn_readfirstlane(st.ctl[0]);
-  if (beg + cnt > kKspArena) return UINT32_MAX;
+  if (beg + cnt > st.arena_cap) return UINT32_MAX;
   for (uint32_t i = lane; i < cnt; i += kWave) {
     const uint64_t kd = st.skd[i], kr = st.skr[i];
     uint32_t rank = 0;
@@ -433,7 +437,7 @@ __device__ int trace_one(const KspState& st, uint32_t dst) {
     }
     lds_fence();
     if (!fresh || !live) continue;  // insert() failed, or a subtree known to fail
-    if (sp >= kKspMaxDepth) return -2;
+    if (sp >= st.max_depth) return -2;
     const uint32_t re = st.ar_e[beg + idx];
     if (u == st.src) {
       if (lane == 0) st.fr_edge[sp] = re;
@@ -460,7 +464,10 @@ __device__ int trace_one(const KspState& st, uint32_t dst) {
   return -1;
 }
 
-// Pairs [first, first + n) of a chunk; k = pair - first.
+// Pairs [first, first + n) of a chunk; k = pair - first. With `list` the launch covers
+// only the chunk-local k of list[0 .. *list_count) (the full-tier re-run). With
+// `retry_list` (small tier) a pair whose DFS outgrows the tier's frames / arena is
+// appended there instead of being marked bad; the full tier re-runs it.
 // KIND 1: k = 1 over the base rows (row = prow[pair]); the links of the paths found are
 //         written to ign_io[k * ign_cap, ign_end[k]).
 // KIND 2: k = 2 over the chunk's rows (row k); those links start out used (the second
@@ -471,10 +478,13 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           const uint64_t* rows, uint32_t* ign_io, uint32_t* ign_end,
                                                           uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap,
                                                           uint32_t* status, uint32_t* qbuf, uint32_t probe_after,
-                                                          uint32_t use_d16, unsigned long long* gstats) {
+                                                          uint32_t use_d16, unsigned long long* gstats,
+                                                          uint32_t frames, uint32_t arena, const uint32_t* list,
+                                                          const uint32_t* list_count, uint32_t* retry_list,
+                                                          uint32_t* retry_count, uint32_t* work_ctr) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, use_d16 != 0);
+  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, use_d16 != 0);
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
   st.g = &g;
@@ -496,14 +506,21 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
   st.seen = reinterpret_cast<uint32_t*>(base + lay.seen);
   st.q = qbuf + (size_t)blockIdx.x * V;
   st.probe_after = probe_after;
+  st.max_depth = frames;
+  st.arena_cap = arena;
   st.stats = gstats ? reinterpret_cast<uint64_t*>(base + lay.stats) : nullptr;
   const uint32_t lane = threadIdx.x, lw = (g.L + 31u) / 32u, vw = (V + 31u) / 32u;
   if (st.stats && lane < kKspStats) st.stats[lane] = 0;
   uint16_t* d16 = lay.d16 ? reinterpret_cast<uint16_t*>(base + lay.d16) : nullptr;
   st.d16 = d16;
   uint32_t d16_row = UINT32_MAX;  // KIND 1: the base row already in d16
-  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+  const uint32_t n_units = list ? *list_count : n;
+  // dynamic scheduling: pair costs differ by an order of magnitude between destination
+  // tiers, so a static stride leaves waves idle; the first gridDim.x units are static
+  for (uint32_t unit = blockIdx.x; unit < n_units;
+       unit = gridDim.x + __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(work_ctr, 1u) : 0u)) {
     const uint64_t tp = st.stats ? clock64() : 0;
+    const uint32_t k = list ? list[unit] : unit;
     const uint32_t pair = first + k;
     const uint32_t row = prow[pair];
     const uint32_t src = sources[row], dst = pdst[pair];
@@ -530,7 +547,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
       lds_fence();
     }
     uint32_t npaths = 0, pos = 1, nign = 0;
-    bool bad = src >= V || dst >= V;
+    bool bad = src >= V || dst >= V, retry = false;
     // res.count(dest); src == dest traces an empty path, which ends the loop at once
     stat_add(st, kStPairs, 1);
     if (st.stats) stat_add(st, kStCycInit, clock64() - tp);
@@ -546,8 +563,9 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
             stat_add(st, kStEntFail, st.stats[kStEntries] - e0);
           }
         }
-        if (len == -2) {
-          bad = true;
+        if (len == -2) {  // frames / arena exhausted: the full tier re-runs the pair
+          if (retry_list) retry = true;
+          else bad = true;
           break;
         }
         if (len <= 0) break;  // while (path && !path->empty())
@@ -568,9 +586,14 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
       }
     }
     if (lane == 0) {
-      if (KIND == 1) ign_end[k] = k * ign_cap + (bad ? 0u : nign);
-      out[0] = bad ? 0xFFFFFFFFu : npaths;
-      if (bad) atomicOr(status, 1u);
+      if (retry) {
+        retry_list[atomicAdd(retry_count, 1u)] = k;
+        if (KIND == 1) ign_end[k] = k * ign_cap;
+      } else {
+        if (KIND == 1) ign_end[k] = k * ign_cap + (bad ? 0u : nign);
+        out[0] = bad ? 0xFFFFFFFFu : npaths;
+        if (bad) atomicOr(status, 1u);
+      }
     }
     if (st.stats) {
       stat_add(st, kStPaths, npaths);
@@ -599,24 +622,55 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 // wavefronts per CU; measured slower on the fabric, kept as a tuning knob)
 bool ksp_use_d16() { return bfs::env_u32("OPENR_SPF_KSP_D16", 0u, 0u, 1u) != 0; }
 
+// Small tier: a traced path has at most as many hops as the source's BFS depth on
+// uniform-cost graphs; 2x the sampled depth + 8 covers the sample's misses and weighted
+// graphs' longer hop counts, and the arena holds that many frames of typical width.
+// Everything it cannot hold re-runs in the full tier (kKspMaxDepth / kKspArena).
+KspCaps ksp_caps(const DevGraph& g, bool full) {
+  KspCaps c{kKspMaxDepth, kKspArena};
+  if (full || bfs::env_u32("OPENR_SPF_KSP_TIER", 1u, 0u, 1u) == 0) return c;
+  c.frames = std::min<uint32_t>(kKspMaxDepth, std::max<uint32_t>(16u, 2u * g.est_depth + 8u));
+  // half-full frames on average (measured on the fabric: arena 256 > 320 > 512 in speed,
+  // the LDS it frees buys wavefronts; the rare deeper DFS re-runs in the full tier)
+  const uint32_t want = (g.est_depth + 2u) * std::max<uint32_t>(g.max_deg, 1u) / 2u;
+  c.arena = std::min<uint32_t>(kKspArena, std::max<uint32_t>(256u, (want + 63u) & ~63u));
+  // test hooks: force tiny small-tier capacities so most pairs take the full-tier re-run
+  c.frames = bfs::env_u32("OPENR_SPF_KSP_SMALL_FRAMES", c.frames, 1u, kKspMaxDepth);
+  c.arena = bfs::env_u32("OPENR_SPF_KSP_SMALL_ARENA", c.arena, 1u, kKspArena);
+  return c;
+}
+
+uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full) {
+  const KspCaps c = ksp_caps(g, full);
+  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16()).total;
+  return t <= kMaxLds ? t : 0;
+}
+
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
-  return blocks_for(UINT32_MAX, ksp_lds_bytes(g.V, g.L, g.max_deg), num_cus, kWave);
+  return std::max(blocks_for(UINT32_MAX, ksp_tier_lds_bytes(g, false), num_cus, kWave),
+                  blocks_for(UINT32_MAX, ksp_tier_lds_bytes(g, true), num_cus, kWave));
 }
 
 uint32_t ksp_stats_count() { return kKspStats; }
 
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
-  const uint32_t t = ksp_layout(V, L, max_deg, ksp_use_d16()).total;
+  const uint32_t t = ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16()).total;
   return t <= kMaxLds ? t : 0;
 }
 
 hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
                             const uint32_t* pdst, uint32_t first, uint32_t n, const uint64_t* rows, uint32_t* ign_io,
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
-                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats) {
+                            uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
+                            const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
+                            uint32_t* retry_count, uint32_t* work_ctr) {
   if (!n) return hipSuccess;
-  const uint32_t lds = ksp_lds_bytes(g.V, g.L, g.max_deg);
+  if (!work_ctr) return hipErrorInvalidValue;
+  const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
+  const KspCaps caps = ksp_caps(g, full);
+  const uint32_t lds = ksp_tier_lds_bytes(g, full);
   if (!lds || !qbuf) return hipErrorInvalidValue;
+  // a re-run launch covers the listed pairs only; its surplus wavefronts exit at once
   const uint32_t grid = blocks_for(n, lds, num_cus, kWave);  // <= ksp_max_grid: qbuf holds grid * V
   auto k = kind == 1 ? ksp_trace_kernel<1> : ksp_trace_kernel<2>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -625,7 +679,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
                      bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16() ? 1u : 0u,
-                     stats);
+                     stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr);
   return hipGetLastError();
 }
 

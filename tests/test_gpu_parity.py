@@ -572,3 +572,22 @@ def test_whatif_overloads_parallel_links_hubs(eng, whatif_mode):
     for use_metric in (True, False):
         changed, _ = eng.whatif(links, srcs, use_metric)
         np.testing.assert_array_equal(changed, whatif_oracle(g, links, srcs, use_metric))
+
+
+@pytest.mark.parametrize("tier", [{"OPENR_SPF_KSP_SMALL_FRAMES": "2", "OPENR_SPF_KSP_SMALL_ARENA": "8"},
+                                  {"OPENR_SPF_KSP_SMALL_FRAMES": "3"}, {"OPENR_SPF_KSP_TIER": "0"}],
+                         ids=["tiny", "frames3", "full-only"])
+def test_ksp2_device_capacity_tiers(eng, tier, monkeypatch):
+    """The tracer runs a small-capacity tier (DFS frames / arena sized from the graph's
+    depth, for occupancy) and re-runs the pairs it cannot hold in the full tier. Forcing
+    tiny small-tier capacities sends most pairs through the re-run list; results must
+    not change (k = 1 re-runs also rewrite the pair's ignore set for the second SPF)."""
+    for k, v in tier.items():
+        monkeypatch.setenv(k, v)
+    g = random_graph(411, 70, 160, 9, p_ovl=0.08, p_down=0.05, p_par=0.15)
+    rng = np.random.default_rng(7)
+    check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
+    g = T.fabric(288 + 56)
+    check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (200, 2))])
+    g = hub_graph(21, V=220, L=500)
+    check_ksp2_against_oracle(eng, g, [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 30)])
