@@ -74,10 +74,12 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.ar_e = take(4u * arena);
   l.ar_l = take(4u * arena);
   l.ar_u = take(4u * arena);
-  l.skd = take(8u * deg);
-  l.skr = take(8u * deg);
-  l.sl = take(4u * deg);
-  l.su = take(4u * deg);
+  // candidate scratch of load_path_links_long only: rows of <= 128 in-edges rank in registers
+  const uint32_t sdeg = deg > 2u * kWave ? deg : 0u;
+  l.skd = take(8u * sdeg);
+  l.skr = take(8u * sdeg);
+  l.sl = take(4u * sdeg);
+  l.su = take(4u * sdeg);
   l.seen = take(4u * ((V + 31u) / 32u));
   l.stats = take(8u * kKspStats);
   l.d16 = 0;
