@@ -357,12 +357,27 @@ bool LinkState::hasHolds() const {
   return false;
 }
 
+void LinkState::indexAdjacencies(const std::string& nodeName) {
+  auto& idx = ifIndex_[nodeName];
+  idx.clear();
+  const auto& adjs = adjacencyDatabases_.at(nodeName).adjacencies;
+  for (uint32_t i = 0; i < adjs.size(); ++i) idx[adjs[i].ifName].push_back(i);
+}
+
 std::shared_ptr<Link> LinkState::maybeMakeLink(const std::string& nodeName, const thrift::Adjacency& adj) const {
-  // a Link exists only if the other end advertises the reverse adjacency
+  // a Link exists only if the other end advertises the reverse adjacency: the first
+  // adjacency of the other node (LinkState.cpp:531-547 scans its list in order) with
+  // otherNodeName == nodeName, ifName == adj.otherIfName, otherIfName == adj.ifName;
+  // only positions whose ifName matches can qualify, so the index lists exactly those
   auto it = adjacencyDatabases_.find(adj.otherNodeName);
   if (it == adjacencyDatabases_.end()) return nullptr;
-  for (const auto& back : it->second.adjacencies) {
-    if (back.otherNodeName == nodeName && adj.otherIfName == back.ifName && adj.ifName == back.otherIfName)
+  auto ix = ifIndex_.find(adj.otherNodeName);
+  if (ix == ifIndex_.end()) return nullptr;
+  auto pos = ix->second.find(adj.otherIfName);
+  if (pos == ix->second.end()) return nullptr;
+  for (uint32_t i : pos->second) {
+    const auto& back = it->second.adjacencies[i];
+    if (back.otherNodeName == nodeName && adj.ifName == back.otherIfName)
       return std::make_shared<Link>(area_, nodeName, adj, adj.otherNodeName, back);
   }
   return nullptr;
@@ -386,6 +401,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
 
   thrift::AdjacencyDatabase prior(std::move(adjacencyDatabases_[nodeName]));
   adjacencyDatabases_[nodeName] = newDb;
+  indexAdjacencies(nodeName);
 
   // both sides ordered by <hash, names> so one merge pass finds adds/removes/updates
   const auto oldLinks = orderedLinksFromNode(nodeName);
@@ -448,6 +464,7 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string&
   if (it != adjacencyDatabases_.end()) {
     removeNode(nodeName);
     adjacencyDatabases_.erase(it);
+    ifIndex_.erase(nodeName);
     spfResults_.clear();
     kthPathResults_.clear();
     markMirrorDirty();

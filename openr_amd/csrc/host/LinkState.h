@@ -333,6 +333,10 @@ class LinkState {
   LinkSet allLinks_;
   std::unordered_map<std::string, HoldableValue<bool>> nodeOverloads_;
   std::unordered_map<std::string, thrift::AdjacencyDatabase> adjacencyDatabases_;
+  // per node: ifName -> positions in its adjacency list (increasing), so maybeMakeLink
+  // finds the reverse adjacency without scanning the other node's whole list
+  std::unordered_map<std::string, std::unordered_map<std::string, std::vector<uint32_t>>> ifIndex_;
+  void indexAdjacencies(const std::string& nodeName);
 
   mutable CsrMirror mirror_;
   mutable bool mirrorDirty_ = true;

@@ -212,6 +212,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
         lvl[src] = 0;
+        lvl[V] = 0;  // ELL sentinel (ellv): level 0 is never > L, so a sentinel slot is never tight
         if (!ELECT) vis[src >> 5] = 1u << (src & 31u);
       }
       __syncthreads();
@@ -269,11 +270,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           const uint32_t idx = fb + group;
           const bool live = idx < tail;
           uint32_t u = 0, beg = 0, end = 0;
-          uint4 ell = make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
+          uint4 ell = ELLM == 2 ? make_uint4(V, V, V, V) : make_uint4(kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown);
           if (live) {
             u = ring[RING ? (idx & rmask) : idx];
             if (ELLM == 2) {
-              ell = g.ellt[u];
+              ell = g.ellv[u];  // down / padding / sink-row slots hold the sentinel V
             } else {
               const uint2 r = g.row2t[u];  // empty (begin flagged) for overloaded nodes (sinks)
               beg = r.x;
@@ -311,9 +312,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j * G;
+              if (ELLM == 2) {  // ellv: a node id or the sentinel V (lvl[V] == 0); ELLM 2 is never GENERIC
+                vv[j] = av[j];
+                tight[j] = lvl[vv[j]] > L;
+                continue;
+              }
               vv[j] = av[j] & ~(kEdgeDown | kNodeSink);  // always a valid node id
-              const bool ok = !(av[j] & kEdgeDown) && (ELLM == 2 || e < end) && !(has_ign && test_bit(ign, lv[j]));
-              const uint32_t l = lvl[ok ? vv[j] : V];  // lvl[V] is padding
+              const bool ok = !(av[j] & kEdgeDown) && e < end && !(has_ign && test_bit(ign, lv[j]));
+              const uint32_t l = lvl[ok ? vv[j] : V];  // lvl[V] is padding (0: never tight)
               tight[j] = ok && l > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
             }
 #ifdef OPENR_SPF_PROFILE

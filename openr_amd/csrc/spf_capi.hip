@@ -100,7 +100,7 @@ hipError_t reserve_counters(Device& d) {
 }
 
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.adj,    g.w,
+  void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.ellv, g.adj,    g.w,
                    g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge, g.rank, g.erec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -813,6 +813,11 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.row2t, row2t.data(), V);
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
     if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
+    if (err == hipSuccess) {
+      std::vector<uint4> ellv(V);
+      for (uint32_t u = 0; u < V; ++u) ellv[u] = ellv_of(ellt[u], V);
+      err = up(&g.ellv, ellv.data(), V);
+    }
     if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
@@ -963,6 +968,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     else ctx->ovl_bits[u >> 5] &= ~(1u << (u & 31u));
     dirty_bits[u >> 5] = 1;
     rec(kPatchEllt, u, ctx->ellt[u]);
+    rec(kPatchEllv, u, ellv_of(ctx->ellt[u], V));
     rec(kPatchRow2t, u, make_uint4(ctx->row2t[u].x, ctx->row2t[u].y, 0, 0));
     rec(kPatchOvl, u, make_uint4(ctx->ovl[u], 0, 0, 0));
   }

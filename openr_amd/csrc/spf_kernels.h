@@ -24,6 +24,8 @@ struct DevGraph {
                                //     (an overloaded node other than the source is never expanded)
   uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
   uint4* ellt = nullptr;       // [V] first 4 edges of each transit row (adj encoding, kEdgeDown-padded)
+  uint4* ellv = nullptr;       // [V] ellt with every down / padding slot replaced by the node id V (a
+                               //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
   uint32_t* win = nullptr;     // [E] metric of the reverse edge (col -> row owner)
@@ -44,6 +46,11 @@ constexpr uint32_t kEdgeDown = 0x80000000u;
 // (row2t of a sink is an empty range whose begin carries the flag, so it never loops.)
 constexpr uint32_t kNodeSink = 0x40000000u;
 constexpr uint32_t kBlock = 256;
+// ellv slot of an ellt slot: the column, or V for a down / padding / sink-row slot
+__host__ __device__ inline uint4 ellv_of(uint4 t, uint32_t V) {
+  auto f = [V](uint32_t x) { return (x & kEdgeDown) ? V : x; };
+  return make_uint4(f(t.x), f(t.y), f(t.z), f(t.w));
+}
 constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
 constexpr uint32_t kBfsTargetWgs = 12;    // lvl BFS sizes its ring for this many workgroups per CU (G100: 8 -> 1.06 ms, 9..16 -> 1.02 ms)
 
@@ -169,7 +176,8 @@ uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
 // In-place attribute patch of the device mirror: each record overwrites one element of
 // one DevGraph array (structure — rows, columns, link ids — never changes).
 enum PatchArray : uint32_t {
-  kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kNumPatchArrays
+  kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kPatchEllv,
+  kNumPatchArrays
 };
 struct PatchRec {
   uint32_t arr, idx, pad0, pad1;
