@@ -324,18 +324,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             OPENR_PROF_STAMP(t3);
             OPENR_PROF_ADD(2, t2, t3);
 #endif
-            // (3) wave-aggregated append: 3 ballots + one ds_add per wave
-            uint32_t total;
-            uint32_t slot = wave_prefix_small((uint32_t)__popc(fresh_mask), &total);
+            // (3) wave-aggregated append: one ballot per edge slot j, one ds_add per wave;
+            //     arrival (lane, j) takes slot base + (fresh arrivals of slots < j) +
+            //     (fresh arrivals of slot j in lower lanes)
+            unsigned long long bj[K];
+            uint32_t off[K + 1];
+            off[0] = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              bj[j] = __ballot((fresh_mask >> j) & 1u);
+              off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+            }
+            const uint32_t total = off[K];
             if (total) {  // wave-uniform
               const int leader = __ffsll((long long)__ballot(1)) - 1;
               uint32_t wbase = 0;
               if ((int)lane == leader) wbase = atomicAdd(cnt, total);
-              slot += tail + __builtin_amdgcn_readfirstlane(wbase);
+              const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
               bool lost = false;
 #pragma unroll
               for (int j = 0; j < K; ++j) {
                 if ((fresh_mask >> j) & 1u) {
+                  const uint32_t slot =
+                      base + off[j] +
+                      __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
                   if (!RING) {
                     ring[slot] = (uint16_t)vv[j];
                   } else if (slot - head < ring_cap) {
@@ -343,7 +355,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                   } else {
                     lost = true;  // two adjacent levels exceed the ring
                   }
-                  ++slot;
                 }
               }
               if (RING && __any(lost) && (int)lane == leader) ctl[4] = 1;
