@@ -308,13 +308,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
             // (1) tight test: the K level reads are issued together (no branches)
             bool tight[K];
-            uint32_t vv[K];
+            uint32_t vv[K], lold[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j * G;
               if (ELLM == 2) {  // ellv: a node id or the sentinel V (lvl[V] == 0); ELLM 2 is never GENERIC
                 vv[j] = av[j];
-                tight[j] = lvl[vv[j]] > L;
+                lold[j] = lvl[vv[j]];
+                tight[j] = lold[j] > L;
                 continue;
               }
               vv[j] = av[j] & ~(kEdgeDown | kNodeSink);  // always a valid node id
@@ -351,7 +352,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-              if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              // ELL-only path: store unconditionally (no branch). A non-tight v has a level
+              // <= L that no arrival of this level changes, so writing it back is race-free.
+              if (ELLM == 2) lvl[vv[j]] = (LT)(tight[j] ? L + 1u : lold[j]);
+              else if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
               if (trow && tight[j]) {
                 const uint32_t e = e0 + j * G;
                 atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
