@@ -341,23 +341,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               uint32_t wbase = 0;
               if ((int)lane == leader) wbase = atomicAdd(cnt, total);
               const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
-              bool lost = false;
+              // the wave's slots are [base, base + total): one wave-uniform test tells
+              // whether all of them fit the ring (two adjacent levels); if not, the
+              // solve is flagged and re-run, so none of them needs storing
+              if (!RING || base + total - head <= ring_cap) {
 #pragma unroll
-              for (int j = 0; j < K; ++j) {
-                if ((fresh_mask >> j) & 1u) {
-                  const uint32_t slot =
-                      base + off[j] +
-                      __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
-                  if (!RING) {
-                    ring[slot] = (uint16_t)vv[j];
-                  } else if (slot - head < ring_cap) {
-                    ring[slot & rmask] = (uint16_t)vv[j];
-                  } else {
-                    lost = true;  // two adjacent levels exceed the ring
+                for (int j = 0; j < K; ++j) {
+                  if ((fresh_mask >> j) & 1u) {
+                    const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                    ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
                   }
                 }
+              } else if ((int)lane == leader) {
+                ctl[4] = 1;  // two adjacent levels exceed the ring
               }
-              if (RING && __any(lost) && (int)lane == leader) ctl[4] = 1;
             }
 #ifdef OPENR_SPF_PROFILE
             OPENR_PROF_STAMP(t4);

@@ -282,14 +282,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               if (ELLM == 1) ell = g.ellt[u];
             }
           }
-          if (ELLM == 2 && live) end = 4;  // kEdgeDown-padded ELL slots stand for the row end
           const typename N::Val nhu = N::load(nh, u);  // final: u was reached a level ago
 #ifdef OPENR_SPF_PROFILE
           OPENR_PROF_STAMP(t1);
           OPENR_PROF_ADD(0, t0, t1);
           pc[7] += 1;
 #endif
-          for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; __any(e0 < end); e0 += G * K) {
+          // ELL-only: one pass over the 4 slots (a lane with no frontier node holds the
+          // sentinel row, which is never tight)
+          for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; ELLM == 2 ? e0 == 0u : __any(e0 < end); e0 += G * K) {
             uint32_t av[K], lv[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -382,23 +383,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               uint32_t wbase = 0;
               if ((int)lane == leader) wbase = atomicAdd(cnt, total);
               const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
-              bool lost = false;
+              // the wave's slots are [base, base + total): one wave-uniform test tells
+              // whether all of them fit the ring (two adjacent levels); if not, the
+              // solve is flagged and re-run, so none of them needs storing
+              if (!RING || base + total - head <= ring_cap) {
 #pragma unroll
-              for (int j = 0; j < K; ++j) {
-                if ((fresh_mask >> j) & 1u) {
-                  const uint32_t slot =
-                      base + off[j] +
-                      __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
-                  if (!RING) {
-                    ring[slot] = (uint16_t)vv[j];
-                  } else if (slot - head < ring_cap) {
-                    ring[slot & rmask] = (uint16_t)vv[j];
-                  } else {
-                    lost = true;  // two adjacent levels exceed the ring
+                for (int j = 0; j < K; ++j) {
+                  if ((fresh_mask >> j) & 1u) {
+                    const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                    ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
                   }
                 }
+              } else if ((int)lane == leader) {
+                ctl[4] = 1;  // two adjacent levels exceed the ring
               }
-              if (RING && __any(lost) && (int)lane == leader) ctl[4] = 1;
             }
 #ifdef OPENR_SPF_PROFILE
             OPENR_PROF_STAMP(t4);
