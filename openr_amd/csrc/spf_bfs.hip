@@ -311,10 +311,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #pragma unroll
             for (int j = 0; j < K; ++j)
               old[j] = atomicOr(tight[j] ? &st[S::word(vv[j])] : &dummy[lane], tight[j] ? xu << S::shift(vv[j]) : 0u);
-            uint32_t fresh_mask = 0;
+            bool fresh[K];  // this arrival appends v (kept as lane masks: ballots read them directly)
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-              fresh_mask |= (tight[j] && ((old[j] >> S::shift(vv[j])) & kCodeMask) == 0u) ? (1u << j) : 0u;
+              fresh[j] = tight[j] && ((old[j] >> S::shift(vv[j])) & kCodeMask) == 0u;
               if (trow && tight[j]) {
                 const uint32_t e = e0 + j * G;
                 atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             off[0] = 0;
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-              bj[j] = __ballot((fresh_mask >> j) & 1u);
+              bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
               off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
             }
             const uint32_t total = off[K];
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               if (!RING || base + total - head <= ring_cap) {
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                  if ((fresh_mask >> j) & 1u) {
+                  if (fresh[j]) {
                     const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
                                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
                     ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
@@ -378,6 +378,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         cnext = cnext == 3u ? 1u : cnext + 1u;
         if (RING && ctl[4]) {  // ring overflow; ctl[4] is uniform after the barrier
           overflow = true;
+          break;
+        }
+        if (tail == V) {
+          // every node is reached: no edge out of level [head, tail) can be tight (its
+          // heads are settled at levels <= L), so the level is only settled here
+          const uint64_t dT = (uint64_t)L * cost;
+          if (own_dist)
+            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dT;
           break;
         }
         if (!SLICED && a.target && a.dist_only) {

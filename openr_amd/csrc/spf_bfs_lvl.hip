@@ -330,7 +330,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
             // (2) addNextHops(nh(u)) + election of the appending arrival: K atomics in
             //     flight together; non-tight edges OR 0 into the lane's own dummy word
-            uint32_t fresh_mask = 0;
+            bool fresh[K];  // this arrival appends v (kept as lane masks: ballots read them directly)
             if constexpr (ELECT) {
               const uint32_t x = nhu.x;
               uint32_t old[K];
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 old[j] = atomicOr(tight[j] ? &nh[N::word(vv[j])] : &dummy[lane], tight[j] ? x << N::shift(vv[j]) : 0u);
 #pragma unroll
               for (int j = 0; j < K; ++j)
-                fresh_mask |= (tight[j] && ((old[j] >> N::shift(vv[j])) & N::kMask) == 0u) ? (1u << j) : 0u;
+                fresh[j] = tight[j] && ((old[j] >> N::shift(vv[j])) & N::kMask) == 0u;
             } else {
               uint32_t old[K];
 #pragma unroll
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 old[j] = atomicOr(tight[j] ? &vis[vv[j] >> 5] : &dummy[lane], tight[j] ? 1u << (vv[j] & 31u) : 0u);
 #pragma unroll
               for (int j = 0; j < K; ++j) {
-                fresh_mask |= (tight[j] && !((old[j] >> (vv[j] & 31u)) & 1u)) ? (1u << j) : 0u;
+                fresh[j] = tight[j] && !((old[j] >> (vv[j] & 31u)) & 1u);
                 if (tight[j]) N::or_val(nh, vv[j], nhu);
               }
             }
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             off[0] = 0;
 #pragma unroll
             for (int j = 0; j < K; ++j) {
-              bj[j] = __ballot((fresh_mask >> j) & 1u);
+              bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
               off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
             }
             const uint32_t total = off[K];
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               if (!RING || base + total - head <= ring_cap) {
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                  if ((fresh_mask >> j) & 1u) {
+                  if (fresh[j]) {
                     const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
                                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
                     ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
@@ -421,6 +421,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           overflow = true;
           break;
         }
+        // every node is reached: no edge out of level [head, tail) can be tight (its
+        // heads have levels <= L), and the level's levels / next hops are final
+        if (tail == V) break;
       }
       if (RING && overflow) {  // re-run by the full-order variant (from the list)
         if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = uid;
