@@ -238,6 +238,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         uint32_t* cnt = &ctl[L & 3u];
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
         const uint64_t dL = (uint64_t)L * cost;
+        if (!SLICED && a.target && a.dist_only) {
+          // pull test for the target (KSP2 second SPF): an unreached target with a usable
+          // edge to a level-L node (not a sink) lies on level L+1. A trace to it reads no
+          // node at its distance or farther (LinkState.cpp:398-419 walks tight in-edges),
+          // so level L is settled without expanding it and the solve ends.
+          const uint32_t t = a.target[sid];  // block-uniform
+          if (t < V && wave == 0) {
+            bool hit = false;
+            if ((S::field(st, t) & kCodeMask) == 0u) {
+              const uint2 rt = g.row2[t];
+              const uint32_t cL = level_code(L);
+              for (uint32_t e = rt.x + lane; e < rt.y; e += 64u) {
+                const uint4 rec = g.erec[e];  // t->u: {u | flags, ., link, .}
+                const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+                hit |= !(rec.x & (kEdgeDown | kNodeSink)) && !(has_ign && test_bit(ign, rec.z)) &&
+                       (S::field(st, u) & kCodeMask) == cL;
+              }
+            }
+            const bool any = __any(hit);
+            if (lane == 0) ctl[5] = any ? 1u : 0u;
+          }
+          lds_barrier();
+          if (t < V && ctl[5]) {
+            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dL;
+            if (tid == t % BLOCK) {  // the thread write_out reads t's field with
+              drow[t] = dL + cost;
+              atomicOr(&st[S::word(t)], cnext << S::shift(t));
+            }
+            break;
+          }
+        }
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
           if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
           OPENR_PROF_STAMP(t0);

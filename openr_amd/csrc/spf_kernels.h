@@ -90,9 +90,9 @@ struct SolveArgs {
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
   uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class)
-  // nullable, honoured by dist_only code-family solves: solve sid may stop at the level of
-  // target[sid]; nodes farther than the target then read UINT64_MAX (a KSP trace to the
-  // target only reads nodes no farther than it)
+  // nullable, honoured by dist_only code-family solves: solve sid may stop once the level
+  // of target[sid] is known; nodes at the target's distance or farther, other than the
+  // target, then read UINT64_MAX (a KSP trace to the target only reads nodes nearer)
   const uint32_t* target;
   // nullable: solve sid writes its dist / nh / tight rows at row out_row[sid] instead of
   // sid (openr_spf_refresh re-solves a scattered subset of resident rows in place; the
