@@ -239,34 +239,55 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
         const uint64_t dL = (uint64_t)L * cost;
         if (!SLICED && a.target && a.dist_only) {
-          // pull test for the target (KSP2 second SPF): an unreached target with a usable
-          // edge to a level-L node (not a sink) lies on level L+1. A trace to it reads no
-          // node at its distance or farther (LinkState.cpp:398-419 walks tight in-edges),
-          // so level L is settled without expanding it and the solve ends.
+          // pull tests for the target (KSP2 second SPF). A trace to the target walks tight
+          // in-edges (LinkState.cpp:398-419), so it reads only nodes on shortest paths to
+          // it; every other node may read UINT64_MAX. With the target unreached:
+          //  (1) a usable edge to a level-L node (not a sink) puts it on level L+1;
+          //  (2) else each unreached neighbour w (not a sink) with a usable edge to a
+          //      level-L node (not a sink) lies on level L+1, and then the target on L+2.
+          // Either way level L is settled without expanding it and the solve ends.
           const uint32_t t = a.target[sid];  // block-uniform
-          if (t < V && wave == 0) {
-            bool hit = false;
+          if (t < V) {
+            bool hit1 = false, hit2 = false;  // wave-uniform
             if ((S::field(st, t) & kCodeMask) == 0u) {
               const uint2 rt = g.row2[t];
               const uint32_t cL = level_code(L);
-              for (uint32_t e = rt.x + lane; e < rt.y; e += 64u) {
-                const uint4 rec = g.erec[e];  // t->u: {u | flags, ., link, .}
-                const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-                hit |= !(rec.x & (kEdgeDown | kNodeSink)) && !(has_ign && test_bit(ign, rec.z)) &&
-                       (S::field(st, u) & kCodeMask) == cL;
+              for (uint32_t i = rt.x + wave; i < rt.y; i += BLOCK / 64u) {
+                const uint4 rw = g.erec[i];  // t->w: {w | flags, ., link, .} (same for all lanes)
+                if ((rw.x & (kEdgeDown | kNodeSink)) || (has_ign && test_bit(ign, rw.z))) continue;
+                const uint32_t w = rw.x & ~(kEdgeDown | kNodeSink);
+                const uint32_t cw = S::field(st, w) & kCodeMask;
+                if (cw == cL) hit1 = true;
+                if (cw != 0u) continue;
+                const uint2 rr = g.row2[w];
+                bool q = false;
+                for (uint32_t e = rr.x + lane; e < rr.y; e += 64u) {
+                  const uint4 rx = g.erec[e];  // w->x
+                  const uint32_t x = rx.x & ~(kEdgeDown | kNodeSink);
+                  q |= !(rx.x & (kEdgeDown | kNodeSink)) && !(has_ign && test_bit(ign, rx.z)) &&
+                       (S::field(st, x) & kCodeMask) == cL;
+                }
+                if (__any(q)) {  // w lies on level L+1 (its code was 0, so no level-L test reads it)
+                  hit2 = true;
+                  if (lane == 0) {
+                    atomicOr(&st[S::word(w)], cnext << S::shift(w));
+                    drow[w] = dL + cost;
+                  }
+                }
               }
             }
-            const bool any = __any(hit);
-            if (lane == 0) ctl[5] = any ? 1u : 0u;
-          }
-          lds_barrier();
-          if (t < V && ctl[5]) {
-            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dL;
-            if (tid == t % BLOCK) {  // the thread write_out reads t's field with
-              drow[t] = dL + cost;
-              atomicOr(&st[S::word(t)], cnext << S::shift(t));
+            if (lane == 0 && (hit1 || hit2)) atomicOr(&ctl[5], hit1 ? 1u : 2u);  // zero until a hit
+            lds_barrier();
+            const uint32_t f = ctl[5];
+            if (f) {
+              for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dL;
+              if (tid == t % BLOCK) {  // the thread write_out reads t's field with
+                const bool near = (f & 1u) != 0u;
+                drow[t] = dL + (near ? cost : 2u * cost);
+                atomicOr(&st[S::word(t)], (near ? cnext : level_code(L + 2u)) << S::shift(t));
+              }
+              break;
             }
-            break;
           }
         }
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
