@@ -551,7 +551,7 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r01e/pmc_traffic_<topology>.json")
+                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r01f/pmc_traffic_<topology>.json")
     ap.add_argument("--ksp-sources", type=int, default=0,
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
@@ -659,7 +659,7 @@ def main():
     achieved = bytes_launch / mean_kernel_s / 1e9 if mean_kernel_s > 0 else 0.0
     traffic = None
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r01e", f"pmc_traffic_{args.topology}.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r01f", f"pmc_traffic_{args.topology}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
