@@ -95,7 +95,7 @@ __host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has
 // expanded) and the next-hop bytes of every node, coalesced. Sliced classes: slice s
 // owns next-hop bytes [3s, 3s + 3); slice 0 also zero-fills the bytes past the last
 // slice.
-template <int FB, int BLOCK, bool SLICED>
+template <int FB, int BLOCK, bool SLICED, bool GENERIC>
 __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
                                           const uint32_t* st, bool nt) {
   using S = State<FB>;
@@ -103,6 +103,12 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
   uint64_t* drow = a.dist + out_row_of(a, sid) * V;
   const uint32_t nb = a.nh_bytes;
   uint8_t* nrow = a.nh ? a.nh + out_row_of(a, sid) * V * nb : nullptr;
+  if (GENERIC && a.lvl16) {  // u16 level row (dist-only, never sliced)
+    uint16_t* lrow = a.lvl16 + out_row_of(a, sid) * V;
+    for (uint32_t v = tid; v < V; v += BLOCK)
+      if ((S::field(st, v) & kCodeMask) == 0u) lrow[v] = 0xFFFFu;
+    return;
+  }
   if (!SLICED || slice == 0)
     for (uint32_t v = tid; v < V; v += BLOCK)
       if ((S::field(st, v) & kCodeMask) == 0u) drow[v] = ~0ull;
@@ -186,6 +192,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       OPENR_PROF_STAMP(t0);
       const bool own_dist = !SLICED || slice == 0;
       uint64_t* drow = a.dist + out_row_of(a, sid) * V;
+      uint16_t* lrow = (GENERIC && a.lvl16) ? a.lvl16 + out_row_of(a, sid) * V : nullptr;
+      // settle node u on level l (distance l * cost): u64 distance or u16 level row
+      auto put = [&](uint32_t u, uint32_t l) {
+        if (GENERIC && lrow) lrow[u] = (uint16_t)l;
+        else drow[u] = (uint64_t)l * cost;
+      };
       for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
       if (has_ign)
         for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
@@ -194,7 +206,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
         atomicOr(&st[S::word(src)], level_code(0) << S::shift(src));
-        if (own_dist) drow[src] = 0;
+        if (own_dist) put(src, 0u);
       }
       __syncthreads();
       uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
@@ -271,7 +283,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                   hit2 = true;
                   if (lane == 0) {
                     atomicOr(&st[S::word(w)], cnext << S::shift(w));
-                    drow[w] = dL + cost;
+                    put(w, L + 1u);
                   }
                 }
               }
@@ -280,10 +292,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             lds_barrier();
             const uint32_t f = ctl[5];
             if (f) {
-              for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dL;
+              for (uint32_t i = head + tid; i < tail; i += BLOCK) put(ring[RING ? (i & rmask) : i], L);
               if (tid == t % BLOCK) {  // the thread write_out reads t's field with
                 const bool near = (f & 1u) != 0u;
-                drow[t] = dL + (near ? cost : 2u * cost);
+                put(t, near ? L + 1u : L + 2u);
                 atomicOr(&st[S::word(t)], (near ? cnext : level_code(L + 2u)) << S::shift(t));
               }
               break;
@@ -311,7 +323,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
               if (ELLM == 1) ell = g.ellt[u];
             }
             if (lane_g == 0) {
-              if (own_dist) drow[u] = dL;  // u settled on level L
+              if (own_dist) {  // u settled on level L
+                if (GENERIC && lrow) lrow[u] = (uint16_t)L;
+                else drow[u] = dL;
+              }
               if (sink) atomicOr(&st[S::word(u)], kCodeSettledSink << S::shift(u));
             }
           }
@@ -435,9 +450,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
         if (tail == V) {
           // every node is reached: no edge out of level [head, tail) can be tight (its
           // heads are settled at levels <= L), so the level is only settled here
-          const uint64_t dT = (uint64_t)L * cost;
           if (own_dist)
-            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dT;
+            for (uint32_t i = head + tid; i < tail; i += BLOCK) put(ring[RING ? (i & rmask) : i], L);
           break;
         }
         if (!SLICED && a.target && a.dist_only) {
@@ -445,8 +459,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           // target's level [head, tail) gets its distances here instead of on expansion
           const uint32_t t = a.target[sid];
           if (t < V && (S::field(st, t) & kCodeMask) != 0u) {
-            const uint64_t dT = (uint64_t)L * cost;
-            for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[RING ? (i & rmask) : i]] = dT;
+            for (uint32_t i = head + tid; i < tail; i += BLOCK) put(ring[RING ? (i & rmask) : i], L);
             break;
           }
         }
@@ -457,7 +470,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t0);
 #endif
-        write_out<FB, BLOCK, SLICED>(a, sid, slice, V, st, nt != 0);
+        write_out<FB, BLOCK, SLICED, GENERIC>(a, sid, slice, V, st, nt != 0);
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t1);
         OPENR_PROF_ADD(6, t0, t1);

@@ -82,6 +82,7 @@ struct Device {
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
+  DevBuf<uint16_t> krows16;  // KSP2 second SPFs on the code family: u16 level rows
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
@@ -513,9 +514,13 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
   const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
+  // uniform-cost second SPFs on the code family are distance-only: u16 level rows
+  const bool rows16 = ign_plan.bfs && ign_plan.family == kFamCode;
+  const size_t row_bytes = (size_t)V * (rows16 ? 2u : 8u);
   const uint32_t chunk =
-      (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / ((size_t)V * 8u + 4u * ign_cap)));
-  OPENR_TRY(d.krows.reserve((size_t)chunk * V));
+      (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / (row_bytes + 4u * ign_cap)));
+  if (rows16) OPENR_TRY(d.krows16.reserve((size_t)chunk * V));
+  else OPENR_TRY(d.krows.reserve((size_t)chunk * V));
   OPENR_TRY(d.kign.reserve((size_t)chunk * ign_cap));
   OPENR_TRY(d.kend.reserve(chunk));
   OPENR_TRY(d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V));
@@ -552,18 +557,21 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, kend[k])
     b.ign_end = d.kend.p;
     b.ign_links = d.kign.p;
-    b.dist = d.krows.p;
+    b.dist = rows16 ? nullptr : d.krows.p;
+    b.lvl16 = rows16 ? d.krows16.p : nullptr;
     b.nh_bits = ctx->nh_bits;
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
     b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
     OPENR_TRY(launch(ctx, d, ign_plan, b, s));
-    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, nullptr,
-                               nullptr, rlist2, rcount + 1, wctr + 2));
-    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, d.krows.p, d.kign.p, d.kend.p, ign_cap,
-                               d_tok2, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, rlist2,
-                               rcount + 1, nullptr, nullptr, wctr + 3));
+    const uint64_t* r2 = rows16 ? nullptr : d.krows.p;
+    const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
+                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, nullptr, nullptr,
+                               rlist2, rcount + 1, wctr + 2, r16, ign_plan.cost));
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
+                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, rlist2,
+                               rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.cost));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);
@@ -668,7 +676,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
-                     d.kbase.p,     d.krows.p,      d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
+                     d.kbase.p,     d.krows.p,      d.krows16.p, d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);

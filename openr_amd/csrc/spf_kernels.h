@@ -94,6 +94,10 @@ struct SolveArgs {
   // of target[sid] is known; nodes at the target's distance or farther, other than the
   // target, then read UINT64_MAX (a KSP trace to the target only reads nodes nearer)
   const uint32_t* target;
+  // nullable, dist_only code-family solves (GENERIC kernels) only: write u16 level rows
+  // [n][V] here instead of u64 distance rows (0xFFFF = unreached; dist = level * cost;
+  // levels stay below V <= 65535). KSP2 second SPFs: 4x fewer bytes per pair row.
+  uint16_t* lvl16;
   // nullable: solve sid writes its dist / nh / tight rows at row out_row[sid] instead of
   // sid (openr_spf_refresh re-solves a scattered subset of resident rows in place; the
   // launcher then leaves zeroing those tight rows to the caller)
@@ -217,7 +221,9 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats = nullptr,
                             const uint32_t* list = nullptr, const uint32_t* list_count = nullptr,
                             uint32_t* retry_list = nullptr, uint32_t* retry_count = nullptr,
-                            uint32_t* work_ctr = nullptr);  // zeroed dynamic-scheduling counter (required)
+                            uint32_t* work_ctr = nullptr,  // zeroed dynamic-scheduling counter (required)
+                            const uint16_t* rows16 = nullptr,  // kind 2: u16 level rows (SolveArgs::lvl16)
+                            uint64_t lcost = 0);               // instead of `rows`; dist = level * lcost
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);

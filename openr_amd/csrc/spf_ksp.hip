@@ -108,6 +108,8 @@ struct KspState {
   uint64_t* stats;  // LDS counters (lane 0 updates), null unless enabled
   const uint16_t* d16;  // LDS copy of drow saturated at 0xFFFF, valid when use16
   bool use16;
+  const uint16_t* l16;  // non-null: the pair's row is u16 levels (0xFFFF unreached), dist = level * lcost
+  uint64_t lcost;
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -117,6 +119,10 @@ __device__ __forceinline__ uint64_t dist_of(const KspState& st, uint32_t u) {
   if (st.use16) {
     const uint32_t d = st.d16[u];
     return d == 0xFFFFu ? kNoKey : (uint64_t)d;
+  }
+  if (st.l16) {
+    const uint32_t l = st.l16[u];
+    return l == 0xFFFFu ? kNoKey : (uint64_t)l * st.lcost;
   }
   return st.drow[u];
 }
@@ -483,7 +489,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t use_d16, unsigned long long* gstats,
                                                           uint32_t frames, uint32_t arena, const uint32_t* list,
                                                           const uint32_t* list_count, uint32_t* retry_list,
-                                                          uint32_t* retry_count, uint32_t* work_ctr) {
+                                                          uint32_t* retry_count, uint32_t* work_ctr,
+                                                          const uint16_t* rows16, uint64_t lcost) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, use_d16 != 0);
@@ -528,9 +535,11 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     const uint32_t src = sources[row], dst = pdst[pair];
     st.src = src;
     st.drow = rows + (size_t)(KIND == 1 ? row : k) * V;
+    st.l16 = (KIND == 2 && rows16) ? rows16 + (size_t)k * V : nullptr;
+    st.lcost = lcost;
     st.use16 = false;
-    const uint64_t ddst = dst < V ? st.drow[dst] : kNoKey;
-    if (d16 && ddst < 0xFFFFull) {
+    const uint64_t ddst = dst < V ? dist_of(st, dst) : kNoKey;
+    if (d16 && !st.l16 && ddst < 0xFFFFull) {
       if (KIND == 2 || row != d16_row) copy_row16(d16, st.drow, V);
       d16_row = KIND == 1 ? row : UINT32_MAX;
       st.use16 = true;
@@ -665,7 +674,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
                             const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
-                            uint32_t* retry_count, uint32_t* work_ctr) {
+                            uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost) {
   if (!n) return hipSuccess;
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
@@ -681,7 +690,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
                      bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16() ? 1u : 0u,
-                     stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr);
+                     stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
+                     lcost);
   return hipGetLastError();
 }
 
