@@ -499,6 +499,29 @@ def test_ksp2_device_fabric_sample(eng, ksp_probe):
     assert any(len(k1) > 1 for k1, _ in got)  # ECMP: several edge-disjoint first paths
 
 
+def fabric_with_faults(seed, n_ovl=12, n_down=60):
+    """The fabric with overloaded switches (sinks) and down links."""
+    g = T.fabric(288 + 56)
+    rng = np.random.default_rng(seed)
+    nodes = rng.choice(g.num_nodes, n_ovl, replace=False)
+    links = rng.choice(g.num_links, n_down, replace=False)
+    return g.patched([], [], links, [0] * len(links), nodes, [1] * len(nodes)), nodes
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_fabric_faults_all_sources_and_ksp2(eng, seed):
+    """Last-level skip (every node reached) and the KSP2 second SPF's target pull tests
+    next to sinks and down links: all-sources rows and traced paths vs the oracle,
+    with pairs whose target neighbours an overloaded switch."""
+    g, ovl = fabric_with_faults(seed)
+    rng = np.random.default_rng(100 + seed)
+    check_against_oracle(eng, g, rng.integers(0, g.num_nodes, 96).tolist() + [int(x) for x in ovl[:4]])
+    nbrs = [int(g.col[e]) for x in ovl[:6] for e in range(g.row_ptr[x], g.row_ptr[x + 1])][::7]
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (160, 2))]
+    pairs += [(int(rng.integers(0, g.num_nodes)), d) for d in nbrs] + [(int(s), (int(s) + 1) % g.num_nodes) for s in ovl[:6]]
+    check_ksp2_against_oracle(eng, g, pairs)
+
+
 @pytest.mark.parametrize("seed", [0, 1])
 def test_distance_only_solves(eng, seed):
     """No next-hop output: the code family solves every source in one 8-bit-field class
