@@ -546,10 +546,10 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst, nullptr, nullptr, rlist1,
-                               rcount, wctr));
+                               rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u));
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst, rlist1, rcount, nullptr,
-                               nullptr, wctr + 1));
+                               nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u));
     OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, s));
     SolveArgs b{};
     b.sources = d.ksrc.p;
@@ -568,10 +568,10 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, nullptr, nullptr,
-                               rlist2, rcount + 1, wctr + 2, r16, ign_plan.cost));
+                               rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, rlist2,
-                               rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.cost));
+                               rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);

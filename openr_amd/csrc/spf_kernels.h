@@ -223,7 +223,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* retry_list = nullptr, uint32_t* retry_count = nullptr,
                             uint32_t* work_ctr = nullptr,  // zeroed dynamic-scheduling counter (required)
                             const uint16_t* rows16 = nullptr,  // kind 2: u16 level rows (SolveArgs::lvl16)
-                            uint64_t lcost = 0);               // instead of `rows`; dist = level * lcost
+                            uint64_t lcost = 0);  // instead of `rows`: dist = level * lcost; non-zero lcost
+                                                  // also marks a uniform-cost graph (rank by name / edge)
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);

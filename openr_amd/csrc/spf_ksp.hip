@@ -109,7 +109,7 @@ struct KspState {
   const uint16_t* d16;  // LDS copy of drow saturated at 0xFFFF, valid when use16
   bool use16;
   const uint16_t* l16;  // non-null: the pair's row is u16 levels (0xFFFF unreached), dist = level * lcost
-  uint64_t lcost;
+  uint64_t lcost;       // non-zero: every usable edge costs lcost (uniform-cost graph)
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -195,7 +195,17 @@ __device__ __forceinline__ uint32_t key_less(uint64_t od, uint64_t orr, const Pa
 
 // rank of c.kd/kr among the candidates of ballot m held by (kd, kr) registers
 __device__ __forceinline__ void rank_against(uint64_t m, const PathCand& src, const PathCand& a, const PathCand& b,
-                                             uint32_t& ra, uint32_t& rb) {
+                                             uint32_t& ra, uint32_t& rb, bool kr_only) {
+  if (kr_only) {  // uniform cost: every candidate has dist[u] = dist[v] - cost, so kd ties
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const uint64_t orr = readlane64(src.kr, j);
+      ra += orr < a.kr ? 1u : 0u;
+      rb += orr < b.kr ? 1u : 0u;
+    }
+    return;
+  }
   while (m) {
     const uint32_t j = (uint32_t)__builtin_ctzll(m);
     m &= m - 1;
@@ -220,8 +230,8 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
   const uint32_t cnt = (uint32_t)(__popcll(m0) + __popcll(m1));
   if (beg + cnt > st.arena_cap) return UINT32_MAX;
   uint32_t r0 = 0, r1 = 0;
-  rank_against(m0, c0, c0, c1, r0, r1);
-  rank_against(m1, c1, c0, c1, r0, r1);
+  rank_against(m0, c0, c0, c1, r0, r1, st.lcost != 0u);
+  rank_against(m1, c1, c0, c1, r0, r1, st.lcost != 0u);
   if (c0.ok) {
     st.ar_e[beg + r0] = (uint32_t)c0.kr;
     st.ar_l[beg + r0] = c0.link;
