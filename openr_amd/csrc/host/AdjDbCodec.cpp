@@ -528,7 +528,7 @@ AdjPublicationResult applyAdjacencyPublication(LinkState& linkState,
       throw std::invalid_argument("adj key " + keyVals[idx[j]].first + " carries node " + dbs[j].thisNodeName);
     }
     dbs[j].area = linkState.getArea();  // Decision.cpp:1762
-    const auto change = linkState.updateAdjacencyDatabase(dbs[j], 0, 0);
+    const auto change = linkState.updateAdjacencyDatabase(std::move(dbs[j]), 0, 0);
     res.topologyChanged |= change.topologyChanged;
     res.linkAttributesChanged |= change.linkAttributesChanged;
     res.nodeLabelChanged |= change.nodeLabelChanged;

@@ -395,12 +395,20 @@ std::vector<std::shared_ptr<Link>> LinkState::getOrderedLinkSet(const thrift::Ad
 LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyDatabase const& newDb,
                                                               LinkStateMetric holdUpTtl,
                                                               LinkStateMetric holdDownTtl) {
+  return updateAdjacencyDatabase(thrift::AdjacencyDatabase(newDb), holdUpTtl, holdDownTtl);
+}
+
+LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyDatabase&& db,
+                                                              LinkStateMetric holdUpTtl,
+                                                              LinkStateMetric holdDownTtl) {
   LinkStateChange change;
-  const std::string nodeName = newDb.thisNodeName;
+  const std::string nodeName = db.thisNodeName;
   markMirrorDirty();
 
-  thrift::AdjacencyDatabase prior(std::move(adjacencyDatabases_[nodeName]));
-  adjacencyDatabases_[nodeName] = newDb;
+  thrift::AdjacencyDatabase& stored = adjacencyDatabases_[nodeName];
+  thrift::AdjacencyDatabase prior(std::move(stored));
+  stored = std::move(db);
+  const thrift::AdjacencyDatabase& newDb = stored;
   indexAdjacencies(nodeName);
 
   // both sides ordered by <hash, names> so one merge pass finds adds/removes/updates

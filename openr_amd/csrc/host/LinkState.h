@@ -275,6 +275,9 @@ class LinkState {
   LinkStateChange decrementHolds();
   LinkStateChange updateAdjacencyDatabase(thrift::AdjacencyDatabase const& adjacencyDb,
                                           LinkStateMetric holdUpTtl = 0, LinkStateMetric holdDownTtl = 0);
+  // same, taking ownership of a database the caller no longer needs (bulk loads: no copy)
+  LinkStateChange updateAdjacencyDatabase(thrift::AdjacencyDatabase&& adjacencyDb, LinkStateMetric holdUpTtl = 0,
+                                          LinkStateMetric holdDownTtl = 0);
   LinkStateChange deleteAdjacencyDatabase(const std::string& nodeName);
 
   std::optional<LinkStateMetric> getMetricFromAToB(std::string const& a, std::string const& b,

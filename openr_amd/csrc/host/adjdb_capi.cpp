@@ -208,7 +208,7 @@ int openr_adjdb_build_graph(const openr_adjdb_batch* b, const char* area, openr_
     for (const auto& db : b->dbs) {
       openr::thrift::AdjacencyDatabase stamped = db;
       stamped.area = area;
-      g->linkState->updateAdjacencyDatabase(stamped, 0, 0);
+      g->linkState->updateAdjacencyDatabase(std::move(stamped), 0, 0);
     }
     g->mirror = &g->linkState->csrMirror();
     *out = g.release();

@@ -253,6 +253,16 @@ TEST_CPU(AdjDbCodec_PublicationMatchesDirectUpdates) {
   EXPECT_TRUE(a.metric == b.metric);
   EXPECT_TRUE(a.edgeUp == b.edgeUp);
   EXPECT_TRUE(a.overloaded == b.overloaded);
+  // a re-advertisement moved in (bulk path) reports and applies the same change as a copy
+  auto db1b = db1;
+  db1b.adjacencies[0].metric = 9;
+  db1b.nodeLabel = 77;
+  const auto cd = direct.updateAdjacencyDatabase(db1b, 0, 0);
+  const auto cb = bulk.updateAdjacencyDatabase(thrift::AdjacencyDatabase(db1b), 0, 0);
+  EXPECT_TRUE(cd.topologyChanged && cb.topologyChanged);
+  EXPECT_TRUE(cd.nodeLabelChanged && cb.nodeLabelChanged);
+  EXPECT_TRUE(direct.csrMirror().metric == bulk.csrMirror().metric);
+  EXPECT_EQ(bulk.getAdjacencyDatabases().at(n1).nodeLabel, 77);
   // decoded struct equals the original, perf events included
   auto rt = serializer::readAdjacencyDatabase(serializer::writeAdjacencyDatabase(db1));
   EXPECT_TRUE(rt.perfEvents.has_value() && rt.perfEvents->events.size() == 1 &&
