@@ -559,6 +559,15 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   m.nameRank.resize(V);
   for (uint32_t i = 0; i < V; ++i) m.nameRank[i] = i;
   std::unordered_map<const Link*, uint32_t> linkIds;
+  // every link appears in the rows of its two ends: size the columns once
+  const size_t maxE = 2 * allLinks_.size();
+  linkIds.reserve(allLinks_.size());
+  m.links.reserve(allLinks_.size());
+  m.col.reserve(maxE);
+  m.metric.reserve(maxE);
+  m.linkId.reserve(maxE);
+  m.edgeUp.reserve(maxE);
+  m.edgeOwner.reserve(maxE);
   m.rowPtr.assign(V + 1, 0);
   m.overloaded.assign(V, 0);
   for (uint32_t u = 0; u < V; ++u) {
