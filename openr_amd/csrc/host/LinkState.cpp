@@ -555,6 +555,7 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
     if (!adjacencyDatabases_.count(kv.first)) m.names.push_back(kv.first);
   std::sort(m.names.begin(), m.names.end());
   const uint32_t V = (uint32_t)m.names.size();
+  m.id.reserve(V);  // lookup-only: bucket count is not observable
   for (uint32_t i = 0; i < V; ++i) m.id.emplace(m.names[i], i);
   m.nameRank.resize(V);
   for (uint32_t i = 0; i < V; ++i) m.nameRank[i] = i;
