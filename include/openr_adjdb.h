@@ -30,6 +30,10 @@ typedef struct openr_adjdb_graph openr_adjdb_graph;
 
 const char* openr_adjdb_last_error(void);
 
+/* Build id of libopenr_decision.so: "<sha256/16 of its sources> <source files>"
+ * (Makefile build_id; checked against the tree by openr_amd/provenance.py). */
+const char* openr_decision_build_id(void);
+
 /* Decode n compact-protocol AdjacencyDatabase values. Value i is
  * data[offsets[i] .. offsets[i+1]) (offsets has n+1 entries). n_threads = 0 uses
  * every hardware thread. A malformed value fails the whole call (EBADMSG, message

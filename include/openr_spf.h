@@ -113,6 +113,9 @@ typedef struct {
 } openr_spf_stats_t;
 
 int openr_spf_abi_version(void);
+/* "<sha256/16 of the engine sources> <source files>" (Makefile build_id): lets the host
+   verify the library was built from the sources it ships with. */
+const char* openr_spf_build_id(void);
 const char* openr_spf_last_error(void);
 void openr_spf_limits(openr_spf_limits_t* out);
 

@@ -16,6 +16,7 @@ from typing import Dict, List, Sequence
 
 import numpy as np
 
+from .provenance import check_build_id
 from .topology import CsrGraph
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +72,10 @@ def load_library():
     l.openr_adjdb_graph_free.restype = None
     l.openr_adjdb_graph_info.argtypes = [vp, P(GraphInfo)]
     l.openr_adjdb_graph_export.argtypes = [vp] + [vp] * 9
+    l.openr_topogen_wan.argtypes = [u32, u32, u32, u64, u32, vp, vp, vp]
+    l.openr_topogen_wan.restype = ctypes.c_int
+    l.openr_decision_build_id.restype = ctypes.c_char_p
+    check_build_id(l.openr_decision_build_id().decode(), LIB_PATH)
     _lib = l
     return l
 

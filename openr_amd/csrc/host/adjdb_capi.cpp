@@ -43,7 +43,13 @@ int guarded(F&& f) {
 }
 }  // namespace
 
+#ifndef OPENR_DECISION_BUILD_ID
+#define OPENR_DECISION_BUILD_ID "unknown"
+#endif
+
 extern "C" {
+
+const char* openr_decision_build_id(void) { return OPENR_DECISION_BUILD_ID; }
 
 const char* openr_adjdb_last_error(void) { return g_error.c_str(); }
 

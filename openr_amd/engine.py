@@ -12,6 +12,8 @@ from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
+from .provenance import check_build_id
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libopenr_spf.so")
 
@@ -23,6 +25,7 @@ OK, EIO, ENOMEM, ENODEV, EINVAL, E2BIG, ENOTSUP = 0, -5, -12, -19, -22, -7, -95
 # Exported symbols of include/openr_spf.h (checked by tests/test_capi_symbols.py).
 EXPORTS = (
     "openr_spf_abi_version",
+    "openr_spf_build_id",
     "openr_spf_last_error",
     "openr_spf_limits",
     "openr_spf_create",
@@ -107,6 +110,8 @@ def load_library():
     l = ctypes.CDLL(LIB_PATH)
     vp, u32, P = ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER
     l.openr_spf_abi_version.restype = ctypes.c_int
+    l.openr_spf_build_id.restype = ctypes.c_char_p
+    check_build_id(l.openr_spf_build_id().decode(), LIB_PATH)
     l.openr_spf_last_error.restype = ctypes.c_char_p
     l.openr_spf_limits.argtypes = [P(SpfLimits)]
     l.openr_spf_limits.restype = None
@@ -128,7 +133,7 @@ def load_library():
     l.openr_spf_refresh_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, u32, vp, vp, P(u32)]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
     for name in EXPORTS:
-        if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy"):
+        if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy", "openr_spf_build_id"):
             getattr(l, name).restype = ctypes.c_int
     _lib = l
     return l

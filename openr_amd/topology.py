@@ -401,49 +401,28 @@ def _csr_from_adjacency_lists(names: List[str], adj: List[List[int]], metric=Non
     )
 
 
-class SplitMix64:
-    """Deterministic 64-bit generator for the WAN topology.
-
-    The WAN topology is new (not in the reference), so its RNG is ours:
-    splitmix64 (Steele et al. 2014), identical on every host.
-    """
-
-    def __init__(self, seed: int) -> None:
-        self.s = seed & 0xFFFFFFFFFFFFFFFF
-
-    def next(self) -> int:
-        self.s = (self.s + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
-        z = self.s
-        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
-        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
-        return z ^ (z >> 31)
-
-
 def wan(num_nodes: int = 1000, num_links: int = 3000, max_metric: int = 64, seed: int = 1,
         parallel_fraction: float = 0.0) -> CsrGraph:
-    """WAN-like topology: ring + uniform random chords, asymmetric metrics
-    1 + rng % max_metric per direction; optional parallel links."""
-    rng = SplitMix64(seed)
-    names = [f"wan{i}" for i in range(num_nodes)]
-    links: List[Tuple[int, int]] = [(i, (i + 1) % num_nodes) for i in range(num_nodes)]
-    seen = {tuple(sorted(l)) for l in links}
-    while len(links) < num_links:
-        a = rng.next() % num_nodes
-        b = rng.next() % num_nodes
-        if a == b:
-            continue
-        key = (min(a, b), max(a, b))
-        if key in seen:
-            continue
-        seen.add(key)
-        links.append((int(a), int(b)))
+    """WAN-like topology of BASELINE config 4: ring +
+    uniform random chords, asymmetric metrics 1 + rng() % max_metric per direction,
+    optional parallel links. The links and metrics come from the C++ generator
+    (openr_topogen_wan, std::mt19937_64(seed), include/openr_topogen.h); only the CSR
+    packing happens here."""
+    from openr_amd import adjdb
+
+    lib = adjdb.load_library()
     npar = int(parallel_fraction * num_links)
-    for i in range(npar):
-        links.append(links[rng.next() % num_links])
-    L = len(links)
-    m_uv = np.array([1 + rng.next() % max_metric for _ in range(L)], dtype=np.uint64)
-    m_vu = np.array([1 + rng.next() % max_metric for _ in range(L)], dtype=np.uint64)
-    return csr_from_links(names, np.array(links, dtype=np.int64), m_uv, m_vu)
+    L = num_links + npar
+    ends = np.zeros(2 * L, dtype=np.uint32)
+    m_uv = np.zeros(L, dtype=np.uint32)
+    m_vu = np.zeros(L, dtype=np.uint32)
+    rc = lib.openr_topogen_wan(num_nodes, num_links, max_metric, seed, npar, ends.ctypes.data, m_uv.ctypes.data,
+                               m_vu.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"openr_topogen_wan({num_nodes}, {num_links}, {max_metric}) failed: {rc}")
+    names = [f"wan{i}" for i in range(num_nodes)]
+    return csr_from_links(names, ends.reshape(-1, 2).astype(np.int64), m_uv.astype(np.uint64),
+                          m_vu.astype(np.uint64))
 
 
 def grid_fast(n: int) -> CsrGraph:

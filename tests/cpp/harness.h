@@ -53,9 +53,21 @@ struct Reg {
   static void name()
 
 
-inline int run_tests(int argc, char** argv) {
+#ifndef OPENR_TEST_BUILD_ID
+#define OPENR_TEST_BUILD_ID "unknown"
+#endif
 
+// extern "C" so the test binaries can read the libraries' build ids without the headers
+extern "C" const char* openr_spf_build_id(void);
+extern "C" const char* openr_decision_build_id(void);
+
+inline int run_tests(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "cpu";
+  // provenance (Makefile build_id): this binary's sources and the libraries it loaded
+  std::printf("build-id: %s\n", OPENR_TEST_BUILD_ID);
+  std::printf("engine-build-id: %s\n", openr_spf_build_id());
+  std::printf("host-build-id: %s\n", openr_decision_build_id());
+  if (mode == "build-id") return 0;
   int ran = 0;
   for (auto const& t : registry()) {
     if (t.gpu != (mode == "gpu") && mode != "all") continue;

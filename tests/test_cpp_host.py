@@ -9,6 +9,8 @@ import subprocess
 
 import pytest
 
+from openr_amd.provenance import check_build_id
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tests", "cpp", "build", "linkstate_test")
 DEC_BIN = os.path.join(ROOT, "tests", "cpp", "build", "decision_test")
@@ -20,6 +22,11 @@ def run(group, binary=BIN):
     print(p.stdout)
     print(p.stderr)
     assert p.returncode == 0, p.stdout + p.stderr
+    # provenance: the binary and the libraries it loaded were built from this tree
+    for key in ("build-id: ", "engine-build-id: ", "host-build-id: "):
+        line = [l for l in p.stdout.splitlines() if l.startswith(key)]
+        assert line, key
+        check_build_id(line[0][len(key):], f"{os.path.basename(binary)} {key.strip(': ')}")
     return p.stdout
 
 
