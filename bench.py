@@ -120,9 +120,9 @@ def whatif_cpu_baseline(g, seconds: float, use_metric: bool):
 def whatif_main(args):
     """BASELINE config 4: per-link-failure what-if sweep on the 1k-node WAN topology
     (heterogeneous metrics U[1,64]); a step = every (failed link, source) unit, one
-    openr_spf_whatif_device call (base SPF, affected-unit filter, chunked solves,
-    row comparison). Per rank: its contiguous block of links (shard.py), weak scaling
-    is one WAN per GPU like the all-sources bench."""
+    openr_spf_whatif_device call (base SPF, affected-unit filter, incremental repairs,
+    row comparison). Strong scaling: rank r takes the contiguous block
+    shard_range(L, r, N) of the links (shard.py), no collective on the data path."""
     import torch
     import torch.distributed as dist
 
@@ -142,15 +142,19 @@ def whatif_main(args):
     eng = SpfEngine([local_rank])
     eng.set_graph(g)
     use_metric = not args.no_metric
-    links = torch.arange(0, L, dtype=torch.int32, device=dev)
+    from openr_amd.shard import shard_range
+
+    llo, lhi = shard_range(L, rank, world)  # strong: the ranks split ONE WAN's links
+    n_links = lhi - llo
+    links = torch.arange(llo, lhi, dtype=torch.int32, device=dev)
     srcs = torch.arange(0, V, dtype=torch.int32, device=dev)
-    changed = torch.empty((L, V), dtype=torch.int32, device=dev)
+    changed = torch.empty((max(n_links, 1), V), dtype=torch.int32, device=dev)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     solved = [0]
 
     def step():
-        solved[0] = eng.whatif_device(links.data_ptr(), L, srcs.data_ptr(), V, changed.data_ptr(), use_metric,
+        solved[0] = eng.whatif_device(links.data_ptr(), n_links, srcs.data_ptr(), V, changed.data_ptr(), use_metric,
                                       stream=stream.cuda_stream)
 
     def barrier():
@@ -167,7 +171,7 @@ def whatif_main(args):
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     units = L * V
-    value = units * world * args.steps / elapsed
+    value = units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     srcs_np = np.arange(V)
     per_src = algorithmic_bytes(g, srcs_np) / V  # mean B(src)
@@ -189,11 +193,11 @@ def whatif_main(args):
         out = {
             "metric": "per-link-failure what-if SPF units/sec (link x source), 1k-node WAN, U[1,64] metrics",
             "value": value, "unit": "units/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "u64", "data": "synthetic (seeded WAN generator, SURVEY.md Appendix B)",
             "config": dict(cfg, workload="wan1k-whatif-all-links-x-all-sources", units_per_step=units,
                            spf_solved_per_step=solved[0], use_link_metric=use_metric,
-                           parallelism=f"area-per-GPU x{world}"),
+                           parallelism=f"link-sharded x{world}"),
             "solved_per_s": solved[0] * world * args.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -539,6 +543,24 @@ def adjdb_main(args):
     eng.close()
 
 
+def relaunch_distributed(n: int) -> int:
+    """`bench.py --gpus N` started without torch.distributed.run: launch N ranks (one
+    process per GPU) under torch.distributed.run as a CHILD process and return its exit
+    code. This process never touches the GPU (no HIP call before or after), so no exec
+    of an initialised process happens (the box forbids it)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -549,9 +571,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default, BASELINE config 3): the V sources of ONE topology are split over the "
+                         "ranks and the result shards all-gathered over RCCL; weak: every rank solves its own "
+                         "full all-sources replica (one OpenR area per GPU)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r01f/pmc_traffic_<topology>.json")
+                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r02/pmc_traffic_<topology>.json")
     ap.add_argument("--ksp-sources", type=int, default=0,
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
@@ -560,6 +585,11 @@ def main():
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
                          "(BASELINE config 4)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch_distributed(args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_env}")
     if args.workload == "whatif":
         return whatif_main(args)
     if args.workload == "ksp2":
@@ -568,7 +598,17 @@ def main():
         return update_main(args)
     if args.workload == "adjdb":
         return adjdb_main(args)
+    return all_sources_main(args)
 
+
+def all_sources_main(args):
+    """BASELINE config 3 (default; config 2 with --topology fabric): all-sources SPF.
+
+    strong: rank r solves the contiguous source block shard_range(V, r, N) of the one
+    topology (no collective on the data path); `value` = V solves per step / the slowest
+    rank's step time. The RCCL all-gather of the dist / next-hop shards (the exchange
+    step of config 3) is timed in a second loop of K (solve + all-gather) steps and
+    reported as gather.gather_inclusive_value / ms_per_step."""
     import torch
     import torch.distributed as dist
 
@@ -577,11 +617,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     from openr_amd.engine import SpfEngine
+    from openr_amd.shard import max_over_ranks, shard_range
 
     g, cfg = build_topology(args.topology)
     V = g.num_nodes
@@ -589,15 +631,13 @@ def main():
     eng.set_graph(g)
     nb = eng.nh_bytes
     use_metric = not args.no_metric
+    strong = args.scaling == "strong"
 
-    # contiguous source blocks per rank (shard.py semantics)
-    from openr_amd.shard import shard_range
-
-    lo, hi = shard_range(V, rank, world) if args.scaling == "strong" else (0, V)
+    lo, hi = shard_range(V, rank, world) if strong else (0, V)
     n_local = hi - lo
     src = torch.arange(lo, hi, dtype=torch.int32, device=dev)
-    d_dist = torch.empty((n_local, V), dtype=torch.int64, device=dev)
-    d_nh = torch.empty((n_local, V, nb), dtype=torch.uint8, device=dev)
+    d_dist = torch.empty((max(n_local, 1), V), dtype=torch.int64, device=dev)
+    d_nh = torch.empty((max(n_local, 1), V, nb), dtype=torch.uint8, device=dev)
     stream = torch.cuda.Stream(device=dev)  # a real (non-null) stream shared by launches and events
     torch.cuda.set_stream(stream)
 
@@ -612,7 +652,6 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    barrier()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
@@ -623,8 +662,6 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
-    from openr_amd.shard import max_over_ranks
-
     elapsed = max_over_ranks(elapsed, dev)  # the slowest rank's clock
 
     # correctness spot check (grid: Manhattan distances) outside the timed region
@@ -638,19 +675,34 @@ def main():
             assert np.array_equal(host[rows.index(r)].astype(np.int64), exp), "bench result check failed"
 
     gather = None
-    if world > 1 and args.scaling == "strong" and not args.no_gather:
-        from openr_amd.shard import allgather_results
+    if world > 1 and strong and not args.no_gather:
+        from openr_amd.shard import GatherBuffers
 
-        torch.cuda.synchronize(dev)
-        dist.barrier()
+        gb = GatherBuffers(d_dist[:n_local], d_nh[:n_local], V, world)
+        for _ in range(max(1, args.warmup)):
+            step()
+            gb.allgather()
+        barrier()
         tg = time.perf_counter()
-        allgather_results(d_dist, d_nh, V, world)
-        torch.cuda.synchronize(dev)
-        gms = max_over_ranks((time.perf_counter() - tg) * 1e3, dev)
-        gather = {"ms": gms, "bytes": int(V * V * (8 + nb)),
-                  "gather_inclusive_value": V / (elapsed / args.steps + gms / 1e3)}
+        for _ in range(args.steps):
+            step()
+            gb.allgather()
+        barrier()
+        gel = max_over_ranks(time.perf_counter() - tg, dev)
+        # the gathered rows are the full all-sources result on every rank
+        if args.topology == "grid100":
+            full = gb.full_dist()
+            r_chk = [0, V // 2, V - 1]
+            host = full[r_chk].cpu().numpy().view(np.uint64)
+            a = np.arange(V)
+            for i, s in enumerate(r_chk):
+                exp = np.abs(s % 100 - a % 100) + np.abs(s // 100 - a // 100)
+                assert np.array_equal(host[i].astype(np.int64), exp), "gathered result check failed"
+        gather = {"ms_per_step": gel / args.steps * 1e3, "bytes_per_rank": int(V * V * (8 + nb)),
+                  "gather_inclusive_value": V * args.steps / gel,
+                  "collective": "all_gather_into_tensor (RCCL) of dist u64 + next-hop rows, solve included"}
 
-    solves_total = (V if args.scaling == "strong" else V * world) * args.steps
+    solves_total = (V if strong else V * world) * args.steps
     value = solves_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     sources_local = np.arange(lo, hi)
@@ -659,7 +711,7 @@ def main():
     achieved = bytes_launch / mean_kernel_s / 1e9 if mean_kernel_s > 0 else 0.0
     traffic = None
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r01f", f"pmc_traffic_{args.topology}.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{args.topology}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -681,10 +733,11 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (reference benchmark grid generator, unit metrics)",
-            "config": dict(cfg, **{"sources_per_step": solves_total // args.steps, "use_link_metric": use_metric,
-                                   "parallelism": (f"source-sharded x{world}" if args.scaling == "strong"
-                                                   else f"area-per-GPU x{world}")}),
+            "data": "synthetic (reference benchmark grid generator, unit metrics)"
+                    if args.topology == "grid100" else "synthetic (benchmark generators)",
+            "config": dict(cfg, **{"sources_per_step": solves_total // args.steps, "sources_per_rank": n_local,
+                                   "use_link_metric": use_metric,
+                                   "parallelism": (f"source-sharded x{world}" if strong else f"area-per-GPU x{world}")}),
             "edge_relax_per_s": value * g.num_dir_edges,
             "roofline": {
                 "bound": "hbm",
@@ -695,6 +748,8 @@ def main():
                 "traffic": traffic,
                 "kernel_ms_mean": mean_kernel_s * 1e3,
                 "bytes_per_launch": bytes_launch,
+                "note": "per GPU (rank 0): SURVEY.md 8d B(src) summed over the rank's sources / mean launch "
+                        "duration (HIP events on the launch stream)",
             },
         }
         if gather is not None:
@@ -708,4 +763,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

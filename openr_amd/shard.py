@@ -26,28 +26,63 @@ def shard_sizes(n_units: int, world: int):
 
 
 def allgather_results(dist_shard, nh_shard, n_units: int, world: int):
-    """All-gather per-rank [n_r, V] distance and [n_r, V, B] next-hop shards.
+    """All-gather per-rank [n_r, V] distance and [n_r, V, B] next-hop shards (uneven
+    shards allowed); returns the full [n_units, ...] tensors (or None for a None shard)."""
+    gb = GatherBuffers(dist_shard, nh_shard, n_units, world)
+    gb.allgather()
+    return (gb.full_dist() if dist_shard is not None else None,
+            gb.full_nh() if nh_shard is not None else None)
 
-    Shards may be uneven (n_units % world != 0); each is padded to the largest
-    shard for the collective and trimmed afterwards. Returns full tensors.
+
+class GatherBuffers:
+    """Preallocated all-gather of per-rank result shards (the config-3 exchange step).
+
+    ``dist_shard`` [n_r, V] / ``nh_shard`` [n_r, V, B] are this rank's rows (device
+    tensors for RCCL, host tensors for gloo). ``allgather()`` fills ``full`` buffers of
+    [world * max_shard, ...] with one ``all_gather_into_tensor`` per array; shards
+    smaller than the largest are staged through a padded send buffer. Rows of rank r
+    sit at [r * max_shard, r * max_shard + n_r).
     """
-    import torch
-    import torch.distributed as dist
 
-    sizes = shard_sizes(n_units, world)
-    m = max(sizes)
-    outs = []
-    for t in (dist_shard, nh_shard):
-        if t is None:
-            outs.append(None)
-            continue
-        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        pad[: t.shape[0]] = t
-        full = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(full, pad)
-        parts = [full[r * m : r * m + sizes[r]] for r in range(world)]
-        outs.append(torch.cat(parts, dim=0))
-    return outs[0], outs[1]
+    def __init__(self, dist_shard, nh_shard, n_units: int, world: int) -> None:
+        import torch
+
+        self.sizes = shard_sizes(n_units, world)
+        self.m = max(self.sizes) if self.sizes else 0
+        self.world = world
+        self.parts = []
+        for t in (dist_shard, nh_shard):
+            if t is None:
+                self.parts.append(None)
+                continue
+            tail = tuple(t.shape[1:])
+            send = t if t.shape[0] == self.m and t.is_contiguous() else torch.zeros((self.m,) + tail, dtype=t.dtype,
+                                                                                    device=t.device)
+            full = torch.empty((world * self.m,) + tail, dtype=t.dtype, device=t.device)
+            self.parts.append((t, send, full))
+
+    def allgather(self) -> None:
+        import torch.distributed as dist
+
+        for p in self.parts:
+            if p is None:
+                continue
+            src, send, full = p
+            if send is not src:
+                send[: src.shape[0]].copy_(src)
+            dist.all_gather_into_tensor(full, send)
+
+    def _rows(self, i):
+        import torch
+
+        full = self.parts[i][2]
+        return torch.cat([full[r * self.m: r * self.m + self.sizes[r]] for r in range(self.world)], dim=0)
+
+    def full_dist(self):
+        return self._rows(0)
+
+    def full_nh(self):
+        return self._rows(1)
 
 
 def max_over_ranks(value: float, device=None) -> float:

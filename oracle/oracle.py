@@ -36,6 +36,15 @@ class OracleGraph(ctypes.Structure):
 _lib = None
 
 
+def default_threads() -> int:
+    """Host threads for the batch drivers: the process's CPU share, at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def build() -> None:
     import subprocess
 
@@ -59,6 +68,12 @@ def lib():
         l.oracle_all_sources.restype = ctypes.c_int
         l.oracle_all_sources.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+        l.oracle_ksp2_batch.restype = ctypes.c_int
+        l.oracle_ksp2_batch.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        l.oracle_whatif.restype = ctypes.c_int
+        l.oracle_whatif.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         l.oracle_num_distinct_neighbors.restype = ctypes.c_uint32
         l.oracle_num_distinct_neighbors.argtypes = [P(OracleGraph), ctypes.c_uint32]
         _lib = l
@@ -131,6 +146,33 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("oracle_all_sources failed")
         return dist, nh
+
+    def ksp2_tokens(self, src: Sequence[int], dst: Sequence[int], tok_cap: int = 256, nthreads: int = 0):
+        """getKthPaths(s, d, 1) and (.., 2) per pair as token rows [n, tok_cap] u32 (the
+        openr_spf_ksp2 layout), on `nthreads` host threads (0 = up to 16)."""
+        s_ = np.ascontiguousarray(src, dtype=np.uint32)
+        d_ = np.ascontiguousarray(dst, dtype=np.uint32)
+        n = int(s_.shape[0])
+        t1 = np.zeros((n, tok_cap), dtype=np.uint32)
+        t2 = np.zeros((n, tok_cap), dtype=np.uint32)
+        rc = lib().oracle_ksp2_batch(ctypes.byref(self._s), _ptr(s_), _ptr(d_), n, tok_cap, _ptr(t1), _ptr(t2),
+                                     nthreads or default_threads())
+        if rc != 0:
+            raise RuntimeError("oracle_ksp2_batch failed")
+        return t1, t2
+
+    def whatif(self, links: Sequence[int], sources: Sequence[int], use_link_metric: bool = True,
+               nthreads: int = 0) -> np.ndarray:
+        """changed[n_links, n_sources] u32: nodes whose dist or next-hop set differ between
+        runSpf(s, {link}) and runSpf(s)."""
+        lk = np.ascontiguousarray(links, dtype=np.uint32)
+        sr = np.ascontiguousarray(sources, dtype=np.uint32)
+        out = np.zeros((lk.shape[0], sr.shape[0]), dtype=np.uint32)
+        rc = lib().oracle_whatif(ctypes.byref(self._s), _ptr(lk), lk.shape[0], _ptr(sr), sr.shape[0],
+                                 int(use_link_metric), _ptr(out), nthreads or default_threads())
+        if rc != 0:
+            raise RuntimeError("oracle_whatif failed")
+        return out
 
     # --- helpers mirroring the reference's SpfResult view -------------------
     def next_hop_names(self, src: int, run: SpfRun, v: int) -> Set[str]:

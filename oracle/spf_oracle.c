@@ -357,66 +357,249 @@ static int64_t trace_one_path(const ws_t* w, const oracle_graph* g,
   return -1;
 }
 
-int64_t oracle_kth_paths(const oracle_graph* g, uint32_t src, uint32_t dest,
-                         uint32_t k, uint32_t* out_path_ptr, uint32_t max_paths,
-                         uint32_t* out_edges, uint32_t max_edges) {
-  if (!g || k < 1 || src >= g->num_nodes || dest >= g->num_nodes) return -1;
+/* Per-thread buffers of getKthPaths (allocated once, reused across pairs). */
+typedef struct {
   ws_t w;
-  if (ws_init(&w, g)) return -1;
-  const uint32_t L = g->num_links, V = g->num_nodes, E = g->num_dir_edges;
-  size_t lw = (L + 63) / 64 + 1;
-  uint64_t* ignore = (uint64_t*)calloc(lw, sizeof(uint64_t));
-  uint64_t* visited = (uint64_t*)calloc(lw, sizeof(uint64_t));
-  uint32_t* owner = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
-  frame_t* stack = (frame_t*)malloc(((size_t)V + 1) * sizeof(frame_t));
-  uint32_t* path = (uint32_t*)malloc(((size_t)V + 1) * sizeof(uint32_t));
-  /* paths of the current level (all levels' links go into `ignore`) */
-  uint32_t* cur_ptr = (uint32_t*)malloc(((size_t)E + 2) * sizeof(uint32_t));
-  uint32_t* cur_edges = (uint32_t*)malloc(((size_t)E * 2 + (size_t)V + 1) * sizeof(uint32_t));
-  int64_t result = -1;
-  if (!ignore || !visited || !owner || !stack || !path || !cur_ptr || !cur_edges) goto done;
-  for (uint32_t u = 0; u < V; ++u)
-    for (uint32_t e = g->row_ptr[u]; e < g->row_ptr[u + 1]; ++e) owner[e] = u;
+  size_t lw;
+  uint64_t* ignore;
+  uint64_t* visited;
+  uint32_t* owner;
+  frame_t* stack;
+  uint32_t* path;
+  uint32_t* cur_ptr;   /* paths of the current level */
+  uint32_t* cur_edges;
+} ksp_ctx;
 
+static void ksp_free(ksp_ctx* c) {
+  free(c->ignore);
+  free(c->visited);
+  free(c->owner);
+  free(c->stack);
+  free(c->path);
+  free(c->cur_ptr);
+  free(c->cur_edges);
+  ws_free(&c->w);
+  memset(c, 0, sizeof(*c));
+}
+
+static int ksp_init(ksp_ctx* c, const oracle_graph* g) {
+  memset(c, 0, sizeof(*c));
+  if (ws_init(&c->w, g)) return -1;
+  const uint32_t L = g->num_links, V = g->num_nodes, E = g->num_dir_edges;
+  c->lw = (L + 63) / 64 + 1;
+  c->ignore = (uint64_t*)calloc(c->lw, sizeof(uint64_t));
+  c->visited = (uint64_t*)calloc(c->lw, sizeof(uint64_t));
+  c->owner = (uint32_t*)malloc((E ? E : 1) * sizeof(uint32_t));
+  c->stack = (frame_t*)malloc(((size_t)V + 1) * sizeof(frame_t));
+  c->path = (uint32_t*)malloc(((size_t)V + 1) * sizeof(uint32_t));
+  c->cur_ptr = (uint32_t*)malloc(((size_t)E + 2) * sizeof(uint32_t));
+  c->cur_edges = (uint32_t*)malloc(((size_t)E * 2 + (size_t)V + 1) * sizeof(uint32_t));
+  if (!c->ignore || !c->visited || !c->owner || !c->stack || !c->path || !c->cur_ptr || !c->cur_edges) {
+    ksp_free(c);
+    return -1;
+  }
+  for (uint32_t u = 0; u < V; ++u)
+    for (uint32_t e = g->row_ptr[u]; e < g->row_ptr[u + 1]; ++e) c->owner[e] = u;
+  return 0;
+}
+
+/* getKthPaths (LinkState.cpp:762-791): level i < k ignores the links of every path
+   found at levels < i; the paths of level k are left in cur_ptr / cur_edges.
+   Returns the number of paths or -1. */
+static int64_t kth_paths_ctx(ksp_ctx* c, const oracle_graph* g, uint32_t src, uint32_t dest, uint32_t k) {
+  memset(c->ignore, 0, c->lw * sizeof(uint64_t));
   uint32_t npaths = 0;
   for (uint32_t level = 1; level <= k; ++level) {
     int any_ignore = 0;
-    for (size_t i = 0; i < lw; ++i) any_ignore |= (ignore[i] != 0);
+    for (size_t i = 0; i < c->lw; ++i) any_ignore |= (c->ignore[i] != 0);
     /* linksToIgnore.empty() ? getSpfResult(src, true) : runSpf(src, true, ignore) */
-    if (run_spf_ws(&w, g, src, 1, any_ignore ? ignore : NULL) < 0) goto done;
+    if (run_spf_ws(&c->w, g, src, 1, any_ignore ? c->ignore : NULL) < 0) return -1;
     npaths = 0;
-    cur_ptr[0] = 0;
-    if (w.settled[dest]) {
-      memset(visited, 0, lw * sizeof(uint64_t));
+    c->cur_ptr[0] = 0;
+    if (c->w.settled[dest]) {
+      memset(c->visited, 0, c->lw * sizeof(uint64_t));
       for (;;) {
-        int64_t len = trace_one_path(&w, g, owner, src, dest, visited, stack, path);
+        int64_t len = trace_one_path(&c->w, g, c->owner, src, dest, c->visited, c->stack, c->path);
         if (len <= 0) break; /* while (path && !path->empty()) */
-        memcpy(cur_edges + cur_ptr[npaths], path, (size_t)len * sizeof(uint32_t));
-        cur_ptr[npaths + 1] = cur_ptr[npaths] + (uint32_t)len;
+        memcpy(c->cur_edges + c->cur_ptr[npaths], c->path, (size_t)len * sizeof(uint32_t));
+        c->cur_ptr[npaths + 1] = c->cur_ptr[npaths] + (uint32_t)len;
         npaths++;
       }
     }
     if (level < k) {
-      for (uint32_t i = 0; i < cur_ptr[npaths]; ++i) {
-        uint32_t link = g->link_id[cur_edges[i]];
-        ignore[link >> 6] |= (uint64_t)1 << (link & 63);
+      for (uint32_t i = 0; i < c->cur_ptr[npaths]; ++i) {
+        uint32_t link = g->link_id[c->cur_edges[i]];
+        c->ignore[link >> 6] |= (uint64_t)1 << (link & 63);
       }
     }
   }
-  if (npaths > max_paths || cur_ptr[npaths] > max_edges) goto done;
-  if (out_path_ptr) memcpy(out_path_ptr, cur_ptr, ((size_t)npaths + 1) * sizeof(uint32_t));
-  if (out_edges) memcpy(out_edges, cur_edges, (size_t)cur_ptr[npaths] * sizeof(uint32_t));
-  result = npaths;
-done:
-  free(ignore);
-  free(visited);
-  free(owner);
-  free(stack);
-  free(path);
-  free(cur_ptr);
-  free(cur_edges);
-  ws_free(&w);
+  return npaths;
+}
+
+int64_t oracle_kth_paths(const oracle_graph* g, uint32_t src, uint32_t dest,
+                         uint32_t k, uint32_t* out_path_ptr, uint32_t max_paths,
+                         uint32_t* out_edges, uint32_t max_edges) {
+  if (!g || k < 1 || src >= g->num_nodes || dest >= g->num_nodes) return -1;
+  ksp_ctx c;
+  if (ksp_init(&c, g)) return -1;
+  int64_t npaths = kth_paths_ctx(&c, g, src, dest, k);
+  int64_t result = -1;
+  if (npaths >= 0 && (uint64_t)npaths <= max_paths && c.cur_ptr[npaths] <= max_edges) {
+    if (out_path_ptr) memcpy(out_path_ptr, c.cur_ptr, ((size_t)npaths + 1) * sizeof(uint32_t));
+    if (out_edges) memcpy(out_edges, c.cur_edges, (size_t)c.cur_ptr[npaths] * sizeof(uint32_t));
+    result = npaths;
+  }
+  ksp_free(&c);
   return result;
+}
+
+/* Token row [n_paths, len_0, e.., len_1, e.., ...] (openr_spf_ksp2 layout); a row that
+   does not fit gets n_paths = 0xFFFFFFFF. */
+static void write_tokens(const ksp_ctx* c, uint32_t npaths, uint32_t* tok, uint32_t cap) {
+  if (1u + npaths + c->cur_ptr[npaths] > cap) {
+    tok[0] = 0xFFFFFFFFu;
+    return;
+  }
+  uint32_t pos = 0;
+  tok[pos++] = npaths;
+  for (uint32_t i = 0; i < npaths; ++i) {
+    const uint32_t len = c->cur_ptr[i + 1] - c->cur_ptr[i];
+    tok[pos++] = len;
+    memcpy(tok + pos, c->cur_edges + c->cur_ptr[i], (size_t)len * sizeof(uint32_t));
+    pos += len;
+  }
+}
+
+typedef struct {
+  const oracle_graph* g;
+  const uint32_t *src, *dst;
+  uint32_t n, tid, nthreads, tok_cap;
+  uint32_t *tok1, *tok2;
+  int rc;
+} ksp_job_t;
+
+static void* ksp_worker(void* arg) {
+  ksp_job_t* j = (ksp_job_t*)arg;
+  ksp_ctx c;
+  if (ksp_init(&c, j->g)) {
+    j->rc = -1;
+    return NULL;
+  }
+  for (uint32_t i = j->tid; i < j->n; i += j->nthreads) {
+    for (uint32_t k = 1; k <= 2; ++k) {
+      int64_t np = kth_paths_ctx(&c, j->g, j->src[i], j->dst[i], k);
+      if (np < 0) {
+        j->rc = -1;
+        break;
+      }
+      write_tokens(&c, (uint32_t)np, (k == 1 ? j->tok1 : j->tok2) + (size_t)i * j->tok_cap, j->tok_cap);
+    }
+  }
+  ksp_free(&c);
+  return NULL;
+}
+
+int oracle_ksp2_batch(const oracle_graph* g, const uint32_t* src, const uint32_t* dst, uint32_t n,
+                      uint32_t tok_cap, uint32_t* tok1, uint32_t* tok2, int nthreads) {
+  if (!g || tok_cap < 1 || (n && (!src || !dst || !tok1 || !tok2))) return -1;
+  for (uint32_t i = 0; i < n; ++i)
+    if (src[i] >= g->num_nodes || dst[i] >= g->num_nodes) return -1;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  ksp_job_t jobs[256];
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t] = (ksp_job_t){g, src, dst, n, (uint32_t)t, (uint32_t)nthreads, tok_cap, tok1, tok2, 0};
+    if (t > 0) pthread_create(&th[t], NULL, ksp_worker, &jobs[t]);
+  }
+  ksp_worker(&jobs[0]);
+  int rc = jobs[0].rc;
+  for (int t = 1; t < nthreads; ++t) {
+    pthread_join(th[t], NULL);
+    rc |= jobs[t].rc;
+  }
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-link-failure what-if counts: runSpf(src, use, {link}) vs runSpf(src)  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const oracle_graph* g;
+  const uint32_t *links, *sources;
+  uint32_t n_links, n_sources, tid, nthreads;
+  int use_link_metric;
+  uint32_t* changed;
+  int rc;
+} whatif_job_t;
+
+static void* whatif_worker(void* arg) {
+  whatif_job_t* j = (whatif_job_t*)arg;
+  const oracle_graph* g = j->g;
+  ws_t w;
+  if (ws_init(&w, g)) {
+    j->rc = -1;
+    return NULL;
+  }
+  const uint32_t V = g->num_nodes, nw = w.nw;
+  const size_t lw = (g->num_links + 63) / 64 + 1;
+  uint64_t* base_d = (uint64_t*)malloc((size_t)(V ? V : 1) * sizeof(uint64_t));
+  uint64_t* base_nh = (uint64_t*)malloc((size_t)(V ? V : 1) * nw * sizeof(uint64_t));
+  uint64_t* ign = (uint64_t*)calloc(lw, sizeof(uint64_t));
+  if (!base_d || !base_nh || !ign) j->rc = -1;
+  for (uint32_t s = j->tid; s < j->n_sources && !j->rc; s += j->nthreads) {
+    const uint32_t src = j->sources[s];
+    if (run_spf_ws(&w, g, src, j->use_link_metric, NULL) < 0) {
+      j->rc = -1;
+      break;
+    }
+    for (uint32_t v = 0; v < V; ++v) base_d[v] = w.settled[v] ? w.dist[v] : U64_MAX_;
+    memcpy(base_nh, w.nh, (size_t)V * nw * sizeof(uint64_t));
+    for (uint32_t i = 0; i < j->n_links; ++i) {
+      const uint32_t l = j->links[i];
+      ign[l >> 6] |= (uint64_t)1 << (l & 63);
+      if (run_spf_ws(&w, g, src, j->use_link_metric, ign) < 0) j->rc = -1;
+      ign[l >> 6] = 0;
+      uint32_t cnt = 0;
+      for (uint32_t v = 0; v < V; ++v) {
+        const uint64_t d = w.settled[v] ? w.dist[v] : U64_MAX_;
+        int diff = d != base_d[v];
+        for (uint32_t k = 0; k < nw && !diff; ++k) diff = w.nh[(size_t)v * nw + k] != base_nh[(size_t)v * nw + k];
+        cnt += (uint32_t)diff;
+      }
+      j->changed[(size_t)i * j->n_sources + s] = cnt;
+    }
+  }
+  free(base_d);
+  free(base_nh);
+  free(ign);
+  ws_free(&w);
+  return NULL;
+}
+
+int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                  uint32_t n_sources, int use_link_metric, uint32_t* changed, int nthreads) {
+  if (!g) return -1;
+  for (uint32_t i = 0; i < n_links; ++i)
+    if (links[i] >= g->num_links) return -1;
+  for (uint32_t i = 0; i < n_sources; ++i)
+    if (sources[i] >= g->num_nodes) return -1;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  whatif_job_t jobs[256];
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t] = (whatif_job_t){g, links, sources, n_links, n_sources, (uint32_t)t, (uint32_t)nthreads,
+                             use_link_metric, changed, 0};
+    if (t > 0) pthread_create(&th[t], NULL, whatif_worker, &jobs[t]);
+  }
+  whatif_worker(&jobs[0]);
+  int rc = jobs[0].rc;
+  for (int t = 1; t < nthreads; ++t) {
+    pthread_join(th[t], NULL);
+    rc |= jobs[t].rc;
+  }
+  return rc;
 }
 
 /* ------------------------------------------------------------------------ */

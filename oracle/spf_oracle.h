@@ -6,6 +6,7 @@
  *   - DijkstraQ / DijkstraQNode     /root/reference/openr/decision/LinkState.h:475-535
  *   - LinkState::getKthPaths        /root/reference/openr/decision/LinkState.cpp:762-791
  *   - LinkState::traceOnePath       /root/reference/openr/decision/LinkState.cpp:398-419
+ * plus multi-threaded batch drivers over them (all-sources, KSP2 pairs, what-if units).
  *
  * It is the CHECKER for the HIP engine (openr_amd/csrc) and the CPU baseline
  * ("port") timed by bench.py. Only tests/, __graft_entry__.smoke() and
@@ -79,6 +80,23 @@ int64_t oracle_kth_paths(const oracle_graph* g, uint32_t src, uint32_t dest,
 int oracle_all_sources(const oracle_graph* g, const uint32_t* sources, uint32_t n,
                        int use_link_metric, uint64_t* dist, uint8_t* nh,
                        uint32_t nh_bytes, int nthreads);
+
+/*
+ * getKthPaths(src[i], dst[i], 1) and (.., 2) for n pairs on `nthreads` pthreads, as
+ * token rows tok1 / tok2 [n][tok_cap] in the openr_spf_ksp2 layout
+ * [n_paths, len_0, e.., len_1, e.., ...]; a pair that does not fit gets
+ * n_paths = 0xFFFFFFFF. Returns 0 on success.
+ */
+int oracle_ksp2_batch(const oracle_graph* g, const uint32_t* src, const uint32_t* dst, uint32_t n,
+                      uint32_t tok_cap, uint32_t* tok1, uint32_t* tok2, int nthreads);
+
+/*
+ * Per-link-failure what-if counts: changed[i][j] = nodes whose distance or next-hop
+ * set differ between runSpf(sources[j], use, {links[i]}) and runSpf(sources[j], use)
+ * (a node leaving the SpfResult counts). Sources are split across `nthreads`.
+ */
+int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                  uint32_t n_sources, int use_link_metric, uint32_t* changed, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,131 @@
+"""Full-size HIP-vs-oracle parity on every BASELINE.json config, one test per config.
+
+Each test is named after the config it covers (BASELINE.json "configs")
+so config coverage reads directly from the test log:
+
+  config1  G10  (10x10 benchmark grid), all-sources getSpfResult      — every source
+  config2  FAB  (intended fabric, 4 992 nodes), all-sources + ECMP    — every source
+  config3  G100 (100x100 grid, 10 000 nodes), all-pairs               — every source
+  config4  WAN  (1k nodes, 3 000 links, U[1,64]) what-if sweep        — all links x 16 sources
+  config5  FAB  KSP2 getKthPaths(k=1,2)                               — every destination of
+                                                                         an SSW, FSW and RSW source
+
+The oracle (oracle/spf_oracle.c, LinkState.cpp:762-882 restated) runs on host threads
+as the checker; every engine call goes through the C-ABI. The multi-GPU halves of
+configs 3 and 5 (source sharding + RCCL all-gather) are covered by
+tests/test_gpu_multirank.py.
+"""
+import numpy as np
+import pytest
+
+from openr_amd import topology as T
+from openr_amd.engine import SpfEngine, decode_paths
+from openr_amd.spf_result import tight_in_edges
+from oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = SpfEngine()
+    yield e
+    e.close()
+
+
+def all_sources_vs_oracle(eng, g, chunk, use_metric=True):
+    """Every source of g: engine dist + next-hop rows == oracle rows, chunk by chunk."""
+    eng.set_graph(g)
+    o = Oracle(g)
+    assert eng.nh_bytes == o.nh_bytes
+    V = g.num_nodes
+    for lo in range(0, V, chunk):
+        srcs = np.arange(lo, min(V, lo + chunk), dtype=np.uint32)
+        dist, nh, _ = eng.solve(srcs, use_metric)
+        odist, onh = o.all_sources(srcs, use_metric, nthreads=16)
+        bad = np.nonzero(np.any(dist != odist, axis=1))[0]
+        assert bad.size == 0, f"dist differs for sources {srcs[bad[:8]].tolist()}"
+        bad = np.nonzero(np.any(nh != onh, axis=(1, 2)))[0]
+        assert bad.size == 0, f"next hops differ for sources {srcs[bad[:8]].tolist()}"
+
+
+def pathlinks_vs_oracle(eng, g, sources, use_metric=True):
+    eng.set_graph(g)
+    o = Oracle(g)
+    dist, _, tight = eng.solve(sources, use_metric, want_tight=True)
+    for i, s in enumerate(sources):
+        run = o.run_spf(int(s), use_metric)
+        pe = tight_in_edges(g, dist[i], tight[i])
+        for v in np.nonzero(run.reachable())[0].tolist():
+            assert pe.get(v, []) == run.pl_edge[run.pl_ptr[v]: run.pl_ptr[v + 1]].tolist(), (s, v)
+
+
+def test_config1_grid10_all_sources():
+    """DecisionBenchmark 10x10 grid (RoutingBenchmarkUtils.cpp:205-240): all 100 sources,
+    link metric and hop count, dist + next hops + pathLinks."""
+    e = SpfEngine()
+    try:
+        g = T.grid(10)
+        for use_metric in (True, False):
+            all_sources_vs_oracle(e, g, 100, use_metric)
+            pathlinks_vs_oracle(e, g, list(range(100)), use_metric)
+        a = np.arange(100)
+        dist, _, _ = e.solve(a, True)
+        assert np.array_equal(dist.astype(np.int64), np.abs(a[:, None] % 10 - a % 10) + np.abs(a[:, None] // 10 - a // 10))
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("faithful", [False, True], ids=["intended", "reference-faithful"])
+def test_config2_fabric5000_all_sources(eng, faithful):
+    """Fabric ~5k nodes (84 pods x 8 planes x 36 SSWs), every one of the
+    4 992 sources, ECMP next-hop sets up to 84 bits wide; both generator variants."""
+    g = T.fabric(5000, faithful=faithful)
+    assert g.num_nodes == 4992 and g.num_links == (56448 if not faithful else 32544)
+    all_sources_vs_oracle(eng, g, 1248)
+    pathlinks_vs_oracle(eng, g, [0, 287, 288, 959, 960, 4991])
+
+
+def test_config3_grid100_all_sources(eng):
+    """100x100 grid, all 10 000 sources (the headline workload; its multi-GPU sharding is
+    tests/test_gpu_multirank.py), plus pathLinks of a source sample."""
+    g = T.grid_fast(100)
+    all_sources_vs_oracle(eng, g, 2500)
+    pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
+
+
+@pytest.mark.parametrize("mode", ["incr", "solve"])
+def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
+    """Per-link-failure sweep on the 1k-node WAN (U[1,64] asymmetric metrics): every one
+    of the 3 000 links x 16 sources, changed-node counts vs oracle re-solves
+    runSpf(src, true, {link}); incremental repair and re-solve modes."""
+    monkeypatch.setenv("OPENR_SPF_WHATIF", mode)
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    links = np.arange(g.num_links, dtype=np.uint32)
+    sources = np.linspace(0, g.num_nodes - 1, 16).astype(np.uint32)
+    changed, solved = eng.whatif(links, sources, True)
+    want = Oracle(g).whatif(links, sources, True)
+    bad = np.argwhere(changed != want)
+    assert bad.size == 0, f"(link, source) units differ: {bad[:8].tolist()}"
+    assert changed.sum() > 0 and solved >= len(sources)
+
+
+def test_config5_fabric_ksp2_all_destinations(eng):
+    """KSP2 on the fabric: getKthPaths(src, dst, 1) and (.., 2) for EVERY destination of an
+    SSW, an FSW and an RSW source (3 x 4 992 pairs), traced on the device, edge for edge
+    against the oracle."""
+    g = T.fabric(5000)
+    eng.set_graph(g)
+    V = g.num_nodes
+    ssw, fsw, rsw = 0, 288, 288 + 84 * 8
+    assert g.names[ssw].startswith("1-") and g.names[fsw].startswith("2-") and g.names[rsw].startswith("3-")
+    src = np.repeat(np.array([ssw, fsw, rsw], dtype=np.uint32), V)
+    dst = np.tile(np.arange(V, dtype=np.uint32), 3)
+    t1, t2 = eng.ksp2_tokens(src, dst, 1024)
+    o1, o2 = Oracle(g).ksp2_tokens(src, dst, 1024)
+    for i in range(len(src)):
+        for k, (a, b) in enumerate(((t1, o1), (t2, o2))):
+            assert decode_paths(a[i]) == decode_paths(b[i]), (int(src[i]), int(dst[i]), k + 1)
+    n2 = np.array([int(r[0]) for r in t2])
+    assert (n2[dst != src] > 0).mean() > 0.9  # second paths exist for almost every pair

@@ -46,8 +46,9 @@ def eng():
 
 
 def check_against_oracle(eng, g, sources, use_metric=True, ignore=None, check_pathlinks=True):
-    """Both engine paths vs the oracle: the plain solve (eligible for the bit-parallel
-    multi-source kernel) and, with check_pathlinks, the tight-edge solve (per-source)."""
+    """Both engine paths vs the oracle: the plain solve (dist + next hops; the
+    specialised non-generic kernel variants) and, with check_pathlinks, the tight-edge
+    solve (generic variants, pathLinks rebuilt in the reference's order)."""
     eng.set_graph(g)
     o = Oracle(g)
     assert eng.nh_bytes == o.nh_bytes
