@@ -156,8 +156,10 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
 template <int MODE, int BLOCK, typename LT, bool RING, int ELLM, bool GENERIC, bool SLICED>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_lvl_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t from_list,
-    uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+    uint32_t* ctr, uint32_t* ovf_count, uint32_t flags) {
   constexpr int K = (int)kBfsEdgesPerLane;
+  const uint32_t nt = flags & 1u;
+  const bool fresh_lvl = (flags & 2u) != 0;  // level stored by the appending arrival only
   constexpr bool ELECT = Nh<MODE>::kSingle && !SLICED;
   const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -355,8 +357,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             for (int j = 0; j < K; ++j) {
               // ELL-only path: store unconditionally (no branch). A non-tight v has a level
               // <= L that no arrival of this level changes, so writing it back is race-free.
-              if (ELLM == 2) lvl[vv[j]] = (LT)(tight[j] ? L + 1u : lold[j]);
-              else if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              if (!fresh_lvl) {
+                if (ELLM == 2) lvl[vv[j]] = (LT)(tight[j] ? L + 1u : lold[j]);
+                else if (tight[j]) lvl[vv[j]] = (LT)(L + 1u);
+              }
               if (trow && tight[j]) {
                 const uint32_t e = e0 + j * G;
                 atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
@@ -393,6 +397,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                     const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
                                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
                     ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
+                    // fresh_lvl: only the appending arrival stores v's level. Another
+                    // arrival of this level that reads lvl[v] before the store sees
+                    // "unset" (> L), i.e. tight, which is what v's level L+1 reads too.
+                    if (fresh_lvl) lvl[vv[j]] = (LT)(L + 1u);
                   }
                 }
               } else if ((int)lane == leader) {
@@ -510,8 +518,9 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
     info->grid = grid;
     info->kernel = RING ? "bfs_lvl_kernel<ring,u8>" : "bfs_lvl_kernel<full,u16>";
   }
+  const uint32_t flags = nt_stores() | (env_u32("OPENR_SPF_FRESH_LVL", 1u, 0u, 1u) << 1);
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
-                     (uint32_t)from_list, ctr, ovf_count, nt_stores());
+                     (uint32_t)from_list, ctr, ovf_count, flags);
   return hipGetLastError();
 }
 
@@ -528,6 +537,257 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   if (err != hipSuccess || (g.V <= ring_cap && g.V <= 254u)) return err;  // nothing can overflow
   return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true, blk + 2,
                                                                       blk + 4, num_cus, s, info);
+}
+
+// ---------------------------------------------------------------------------
+// ell16: the ELL-only fast path (every row <= 4 edges: grids) with ONE u16 state per
+// node, [enc:8 | nh:8], enc = 255 - level (0 = unreached; the source is 255, the
+// sentinel node V is 0xFFFF). An arrival over u->v at level L is tight iff v is
+// unreached or already on level L+1, i.e. iff enc(v) <= 254 - L, i.e. iff
+// state(v) < (255 - L) << 8 — one compare against a wave-uniform threshold. The tight
+// arrival's single atomicOr of ((254 - L) << 8 | nh(u)) both sets v's level (idempotent
+// for later equal-cost arrivals) and merges nh(u) into nh(v) (addNextHops,
+// LinkState.cpp:867-872); it returns v's previous state, and the arrival that saw
+// enc == 0 is the first and appends v. No per-edge level store, no separate level array.
+// Semantics are those of bfs_lvl_kernel (closed form of LinkState::runSpf for uniform
+// cost, LinkState.cpp:808-882); a solve deeper than 253 levels, or whose two adjacent
+// levels overflow the ring, is listed for the u16 full-order re-run like the u8 ring.
+// ---------------------------------------------------------------------------
+struct Ell16Layout {
+  uint32_t st, ring, dummy, total;
+};
+__host__ __device__ inline Ell16Layout ell16_layout(uint32_t V, uint32_t ring_cap) {
+  Ell16Layout l;
+  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4]
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.st = take(4u * ((V + 2u) / 2u));  // u16 per node, node V = sentinel
+  l.ring = take(2u * ring_cap);
+  l.dummy = take(4u * 64u);
+  l.total = off;
+  return l;
+}
+
+__device__ __forceinline__ uint32_t st_get(const uint32_t* st, uint32_t v) {
+  return reinterpret_cast<const uint16_t*>(st)[v];
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void bfs_ell16_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap,
+                                                          uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t s_next;
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const Ell16Layout lay = ell16_layout(V, ring_cap);
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  uint32_t* st = reinterpret_cast<uint32_t*>(base + lay.st);
+  uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
+  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
+  const uint32_t st_words = (V + 2u) / 2u;
+  const uint32_t rmask = ring_cap - 1u;
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+
+  for (uint32_t unit = blockIdx.x; unit < count;) {
+    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
+    const uint32_t src = a.sources[sid];
+    if (src < V) {  // block-uniform
+      for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
+      if (tid < 8) ctl[tid] = 0;
+      __syncthreads();
+      if (tid == 0) {
+        st16[V] = 0xFFFFu;  // sentinel: level 0, never tight
+        st16[src] = 0xFF00u;
+      }
+      __syncthreads();
+      // level 0: the source expands even when overloaded; a direct neighbour's next hop
+      // is the neighbour itself (LinkState.cpp:867-872)
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
+          const uint32_t e = e0 + tid;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && v != src) {
+              const uint32_t sh = (v & 1u) * 16u;
+              const uint32_t old = atomicOr(&st[v >> 1], ((254u << 8) | (1u << g.nbr[e])) << sh);
+              fresh = ((old >> sh) & 0xFF00u) == 0u;
+            }
+          }
+          const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
+          if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap (host-checked)
+        }
+      }
+      __syncthreads();
+
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1;
+      bool overflow = false;  // block-uniform
+      while (head < tail) {
+        if (L >= 254u) {  // enc(L + 1) = 254 - L must stay >= 1
+          overflow = true;
+          break;
+        }
+        uint32_t* cnt = &ctl[L & 3u];
+        if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
+        const uint32_t thr = (255u - L) << 8;  // tight iff state(v) < thr
+        const uint32_t enc1 = (254u - L) << 8;
+        for (uint32_t fb = head; fb < tail; fb += BLOCK) {
+          if (fb + wave * 64u >= tail) continue;  // this wave has no slice (uniform)
+          const uint32_t idx = fb + tid;
+          uint4 ell = make_uint4(V, V, V, V);  // a lane without a node reads the sentinel row
+          uint32_t val = 0;
+          if (idx < tail) {
+            const uint32_t u = ring[idx & rmask];
+            ell = g.ellv[u];  // down / padding / sink-row slots hold the sentinel V
+            val = enc1 | (st_get(st, u) & 0xFFu);
+          }
+          const uint32_t vv[4] = {ell.x, ell.y, ell.z, ell.w};
+          bool tight[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) tight[j] = (uint32_t)st16[vv[j]] < thr;
+          uint32_t old[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            old[j] = atomicOr(tight[j] ? &st[vv[j] >> 1] : &dummy[lane], tight[j] ? val << ((vv[j] & 1u) * 16u) : 0u);
+          bool fresh[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fresh[j] = tight[j] && ((old[j] >> ((vv[j] & 1u) * 16u)) & 0xFF00u) == 0u;
+          // wave-aggregated append (as bfs_lvl_kernel)
+          unsigned long long bj[4];
+          uint32_t off[5];
+          off[0] = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
+            off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+          }
+          const uint32_t total = off[4];
+          if (total) {  // wave-uniform
+            const int leader = __ffsll((long long)__ballot(1)) - 1;
+            uint32_t wbase = 0;
+            if ((int)lane == leader) wbase = atomicAdd(cnt, total);
+            const uint32_t bse = tail + __builtin_amdgcn_readfirstlane(wbase);
+            if (bse + total - head <= ring_cap) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (fresh[j]) {
+                  const uint32_t slot = bse + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                  ring[slot & rmask] = (uint16_t)vv[j];
+                }
+              }
+            } else if ((int)lane == leader) {
+              ctl[4] = 1;  // two adjacent levels exceed the ring
+            }
+          }
+        }
+        lds_barrier();
+        head = tail;
+        tail += *cnt;
+        ++L;
+        if (ctl[4]) {
+          overflow = true;
+          break;
+        }
+        if (tail == V) break;  // every node reached: the newest level cannot expand tightly
+      }
+      if (overflow) {
+        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
+      } else {
+        // rows: dist = level * cost (UINT64_MAX unreached), nh = the low nibble/byte
+        uint64_t* drow = a.dist + out_row_of(a, sid) * V;
+        uint8_t* nrow = a.nh ? a.nh + out_row_of(a, sid) * V * a.nh_bytes : nullptr;
+        const uint32_t nb = a.nh_bytes;
+        const bool fast = ((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0 &&
+                          (!nrow || (nb == 1 && (reinterpret_cast<uintptr_t>(nrow) & 3u) == 0));
+        auto dval = [cost](uint32_t s) -> uint64_t { return s ? (uint64_t)(255u - (s >> 8)) * cost : ~0ull; };
+        if (fast) {
+          uint32_t* n4 = reinterpret_cast<uint32_t*>(nrow);
+          for (uint32_t i = tid; i < V / 4u; i += BLOCK) {  // four nodes per lane
+            const uint2 w = reinterpret_cast<const uint2*>(st)[i];
+            const uint32_t s0 = w.x & 0xFFFFu, s1 = w.x >> 16, s2 = w.y & 0xFFFFu, s3 = w.y >> 16;
+            store_row<uint64_t>(&drow[4 * i], dval(s0), nt);
+            store_row<uint64_t>(&drow[4 * i + 1], dval(s1), nt);
+            store_row<uint64_t>(&drow[4 * i + 2], dval(s2), nt);
+            store_row<uint64_t>(&drow[4 * i + 3], dval(s3), nt);
+            if (n4)
+              store_row<uint32_t>(&n4[i], (s0 & 0xFFu) | ((s1 & 0xFFu) << 8) | ((s2 & 0xFFu) << 16) | ((s3 & 0xFFu) << 24),
+                                  nt);
+          }
+        } else {
+          for (uint32_t v = tid; v < V; v += BLOCK) {
+            const uint32_t s = st16[v];
+            store_row<uint64_t>(&drow[v], dval(s), nt);
+            if (nrow) {
+              uint8_t* o = nrow + (size_t)v * nb;
+              o[0] = (uint8_t)(s & 0xFFu);
+              for (uint32_t j = 1; j < nb; ++j) o[j] = 0;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // every lane is done with this unit's LDS and s_next
+    if (tid == 0) s_next = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unit = s_next;
+  }
+  retire_workgroup(ctr, nullptr);
+}
+
+// ell16 eligibility: ELL-only rows, no ignore set / tight output, one next-hop class of
+// <= 8 bits in the low byte, and a ring that fits the occupancy target. Returns the ring
+// capacity (0 = not eligible).
+uint32_t ell16_ring(const DevGraph& g, const SolveArgs& a, bool has_ign, int cls, uint32_t* per_cu) {
+  if (!env_u32("OPENR_SPF_ELL16", 1u, 0u, 1u)) return 0;
+  if (g.max_deg > 4u || has_ign || a.tight || cls != kLvl4 || g.V > 65534u) return 0;
+  const uint32_t fixed = ell16_layout(g.V, 0).total;
+  const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
+  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u) || g.est_depth + 8u >= 254u) return 0;
+  const uint32_t target = env_u32("OPENR_SPF_E16_WGS", 8u, 1u, 16u);
+  for (uint32_t want = target; want >= 1; --want) {
+    const uint32_t budget = kMaxLds / want;
+    if (budget <= fixed) continue;
+    uint32_t cap = 1;
+    while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
+    if (cap >= need) {
+      const uint32_t forced = env_u32("OPENR_SPF_RING_CAP", 0u, 0u, 65536u);
+      if (forced && (forced & (forced - 1u)) == 0u && forced >= g.max_deg + 2u && forced <= cap) cap = forced;
+      *per_cu = want;
+      return cap;
+    }
+  }
+  return 0;
+}
+
+hipError_t launch_ell16(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t ring_cap, int num_cus,
+                        hipStream_t s, LaunchInfo* info) {
+  constexpr int BLOCK = 128;
+  uint32_t* blk = class_counters(a);
+  const uint32_t lds = ell16_layout(g.V, ring_cap).total;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
+  auto k = bfs_ell16_kernel<BLOCK>;
+  hipError_t err =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  if (info) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = "bfs_ell16_kernel";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, blk, blk + 4, nt_stores());
+  err = hipGetLastError();
+  if (err != hipSuccess || (g.V <= ring_cap && g.V <= 253u)) return err;  // nothing can overflow
+  // the solves the ring flagged: u16 full-order re-run from the list
+  return launch_lvl_variant<kNhNibble, 256, uint16_t, false, 2, false>(g, a, cost, 0, false, g.V, true, blk + 2,
+                                                                       blk + 4, num_cus, s, nullptr);
 }
 
 template <int MODE, bool SLICED>
@@ -573,6 +833,11 @@ hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
   const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
+  if (ellm == 2) {
+    uint32_t per_cu = 0;
+    if (const uint32_t cap = ell16_ring(g, a, has_ign, cls, &per_cu))
+      return launch_ell16(g, a, cost, cap, num_cus, s, info);
+  }
   if (sliced) return launch_lvl_ell<kNhW1, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   switch (lvl_class_mode(cls)) {
     case kNhNibble: return launch_lvl_ell<kNhNibble, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);

@@ -128,4 +128,4 @@ def test_config5_fabric_ksp2_all_destinations(eng):
         for k, (a, b) in enumerate(((t1, o1), (t2, o2))):
             assert decode_paths(a[i]) == decode_paths(b[i]), (int(src[i]), int(dst[i]), k + 1)
     n2 = np.array([int(r[0]) for r in t2])
-    assert (n2[dst != src] > 0).mean() > 0.9  # second paths exist for almost every pair
+    assert (n2[dst != src] > 0).mean() > 0.5  # most pairs have edge-disjoint second paths
