@@ -746,7 +746,7 @@ __global__ __launch_bounds__(BLOCK) void bfs_ell16_kernel(DevGraph g, SolveArgs 
 // <= 8 bits in the low byte, and a ring that fits the occupancy target. Returns the ring
 // capacity (0 = not eligible).
 uint32_t ell16_ring(const DevGraph& g, const SolveArgs& a, bool has_ign, int cls, uint32_t* per_cu) {
-  if (!env_u32("OPENR_SPF_ELL16", 1u, 0u, 1u)) return 0;
+  if (!env_u32("OPENR_SPF_ELL16", 0u, 0u, 1u)) return 0;  // opt-in: 7 vs 10 solves per CU made it slower on G100
   if (g.max_deg > 4u || has_ign || a.tight || cls != kLvl4 || g.V > 65534u) return 0;
   const uint32_t fixed = ell16_layout(g.V, 0).total;
   const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
