@@ -21,7 +21,7 @@ ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/%.o,$(ENGINE_SRCS))
 
 HOST := $(LIBDIR)/libopenr_decision.so
 HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp $(CSRC)/host/AdjDbCodec.cpp $(CSRC)/host/adjdb_capi.cpp $(CSRC)/host/wan_gen.cpp
-HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h $(CSRC)/host/AdjDbCodec.h include/openr_spf.h include/openr_adjdb.h include/openr_topogen.h
+HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h $(CSRC)/host/AdjDbCodec.h include/openr_spf.h include/openr_adjdb.h include/openr_topogen.h include/openr_routes.h
 CXX ?= g++
 CC ?= gcc
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter

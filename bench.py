@@ -189,6 +189,30 @@ def whatif_main(args):
                 "achieved_gbs": traffic / (elapsed / args.steps) / 1e9 if traffic else None}
     if traffic:
         physical["frac"] = physical["achieved_gbs"] / HBM_PEAK_GBS
+    ucmp = None
+    if rank == 0 and not args.no_ucmp:
+        # config 4's "+ UCMP": the WAN's UCMP-weighted route DBs (RibPolicy
+        # set_weight, default 1, neighbour wan{i} 1 + i % 4 for i % 3 == 0) for every node, through
+        # the route-build C-ABI (openr_routes.h): one all-sources SPF batch on the GPU engine, then
+        # SpfSolver + RibPolicy on the host. Outside the sweep's timed region; its own clock.
+        from openr_amd import adjdb
+
+        batch = adjdb.AdjDbBatch.from_columns(adjdb.columns_for_graph(g))
+        rb = adjdb.RouteBuilder(batch, "0")
+        wts = adjdb.wan_ucmp_weights(rb.names())
+        ids = np.arange(rb.num_nodes)
+        rb.build(ids[:16], adjdb.ROUTES_UCMP, 1, wts)  # warm-up (engine context, prefixes)
+        tu = time.perf_counter()
+        st = rb.build(ids, adjdb.ROUTES_UCMP, 1, wts)
+        du = time.perf_counter() - tu
+        ucmp = {"nodes": int(rb.num_nodes), "unicast_routes": int(st.unicast_routes), "nexthops": int(st.nexthops),
+                "ucmp_weighted_nexthops": int(st.weighted_nexthops), "ms": du * 1e3,
+                "routes_per_s": st.unicast_routes / du, "ms_spf_and_route_build": st.ms_build,
+                "ms_rib_policy": st.ms_policy, "checksum": f"{st.checksum:016x}",
+                "note": "SpfSolver::buildRouteDbs (GPU all-sources SPF prefetch + host route build) + "
+                        "RibPolicy::applyPolicy, every node of the WAN"}
+        rb.close()
+        batch.close()
     if rank == 0:
         out = {
             "metric": "per-link-failure what-if SPF units/sec (link x source), 1k-node WAN, U[1,64] metrics",
@@ -210,6 +234,8 @@ def whatif_main(args):
                                  "the repair reads ~V*(8+nb) B per unit instead of solving; see physical",
                          "physical": physical},
         }
+        if ucmp is not None:
+            out["ucmp_routes"] = ucmp
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = whatif_cpu_baseline(g, min(args.cpu_seconds, 10.0), use_metric)
         print(json.dumps(out), flush=True)
@@ -571,6 +597,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-ucmp", action="store_true", help="whatif: skip the UCMP route-build leg")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="strong (default, BASELINE config 3): the V sources of ONE topology are split over the "
                          "ranks and the result shards all-gathered over RCCL; weak: every rank solves its own "

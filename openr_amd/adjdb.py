@@ -47,6 +47,14 @@ class GraphInfo(ctypes.Structure):
                 ("name_bytes", ctypes.c_uint64)]
 
 
+class RouteStats(ctypes.Structure):  # openr_routes_stats_t (include/openr_routes.h)
+    _fields_ = [("unicast_routes", ctypes.c_uint64), ("mpls_routes", ctypes.c_uint64),
+                ("nexthops", ctypes.c_uint64), ("weighted_nexthops", ctypes.c_uint64),
+                ("checksum", ctypes.c_uint64), ("ms_build", ctypes.c_double), ("ms_policy", ctypes.c_double)]
+
+
+ROUTES_LFA, ROUTES_V4, ROUTES_UCMP = 1, 2, 4
+
 _lib = None
 
 
@@ -73,6 +81,8 @@ def load_library():
     l.openr_adjdb_graph_info.argtypes = [vp, P(GraphInfo)]
     l.openr_adjdb_graph_export.argtypes = [vp] + [vp] * 9
     l.openr_topogen_wan.argtypes = [u32, u32, u32, u64, u32, vp, vp, vp]
+    l.openr_routes_build.argtypes = [vp, vp, u32, u32, ctypes.c_int32, vp, P(RouteStats)]
+    l.openr_routes_build.restype = ctypes.c_int
     l.openr_topogen_wan.restype = ctypes.c_int
     l.openr_decision_build_id.restype = ctypes.c_char_p
     check_build_id(l.openr_decision_build_id().decode(), LIB_PATH)
@@ -214,6 +224,67 @@ class AdjDbBatch:
         names = [raw[off[k]:off[k + 1]].decode(errors="surrogateescape") for k in range(V)]
         return CsrGraph(names, row_ptr, col[:E], metric[:E], link_id[:E], up[:E], ovl[:V], rank[:V], gi.num_links,
                         index={n: k for k, n in enumerate(names)})
+
+
+class RouteBuilder:
+    """Batched SpfSolver route build (include/openr_routes.h) over the LinkState that
+    ``batch``'s databases form: SPF on the GPU engine, routes + RibPolicy on the host."""
+
+    def __init__(self, batch: "AdjDbBatch", area: str = "0") -> None:
+        l = load_library()
+        self._g = ctypes.c_void_p()
+        _check(l.openr_adjdb_build_graph(batch._h, area.encode(), ctypes.byref(self._g)))
+        gi = GraphInfo()
+        _check(l.openr_adjdb_graph_info(self._g, ctypes.byref(gi)))
+        self.num_nodes = gi.num_nodes
+
+    def names(self) -> List[str]:
+        """Graph node names by id (ids = name ranks)."""
+        l = load_library()
+        gi = GraphInfo()
+        _check(l.openr_adjdb_graph_info(self._g, ctypes.byref(gi)))
+        V, E = gi.num_nodes, max(1, gi.num_dir_edges)
+        bufs = [np.zeros(V + 1, np.uint32), np.zeros(E, np.uint32), np.zeros(E, np.uint64), np.zeros(E, np.uint32),
+                np.zeros(E, np.uint8), np.zeros(max(1, V), np.uint8), np.zeros(max(1, V), np.uint32),
+                np.zeros(max(1, gi.name_bytes), np.uint8), np.zeros(V + 1, np.uint64)]
+        _check(l.openr_adjdb_graph_export(self._g, *(a.ctypes.data for a in bufs)))
+        raw, off = bufs[7].tobytes(), bufs[8]
+        return [raw[off[k]:off[k + 1]].decode(errors="surrogateescape") for k in range(V)]
+
+    def build(self, node_ids: Sequence[int], flags: int = 0, default_weight: int = 1,
+              neighbor_weight: "np.ndarray | None" = None) -> RouteStats:
+        ids = np.ascontiguousarray(node_ids, dtype=np.uint32)
+        w = None if neighbor_weight is None else np.ascontiguousarray(neighbor_weight, dtype=np.int32)
+        if w is not None and w.shape[0] != self.num_nodes:
+            raise ValueError("neighbor_weight must have one entry per graph node")
+        st = RouteStats()
+        _check(load_library().openr_routes_build(self._g, ids.ctypes.data if ids.size else None, ids.shape[0], flags,
+                                                 default_weight, None if w is None else w.ctypes.data,
+                                                 ctypes.byref(st)))
+        return st
+
+    def close(self) -> None:
+        if self._g:
+            load_library().openr_adjdb_graph_free(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def wan_ucmp_weights(names: Sequence[str]) -> np.ndarray:
+    """SURVEY.md §8d row 4 RibPolicy neighbour weights: node wan{i} weighs 1 + i % 4 when
+    i % 3 == 0 (others: none, i.e. the default weight 1)."""
+    w = np.zeros(len(names), np.int32)
+    for k, nm in enumerate(names):
+        if nm.startswith("wan"):
+            i = int(nm[3:])
+            if i % 3 == 0:
+                w[k] = 1 + i % 4
+    return w
 
 
 def strings(cols: Dict[str, np.ndarray]) -> List[str]:

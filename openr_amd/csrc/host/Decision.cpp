@@ -600,7 +600,10 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& route) const {
       newNexthops.emplace(std::move(n));
     }
   }
-  if (newNexthops.empty()) return false;  // every next-hop dropped: keep the route as is
+  if (newNexthops.empty()) {  // every next-hop dropped: keep the route as is (RibPolicy.cpp:98-104)
+    ++RibPolicyCounters::get().invalidatedRoutes;
+    return false;
+  }
   route.nexthops = std::move(newNexthops);
   return true;
 }
@@ -611,6 +614,11 @@ RibPolicy::RibPolicy(std::vector<RibPolicyStatement> statements, int64_t ttlSecs
   if (statements_.empty()) throw std::invalid_argument("Missing policy.statements attribute");
   for (auto const& s : statements_)
     if (s.prefixes.empty()) throw std::invalid_argument("Missing policy_statement.matcher.prefixes attribute");
+}
+
+RibPolicyCounters& RibPolicyCounters::get() {
+  static RibPolicyCounters c;
+  return c;
 }
 
 bool RibPolicy::isActive() const { return validUntil_ > std::chrono::steady_clock::now(); }

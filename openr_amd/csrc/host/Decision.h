@@ -246,6 +246,12 @@ struct RibPolicyStatement {
   bool applyAction(RibUnicastEntry& route) const;
 };
 
+// fb303 decision.rib_policy.* counters (process-wide, like fb303::fbData)
+struct RibPolicyCounters {
+  static RibPolicyCounters& get();
+  uint64_t invalidatedRoutes = 0;  // decision.rib_policy.invalidated_routes (RibPolicy.cpp:98-104)
+};
+
 class RibPolicy {
  public:
   explicit RibPolicy(std::vector<RibPolicyStatement> statements, int64_t ttlSecs = 3600);

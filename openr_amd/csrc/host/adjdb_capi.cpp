@@ -1,5 +1,7 @@
 // adjdb_capi.cpp — extern "C" wrapper of AdjDbCodec (include/openr_adjdb.h).
 #include <cerrno>
+#include <chrono>
+#include <unordered_map>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -7,15 +9,21 @@
 #include <vector>
 
 #include "../../../include/openr_adjdb.h"
+#include "../../../include/openr_routes.h"
 #include "AdjDbCodec.h"
+#include "Decision.h"
 
 struct openr_adjdb_batch {
   std::vector<openr::thrift::AdjacencyDatabase> dbs;
 };
 
 struct openr_adjdb_graph {
-  std::unique_ptr<openr::LinkState> linkState;
+  // the area's LinkState, held in the areaLinkStates map SpfSolver consumes
+  std::unordered_map<std::string, openr::LinkState> als;
+  openr::LinkState* linkState = nullptr;
   const openr::LinkState::CsrMirror* mirror = nullptr;
+  std::unique_ptr<openr::PrefixState> prefixes;  // openr_routes_build: fd00::<id>/128 per node
+  std::vector<openr::thrift::IpPrefix> prefixList;
 };
 
 namespace {
@@ -210,7 +218,7 @@ int openr_adjdb_build_graph(const openr_adjdb_batch* b, const char* area, openr_
   *out = nullptr;
   return guarded([&] {
     auto g = std::make_unique<openr_adjdb_graph>();
-    g->linkState = std::make_unique<openr::LinkState>(area);
+    g->linkState = &g->als.emplace(area, openr::LinkState(area)).first->second;
     for (const auto& db : b->dbs) {
       openr::thrift::AdjacencyDatabase stamped = db;
       stamped.area = area;
@@ -265,3 +273,90 @@ int openr_adjdb_graph_export(const openr_adjdb_graph* g, uint32_t* row_ptr, uint
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// openr_routes_build (include/openr_routes.h)
+// ---------------------------------------------------------------------------
+namespace {
+uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ULL;
+  return h ^ (h >> 33);
+}
+uint64_t hashStr(uint64_t h, const std::string& s) {
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ULL;
+  return mix64(h ^ s.size());
+}
+}  // namespace
+
+extern "C" int openr_routes_build(openr_adjdb_graph* g, const uint32_t* node_ids, uint32_t n, uint32_t flags,
+                                  int32_t default_weight, const int32_t* neighbor_weight,
+                                  openr_routes_stats_t* out) {
+  if (!g || !out || (n && !node_ids)) return fail(OPENR_ADJDB_EINVAL, "null argument");
+  const auto& m = *g->mirror;
+  const uint32_t V = (uint32_t)m.names.size();
+  for (uint32_t i = 0; i < n; ++i)
+    if (node_ids[i] >= V) return fail(OPENR_ADJDB_EINVAL, "node id " + std::to_string(node_ids[i]) + " out of range");
+  return guarded([&] {
+    using clock = std::chrono::steady_clock;
+    if (!g->prefixes) {  // one loopback prefix per node, originated once per graph
+      g->prefixes = std::make_unique<openr::PrefixState>();
+      const std::string area = g->linkState->getArea();
+      for (uint32_t v = 0; v < V; ++v) {
+        char buf[48];
+        std::snprintf(buf, sizeof(buf), "fd00::%x", v);
+        openr::thrift::PrefixEntry e;
+        e.prefix = openr::thrift::IpPrefix{buf, 128};
+        g->prefixList.push_back(e.prefix);
+        g->prefixes->updatePrefix(m.names[v], area, e);
+      }
+    }
+    *out = openr_routes_stats_t{};
+    if (!n) return 0;
+    std::vector<std::string> nodes;
+    nodes.reserve(n);
+    for (uint32_t i = 0; i < n; ++i) nodes.push_back(m.names[node_ids[i]]);
+    openr::SpfSolver solver(nodes[0], (flags & OPENR_ROUTES_V4) != 0, (flags & OPENR_ROUTES_LFA) != 0);
+    const auto t0 = clock::now();
+    auto dbs = solver.buildRouteDbs(nodes, g->als, *g->prefixes);
+    const auto t1 = clock::now();
+    if (flags & OPENR_ROUTES_UCMP) {  // RibPolicy set_weight over every route (Decision.cpp applies it per rebuild)
+      openr::RibPolicyStatement st;
+      st.name = "ucmp";
+      st.prefixes = std::set<openr::thrift::IpPrefix>(g->prefixList.begin(), g->prefixList.end());
+      st.defaultWeight = default_weight;
+      if (neighbor_weight)
+        for (uint32_t v = 0; v < V; ++v)
+          if (neighbor_weight[v] > 0) st.neighborToWeight[m.names[v]] = neighbor_weight[v];
+      openr::RibPolicy policy({st});
+      for (auto& db : dbs)
+        if (db) policy.applyPolicy(db->unicastRoutes);
+    }
+    const auto t2 = clock::now();
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!dbs[i]) continue;
+      const uint64_t hn = hashStr(0xcbf29ce484222325ULL, nodes[i]);
+      out->unicast_routes += dbs[i]->unicastRoutes.size();
+      out->mpls_routes += dbs[i]->mplsRoutes.size();
+      for (auto const& [p, route] : dbs[i]->unicastRoutes) {
+        const uint64_t hp = hashStr(hn, p.addr) ^ (uint64_t)p.prefixLength;
+        for (auto const& nh : route.nexthops) {
+          ++out->nexthops;
+          out->weighted_nexthops += nh.weight > 1;
+          uint64_t h = hashStr(hp, nh.address.addr);
+          h = hashStr(h, nh.address.ifName.value_or(""));
+          h = hashStr(h, nh.neighborNodeName.value_or(""));
+          h = mix64(h ^ ((uint64_t)(uint32_t)nh.metric << 32) ^ (uint32_t)nh.weight);
+          sum += h;  // order-independent
+        }
+      }
+    }
+    out->checksum = sum;
+    out->ms_build = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    out->ms_policy = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    return 0;
+  });
+}

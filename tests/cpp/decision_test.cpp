@@ -5,12 +5,18 @@
 // (file:line per test) and RibPolicy / best-route-selection semantics. SPF results come
 // from the engine, so route-building tests are in the gpu group.
 //   decision_test cpu | gpu | all
+#include <algorithm>
+#include <chrono>
+#include <map>
 #include <cstdlib>
+#include <thread>
 #include <set>
 #include <string>
 #include <vector>
 
+#include "../../include/openr_topogen.h"
 #include "../../openr_amd/csrc/host/Decision.h"
+#include "../../oracle/spf_oracle.h"
 #include "harness.h"
 
 using namespace openr;
@@ -327,6 +333,400 @@ static void ringKsp2(bool v4) {
 TEST_GPU(SimpleRing_Ksp2EdEcmp_v6) { ringKsp2(false); }
 TEST_GPU(SimpleRing_Ksp2EdEcmp_v4) { ringKsp2(true); }
 
+
+// KSP2 corner case of traceEdgeDisjointPaths (DecisionTest.cpp:2455-2475): adj12 and
+// node 3 overloaded -> from node 1 no route to 2 or 4, addr3 only over adj13
+static void ringKsp2Overload(bool v4) {
+  Ring r(v4, true);
+  SpfSolver solver("1", v4, true);
+  r.db1.adjacencies[0].isOverloaded = true;
+  r.db3.isOverloaded = true;
+  auto& ls = r.als.at(kDefaultArea);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db1).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db3).topologyChanged);
+  auto m = getRouteMap(solver, {"1"}, r.als, r.ps);
+  auto P = [&](const thrift::IpPrefix& a6, const thrift::IpPrefix& a4) { return v4 ? a4 : a6; };
+  EXPECT_TRUE(m.find({"1", P(addr4, addr4V4).toString()}) == m.end());
+  EXPECT_EQ(at(m, "1", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj13, v4, 10, std::nullopt)}));
+  EXPECT_TRUE(m.find({"1", P(addr2, addr2V4).toString()}) == m.end());
+}
+TEST_GPU(SimpleRing_Ksp2EdEcmp_OverloadCorner_v6) { ringKsp2Overload(false); }
+TEST_GPU(SimpleRing_Ksp2EdEcmp_OverloadCorner_v4) { ringKsp2Overload(true); }
+
+// SimpleRingTopologyFixture.OverloadNodeTest (DecisionTest.cpp:2821-2930): nodes 2 and 3
+// overloaded (reached, never transit), LFA on
+static void ringOverloadNode(bool v4) {
+  Ring r(v4, false);
+  SpfSolver solver("1", v4, true);
+  r.db2.isOverloaded = true;
+  r.db3.isOverloaded = true;
+  auto& ls = r.als.at(kDefaultArea);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db2).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db3).topologyChanged);
+  auto m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 32u);  // unicast 2+3+3+2, node labels 3+4+4+3, adj labels 4*2
+  auto P = [&](const thrift::IpPrefix& a6, const thrift::IpPrefix& a4) { return v4 ? a4 : a6; };
+  const auto swap = [](int l) { return mpls(MplsActionCode::SWAP, l); };
+  const auto php = mpls(MplsActionCode::PHP);
+  EXPECT_EQ(at(m, "1", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj13, v4, 10)}));
+  EXPECT_EQ(at(m, "1", 3), NextHopSet({nhFromAdj(adj13, false, 10, php)}));
+  EXPECT_EQ(at(m, "1", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj12, v4, 10)}));
+  EXPECT_EQ(at(m, "1", 2), NextHopSet({nhFromAdj(adj12, false, 10, php)}));
+  validatePopLabelRoute(m, "1", 1);
+  validateAdjLabelRoutes(m, "1", r.db1.adjacencies);
+  EXPECT_EQ(at(m, "2", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj24, v4, 10)}));  // no LFA
+  EXPECT_EQ(at(m, "2", 4), NextHopSet({nhFromAdj(adj24, false, 10, php)}));
+  EXPECT_EQ(at(m, "2", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj21, v4, 20), nhFromAdj(adj24, v4, 20)}));
+  EXPECT_EQ(at(m, "2", 3), NextHopSet({nhFromAdj(adj21, false, 20, swap(3)), nhFromAdj(adj24, false, 20, swap(3))}));
+  EXPECT_EQ(at(m, "2", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj21, v4, 10)}));
+  EXPECT_EQ(at(m, "2", 1), NextHopSet({nhFromAdj(adj21, false, 10, php)}));
+  validatePopLabelRoute(m, "2", 2);
+  validateAdjLabelRoutes(m, "2", r.db2.adjacencies);
+  EXPECT_EQ(at(m, "3", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj34, v4, 10)}));
+  EXPECT_EQ(at(m, "3", 4), NextHopSet({nhFromAdj(adj34, false, 10, php)}));
+  EXPECT_EQ(at(m, "3", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj31, v4, 20), nhFromAdj(adj34, v4, 20)}));
+  EXPECT_EQ(at(m, "3", 2), NextHopSet({nhFromAdj(adj31, false, 20, swap(2)), nhFromAdj(adj34, false, 20, swap(2))}));
+  EXPECT_EQ(at(m, "3", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj31, v4, 10)}));
+  EXPECT_EQ(at(m, "3", 1), NextHopSet({nhFromAdj(adj31, false, 10, php)}));
+  validatePopLabelRoute(m, "3", 3);
+  validateAdjLabelRoutes(m, "3", r.db3.adjacencies);
+  EXPECT_EQ(at(m, "4", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj43, v4, 10)}));
+  EXPECT_EQ(at(m, "4", 3), NextHopSet({nhFromAdj(adj43, false, 10, php)}));
+  EXPECT_EQ(at(m, "4", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj42, v4, 10)}));
+  EXPECT_EQ(at(m, "4", 2), NextHopSet({nhFromAdj(adj42, false, 10, php)}));
+  validatePopLabelRoute(m, "4", 4);
+  validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
+}
+TEST_GPU(SimpleRing_OverloadNodeTest_v6) { ringOverloadNode(false); }
+TEST_GPU(SimpleRing_OverloadNodeTest_v4) { ringOverloadNode(true); }
+
+// SimpleRingTopologyFixture.OverloadLinkTest (DecisionTest.cpp:2936-3113): adj31, then also
+// adj34, overloaded (Link::isUp false in both directions), LFA on
+static void ringOverloadLink(bool v4) {
+  Ring r(v4, false);
+  SpfSolver solver("1", v4, true);
+  r.db3.adjacencies[0].isOverloaded = true;  // adj31
+  auto& ls = r.als.at(kDefaultArea);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db3).topologyChanged);
+  auto m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 36u);
+  auto P = [&](const thrift::IpPrefix& a6, const thrift::IpPrefix& a4) { return v4 ? a4 : a6; };
+  const auto swap = [](int l) { return mpls(MplsActionCode::SWAP, l); };
+  const auto php = mpls(MplsActionCode::PHP);
+  EXPECT_EQ(at(m, "1", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj12, v4, 20)}));
+  EXPECT_EQ(at(m, "1", 4), NextHopSet({nhFromAdj(adj12, false, 20, swap(4))}));
+  EXPECT_EQ(at(m, "1", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj12, v4, 30)}));
+  EXPECT_EQ(at(m, "1", 3), NextHopSet({nhFromAdj(adj12, false, 30, swap(3))}));
+  EXPECT_EQ(at(m, "1", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj12, v4, 10)}));
+  EXPECT_EQ(at(m, "1", 2), NextHopSet({nhFromAdj(adj12, false, 10, php)}));
+  validatePopLabelRoute(m, "1", 1);
+  validateAdjLabelRoutes(m, "1", r.db1.adjacencies);
+  EXPECT_EQ(at(m, "2", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj24, v4, 10)}));
+  EXPECT_EQ(at(m, "2", 4), NextHopSet({nhFromAdj(adj24, false, 10, php)}));
+  EXPECT_EQ(at(m, "2", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj24, v4, 20)}));
+  EXPECT_EQ(at(m, "2", 3), NextHopSet({nhFromAdj(adj24, false, 20, swap(3))}));
+  EXPECT_EQ(at(m, "2", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj21, v4, 10)}));
+  EXPECT_EQ(at(m, "2", 1), NextHopSet({nhFromAdj(adj21, false, 10, php)}));
+  validatePopLabelRoute(m, "2", 2);
+  validateAdjLabelRoutes(m, "2", r.db2.adjacencies);
+  EXPECT_EQ(at(m, "3", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj34, v4, 10)}));
+  EXPECT_EQ(at(m, "3", 4), NextHopSet({nhFromAdj(adj34, false, 10, php)}));
+  EXPECT_EQ(at(m, "3", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj34, v4, 20)}));
+  EXPECT_EQ(at(m, "3", 2), NextHopSet({nhFromAdj(adj34, false, 20, swap(2))}));
+  EXPECT_EQ(at(m, "3", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj34, v4, 30)}));
+  EXPECT_EQ(at(m, "3", 1), NextHopSet({nhFromAdj(adj34, false, 30, swap(1))}));
+  validatePopLabelRoute(m, "3", 3);
+  validateAdjLabelRoutes(m, "3", r.db3.adjacencies);  // adj label routes stay for a down link
+  EXPECT_EQ(at(m, "4", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj43, v4, 10)}));
+  EXPECT_EQ(at(m, "4", 3), NextHopSet({nhFromAdj(adj43, false, 10, php)}));
+  EXPECT_EQ(at(m, "4", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj42, v4, 10)}));
+  EXPECT_EQ(at(m, "4", 2), NextHopSet({nhFromAdj(adj42, false, 10, php)}));
+  EXPECT_EQ(at(m, "4", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj42, v4, 20)}));
+  EXPECT_EQ(at(m, "4", 1), NextHopSet({nhFromAdj(adj42, false, 20, swap(1))}));
+  validatePopLabelRoute(m, "4", 4);
+  validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
+
+  // adj34 overloaded too: node 3 is disconnected
+  r.db3.adjacencies[1].isOverloaded = true;
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db3).topologyChanged);
+  m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 24u);  // unicast 2+2+0+2, node labels 3*3+1, adj labels 4*2
+  EXPECT_EQ(at(m, "1", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj12, v4, 20)}));
+  EXPECT_EQ(at(m, "1", 4), NextHopSet({nhFromAdj(adj12, false, 20, swap(4))}));
+  EXPECT_EQ(at(m, "1", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj12, v4, 10)}));
+  EXPECT_EQ(at(m, "1", 2), NextHopSet({nhFromAdj(adj12, false, 10, php)}));
+  validatePopLabelRoute(m, "1", 1);
+  validateAdjLabelRoutes(m, "1", r.db1.adjacencies);
+  EXPECT_EQ(at(m, "2", P(addr4, addr4V4)), NextHopSet({nhFromAdj(adj24, v4, 10)}));
+  EXPECT_EQ(at(m, "2", 4), NextHopSet({nhFromAdj(adj24, false, 10, php)}));
+  EXPECT_EQ(at(m, "2", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj21, v4, 10)}));
+  EXPECT_EQ(at(m, "2", 1), NextHopSet({nhFromAdj(adj21, false, 10, php)}));
+  validatePopLabelRoute(m, "2", 2);
+  validateAdjLabelRoutes(m, "2", r.db2.adjacencies);
+  validatePopLabelRoute(m, "3", 3);
+  validateAdjLabelRoutes(m, "3", r.db3.adjacencies);
+  EXPECT_EQ(at(m, "4", P(addr2, addr2V4)), NextHopSet({nhFromAdj(adj42, v4, 10)}));
+  EXPECT_EQ(at(m, "4", 2), NextHopSet({nhFromAdj(adj42, false, 10, php)}));
+  EXPECT_EQ(at(m, "4", P(addr1, addr1V4)), NextHopSet({nhFromAdj(adj42, v4, 20)}));
+  EXPECT_EQ(at(m, "4", 1), NextHopSet({nhFromAdj(adj42, false, 20, swap(1))}));
+  validatePopLabelRoute(m, "4", 4);
+  validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
+}
+TEST_GPU(SimpleRing_OverloadLinkTest_v6) { ringOverloadLink(false); }
+TEST_GPU(SimpleRing_OverloadLinkTest_v4) { ringOverloadLink(true); }
+
+// --- ParallelAdjRingTopologyFixture (DecisionTest.cpp:3136-3705) ---------------------
+namespace {
+struct ParallelRing {  // CustomSetUp :3143-3222
+  std::unordered_map<std::string, LinkState> als;
+  PrefixState ps;
+  thrift::Adjacency adj12_1 = createAdjacency("2", "2/1", "1/1", "fe80::2:1", "192.168.2.1", 11, 201),
+                    adj12_2 = createAdjacency("2", "2/2", "1/2", "fe80::2:2", "192.168.2.2", 11, 202),
+                    adj12_3 = createAdjacency("2", "2/3", "1/3", "fe80::2:3", "192.168.2.3", 20, 203),
+                    adj13_1 = createAdjacency("3", "3/1", "1/1", "fe80::3:1", "192.168.3.1", 11, 301),
+                    adj21_1 = createAdjacency("1", "1/1", "2/1", "fe80::1:1", "192.168.1.1", 11, 101),
+                    adj21_2 = createAdjacency("1", "1/2", "2/2", "fe80::1:2", "192.168.1.2", 11, 102),
+                    adj21_3 = createAdjacency("1", "1/3", "2/3", "fe80::1:3", "192.168.1.3", 20, 103),
+                    adj24_1 = createAdjacency("4", "4/1", "2/1", "fe80::4:1", "192.168.4.1", 11, 401),
+                    adj31_1 = createAdjacency("1", "1/1", "3/1", "fe80::1:1", "192.168.1.1", 11, 101),
+                    adj34_1 = createAdjacency("4", "4/1", "3/1", "fe80::4:1", "192.168.4.1", 11, 401),
+                    adj34_2 = createAdjacency("4", "4/2", "3/2", "fe80::4:2", "192.168.4.2", 20, 402),
+                    adj34_3 = createAdjacency("4", "4/3", "3/3", "fe80::4:3", "192.168.4.3", 20, 403),
+                    adj42_1 = createAdjacency("2", "2/1", "4/1", "fe80::2:1", "192.168.2.1", 11, 201),
+                    adj43_1 = createAdjacency("3", "3/1", "4/1", "fe80::3:1", "192.168.3.1", 11, 301),
+                    adj43_2 = createAdjacency("3", "3/2", "4/2", "fe80::3:2", "192.168.3.2", 20, 302),
+                    adj43_3 = createAdjacency("3", "3/3", "4/3", "fe80::3:3", "192.168.3.3", 20, 303);
+  thrift::AdjacencyDatabase db1, db2, db3, db4;
+  explicit ParallelRing(bool ksp2) {
+    db1 = createAdjDb("1", {adj12_1, adj12_2, adj12_3, adj13_1}, 1);
+    db2 = createAdjDb("2", {adj21_1, adj21_2, adj21_3, adj24_1}, 2);
+    db3 = createAdjDb("3", {adj31_1, adj34_1, adj34_2, adj34_3}, 3);
+    db4 = createAdjDb("4", {adj42_1, adj43_1, adj43_2, adj43_3}, 4);
+    als.emplace(kDefaultArea, LinkState(kDefaultArea));
+    auto& ls = als.at(kDefaultArea);
+    EXPECT_FALSE(ls.updateAdjacencyDatabase(db1).topologyChanged);
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db2).topologyChanged);
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db3).topologyChanged);
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db4).topologyChanged);
+    const thrift::IpPrefix p6[] = {addr1, addr2, addr3, addr4};
+    for (int i = 0; i < 4; ++i) ps.updatePrefix(std::to_string(i + 1), kDefaultArea, createPrefixEntry(p6[i], ksp2));
+  }
+};
+}  // namespace
+
+TEST_GPU(ParallelAdjRing_ShortestPathTest) {  // :3226-3335
+  ParallelRing r(false);
+  SpfSolver solver("1", false, false);
+  auto m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 44u);
+  const auto swap = [](int l) { return mpls(MplsActionCode::SWAP, l); };
+  const auto php = mpls(MplsActionCode::PHP);
+  EXPECT_EQ(at(m, "1", addr4), NextHopSet({nhFromAdj(r.adj12_2, false, 22), nhFromAdj(r.adj13_1, false, 22),
+                                           nhFromAdj(r.adj12_1, false, 22)}));
+  EXPECT_EQ(at(m, "1", 4), NextHopSet({nhFromAdj(r.adj12_2, false, 22, swap(4)), nhFromAdj(r.adj13_1, false, 22, swap(4)),
+                                       nhFromAdj(r.adj12_1, false, 22, swap(4))}));
+  EXPECT_EQ(at(m, "1", addr3), NextHopSet({nhFromAdj(r.adj13_1, false, 11)}));
+  EXPECT_EQ(at(m, "1", 3), NextHopSet({nhFromAdj(r.adj13_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(r.adj12_2, false, 11), nhFromAdj(r.adj12_1, false, 11)}));
+  EXPECT_EQ(at(m, "1", 2), NextHopSet({nhFromAdj(r.adj12_2, false, 11, php), nhFromAdj(r.adj12_1, false, 11, php)}));
+  validatePopLabelRoute(m, "1", 1);
+  validateAdjLabelRoutes(m, "1", r.db1.adjacencies);
+  EXPECT_EQ(at(m, "2", addr4), NextHopSet({nhFromAdj(r.adj24_1, false, 11)}));
+  EXPECT_EQ(at(m, "2", 4), NextHopSet({nhFromAdj(r.adj24_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "2", addr3), NextHopSet({nhFromAdj(r.adj21_2, false, 22), nhFromAdj(r.adj21_1, false, 22),
+                                           nhFromAdj(r.adj24_1, false, 22)}));
+  EXPECT_EQ(at(m, "2", 3), NextHopSet({nhFromAdj(r.adj21_2, false, 22, swap(3)), nhFromAdj(r.adj21_1, false, 22, swap(3)),
+                                       nhFromAdj(r.adj24_1, false, 22, swap(3))}));
+  EXPECT_EQ(at(m, "2", addr1), NextHopSet({nhFromAdj(r.adj21_2, false, 11), nhFromAdj(r.adj21_1, false, 11)}));
+  EXPECT_EQ(at(m, "2", 1), NextHopSet({nhFromAdj(r.adj21_2, false, 11, php), nhFromAdj(r.adj21_1, false, 11, php)}));
+  validatePopLabelRoute(m, "2", 2);
+  validateAdjLabelRoutes(m, "2", r.db2.adjacencies);
+  EXPECT_EQ(at(m, "3", addr4), NextHopSet({nhFromAdj(r.adj34_1, false, 11)}));
+  EXPECT_EQ(at(m, "3", 4), NextHopSet({nhFromAdj(r.adj34_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "3", addr2), NextHopSet({nhFromAdj(r.adj31_1, false, 22), nhFromAdj(r.adj34_1, false, 22)}));
+  EXPECT_EQ(at(m, "3", 2), NextHopSet({nhFromAdj(r.adj31_1, false, 22, swap(2)), nhFromAdj(r.adj34_1, false, 22, swap(2))}));
+  EXPECT_EQ(at(m, "3", addr1), NextHopSet({nhFromAdj(r.adj31_1, false, 11)}));
+  EXPECT_EQ(at(m, "3", 1), NextHopSet({nhFromAdj(r.adj31_1, false, 11, php)}));
+  validatePopLabelRoute(m, "3", 3);
+  validateAdjLabelRoutes(m, "3", r.db3.adjacencies);
+  EXPECT_EQ(at(m, "4", addr3), NextHopSet({nhFromAdj(r.adj43_1, false, 11)}));
+  EXPECT_EQ(at(m, "4", 3), NextHopSet({nhFromAdj(r.adj43_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "4", addr2), NextHopSet({nhFromAdj(r.adj42_1, false, 11)}));
+  EXPECT_EQ(at(m, "4", 2), NextHopSet({nhFromAdj(r.adj42_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "4", addr1), NextHopSet({nhFromAdj(r.adj42_1, false, 22), nhFromAdj(r.adj43_1, false, 22)}));
+  EXPECT_EQ(at(m, "4", 1), NextHopSet({nhFromAdj(r.adj42_1, false, 22, swap(1)), nhFromAdj(r.adj43_1, false, 22, swap(1))}));
+  validatePopLabelRoute(m, "4", 4);
+  validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
+}
+
+TEST_GPU(ParallelAdjRing_MultiPathTest) {  // :3340-3512 (LFA: parallel links of larger metric too)
+  ParallelRing r(false);
+  SpfSolver solver("1", false, true);
+  auto m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 44u);
+  const auto swap = [](int l) { return mpls(MplsActionCode::SWAP, l); };
+  const auto php = mpls(MplsActionCode::PHP);
+  EXPECT_EQ(at(m, "1", addr4), NextHopSet({nhFromAdj(r.adj12_1, false, 22), nhFromAdj(r.adj12_2, false, 22),
+                                           nhFromAdj(r.adj12_3, false, 31), nhFromAdj(r.adj13_1, false, 22)}));
+  EXPECT_EQ(at(m, "1", 4), NextHopSet({nhFromAdj(r.adj12_1, false, 22, swap(4)), nhFromAdj(r.adj12_2, false, 22, swap(4)),
+                                       nhFromAdj(r.adj12_3, false, 31, swap(4)), nhFromAdj(r.adj13_1, false, 22, swap(4))}));
+  EXPECT_EQ(at(m, "1", addr3), NextHopSet({nhFromAdj(r.adj13_1, false, 11)}));
+  EXPECT_EQ(at(m, "1", 3), NextHopSet({nhFromAdj(r.adj13_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(r.adj12_1, false, 11), nhFromAdj(r.adj12_2, false, 11),
+                                           nhFromAdj(r.adj12_3, false, 20)}));
+  EXPECT_EQ(at(m, "1", 2), NextHopSet({nhFromAdj(r.adj12_1, false, 11, php), nhFromAdj(r.adj12_2, false, 11, php),
+                                       nhFromAdj(r.adj12_3, false, 20, php)}));
+  validatePopLabelRoute(m, "1", 1);
+  validateAdjLabelRoutes(m, "1", r.db1.adjacencies);
+  EXPECT_EQ(at(m, "2", addr4), NextHopSet({nhFromAdj(r.adj24_1, false, 11)}));
+  EXPECT_EQ(at(m, "2", 4), NextHopSet({nhFromAdj(r.adj24_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "2", addr3), NextHopSet({nhFromAdj(r.adj21_1, false, 22), nhFromAdj(r.adj21_2, false, 22),
+                                           nhFromAdj(r.adj21_3, false, 31), nhFromAdj(r.adj24_1, false, 22)}));
+  EXPECT_EQ(at(m, "2", 3), NextHopSet({nhFromAdj(r.adj21_1, false, 22, swap(3)), nhFromAdj(r.adj21_2, false, 22, swap(3)),
+                                       nhFromAdj(r.adj21_3, false, 31, swap(3)), nhFromAdj(r.adj24_1, false, 22, swap(3))}));
+  EXPECT_EQ(at(m, "2", addr1), NextHopSet({nhFromAdj(r.adj21_1, false, 11), nhFromAdj(r.adj21_2, false, 11),
+                                           nhFromAdj(r.adj21_3, false, 20)}));
+  EXPECT_EQ(at(m, "2", 1), NextHopSet({nhFromAdj(r.adj21_1, false, 11, php), nhFromAdj(r.adj21_2, false, 11, php),
+                                       nhFromAdj(r.adj21_3, false, 20, php)}));
+  validatePopLabelRoute(m, "2", 2);
+  validateAdjLabelRoutes(m, "2", r.db2.adjacencies);
+  EXPECT_EQ(at(m, "3", addr4), NextHopSet({nhFromAdj(r.adj34_1, false, 11), nhFromAdj(r.adj34_2, false, 20),
+                                           nhFromAdj(r.adj34_3, false, 20)}));
+  EXPECT_EQ(at(m, "3", 4), NextHopSet({nhFromAdj(r.adj34_1, false, 11, php), nhFromAdj(r.adj34_2, false, 20, php),
+                                       nhFromAdj(r.adj34_3, false, 20, php)}));
+  EXPECT_EQ(at(m, "3", addr2), NextHopSet({nhFromAdj(r.adj31_1, false, 22), nhFromAdj(r.adj34_1, false, 22),
+                                           nhFromAdj(r.adj34_2, false, 31), nhFromAdj(r.adj34_3, false, 31)}));
+  EXPECT_EQ(at(m, "3", 2), NextHopSet({nhFromAdj(r.adj31_1, false, 22, swap(2)), nhFromAdj(r.adj34_1, false, 22, swap(2)),
+                                       nhFromAdj(r.adj34_2, false, 31, swap(2)), nhFromAdj(r.adj34_3, false, 31, swap(2))}));
+  EXPECT_EQ(at(m, "3", addr1), NextHopSet({nhFromAdj(r.adj31_1, false, 11)}));
+  EXPECT_EQ(at(m, "3", 1), NextHopSet({nhFromAdj(r.adj31_1, false, 11, php)}));
+  validatePopLabelRoute(m, "3", 3);
+  validateAdjLabelRoutes(m, "3", r.db3.adjacencies);
+  EXPECT_EQ(at(m, "4", addr3), NextHopSet({nhFromAdj(r.adj43_1, false, 11), nhFromAdj(r.adj43_2, false, 20),
+                                           nhFromAdj(r.adj43_3, false, 20)}));
+  EXPECT_EQ(at(m, "4", 3), NextHopSet({nhFromAdj(r.adj43_1, false, 11, php), nhFromAdj(r.adj43_2, false, 20, php),
+                                       nhFromAdj(r.adj43_3, false, 20, php)}));
+  EXPECT_EQ(at(m, "4", addr2), NextHopSet({nhFromAdj(r.adj42_1, false, 11)}));
+  EXPECT_EQ(at(m, "4", 2), NextHopSet({nhFromAdj(r.adj42_1, false, 11, php)}));
+  EXPECT_EQ(at(m, "4", addr1), NextHopSet({nhFromAdj(r.adj42_1, false, 22), nhFromAdj(r.adj43_1, false, 22),
+                                           nhFromAdj(r.adj43_2, false, 31), nhFromAdj(r.adj43_3, false, 31)}));
+  EXPECT_EQ(at(m, "4", 1), NextHopSet({nhFromAdj(r.adj42_1, false, 22, swap(1)), nhFromAdj(r.adj43_1, false, 22, swap(1)),
+                                       nhFromAdj(r.adj43_2, false, 31, swap(1)), nhFromAdj(r.adj43_3, false, 31, swap(1))}));
+  validatePopLabelRoute(m, "4", 4);
+  validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
+}
+
+TEST_GPU(ParallelAdjRing_Ksp2EdEcmp) {  // :3517-3705 (prefix type unset)
+  ParallelRing r(true);
+  SpfSolver solver("1", false, true);
+  auto push = [](std::vector<int32_t> l) { return mpls(MplsActionCode::PUSH, std::nullopt, l); };
+  auto m = getRouteMap(solver, {"1"}, r.als, r.ps);
+  // parallel links between node 1 and node 2
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(r.adj12_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj12_2, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj12_3, false, 20, std::nullopt)}));
+  // minNexthop: an SR_MPLS / KSP2 loopback prefix of node 4 with threshold 4 is dropped,
+  // with 2 it has the edge-disjoint pair adj12_2, adj13_1 (the adj12_2 choice is the
+  // folly-hash linksFromNode order, :3596-3599)
+  const auto bgpAddr1 = pfx("2401:1::10.1.1.1/32");
+  thrift::PrefixEntry np;
+  np.prefix = bgpAddr1;
+  np.type = thrift::PrefixType::LOOPBACK;
+  np.forwardingType = thrift::PrefixForwardingType::SR_MPLS;
+  np.forwardingAlgorithm = thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP;
+  np.minNexthop = 4;
+  r.ps.updatePrefix("4", kDefaultArea, np);
+  m = getRouteMap(solver, {"1"}, r.als, r.ps);
+  EXPECT_TRUE(m.find({"1", bgpAddr1.toString()}) == m.end());
+  np.minNexthop = 2;
+  r.ps.updatePrefix("4", kDefaultArea, np);
+  m = getRouteMap(solver, {"1"}, r.als, r.ps);
+  EXPECT_EQ(at(m, "1", bgpAddr1), NextHopSet({nhFromAdj(r.adj12_2, false, 22, push({4})),
+                                              nhFromAdj(r.adj13_1, false, 22, push({4}))}));
+  // node 3 announces it too with threshold 4: the anycast threshold is 4, route dropped
+  np.minNexthop = 4;
+  r.ps.updatePrefix("3", kDefaultArea, np);
+  m = getRouteMap(solver, {"1"}, r.als, r.ps);
+  EXPECT_TRUE(m.find({"1", bgpAddr1.toString()}) == m.end());
+  r.ps.deletePrefix("4", kDefaultArea, bgpAddr1);
+  r.ps.deletePrefix("3", kDefaultArea, bgpAddr1);
+
+  // adj12_2 and adj34_2 down
+  r.db1.adjacencies.at(1).isOverloaded = true;
+  r.db3.adjacencies.at(2).isOverloaded = true;
+  auto& ls = r.als.at(kDefaultArea);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db1).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(r.db3).topologyChanged);
+  m = getRouteMap(solver, {"1", "2", "3", "4"}, r.als, r.ps);
+  EXPECT_EQ(m.size(), 44u);
+  EXPECT_EQ(at(m, "1", addr4), NextHopSet({nhFromAdj(r.adj12_1, false, 22, push({4})),
+                                           nhFromAdj(r.adj13_1, false, 22, push({4}))}));
+  EXPECT_EQ(at(m, "1", addr3), NextHopSet({nhFromAdj(r.adj13_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj12_1, false, 33, push({3, 4}))}));
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(r.adj12_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj12_3, false, 20, std::nullopt)}));
+  EXPECT_EQ(at(m, "2", addr4), NextHopSet({nhFromAdj(r.adj24_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj21_1, false, 33, push({4, 3}))}));
+  EXPECT_EQ(at(m, "2", addr3), NextHopSet({nhFromAdj(r.adj21_1, false, 22, push({3})),
+                                           nhFromAdj(r.adj24_1, false, 22, push({3}))}));
+  EXPECT_EQ(at(m, "2", addr1), NextHopSet({nhFromAdj(r.adj21_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj21_3, false, 20, std::nullopt)}));
+  EXPECT_EQ(at(m, "3", addr4), NextHopSet({nhFromAdj(r.adj34_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj34_3, false, 20, std::nullopt)}));
+  EXPECT_EQ(at(m, "3", addr2), NextHopSet({nhFromAdj(r.adj31_1, false, 22, push({2})),
+                                           nhFromAdj(r.adj34_1, false, 22, push({2}))}));
+  EXPECT_EQ(at(m, "3", addr1), NextHopSet({nhFromAdj(r.adj31_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj34_1, false, 33, push({1, 2}))}));
+  EXPECT_EQ(at(m, "4", addr3), NextHopSet({nhFromAdj(r.adj43_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj43_3, false, 20, std::nullopt)}));
+  EXPECT_EQ(at(m, "4", addr2), NextHopSet({nhFromAdj(r.adj42_1, false, 11, std::nullopt),
+                                           nhFromAdj(r.adj43_1, false, 33, push({2, 1}))}));
+  EXPECT_EQ(at(m, "4", addr1), NextHopSet({nhFromAdj(r.adj42_1, false, 22, push({1})),
+                                           nhFromAdj(r.adj43_1, false, 22, push({1}))}));
+}
+
+// --- DecisionTestFixture.LoopFreeAlternatePaths (DecisionTest.cpp:5702-5837) ----------
+// Triangle 1-2 (10), 1-3 (8), 2-3 (9), LFA on: RFC 5286 alternates d(n,dst) < d(me,dst) +
+// d(n,me) (Decision.cpp:1170-1204) with real alternates, then none after 1-2 goes to 100.
+TEST_GPU(LoopFreeAlternatePaths) {
+  auto a12 = createAdjacency("2", "1/2", "2/1", "fe80::2", "192.168.0.2", 10, 0);
+  auto a13 = createAdjacency("3", "1/3", "3/1", "fe80::3", "192.168.0.3", 8, 0);
+  auto a21 = createAdjacency("1", "2/1", "1/2", "fe80::1", "192.168.0.1", 10, 0);
+  auto a23 = createAdjacency("3", "2/3", "3/2", "fe80::3", "192.168.0.3", 9, 0);
+  auto a31 = createAdjacency("1", "3/1", "1/3", "fe80::1", "192.168.0.1", 8, 0);
+  auto a32 = createAdjacency("2", "3/2", "2/3", "fe80::2", "192.168.0.2", 9, 0);
+  std::unordered_map<std::string, LinkState> als;
+  als.emplace(kDefaultArea, LinkState(kDefaultArea));
+  auto& ls = als.at(kDefaultArea);
+  ls.updateAdjacencyDatabase(createAdjDb("1", {a12, a13}, 0));
+  ls.updateAdjacencyDatabase(createAdjDb("2", {a21, a23}, 0));
+  ls.updateAdjacencyDatabase(createAdjDb("3", {a31, a32}, 0));
+  PrefixState ps;
+  ps.updatePrefix("1", kDefaultArea, createPrefixEntry(addr1));
+  ps.updatePrefix("2", kDefaultArea, createPrefixEntry(addr2));
+  ps.updatePrefix("3", kDefaultArea, createPrefixEntry(addr3));
+  SpfSolver solver("1", false, true);
+  auto m = getRouteMap(solver, {"1", "2", "3"}, als, ps);
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(a12, false, 10), nhFromAdj(a13, false, 17)}));
+  EXPECT_EQ(at(m, "1", addr3), NextHopSet({nhFromAdj(a12, false, 19), nhFromAdj(a13, false, 8)}));
+  EXPECT_EQ(at(m, "2", addr1), NextHopSet({nhFromAdj(a21, false, 10), nhFromAdj(a23, false, 17)}));
+  EXPECT_EQ(at(m, "2", addr3), NextHopSet({nhFromAdj(a21, false, 18), nhFromAdj(a23, false, 9)}));
+  EXPECT_EQ(at(m, "3", addr1), NextHopSet({nhFromAdj(a31, false, 8), nhFromAdj(a32, false, 19)}));
+  EXPECT_EQ(at(m, "3", addr2), NextHopSet({nhFromAdj(a31, false, 18), nhFromAdj(a32, false, 9)}));
+  // node1 -- node2 metric 100: node 3 loses its loop-free alternates
+  a12.metric = 100;
+  a21.metric = 100;
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("1", {a12, a13}, 0)).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("2", {a21, a23}, 0)).topologyChanged);
+  m = getRouteMap(solver, {"1", "2", "3"}, als, ps);
+  EXPECT_EQ(at(m, "1", addr2), NextHopSet({nhFromAdj(a12, false, 100), nhFromAdj(a13, false, 17)}));
+  EXPECT_EQ(at(m, "1", addr3), NextHopSet({nhFromAdj(a12, false, 109), nhFromAdj(a13, false, 8)}));
+  EXPECT_EQ(at(m, "2", addr1), NextHopSet({nhFromAdj(a21, false, 100), nhFromAdj(a23, false, 17)}));
+  EXPECT_EQ(at(m, "2", addr3), NextHopSet({nhFromAdj(a21, false, 108), nhFromAdj(a23, false, 9)}));
+  EXPECT_EQ(at(m, "3", addr1), NextHopSet({nhFromAdj(a31, false, 8)}));
+  EXPECT_EQ(at(m, "3", addr2), NextHopSet({nhFromAdj(a32, false, 9)}));
+}
+
 // --- GridTopologyFixture.ShortestPathTest (DecisionTest.cpp:4206-4355) ------------
 static int gridDistance(int a, int b, int n) { return std::abs(a % n - b % n) + std::abs(a / n - b / n); }
 
@@ -441,6 +841,270 @@ TEST_CPU(RibPolicy_ApplyAction) {  // RibPolicy.cpp:61-111 (RibPolicyTest semant
   }
   EXPECT_TRUE(threw);
   EXPECT_FALSE(RibPolicy({st}, 0).isActive());
+}
+
+// --- BASELINE config 4 routes: WAN + UCMP (RibPolicy set_weight), engine vs oracle ------
+// The WAN of SURVEY.md §8d row 4 (openr_topogen_wan, std::mt19937_64) as AdjacencyDatabases;
+// every node originates one prefix; SpfSolver builds the route DBs over ENGINE SPF results
+// (one all-sources prefetch) and RibPolicy applies the UCMP weights (default 1, neighbour
+// wan{i} weight 1 + i % 4 for i % 3 == 0). Expected routes are rebuilt here from ORACLE
+// SPF runs (oracle/spf_oracle.c) with the reference's next-hop rules: shortest next-hop
+// nodes of dst (Decision.cpp:1160-1166), LFA neighbours per RFC 5286 (:1170-1204), link
+// expansion with the distOverLink == minMetric filter when LFA is off (:1224-1257), i32
+// metric, and the RibPolicy weight precedence (RibPolicy.cpp:61-111).
+namespace {
+struct Wan {
+  std::unordered_map<std::string, LinkState> als;
+  PrefixState ps;
+  std::vector<std::string> names;
+  std::vector<thrift::IpPrefix> prefix;
+  Wan(uint32_t n, uint32_t L, uint32_t par, uint64_t seed) {
+    std::vector<uint32_t> ends(2 * (L + par)), muv(L + par), mvu(L + par);
+    EXPECT_EQ(openr_topogen_wan(n, L, 64, seed, par, ends.data(), muv.data(), mvu.data()), 0);
+    std::vector<std::vector<thrift::Adjacency>> adjs(n);
+    std::map<std::pair<uint32_t, uint32_t>, int> k;
+    auto nm = [](uint32_t i) { return "wan" + std::to_string(i); };
+    for (uint32_t l = 0; l < L + par; ++l) {
+      const uint32_t u = ends[2 * l], v = ends[2 * l + 1];
+      const int kk = k[{std::min(u, v), std::max(u, v)}]++;
+      const std::string iu = "if_" + std::to_string(u) + "_" + std::to_string(v) + "_" + std::to_string(kk);
+      const std::string iv = "if_" + std::to_string(v) + "_" + std::to_string(u) + "_" + std::to_string(kk);
+      adjs[u].push_back(createAdjacency(nm(v), iu, iv, "fe80::" + std::to_string(v), "10.0.0." + std::to_string(v % 256),
+                                        (int32_t)muv[l], 0));
+      adjs[v].push_back(createAdjacency(nm(u), iv, iu, "fe80::" + std::to_string(u), "10.0.0." + std::to_string(u % 256),
+                                        (int32_t)mvu[l], 0));
+    }
+    als.emplace(kDefaultArea, LinkState(kDefaultArea));
+    for (uint32_t i = 0; i < n; ++i) {
+      names.push_back(nm(i));
+      als.at(kDefaultArea).updateAdjacencyDatabase(createAdjDb(nm(i), adjs[i], 0));
+      prefix.push_back(pfx("fd00::" + std::to_string(i) + "/128"));
+      ps.updatePrefix(nm(i), kDefaultArea, createPrefixEntry(prefix.back()));
+    }
+  }
+  RibPolicy policy() const {
+    RibPolicyStatement st;
+    st.name = "wan-ucmp";
+    st.prefixes = std::set<thrift::IpPrefix>(prefix.begin(), prefix.end());
+    st.defaultWeight = 1;
+    for (uint32_t i = 0; i < names.size(); i += 3) st.neighborToWeight[names[i]] = 1 + (int32_t)(i % 4);
+    return RibPolicy({st});
+  }
+};
+
+// oracle SPF rows of the CSR mirror, memoized per source id
+struct OracleRows {
+  const LinkState::CsrMirror& m;
+  oracle_graph og;
+  std::map<uint32_t, std::pair<std::vector<uint64_t>, std::vector<uint8_t>>> rows;
+  uint32_t nb;
+  explicit OracleRows(const LinkState::CsrMirror& mm)
+      : m(mm),
+        og{(uint32_t)mm.names.size(), (uint32_t)mm.col.size(), (uint32_t)mm.links.size(), mm.rowPtr.data(),
+           mm.col.data(), mm.metric.data(), mm.linkId.data(), mm.edgeUp.data(), mm.overloaded.data(),
+           mm.nameRank.data()} {
+    uint32_t mx = 1;
+    for (uint32_t u = 0; u < og.num_nodes; ++u) mx = std::max(mx, oracle_num_distinct_neighbors(&og, u));
+    nb = (mx + 7) / 8;
+  }
+  const std::pair<std::vector<uint64_t>, std::vector<uint8_t>>& of(uint32_t s) {
+    auto it = rows.find(s);
+    if (it != rows.end()) return it->second;
+    std::vector<uint64_t> d(og.num_nodes);
+    std::vector<uint8_t> h((size_t)og.num_nodes * nb);
+    EXPECT_TRUE(oracle_run_spf(&og, s, 1, nullptr, d.data(), h.data(), nb, nullptr, nullptr, nullptr) >= 0);
+    return rows.emplace(s, std::make_pair(std::move(d), std::move(h))).first->second;
+  }
+};
+
+NextHopSet expectedRoute(OracleRows& o, uint32_t me, uint32_t dst, bool lfa, const RibPolicy& pol,
+                         const thrift::IpPrefix& p) {
+  const auto& m = o.m;
+  const auto& [dm, hm] = o.of(me);
+  NextHopSet out;
+  if (dst == me || dm[dst] == UINT64_MAX) return out;
+  std::vector<uint32_t> nbrs;  // distinct neighbours of me in row order (next-hop bit order)
+  for (uint32_t e = m.rowPtr[me]; e < m.rowPtr[me + 1]; ++e)
+    if (std::find(nbrs.begin(), nbrs.end(), m.col[e]) == nbrs.end()) nbrs.push_back(m.col[e]);
+  std::map<uint32_t, uint64_t> nhNodes;  // next-hop node -> its distance to dst
+  for (size_t i = 0; i < nbrs.size(); ++i)
+    if ((hm[(size_t)dst * o.nb + i / 8] >> (i % 8)) & 1u) nhNodes[nbrs[i]] = dm[dst] - dm[nbrs[i]];
+  if (lfa) {
+    for (uint32_t e = m.rowPtr[me]; e < m.rowPtr[me + 1]; ++e) {
+      if (!m.edgeUp[e]) continue;
+      const uint32_t n = m.col[e];
+      const auto& dn = o.of(n).first;
+      if (dn[dst] == UINT64_MAX) continue;
+      if (dn[dst] < dm[dst] + dn[me]) {
+        auto it = nhNodes.find(n);
+        if (it == nhNodes.end() || it->second > dn[dst]) nhNodes[n] = dn[dst];
+      }
+    }
+  }
+  for (uint32_t e = m.rowPtr[me]; e < m.rowPtr[me + 1]; ++e) {
+    const uint32_t n = m.col[e];
+    auto it = nhNodes.find(n);
+    if (it == nhNodes.end() || !m.edgeUp[e]) continue;
+    const uint64_t over = m.metric[e] + it->second;
+    if (!lfa && over != dm[dst]) continue;
+    const auto& link = m.links[m.linkId[e]];
+    const auto& meName = m.names[me];
+    out.insert(createNextHop(link->getNhV6FromNode(meName), link->getIfaceFromNode(meName), (int32_t)over,
+                             std::nullopt, kDefaultArea, m.names[n]));
+  }
+  RibUnicastEntry r;
+  r.prefix = p;
+  r.nexthops = out;
+  pol.applyAction(r);
+  return r.nexthops;
+}
+
+void wanUcmpRoutes(Wan& w, const std::vector<uint32_t>& nodeIdx, bool lfa) {
+  SpfSolver solver(w.names[0], false, lfa);
+  const auto pol = w.policy();
+  std::vector<std::string> nodes;
+  for (auto i : nodeIdx) nodes.push_back(w.names[i]);
+  auto dbs = solver.buildRouteDbs(nodes, w.als, w.ps);
+  auto const& m = w.als.at(kDefaultArea).csrMirror();
+  OracleRows o(m);
+  std::map<std::string, uint32_t> prefixOwner;
+  for (uint32_t i = 0; i < w.names.size(); ++i) prefixOwner[w.prefix[i].toString()] = m.id.at(w.names[i]);
+  size_t routes = 0, weighted = 0, lfaExtra = 0;
+  bool allSame = true;
+  for (size_t k = 0; k < nodes.size(); ++k) {
+    EXPECT_TRUE(dbs[k].has_value());
+    if (!dbs[k]) continue;
+    auto uni = dbs[k]->unicastRoutes;
+    pol.applyPolicy(uni);
+    const uint32_t me = m.id.at(nodes[k]);
+    EXPECT_EQ(uni.size(), w.names.size() - 1);  // every other node's prefix (the WAN is connected)
+    for (auto const& [p, route] : uni) {
+      const uint32_t dst = prefixOwner.at(p.toString());
+      const auto want = expectedRoute(o, me, dst, lfa, pol, p);
+      allSame &= route.nexthops == want;
+      ++routes;
+      for (auto const& nh : route.nexthops) {
+        weighted += nh.weight > 1;
+        lfaExtra += nh.metric != route.nexthops.begin()->metric;
+      }
+    }
+  }
+  EXPECT_TRUE(allSame);
+  EXPECT_TRUE(routes > 0 && weighted > 0);  // UCMP weights present
+  if (lfa) EXPECT_TRUE(lfaExtra > 0);       // real loop-free alternates present
+  std::printf("  wan routes: %zu, next hops with weight > 1: %zu, lfa: %d, alternates: %zu\n", routes, weighted,
+              (int)lfa, lfaExtra);
+}
+}  // namespace
+
+TEST_GPU(WanUcmpRoutes_vs_Oracle_256) {  // all nodes, parallel links
+  Wan w(256, 768, 15, 3);
+  std::vector<uint32_t> all(256);
+  for (uint32_t i = 0; i < 256; ++i) all[i] = i;
+  wanUcmpRoutes(w, all, false);
+  wanUcmpRoutes(w, all, true);
+}
+
+TEST_GPU(WanUcmpRoutes_vs_Oracle_Config4) {  // the config-4 WAN (1000 nodes, 3000 links)
+  Wan w(1000, 3000, 0, 1);
+  std::vector<uint32_t> sample;
+  for (uint32_t i = 0; i < 1000; i += 63) sample.push_back(i);
+  wanUcmpRoutes(w, sample, false);
+  wanUcmpRoutes(w, sample, true);
+}
+
+// --- RibPolicyTest.cpp:176-301 (RibPolicy.ApplyAction / ApplyPolicy) -----------------
+namespace {
+RibPolicyStatement policyStatement(std::vector<thrift::IpPrefix> prefixes, int32_t dflt,
+                                   std::unordered_map<std::string, int32_t> area,
+                                   std::unordered_map<std::string, int32_t> nbr = {}) {  // :23-37
+  RibPolicyStatement p;
+  p.name = "TestPolicyStatement";
+  p.prefixes = std::set<thrift::IpPrefix>(prefixes.begin(), prefixes.end());
+  p.defaultWeight = dflt;
+  p.areaToWeight = std::move(area);
+  p.neighborToWeight = std::move(nbr);
+  return p;
+}
+thrift::BinaryAddress binAddr(const std::string& a) {
+  thrift::BinaryAddress b;
+  b.addr = a;
+  return b;
+}
+}  // namespace
+
+TEST_CPU(RibPolicyTest_ApplyAction) {  // :180-236 only the first matching statement applies
+  const auto stmt1 = policyStatement({pfx("fc01::/64")}, 1, {{"area1", 99}});
+  const auto stmt2 = policyStatement({pfx("fc00::/64"), pfx("fc02::/64")}, 1, {{"area2", 99}});
+  RibPolicy policy({stmt1, stmt2}, 1);
+  const auto nh1 = createNextHop(binAddr("fe80::1"), std::string("iface1"), 0, std::nullopt, std::string("area1"));
+  const auto nh2 = createNextHop(binAddr("fe80::1"), std::string("iface2"), 0, std::nullopt, std::string("area2"));
+  {
+    RibUnicastEntry e;
+    e.prefix = pfx("fc01::/64");
+    e.nexthops = {nh1, nh2};
+    EXPECT_TRUE(policy.applyAction(e));
+    auto x1 = nh1, x2 = nh2;
+    x1.weight = 99;
+    x2.weight = 1;
+    EXPECT_EQ(e.nexthops, NextHopSet({x1, x2}));
+  }
+  {
+    RibUnicastEntry e;
+    e.prefix = pfx("fc02::/64");
+    e.nexthops = {nh1, nh2};
+    EXPECT_TRUE(policy.applyAction(e));
+    auto x1 = nh1, x2 = nh2;
+    x1.weight = 1;
+    x2.weight = 99;
+    EXPECT_EQ(e.nexthops, NextHopSet({x1, x2}));
+  }
+  {
+    RibUnicastEntry e;
+    e.prefix = pfx("fc03::/64");
+    e.nexthops = {nh1, nh2};
+    const auto before = e.nexthops;
+    EXPECT_FALSE(policy.applyAction(e));
+    EXPECT_EQ(e.nexthops, before);
+  }
+}
+
+TEST_CPU(RibPolicyTest_ApplyPolicy) {  // :238-301 neighbour > area > default, all-dropped kept, TTL
+  const auto stmt1 = policyStatement({pfx("fc01::/64")}, 1, {{"area1", 99}}, {{"nbr3", 98}});
+  const auto stmt2 = policyStatement({pfx("fc00::/64"), pfx("fc02::/64")}, 1, {{"area2", 0}});
+  RibPolicy policy({stmt1, stmt2}, 1);
+  const auto nh1 = createNextHop(binAddr("fe80::1"), std::string("iface1"), 0, std::nullopt, std::string("area1"),
+                                 std::string("nbr1"));
+  const auto nh2 = createNextHop(binAddr("fe80::1"), std::string("iface2"), 0, std::nullopt, std::string("area2"),
+                                 std::string("nbr2"));
+  const auto nh3 = createNextHop(binAddr("fe80::1"), std::string("iface3"), 0, std::nullopt, std::string("area1"),
+                                 std::string("nbr3"));
+  RibUnicastEntry e1, e2;
+  e1.prefix = pfx("fc01::/64");
+  e1.nexthops = {nh1, nh2, nh3};
+  e2.prefix = pfx("fc02::/64");
+  e2.nexthops = {nh2};
+  {
+    std::map<thrift::IpPrefix, RibUnicastEntry> entries{{e1.prefix, e1}, {e2.prefix, e2}};
+    const uint64_t inv0 = RibPolicyCounters::get().invalidatedRoutes;
+    const auto updated = policy.applyPolicy(entries);
+    EXPECT_EQ(updated, std::vector<thrift::IpPrefix>({e1.prefix}));
+    EXPECT_EQ(RibPolicyCounters::get().invalidatedRoutes - inv0, 1u);  // fc02: every next-hop weight 0
+    EXPECT_EQ(entries.size(), 2u);
+    auto x1 = nh1, x2 = nh2, x3 = nh3;
+    x1.weight = 99;
+    x2.weight = 1;
+    x3.weight = 98;
+    EXPECT_EQ(entries.at(e1.prefix).nexthops, NextHopSet({x1, x2, x3}));
+    EXPECT_EQ(entries.at(e2.prefix).nexthops, e2.nexthops);
+  }
+  std::this_thread::sleep_for(std::chrono::milliseconds(1100));  // the policy expires
+  EXPECT_FALSE(policy.isActive());
+  {
+    std::map<thrift::IpPrefix, RibUnicastEntry> entries{{e1.prefix, e1}, {e2.prefix, e2}};
+    EXPECT_TRUE(policy.applyPolicy(entries).empty());
+    EXPECT_EQ(entries.at(e1.prefix).nexthops, e1.nexthops);
+  }
 }
 
 int main(int argc, char** argv) { return run_tests(argc, argv); }

@@ -85,6 +85,20 @@ def test_topogen_library_exports_every_declared_symbol():
         assert hasattr(lib, name)
 
 
+def test_routes_library_exports_every_declared_symbol():
+    """include/openr_routes.h (batched SpfSolver route build + RibPolicy) is exported."""
+    from openr_amd import adjdb
+
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "openr_routes.h")).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(openr_routes_[a-z_0-9]+)\s*\(", text)))
+    assert declared == ["openr_routes_build"]
+    lib = adjdb.load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", adjdb.LIB_PATH], capture_output=True, text=True, check=True)
+    for name in declared:
+        assert re.search(r"\bT " + name + r"\b", out.stdout), name
+        assert hasattr(lib, name)
+
+
 def test_binaries_built_from_this_tree():
     """Build provenance: the engine, the host library and the C++ test binaries embed the
     hash of the sources they were built from (Makefile build_id); it must match this tree
