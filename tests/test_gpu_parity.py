@@ -615,3 +615,21 @@ def test_ksp2_device_capacity_tiers(eng, tier, monkeypatch):
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (200, 2))])
     g = hub_graph(21, V=220, L=500)
     check_ksp2_against_oracle(eng, g, [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 30)])
+
+
+@pytest.mark.parametrize("ring", [None, "256"])
+def test_ell16_kernel_opt_in(eng, monkeypatch, ring):
+    """The opt-in single-u16-state ELL kernel (OPENR_SPF_ELL16=1, spf_bfs_lvl.hip) on grids,
+    a ring forced too small (flagged solves re-run by the full-order pass) and a chain
+    deeper than 253 levels."""
+    monkeypatch.setenv("OPENR_SPF_ELL16", "1")
+    if ring:
+        monkeypatch.setenv("OPENR_SPF_RING_CAP", ring)
+    for n in (10, 33):
+        check_against_oracle(eng, T.grid_fast(n), list(range(n * n)), True, check_pathlinks=False)
+    V = 600
+    g = T.csr_from_links([f"c{i:04d}" for i in range(V)], np.array([(i, i + 1) for i in range(V - 1)]))
+    check_against_oracle(eng, g, [0, 1, 300, 599], True, check_pathlinks=False)
+    g2 = random_graph(7, 400, 700, 1, p_ovl=0.05, p_par=0.0)
+    if int(np.diff(g2.row_ptr).max()) <= 4:
+        check_against_oracle(eng, g2, list(range(g2.num_nodes)), True, check_pathlinks=False)
