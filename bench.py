@@ -62,39 +62,72 @@ def algorithmic_bytes(g, sources: np.ndarray) -> int:
 
 
 def cpu_baseline(g, seconds: float, use_metric: bool):
-    """The oracle (C restatement of LinkState::runSpf, oracle/spf_oracle.c) timed on
-    the host cores: the same all-sources workload, repeated passes over an evenly
-    spaced source sample until about `seconds` of wall time."""
-    from oracle import Oracle
+    """CPU baselines on the host cores of this box, same all-sources workload, evenly spaced
+    source samples sized to ~`seconds` of wall time in all:
+
+      faithful  oracle/spf_faithful.cpp: LinkState::runSpf restated with the reference's own
+                data structures (std::string-keyed maps, shared_ptr DijkstraQ heap,
+                unordered_set<string> next hops) — the reference's cost model. `value`.
+      dense     oracle/spf_oracle.c: the same semantics on dense integer ids (the parity
+                checker; an optimised CPU port, far cheaper than the reference).
+
+    Each at 1 thread and at every thread of this process's CPU share (one LinkState
+    replica per thread, sources strided)."""
+    from oracle.oracle import Oracle, default_threads
 
     o = Oracle(g)
     V = g.num_nodes
-    nthreads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate on a small strided sample, then size the timed sample to ~`seconds`
-    probe = np.arange(0, V, max(1, V // 32), dtype=np.uint32)[:32]
-    t0 = time.perf_counter()
-    o.all_sources(probe, use_metric, nthreads=1, want_dist=True, want_nh=False)
-    per_solve_1t = (time.perf_counter() - t0) / len(probe)
-    want = max(nthreads, int(seconds * nthreads / max(per_solve_1t, 1e-9)))
-    n = int(min(V, want))
-    passes = max(1, want // n)
-    sample = np.linspace(0, V - 1, n).astype(np.uint32)
-    t0 = time.perf_counter()
-    for _ in range(passes):
-        o.all_sources(sample, use_metric, nthreads=nthreads, want_dist=True, want_nh=True)
-    dt = time.perf_counter() - t0
-    n *= passes
+    nthreads = default_threads()
+    rng_all = np.arange(V, dtype=np.uint32)
+
+    def sample(n):
+        n = int(max(1, min(V, n)))
+        return np.linspace(0, V - 1, n).astype(np.uint32)
+
+    def dense(nt, budget):
+        probe = sample(16)
+        t0 = time.perf_counter()
+        o.all_sources(probe, use_metric, nthreads=1, want_dist=True, want_nh=False)
+        per = (time.perf_counter() - t0) / len(probe)
+        want = max(nt, int(budget * nt / max(per, 1e-9)))
+        srcs = sample(want)
+        passes = max(1, want // len(srcs))
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            o.all_sources(srcs, use_metric, nthreads=nt, want_dist=True, want_nh=True)
+        dt = time.perf_counter() - t0
+        return {"solves_per_s": len(srcs) * passes / dt, "threads": nt, "solves": len(srcs) * passes,
+                "seconds": dt}
+
+    def faithful(nt, budget):
+        _, _, sec = o.faithful_all_sources(sample(2), use_metric, nthreads=1)
+        per = sec / 2
+        srcs = sample(max(nt, int(budget * nt / max(per, 1e-9))))
+        _, _, dt = o.faithful_all_sources(srcs, use_metric, nthreads=nt)
+        return {"solves_per_s": len(srcs) / dt, "threads": nt, "solves": len(srcs), "seconds": dt}
+
+    variants = {
+        "faithful_1thread": faithful(1, 0.25 * seconds),
+        f"faithful_{nthreads}threads": faithful(nthreads, 0.35 * seconds),
+        "dense_1thread": dense(1, 0.15 * seconds),
+        f"dense_{nthreads}threads": dense(nthreads, 0.25 * seconds),
+    }
+    del rng_all
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         cpu_model = "unknown"
+    main = variants[f"faithful_{nthreads}threads"]
     return {
-        "value": n / dt,
+        "value": main["solves_per_s"],
         "unit": "solves/s",
         "cores": nthreads,
         "kind": "port",
-        "sample": f"{n} solves ({passes} pass(es) over {n // passes} of {V} sources, evenly spaced), dist+next-hops, "
-                  f"{nthreads} pthreads, {dt:.1f}s; {cpu_model}",
+        "cost_model": "faithful: reference data structures (oracle/spf_faithful.cpp)",
+        "sample": f"{main['solves']} evenly spaced sources of {V}, runSpf with std::string-keyed LinkState "
+                  f"replicas, {nthreads} threads (this process's CPU share of the box), {main['seconds']:.1f}s; "
+                  f"{cpu_model}",
+        "variants": variants,
     }
 
 

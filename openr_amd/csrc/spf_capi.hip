@@ -431,6 +431,22 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   a.ovf_list = d.ovf.p;
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
+  const char* mode = std::getenv("OPENR_SPF_WHATIF");
+  const bool dist64 = use_link_metric && (uint64_t)V * ctx->w_max >= 0xFFFFFFFFull;
+  if (!mode || !std::strcmp(mode, "group")) {
+    // default: grouped repair (base rows staged once per (source, link chunk), fused filter)
+    if (whatif_group_lds_bytes(V, ctx->E, nb, dist64)) {
+      OPENR_TRY(d.wcount.reserve(1));
+      OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
+                                    d.base_tight.p, nb, !use_link_metric, dist64, d_changed, d.wcount.p,
+                                    d.work.p + kIncrCtr, d.num_cus, s));
+      uint32_t count = 0;
+      OPENR_TRY(hipMemcpyAsync(&count, d.wcount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      OPENR_TRY(hipStreamSynchronize(s));
+      *solved = count;
+      return hipSuccess;
+    }
+  }
   const size_t units = (size_t)n_links * n_src;
   OPENR_TRY(d.wsrc.reserve(units));
   OPENR_TRY(d.wlink.reserve(units));
@@ -443,10 +459,8 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(hipStreamSynchronize(s));
   *solved = count;
   if (!count) return hipSuccess;
-  // incremental by default: each affected unit is repaired from the base rows (A set,
-  // distances inside A, dirty next hops); OPENR_SPF_WHATIF=solve re-solves every unit
-  const char* mode = std::getenv("OPENR_SPF_WHATIF");
-  const bool dist64 = use_link_metric && (uint64_t)V * ctx->w_max >= 0xFFFFFFFFull;
+  // OPENR_SPF_WHATIF=incr: one wavefront per affected unit repairs it from the base rows it
+  // re-reads (A set, distances inside A, dirty next hops); =solve re-solves every unit
   if (!(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
     return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
                               !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);

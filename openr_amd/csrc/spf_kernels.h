@@ -175,6 +175,15 @@ hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uin
                               uint32_t nb, bool unit_cost, bool dist64, uint32_t* changed, uint32_t* ctr,
                               int num_cus, hipStream_t s);
 uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
+// Grouped what-if (spf_sweep.hip, the default): one workgroup per (source, chunk of links)
+// stages the source's base rows (dist, next hops, tight mask) in LDS once; its wavefronts
+// filter the links (no tight edge -> 0) and repair the affected ones on private overlays.
+// Writes every changed[i * n_src + j]; *affected = affected units (zeroed by the launcher).
+hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                               uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
+                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64,
+                               uint32_t* changed, uint32_t* affected, uint32_t* ctr, int num_cus, hipStream_t s);
+uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64);
 
 // Incremental mirror updates (spf_update.hip).
 // In-place attribute patch of the device mirror: each record overwrites one element of

@@ -10,6 +10,8 @@
 // The rest are solved in chunks by the ordinary batched kernels (one (source,
 // {link}) ignore set per solve) and reduced against the base rows by rows_compare.
 // Integer / byte work only: HBM-bound, coalesced row reads, one workgroup per unit.
+#include <algorithm>
+
 #include "spf_bfs_common.h"
 #include "spf_kernels.h"
 
@@ -436,6 +438,421 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
   bfs::retire_workgroup(ctr, nullptr);
 }
 
+// --- grouped what-if: one workgroup per (source, chunk of links) -----------------------
+//
+// The same repair as whatif_incr_kernel (A set by decremental propagation, distances
+// inside A, next hops over the dirty set in increasing new distance), restructured so a
+// source's base rows are read from HBM/L2 ONCE per work item instead of once per unit:
+// the workgroup stages dist / next hops / tight mask of source j in LDS (read-only, shared
+// by its 4 wavefronts) and every wavefront repairs the affected links of the item one
+// after another on a private OVERLAY: new distances of A nodes (valid where the wave's A
+// bit is set) and rewritten next-hop sets (valid where its nh bit is set); everything else
+// reads the shared base. Per unit only three V-bit masks are cleared. The link filter is
+// fused (a link with no tight edge of the base SPF of j is unaffected: changed = 0), so
+// there is no global work list and no host round trip. Unit (i, j) writes
+// changed[i * n_src + j].
+constexpr uint32_t kGrpBlock = 256;
+constexpr uint32_t kGrpWaves = kGrpBlock / 64u;
+
+struct GrpLayout {
+  uint32_t bdist, bnh, btight, wave0, wstride;  // wave w's block at wave0 + w * wstride
+  uint32_t w_ina, w_dq, w_nhm, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
+  uint32_t total;
+};
+
+__host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t nb, uint32_t dist_bytes) {
+  GrpLayout l;
+  uint32_t off = 16;  // workgroup control: [0] next link group of the item
+  auto take = [](uint32_t& o, uint32_t bytes) {
+    const uint32_t r = o;
+    o += (bytes + 15u) & ~15u;
+    return r;
+  };
+  const uint32_t vw = (V + 31u) / 32u;
+  l.bdist = take(off, dist_bytes * V);
+  l.bnh = take(off, nb * V);
+  l.btight = take(off, 8u * ((E + 63u) / 64u));
+  uint32_t w = 16;  // wave control: [0] A count, [1] dirty count, [2] flag
+  l.w_ina = take(w, 4u * vw);
+  l.w_dq = take(w, 4u * vw);
+  l.w_nhm = take(w, 4u * vw);
+  l.w_adist = take(w, dist_bytes * V);
+  l.w_anh = take(w, nb * V);
+  l.w_alist = take(w, 2u * V);
+  l.w_dlist = take(w, 2u * V);
+  l.wave0 = off;
+  l.wstride = w;
+  l.total = off + kGrpWaves * w;
+  return l;
+}
+
+template <typename D>
+struct GrpWave {
+  const DevGraph* g;
+  uint32_t src, link, nb;
+  bool unit;
+  const D* bdist;
+  const uint8_t* bnh;
+  D* adist;
+  uint8_t* anh;
+  uint32_t *ina, *dq, *nhm, *ctl;
+  uint16_t *alist, *dlist;
+  __device__ uint32_t wout(uint32_t e) const { return unit ? 1u : g->w[e]; }
+  __device__ bool expands(uint32_t x) const { return x == src || !g->ovl[x]; }
+  // distance after the repair of (2): A nodes from the overlay, the rest from the base
+  __device__ D dist(uint32_t u) const { return bit_of(ina, u) ? adist[u] : bdist[u]; }
+  __device__ const uint8_t* nh(uint32_t u) const {
+    return bit_of(nhm, u) ? anh + (size_t)u * nb : bnh + (size_t)u * nb;
+  }
+};
+
+// live tight in-edge of v from outside A (base distances; step (1) only), wave-parallel
+template <typename D>
+__device__ bool grp_live_pred(const GrpWave<D>& c, uint32_t v, uint32_t lane) {
+  const DevGraph& g = *c.g;
+  constexpr D INF = (D)~(D)0;
+  const D dv = c.bdist[v];
+  const uint2 r = g.row2[v];
+  for (uint32_t e = r.x + lane; __any(e < r.y); e += 64u) {
+    bool ok = false;
+    if (e < r.y) {
+      const uint4 rec = g.erec[e];  // v->u: {u | down | sink(u), w(u->v), link, rev}
+      const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+      if (!(rec.x & kEdgeDown) && rec.z != c.link && (u == c.src || !(rec.x & kNodeSink)) && !bit_of(c.ina, u)) {
+        const D du = c.bdist[u];
+        ok = du != INF && (uint64_t)du + (c.unit ? 1u : rec.y) == (uint64_t)dv;
+      }
+    }
+    if (__any(ok)) return true;
+  }
+  return false;
+}
+
+template <typename D>
+__device__ bool grp_live_pred_lane(const GrpWave<D>& c, uint32_t v) {
+  const DevGraph& g = *c.g;
+  constexpr D INF = (D)~(D)0;
+  const D dv = c.bdist[v];
+  const uint2 r = g.row2[v];
+  for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+    uint4 rec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+      if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
+      if (u != c.src && (rec[q].x & kNodeSink)) continue;
+      const D du = c.bdist[u];
+      if (du != INF && (uint64_t)du + (c.unit ? 1u : rec[q].y) == (uint64_t)dv) return true;
+    }
+  }
+  return false;
+}
+
+// One affected unit: returns the changed-node count (uniform across the wave).
+template <typename D>
+__device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
+  const DevGraph& g = *c.g;
+  constexpr D INF = (D)~(D)0;
+  const uint32_t vw = (V + 31u) / 32u, nb = c.nb;
+  for (uint32_t i = lane; i < vw; i += 64u) {
+    c.ina[i] = 0;
+    c.dq[i] = 0;
+    c.nhm[i] = 0;
+  }
+  if (lane == 0) c.ctl[0] = c.ctl[1] = 0;
+  lds_fence();
+  // the tight direction a->b of the link (the caller checked one is tight)
+  const uint2 ee = g.ledge[c.link];
+  uint32_t bnode = UINT32_MAX;
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t e = t ? ee.y : ee.x;
+    const uint32_t av = g.adj[e];
+    const uint32_t head = av & ~kEdgeDown, tail = g.adj[g.rev[e]] & ~kEdgeDown;
+    if ((av & kEdgeDown) || !c.expands(tail)) continue;
+    const D dt = c.bdist[tail], dh = c.bdist[head];
+    if (dt != INF && dh != INF && (uint64_t)dt + c.wout(e) == (uint64_t)dh) bnode = head;
+  }
+  if (bnode == UINT32_MAX) return 0;
+  // (1) A by decremental propagation over the base tight DAG (base distances)
+  if (lane == 0) {
+    c.dq[bnode >> 5] |= 1u << (bnode & 31u);
+    c.dlist[c.ctl[1]++] = (uint16_t)bnode;
+  }
+  if (!grp_live_pred(c, bnode, lane) && lane == 0) {
+    c.ina[bnode >> 5] |= 1u << (bnode & 31u);
+    c.alist[c.ctl[0]++] = (uint16_t)bnode;
+  }
+  lds_fence();
+  // 8-lane groups: eight A members per wave pass (A only grows, so a successor tested by
+  // several groups is added once, by the bit's atomicOr; a pred that joins A later is
+  // itself processed later and re-tests its successors)
+  for (uint32_t idx0 = 0; idx0 < __builtin_amdgcn_readfirstlane(c.ctl[0]); idx0 += 8u) {
+    const uint32_t na0 = __builtin_amdgcn_readfirstlane(c.ctl[0]);
+    const uint32_t idx = idx0 + (lane >> 3), sub = lane & 7u;
+    if (idx < na0) {
+      const uint32_t x = c.alist[idx];
+      if (c.expands(x)) {
+        const D dx = c.bdist[x];
+        const uint2 r = g.row2[x];
+        for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
+          const uint32_t av = g.adj[e];
+          const uint32_t y = av & ~kEdgeDown;
+          if (!(av & kEdgeDown) && g.lid[e] != c.link && !bit_of(c.ina, y) && c.bdist[y] != INF &&
+              (uint64_t)dx + c.wout(e) == (uint64_t)c.bdist[y]) {
+            const uint32_t bit = 1u << (y & 31u);
+            if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
+            if (!grp_live_pred_lane(c, y)) {
+              if (!(atomicOr(&c.ina[y >> 5], bit) & bit)) c.alist[atomicAdd(&c.ctl[0], 1u)] = (uint16_t)y;
+            }
+          }
+        }
+      }
+    }
+    lds_fence();
+  }
+  const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
+  // (2) new distances inside A: best entry from outside A, then relaxation within A
+  for (uint32_t i = lane; i < na; i += 64u) {
+    const uint32_t x = c.alist[i];
+    const uint2 r = g.row2[x];
+    D best = INF;
+    for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+      uint4 rec[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+        if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
+        if (u != c.src && (rec[q].x & kNodeSink)) continue;
+        const D du = c.bdist[u];
+        if (du == INF) continue;
+        const D cand = du + (D)(c.unit ? 1u : rec[q].y);
+        best = cand < best ? cand : best;
+      }
+    }
+    c.adist[x] = best;
+  }
+  lds_fence();
+  for (;;) {
+    if (lane == 0) c.ctl[2] = 0;
+    lds_fence();
+    for (uint32_t i = lane; i < na; i += 64u) {
+      const uint32_t x = c.alist[i];
+      const D dx = c.adist[x];
+      if (dx == INF || !c.expands(x)) continue;
+      const uint2 r = g.row2[x];
+      for (uint32_t e = r.x; e < r.y; ++e) {
+        const uint32_t av = g.adj[e];
+        const uint32_t y = av & ~kEdgeDown;
+        if ((av & kEdgeDown) || g.lid[e] == c.link || !bit_of(c.ina, y)) continue;
+        const D cand = dx + (D)c.wout(e);
+        if (cand < c.adist[y]) {
+          atomicMin(&c.adist[y], cand);
+          c.ctl[2] = 1;
+        }
+      }
+    }
+    lds_fence();
+    if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
+  }
+  // (3) next hops in increasing new distance over the dirty set
+  uint32_t nchanged = 0;
+  uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
+  while (done < nd) {
+    D mn = INF;
+    for (uint32_t i = done + lane; i < nd; i += 64u) {
+      const D d = c.dist(c.dlist[i]);
+      mn = d < mn ? d : mn;
+    }
+    mn = wave_min_t(mn);
+    uint32_t nm = 0, nr = 0;
+    for (uint32_t i0 = done; i0 < nd; i0 += 64u) {
+      const uint32_t i = i0 + lane;
+      const bool live = i < nd;
+      const uint32_t v = live ? c.dlist[i] : 0u;
+      const bool in = live && c.dist(v) == mn;
+      const unsigned long long mi = __ballot(in), mr = __ballot(live && !in);
+      const unsigned long long lt = (1ull << lane) - 1ull;
+      if (in) c.alist[nm + (uint32_t)__popcll(mi & lt)] = (uint16_t)v;
+      if (live && !in) c.alist[V - 1u - (nr + (uint32_t)__popcll(mr & lt))] = (uint16_t)v;
+      nm += (uint32_t)__popcll(mi);
+      nr += (uint32_t)__popcll(mr);
+    }
+    lds_fence();
+    for (uint32_t i = lane; i < nm + nr; i += 64u)
+      c.dlist[done + i] = i < nm ? c.alist[i] : c.alist[V - 1u - (i - nm)];
+    if (lane == 0) c.ctl[1] = nd;
+    lds_fence();
+    uint32_t cnt_changed = 0;
+    for (uint32_t i0 = 0; i0 < nm; i0 += 64u) {
+      const uint32_t i = i0 + lane;
+      bool counted = false;
+      if (i < nm) {
+        const uint32_t v = c.dlist[done + i];
+        uint8_t acc[32];
+        uint32_t acc1 = 0;
+        if (nb > 1)
+          for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
+        const D dv = c.dist(v);
+        const uint2 r = g.row2[v];
+        if (dv != INF)
+          for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
+            uint4 rec[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
+              if ((rec[q].x & kEdgeDown) || rec[q].z == c.link) continue;
+              if (u != c.src && (rec[q].x & kNodeSink)) continue;
+              const D du = c.dist(u);
+              if (du == INF || (uint64_t)du + (c.unit ? 1u : rec[q].y) != (uint64_t)dv) continue;
+              if (u == c.src) {
+                const uint32_t bit = g.nbr[rec[q].w];
+                if (nb == 1) acc1 |= 1u << bit;
+                else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
+              } else {
+                const uint8_t* hu = c.nh(u);
+                if (nb == 1) acc1 |= hu[0];
+                else
+                  for (uint32_t b = 0; b < nb; ++b) acc[b] |= hu[b];
+              }
+            }
+          }
+        const uint8_t* hv = c.nh(v);
+        bool diff = false;
+        if (nb == 1) diff = (uint8_t)acc1 != hv[0];
+        else
+          for (uint32_t b = 0; b < nb; ++b) diff |= acc[b] != hv[b];
+        if (diff) {
+          uint8_t* o = c.anh + (size_t)v * nb;
+          if (nb == 1) o[0] = (uint8_t)acc1;
+          else
+            for (uint32_t b = 0; b < nb; ++b) o[b] = acc[b];
+          atomicOr(&c.nhm[v >> 5], 1u << (v & 31u));
+        }
+        const bool in_a = bit_of(c.ina, v);
+        counted = in_a || diff;
+        if (diff && !in_a && c.expands(v)) {
+          const uint2 ro = g.row2[v];
+          for (uint32_t e = ro.x; e < ro.y; ++e) {
+            const uint32_t av = g.adj[e];
+            const uint32_t y = av & ~kEdgeDown;
+            if ((av & kEdgeDown) || g.lid[e] == c.link || y == c.src) continue;
+            const D dy = c.dist(y);
+            if (dy == INF || (uint64_t)dv + c.wout(e) != (uint64_t)dy) continue;
+            const uint32_t bit = 1u << (y & 31u);
+            if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
+          }
+        }
+      }
+      cnt_changed += (uint32_t)__popcll(__ballot(counted));
+    }
+    nchanged += cnt_changed;
+    lds_fence();
+    done += nm;
+    nd = __builtin_amdgcn_readfirstlane(c.ctl[1]);
+  }
+  return nchanged;
+}
+
+template <typename D>
+__global__ __launch_bounds__(kGrpBlock) void whatif_group_kernel(DevGraph g, const uint32_t* links, uint32_t n_links,
+                                                                 const uint32_t* sources, uint32_t n_src,
+                                                                 uint32_t chunk, const uint64_t* base_dist,
+                                                                 const uint8_t* base_nh, const uint64_t* base_tight,
+                                                                 uint32_t nb, uint32_t unit, uint32_t* changed,
+                                                                 uint32_t* affected, uint32_t* ctr) {
+  constexpr D INF = (D)~(D)0;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t s_item;
+  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+  const uint32_t tw = (g.E + 63u) / 64u;
+  const GrpLayout lay = grp_layout(V, g.E, nb, sizeof(D));
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* wctl = smem;
+  D* bdist = reinterpret_cast<D*>(base + lay.bdist);
+  uint8_t* bnh = reinterpret_cast<uint8_t*>(base + lay.bnh);
+  uint64_t* btight = reinterpret_cast<uint64_t*>(base + lay.btight);
+  char* wb = base + lay.wave0 + wave * lay.wstride;
+  GrpWave<D> c;
+  c.g = &g;
+  c.nb = nb;
+  c.unit = unit != 0;
+  c.bdist = bdist;
+  c.bnh = bnh;
+  c.ctl = reinterpret_cast<uint32_t*>(wb);
+  c.ina = reinterpret_cast<uint32_t*>(wb + lay.w_ina);
+  c.dq = reinterpret_cast<uint32_t*>(wb + lay.w_dq);
+  c.nhm = reinterpret_cast<uint32_t*>(wb + lay.w_nhm);
+  c.adist = reinterpret_cast<D*>(wb + lay.w_adist);
+  c.anh = reinterpret_cast<uint8_t*>(wb + lay.w_anh);
+  c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
+  c.dlist = reinterpret_cast<uint16_t*>(wb + lay.w_dlist);
+  const uint32_t chunks = (n_links + chunk - 1u) / chunk;
+  const uint32_t items = n_src * chunks;
+  uint32_t n_aff = 0;
+  for (uint32_t item = blockIdx.x; item < items;) {
+    const uint32_t j = item / chunks, ch = item - j * chunks;
+    const uint32_t l0 = ch * chunk, l1 = min(n_links, l0 + chunk);
+    c.src = sources[j];
+    // stage source j's base rows (read once per item)
+    const uint64_t* drow = base_dist + (size_t)j * V;
+    for (uint32_t v = tid; v < V; v += kGrpBlock) {
+      const uint64_t d = drow[v];
+      bdist[v] = d == ~0ull ? INF : (D)d;
+    }
+    const uint8_t* hrow = base_nh + (size_t)j * V * nb;
+    const uint32_t nbytes = V * nb;
+    if (((reinterpret_cast<uintptr_t>(hrow) | nbytes) & 3u) == 0) {
+      for (uint32_t i = tid; i < nbytes / 4u; i += kGrpBlock)
+        reinterpret_cast<uint32_t*>(bnh)[i] = reinterpret_cast<const uint32_t*>(hrow)[i];
+    } else {
+      for (uint32_t i = tid; i < nbytes; i += kGrpBlock) bnh[i] = hrow[i];
+    }
+    const uint64_t* trow = base_tight + (size_t)j * tw;
+    for (uint32_t i = tid; i < tw; i += kGrpBlock) btight[i] = trow[i];
+    if (tid == 0) wctl[0] = 0;
+    __syncthreads();
+    // waves take groups of 64 links dynamically; a lane per link for the fused filter
+    for (;;) {
+      uint32_t grp = 0;
+      if (lane == 0) grp = atomicAdd(&wctl[0], 1u);
+      grp = __builtin_amdgcn_readfirstlane(__shfl(grp, 0));
+      const uint32_t li = l0 + grp * 64u;
+      if (li >= l1) break;
+      const uint32_t i = li + lane;
+      bool hit = false;
+      uint32_t l = 0;
+      if (i < l1) {
+        l = links[i];
+        const uint2 ee = l < g.L ? g.ledge[l] : make_uint2(UINT32_MAX, UINT32_MAX);
+        if (ee.x != UINT32_MAX)
+          hit = ((btight[ee.x >> 6] >> (ee.x & 63u)) & 1ull) || ((btight[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
+        if (!hit) changed[(size_t)i * n_src + j] = 0;
+      }
+      unsigned long long m = __ballot(hit);
+      n_aff += (uint32_t)__popcll(m);
+      while (m) {
+        const uint32_t k = (uint32_t)__ffsll((long long)m) - 1u;
+        m &= m - 1ull;
+        c.link = __builtin_amdgcn_readfirstlane(__shfl(l, (int)k));
+        const uint32_t cnt = grp_repair(c, lane, V);
+        if (lane == 0) changed[(size_t)(li + k) * n_src + j] = cnt;
+      }
+    }
+    __syncthreads();  // every wave is done with this item's shared rows and s_item
+    if (tid == 0) s_item = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    item = s_item;
+  }
+  if (lane == 0 && n_aff) atomicAdd(affected, n_aff);
+  bfs::retire_workgroup(ctr, nullptr);
+}
+
 __global__ __launch_bounds__(256) void iota_u32(uint32_t* p, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) p[i] = i;
 }
@@ -490,6 +907,38 @@ hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uin
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, s, g, wsrc, wlink, wunit, count, n_src, base_dist, base_nh, nb,
                      (uint32_t)unit_cost, changed, ctr);
+  return hipGetLastError();
+}
+
+uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64) {
+  if (V > 65535u || nb > 32u) return 0;
+  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u).total;
+  return t <= kMaxLds ? t : 0;
+}
+
+hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                               uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
+                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64,
+                               uint32_t* changed, uint32_t* affected, uint32_t* ctr, int num_cus, hipStream_t s) {
+  hipError_t err = hipMemsetAsync(affected, 0, sizeof(uint32_t), s);
+  if (err != hipSuccess || !n_links || !n_src) return err;
+  const uint32_t lds = whatif_group_lds_bytes(g.V, g.E, nb, dist64);
+  if (!lds) return hipErrorInvalidValue;
+  const uint32_t per_cu = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxLds / lds, 2048u / kGrpBlock));
+  const uint64_t slots = (uint64_t)num_cus * per_cu;
+  // work items of (source, chunk of links): ~8 per resident workgroup, so the tail is short
+  uint64_t cps = (8u * slots + n_src - 1u) / n_src;
+  cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
+  uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
+  chunk = bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30);
+  const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
+  if (items >= (1ull << 32)) return hipErrorInvalidValue;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
+  auto k = dist64 ? whatif_group_kernel<unsigned long long> : whatif_group_kernel<uint32_t>;
+  err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kGrpBlock), lds, s, g, links, n_links, sources, n_src, chunk, base_dist,
+                     base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr);
   return hipGetLastError();
 }
 

@@ -74,6 +74,10 @@ def lib():
         l.oracle_whatif.restype = ctypes.c_int
         l.oracle_whatif.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                     ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        l.faithful_all_sources.restype = ctypes.c_int
+        l.faithful_all_sources.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double)]
         l.oracle_num_distinct_neighbors.restype = ctypes.c_uint32
         l.oracle_num_distinct_neighbors.argtypes = [P(OracleGraph), ctypes.c_uint32]
         _lib = l
@@ -146,6 +150,28 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("oracle_all_sources failed")
         return dist, nh
+
+    def faithful_all_sources(self, sources: Sequence[int], use_link_metric: bool = True, nthreads: int = 1,
+                             want_dist: bool = False, want_nh: bool = False):
+        """runSpf per source with the reference's data structures (spf_faithful.cpp: string
+        keys, shared_ptr heap, unordered_set next hops): the faithful-cost CPU baseline.
+        Returns (dist | None, nh | None, seconds of solving)."""
+        g = self.g
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        n, V = src.shape[0], g.num_nodes
+        raw = [nm.encode() for nm in g.names]
+        pool = np.frombuffer(b"".join(raw) or b"\0", dtype=np.uint8)
+        off = np.zeros(V + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in raw])
+        dist = np.empty((n, V), dtype=np.uint64) if want_dist else None
+        nh = np.zeros((n, V, self.nh_bytes), dtype=np.uint8) if want_nh else None
+        secs = ctypes.c_double()
+        rc = lib().faithful_all_sources(ctypes.byref(self._s), _ptr(pool), _ptr(off), _ptr(src), n,
+                                        int(use_link_metric), nthreads, _ptr(dist), _ptr(nh), self.nh_bytes,
+                                        ctypes.byref(secs))
+        if rc != 0:
+            raise RuntimeError("faithful_all_sources failed")
+        return dist, nh, secs.value
 
     def ksp2_tokens(self, src: Sequence[int], dst: Sequence[int], tok_cap: int = 256, nthreads: int = 0):
         """getKthPaths(s, d, 1) and (.., 2) per pair as token rows [n, tok_cap] u32 (the

@@ -392,9 +392,10 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["incr", "solve"])
+@pytest.fixture(params=["group", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
-    """What-if units repaired incrementally from the base rows (default) or re-solved."""
+    """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
+    (default), per-unit incremental repair, or full re-solves."""
     monkeypatch.setenv("OPENR_SPF_WHATIF", request.param)
     return request.param
 

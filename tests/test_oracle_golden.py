@@ -102,3 +102,35 @@ def test_overloaded_source_still_expands():
     o = Oracle(g)
     assert set(o.spf_result(g.id("2")).keys()) == {"1", "2", "3"}
     assert set(o.spf_result(g.id("1")).keys()) == {"1", "2"}
+
+
+@pytest.mark.parametrize("make", [lambda: T.grid(10), lambda: T.fabric(288 + 2 * 56),
+                                  lambda: T.wan(200, 600, 64, seed=3, parallel_fraction=0.05)],
+                         ids=["grid10", "fabric", "wan-parallel"])
+def test_faithful_cost_baseline_matches_dense_oracle(make):
+    """oracle/spf_faithful.cpp (the reference-cost CPU baseline bench.py times: string-keyed
+    maps, shared_ptr heap) gives the dense oracle's dist and next-hop rows."""
+    g = make()
+    o = Oracle(g)
+    s = np.arange(g.num_nodes, dtype=np.uint32)
+    for use_metric in (True, False):
+        d, h = o.all_sources(s, use_metric, nthreads=4)
+        fd, fh, secs = o.faithful_all_sources(s, use_metric, nthreads=4, want_dist=True, want_nh=True)
+        assert np.array_equal(d, fd) and np.array_equal(h, fh) and secs > 0
+
+
+def test_faithful_cost_baseline_overloads():
+    rng = np.random.default_rng(4)
+    V = 120
+    links = np.array([(i, int(rng.integers(0, i))) for i in range(1, V)] +
+                     [tuple(rng.integers(0, V, 2)) for _ in range(200)])
+    links = links[links[:, 0] != links[:, 1]]
+    m1 = rng.integers(1, 9, len(links)).astype(np.uint64)
+    m2 = rng.integers(1, 9, len(links)).astype(np.uint64)
+    g = T.csr_from_links([f"x{rng.integers(0, 10**6)}-{i}" for i in range(V)], links, m1, m2,
+                         (rng.random(V) < 0.1).astype(np.uint8), (rng.random(len(links)) > 0.05).astype(np.uint8))
+    o = Oracle(g)
+    s = np.arange(V, dtype=np.uint32)
+    d, h = o.all_sources(s, True)
+    fd, fh, _ = o.faithful_all_sources(s, True, nthreads=3, want_dist=True, want_nh=True)
+    assert np.array_equal(d, fd) and np.array_equal(h, fh)
