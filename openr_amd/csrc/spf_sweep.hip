@@ -588,8 +588,8 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
   // 8-lane groups: eight A members per wave pass (A only grows, so a successor tested by
   // several groups is added once, by the bit's atomicOr; a pred that joins A later is
   // itself processed later and re-tests its successors)
-  for (uint32_t idx0 = 0; idx0 < __builtin_amdgcn_readfirstlane(c.ctl[0]); idx0 += 8u) {
-    const uint32_t na0 = __builtin_amdgcn_readfirstlane(c.ctl[0]);
+  for (uint32_t idx0 = 0, na0; idx0 < (na0 = __builtin_amdgcn_readfirstlane(c.ctl[0]));
+       idx0 += min(8u, na0 - idx0)) {  // members appended during a pass are taken by the next
     const uint32_t idx = idx0 + (lane >> 3), sub = lane & 7u;
     if (idx < na0) {
       const uint32_t x = c.alist[idx];
