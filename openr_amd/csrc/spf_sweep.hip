@@ -441,26 +441,78 @@ __global__ __launch_bounds__(64) void whatif_incr_kernel(DevGraph g, const uint3
 // --- grouped what-if: one workgroup per (source, chunk of links) -----------------------
 //
 // The same repair as whatif_incr_kernel (A set by decremental propagation, distances
-// inside A, next hops over the dirty set in increasing new distance), restructured so a
-// source's base rows are read from HBM/L2 ONCE per work item instead of once per unit:
-// the workgroup stages dist / next hops / tight mask of source j in LDS (read-only, shared
-// by its 4 wavefronts) and every wavefront repairs the affected links of the item one
-// after another on a private OVERLAY: new distances of A nodes (valid where the wave's A
-// bit is set) and rewritten next-hop sets (valid where its nh bit is set); everything else
-// reads the shared base. Per unit only three V-bit masks are cleared. The link filter is
-// fused (a link with no tight edge of the base SPF of j is unaffected: changed = 0), so
-// there is no global work list and no host round trip. Unit (i, j) writes
-// changed[i * n_src + j].
-constexpr uint32_t kGrpBlock = 256;
-constexpr uint32_t kGrpWaves = kGrpBlock / 64u;
+// inside A, next hops over the dirty set in increasing new distance), restructured for
+// the hardware:
+//  * a source's base rows are read ONCE per work item instead of once per unit: the
+//    workgroup stages dist / next hops / tight mask of source j in LDS (read-only, shared
+//    by its wavefronts) and every wavefront repairs affected links of the item one after
+//    another on a private OVERLAY: new distances of A nodes (valid where the wave's A bit
+//    is set) and rewritten next-hop sets (valid where its nh bit is set); everything else
+//    reads the shared base. Per unit only three V-bit masks are cleared;
+//  * the repair is a chain of small dependent graph reads (rows, edge records) — L2
+//    latency dominated it. When the graph fits (V, L <= 32767, usable metrics <= 65535),
+//    each workgroup stages a compact copy of the graph in LDS once per launch
+//    (GraphView<true>: row pointers, 8-byte edge records, next-hop bit of in-edges from
+//    the source, overload bits), so every read of the repair is an LDS read;
+//  * the link filter is fused (a link with no tight edge of the base SPF of j leaves the
+//    unit unchanged: 0), so there is no global work list and no host round trip.
+// Unit (i, j) writes changed[i * n_src + j].
+struct EdgeRec {
+  uint32_t col, lid, wout, win;  // e = x -> col: its link, metric x->col and col->x
+  bool down, sink;               // !Link::isUp(), col overloaded
+};
+
+template <bool LG>
+struct GraphView;
+template <>
+struct GraphView<false> {  // the device mirror in global memory
+  const DevGraph* g;
+  __device__ uint2 row(uint32_t x) const { return g->row2[x]; }
+  __device__ EdgeRec rec(uint32_t e) const {
+    const uint4 r = g->erec[e];
+    EdgeRec o;
+    o.col = r.x & ~(kEdgeDown | kNodeSink);
+    o.down = (r.x & kEdgeDown) != 0;
+    o.sink = (r.x & kNodeSink) != 0;
+    o.win = r.y;
+    o.lid = r.z;
+    o.wout = g->w[e];
+    return o;
+  }
+  __device__ uint32_t nbr_in(uint32_t e) const { return g->nbr[g->erec[e].w]; }
+  __device__ bool ovl(uint32_t x) const { return g->ovl[x] != 0; }
+};
+template <>
+struct GraphView<true> {  // compact LDS copy
+  const uint32_t* rowp;   // [V+1]
+  const uint2* crec;      // [E] {col | down << 15 | lid << 16 | sink << 31, wout | win << 16}
+  const uint8_t* nbrin;   // [E] next-hop bit of the in-edge col -> x when col is the source
+  const uint32_t* ovlb;   // [ceil(V/32)]
+  __device__ uint2 row(uint32_t x) const { return make_uint2(rowp[x], rowp[x + 1]); }
+  __device__ EdgeRec rec(uint32_t e) const {
+    const uint2 r = crec[e];
+    EdgeRec o;
+    o.col = r.x & 0x7FFFu;
+    o.down = (r.x >> 15) & 1u;
+    o.lid = (r.x >> 16) & 0x7FFFu;
+    o.sink = (r.x >> 31) != 0;
+    o.wout = r.y & 0xFFFFu;
+    o.win = r.y >> 16;
+    return o;
+  }
+  __device__ uint32_t nbr_in(uint32_t e) const { return nbrin[e]; }
+  __device__ bool ovl(uint32_t x) const { return (ovlb[x >> 5] >> (x & 31u)) & 1u; }
+};
 
 struct GrpLayout {
-  uint32_t bdist, bnh, btight, wave0, wstride;  // wave w's block at wave0 + w * wstride
+  uint32_t grow, grec, gnbr, govl;                                  // LDS graph (LG only)
+  uint32_t bdist, bnh, btight, wave0, wstride;                      // wave w at wave0 + w * wstride
   uint32_t w_ina, w_dq, w_nhm, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
   uint32_t total;
 };
 
-__host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t nb, uint32_t dist_bytes) {
+__host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t nb, uint32_t dist_bytes, bool lg,
+                                                uint32_t waves) {
   GrpLayout l;
   uint32_t off = 16;  // workgroup control: [0] next link group of the item
   auto take = [](uint32_t& o, uint32_t bytes) {
@@ -469,6 +521,10 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
     return r;
   };
   const uint32_t vw = (V + 31u) / 32u;
+  l.grow = lg ? take(off, 4u * (V + 1u)) : 0u;
+  l.grec = lg ? take(off, 8u * E) : 0u;
+  l.gnbr = lg ? take(off, E) : 0u;
+  l.govl = lg ? take(off, 4u * vw) : 0u;
   l.bdist = take(off, dist_bytes * V);
   l.bnh = take(off, nb * V);
   l.btight = take(off, 8u * ((E + 63u) / 64u));
@@ -482,13 +538,14 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
   l.w_dlist = take(w, 2u * V);
   l.wave0 = off;
   l.wstride = w;
-  l.total = off + kGrpWaves * w;
+  l.total = off + waves * w;
   return l;
 }
 
-template <typename D>
+template <typename D, bool LG>
 struct GrpWave {
-  const DevGraph* g;
+  const DevGraph* g;  // ledge / rev / adj of the unit's link (read once per unit)
+  GraphView<LG> gv;
   uint32_t src, link, nb;
   bool unit;
   const D* bdist;
@@ -497,30 +554,31 @@ struct GrpWave {
   uint8_t* anh;
   uint32_t *ina, *dq, *nhm, *ctl;
   uint16_t *alist, *dlist;
-  __device__ uint32_t wout(uint32_t e) const { return unit ? 1u : g->w[e]; }
-  __device__ bool expands(uint32_t x) const { return x == src || !g->ovl[x]; }
+  __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
+  __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
+  __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
   // distance after the repair of (2): A nodes from the overlay, the rest from the base
   __device__ D dist(uint32_t u) const { return bit_of(ina, u) ? adist[u] : bdist[u]; }
   __device__ const uint8_t* nh(uint32_t u) const {
     return bit_of(nhm, u) ? anh + (size_t)u * nb : bnh + (size_t)u * nb;
   }
+  // in-edge u -> v (the record of v -> u) usable, not the failed link, u may expand
+  __device__ bool in_usable(const EdgeRec& r) const { return !r.down && r.lid != link && (r.col == src || !r.sink); }
 };
 
 // live tight in-edge of v from outside A (base distances; step (1) only), wave-parallel
-template <typename D>
-__device__ bool grp_live_pred(const GrpWave<D>& c, uint32_t v, uint32_t lane) {
-  const DevGraph& g = *c.g;
+template <typename D, bool LG>
+__device__ bool grp_live_pred(const GrpWave<D, LG>& c, uint32_t v, uint32_t lane) {
   constexpr D INF = (D)~(D)0;
   const D dv = c.bdist[v];
-  const uint2 r = g.row2[v];
+  const uint2 r = c.gv.row(v);
   for (uint32_t e = r.x + lane; __any(e < r.y); e += 64u) {
     bool ok = false;
     if (e < r.y) {
-      const uint4 rec = g.erec[e];  // v->u: {u | down | sink(u), w(u->v), link, rev}
-      const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-      if (!(rec.x & kEdgeDown) && rec.z != c.link && (u == c.src || !(rec.x & kNodeSink)) && !bit_of(c.ina, u)) {
-        const D du = c.bdist[u];
-        ok = du != INF && (uint64_t)du + (c.unit ? 1u : rec.y) == (uint64_t)dv;
+      const EdgeRec q = c.gv.rec(e);
+      if (c.in_usable(q) && !bit_of(c.ina, q.col)) {
+        const D du = c.bdist[q.col];
+        ok = du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv;
       }
     }
     if (__any(ok)) return true;
@@ -528,31 +586,23 @@ __device__ bool grp_live_pred(const GrpWave<D>& c, uint32_t v, uint32_t lane) {
   return false;
 }
 
-template <typename D>
-__device__ bool grp_live_pred_lane(const GrpWave<D>& c, uint32_t v) {
-  const DevGraph& g = *c.g;
+template <typename D, bool LG>
+__device__ bool grp_live_pred_lane(const GrpWave<D, LG>& c, uint32_t v) {
   constexpr D INF = (D)~(D)0;
   const D dv = c.bdist[v];
-  const uint2 r = g.row2[v];
-  for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
-    uint4 rec[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
-      if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
-      if (u != c.src && (rec[q].x & kNodeSink)) continue;
-      const D du = c.bdist[u];
-      if (du != INF && (uint64_t)du + (c.unit ? 1u : rec[q].y) == (uint64_t)dv) return true;
-    }
+  const uint2 r = c.gv.row(v);
+  for (uint32_t e = r.x; e < r.y; ++e) {
+    const EdgeRec q = c.gv.rec(e);
+    if (!c.in_usable(q) || bit_of(c.ina, q.col)) continue;
+    const D du = c.bdist[q.col];
+    if (du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv) return true;
   }
   return false;
 }
 
 // One affected unit: returns the changed-node count (uniform across the wave).
-template <typename D>
-__device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
+template <typename D, bool LG>
+__device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
   const DevGraph& g = *c.g;
   constexpr D INF = (D)~(D)0;
   const uint32_t vw = (V + 31u) / 32u, nb = c.nb;
@@ -572,7 +622,7 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
     const uint32_t head = av & ~kEdgeDown, tail = g.adj[g.rev[e]] & ~kEdgeDown;
     if ((av & kEdgeDown) || !c.expands(tail)) continue;
     const D dt = c.bdist[tail], dh = c.bdist[head];
-    if (dt != INF && dh != INF && (uint64_t)dt + c.wout(e) == (uint64_t)dh) bnode = head;
+    if (dt != INF && dh != INF && (uint64_t)dt + (c.unit ? 1u : g.w[e]) == (uint64_t)dh) bnode = head;
   }
   if (bnode == UINT32_MAX) return 0;
   // (1) A by decremental propagation over the base tight DAG (base distances)
@@ -595,12 +645,12 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
       const uint32_t x = c.alist[idx];
       if (c.expands(x)) {
         const D dx = c.bdist[x];
-        const uint2 r = g.row2[x];
+        const uint2 r = c.gv.row(x);
         for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
-          const uint32_t av = g.adj[e];
-          const uint32_t y = av & ~kEdgeDown;
-          if (!(av & kEdgeDown) && g.lid[e] != c.link && !bit_of(c.ina, y) && c.bdist[y] != INF &&
-              (uint64_t)dx + c.wout(e) == (uint64_t)c.bdist[y]) {
+          const EdgeRec q = c.gv.rec(e);
+          const uint32_t y = q.col;
+          if (!q.down && q.lid != c.link && !bit_of(c.ina, y) && c.bdist[y] != INF &&
+              (uint64_t)dx + c.w(q) == (uint64_t)c.bdist[y]) {
             const uint32_t bit = 1u << (y & 31u);
             if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
             if (!grp_live_pred_lane(c, y)) {
@@ -616,22 +666,15 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
   // (2) new distances inside A: best entry from outside A, then relaxation within A
   for (uint32_t i = lane; i < na; i += 64u) {
     const uint32_t x = c.alist[i];
-    const uint2 r = g.row2[x];
+    const uint2 r = c.gv.row(x);
     D best = INF;
-    for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
-      uint4 rec[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
-        if ((rec[q].x & kEdgeDown) || rec[q].z == c.link || bit_of(c.ina, u)) continue;
-        if (u != c.src && (rec[q].x & kNodeSink)) continue;
-        const D du = c.bdist[u];
-        if (du == INF) continue;
-        const D cand = du + (D)(c.unit ? 1u : rec[q].y);
-        best = cand < best ? cand : best;
-      }
+    for (uint32_t e = r.x; e < r.y; ++e) {
+      const EdgeRec q = c.gv.rec(e);
+      if (!c.in_usable(q) || bit_of(c.ina, q.col)) continue;
+      const D du = c.bdist[q.col];
+      if (du == INF) continue;
+      const D cand = du + (D)c.wi(q);
+      best = cand < best ? cand : best;
     }
     c.adist[x] = best;
   }
@@ -643,14 +686,13 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
       const uint32_t x = c.alist[i];
       const D dx = c.adist[x];
       if (dx == INF || !c.expands(x)) continue;
-      const uint2 r = g.row2[x];
+      const uint2 r = c.gv.row(x);
       for (uint32_t e = r.x; e < r.y; ++e) {
-        const uint32_t av = g.adj[e];
-        const uint32_t y = av & ~kEdgeDown;
-        if ((av & kEdgeDown) || g.lid[e] == c.link || !bit_of(c.ina, y)) continue;
-        const D cand = dx + (D)c.wout(e);
-        if (cand < c.adist[y]) {
-          atomicMin(&c.adist[y], cand);
+        const EdgeRec q = c.gv.rec(e);
+        if (q.down || q.lid == c.link || !bit_of(c.ina, q.col)) continue;
+        const D cand = dx + (D)c.w(q);
+        if (cand < c.adist[q.col]) {
+          atomicMin(&c.adist[q.col], cand);
           c.ctl[2] = 1;
         }
       }
@@ -697,29 +739,23 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
         if (nb > 1)
           for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
         const D dv = c.dist(v);
-        const uint2 r = g.row2[v];
+        const uint2 r = c.gv.row(v);
         if (dv != INF)
-          for (uint32_t e0 = r.x; e0 < r.y; e0 += 4u) {
-            uint4 rec[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rec[q] = e0 + q < r.y ? g.erec[e0 + q] : make_uint4(kEdgeDown, 0u, 0u, 0u);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const uint32_t u = rec[q].x & ~(kEdgeDown | kNodeSink);
-              if ((rec[q].x & kEdgeDown) || rec[q].z == c.link) continue;
-              if (u != c.src && (rec[q].x & kNodeSink)) continue;
-              const D du = c.dist(u);
-              if (du == INF || (uint64_t)du + (c.unit ? 1u : rec[q].y) != (uint64_t)dv) continue;
-              if (u == c.src) {
-                const uint32_t bit = g.nbr[rec[q].w];
-                if (nb == 1) acc1 |= 1u << bit;
-                else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
-              } else {
-                const uint8_t* hu = c.nh(u);
-                if (nb == 1) acc1 |= hu[0];
-                else
-                  for (uint32_t b = 0; b < nb; ++b) acc[b] |= hu[b];
-              }
+          for (uint32_t e = r.x; e < r.y; ++e) {
+            const EdgeRec q = c.gv.rec(e);
+            if (!c.in_usable(q)) continue;
+            const uint32_t u = q.col;
+            const D du = c.dist(u);
+            if (du == INF || (uint64_t)du + c.wi(q) != (uint64_t)dv) continue;
+            if (u == c.src) {
+              const uint32_t bit = c.gv.nbr_in(e);
+              if (nb == 1) acc1 |= 1u << bit;
+              else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
+            } else {
+              const uint8_t* hu = c.nh(u);
+              if (nb == 1) acc1 |= hu[0];
+              else
+                for (uint32_t b = 0; b < nb; ++b) acc[b] |= hu[b];
             }
           }
         const uint8_t* hv = c.nh(v);
@@ -737,13 +773,13 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
         const bool in_a = bit_of(c.ina, v);
         counted = in_a || diff;
         if (diff && !in_a && c.expands(v)) {
-          const uint2 ro = g.row2[v];
+          const uint2 ro = c.gv.row(v);
           for (uint32_t e = ro.x; e < ro.y; ++e) {
-            const uint32_t av = g.adj[e];
-            const uint32_t y = av & ~kEdgeDown;
-            if ((av & kEdgeDown) || g.lid[e] == c.link || y == c.src) continue;
+            const EdgeRec q = c.gv.rec(e);
+            const uint32_t y = q.col;
+            if (q.down || q.lid == c.link || y == c.src) continue;
             const D dy = c.dist(y);
-            if (dy == INF || (uint64_t)dv + c.wout(e) != (uint64_t)dy) continue;
+            if (dy == INF || (uint64_t)dv + c.w(q) != (uint64_t)dy) continue;
             const uint32_t bit = 1u << (y & 31u);
             if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
           }
@@ -759,27 +795,50 @@ __device__ uint32_t grp_repair(GrpWave<D>& c, uint32_t lane, uint32_t V) {
   return nchanged;
 }
 
-template <typename D>
-__global__ __launch_bounds__(kGrpBlock) void whatif_group_kernel(DevGraph g, const uint32_t* links, uint32_t n_links,
-                                                                 const uint32_t* sources, uint32_t n_src,
-                                                                 uint32_t chunk, const uint64_t* base_dist,
-                                                                 const uint8_t* base_nh, const uint64_t* base_tight,
-                                                                 uint32_t nb, uint32_t unit, uint32_t* changed,
-                                                                 uint32_t* affected, uint32_t* ctr) {
+constexpr uint32_t kGrpMaxBlock = 512;
+
+template <typename D, bool LG>
+__global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
+    DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
+    const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
+    uint32_t* changed, uint32_t* affected, uint32_t* ctr) {
   constexpr D INF = (D)~(D)0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_item;
-  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
-  const uint32_t tw = (g.E + 63u) / 64u;
-  const GrpLayout lay = grp_layout(V, g.E, nb, sizeof(D));
+  const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+  const uint32_t block = blockDim.x, waves = block >> 6;
+  const uint32_t tw = (E + 63u) / 64u, vw = (V + 31u) / 32u;
+  const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* wctl = smem;
   D* bdist = reinterpret_cast<D*>(base + lay.bdist);
   uint8_t* bnh = reinterpret_cast<uint8_t*>(base + lay.bnh);
   uint64_t* btight = reinterpret_cast<uint64_t*>(base + lay.btight);
   char* wb = base + lay.wave0 + wave * lay.wstride;
-  GrpWave<D> c;
+  GrpWave<D, LG> c;
   c.g = &g;
+  if constexpr (LG) {
+    // stage the compact graph once per workgroup (a launch serves many items)
+    uint32_t* rowp = reinterpret_cast<uint32_t*>(base + lay.grow);
+    uint2* crec = reinterpret_cast<uint2*>(base + lay.grec);
+    uint8_t* nbrin = reinterpret_cast<uint8_t*>(base + lay.gnbr);
+    uint32_t* ovlb = reinterpret_cast<uint32_t*>(base + lay.govl);
+    for (uint32_t v = tid; v <= V; v += block) rowp[v] = g.row[v];
+    for (uint32_t e = tid; e < E; e += block) {
+      const uint4 r = g.erec[e];  // e = x -> col: {col | down | sink(col), w(col -> x), link, rev}
+      const uint32_t col = r.x & ~(kEdgeDown | kNodeSink);
+      crec[e] = make_uint2(col | ((r.x & kEdgeDown) ? 0x8000u : 0u) | (r.z << 16) | ((r.x & kNodeSink) ? 0x80000000u : 0u),
+                           (g.w[e] & 0xFFFFu) | (r.y << 16));
+      nbrin[e] = (uint8_t)g.nbr[r.w];
+    }
+    for (uint32_t i = tid; i < vw; i += block) ovlb[i] = g.ovl_bits[i];
+    c.gv.rowp = rowp;
+    c.gv.crec = crec;
+    c.gv.nbrin = nbrin;
+    c.gv.ovlb = ovlb;
+  } else {
+    c.gv.g = &g;
+  }
   c.nb = nb;
   c.unit = unit != 0;
   c.bdist = bdist;
@@ -801,20 +860,20 @@ __global__ __launch_bounds__(kGrpBlock) void whatif_group_kernel(DevGraph g, con
     c.src = sources[j];
     // stage source j's base rows (read once per item)
     const uint64_t* drow = base_dist + (size_t)j * V;
-    for (uint32_t v = tid; v < V; v += kGrpBlock) {
+    for (uint32_t v = tid; v < V; v += block) {
       const uint64_t d = drow[v];
       bdist[v] = d == ~0ull ? INF : (D)d;
     }
     const uint8_t* hrow = base_nh + (size_t)j * V * nb;
     const uint32_t nbytes = V * nb;
     if (((reinterpret_cast<uintptr_t>(hrow) | nbytes) & 3u) == 0) {
-      for (uint32_t i = tid; i < nbytes / 4u; i += kGrpBlock)
+      for (uint32_t i = tid; i < nbytes / 4u; i += block)
         reinterpret_cast<uint32_t*>(bnh)[i] = reinterpret_cast<const uint32_t*>(hrow)[i];
     } else {
-      for (uint32_t i = tid; i < nbytes; i += kGrpBlock) bnh[i] = hrow[i];
+      for (uint32_t i = tid; i < nbytes; i += block) bnh[i] = hrow[i];
     }
     const uint64_t* trow = base_tight + (size_t)j * tw;
-    for (uint32_t i = tid; i < tw; i += kGrpBlock) btight[i] = trow[i];
+    for (uint32_t i = tid; i < tw; i += block) btight[i] = trow[i];
     if (tid == 0) wctl[0] = 0;
     __syncthreads();
     // waves take groups of 64 links dynamically; a lane per link for the fused filter
@@ -910,21 +969,49 @@ hipError_t launch_whatif_incr(const DevGraph& g, const uint32_t* wsrc, const uin
   return hipGetLastError();
 }
 
+namespace {
+// LDS graph eligibility: ids / link ids / metrics fit the compact record, next-hop bits a byte
+bool grp_lds_graph_ok(const DevGraph& g, uint32_t w_max, uint32_t nh_bits) {
+  return g.V <= 32767u && g.L <= 32767u && w_max <= 65535u && nh_bits <= 256u &&
+         bfs::env_u32("OPENR_SPF_WHATIF_LDSG", 1u, 0u, 1u);
+}
+}  // namespace
+
 uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64) {
   if (V > 65535u || nb > 32u) return 0;
-  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u).total;
+  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u, false, 4).total;
   return t <= kMaxLds ? t : 0;
 }
 
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
-                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64,
-                               uint32_t* changed, uint32_t* affected, uint32_t* ctr, int num_cus, hipStream_t s) {
+                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
+                               uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ctr, int num_cus,
+                               hipStream_t s) {
   hipError_t err = hipMemsetAsync(affected, 0, sizeof(uint32_t), s);
   if (err != hipSuccess || !n_links || !n_src) return err;
-  const uint32_t lds = whatif_group_lds_bytes(g.V, g.E, nb, dist64);
-  if (!lds) return hipErrorInvalidValue;
-  const uint32_t per_cu = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxLds / lds, 2048u / kGrpBlock));
+  const uint32_t db = dist64 ? 8u : 4u;
+  // the LDS-graph variant with as many waves per workgroup (one workgroup per CU) as fit,
+  // else the global-graph variant at 4 waves per workgroup
+  bool lg = false;
+  uint32_t waves = 4, lds = 0;
+  if (grp_lds_graph_ok(g, w_max, nh_bits)) {
+    for (uint32_t w = kGrpMaxBlock / 64u; w >= 2u; --w) {
+      const uint32_t t = grp_layout(g.V, g.E, nb, db, true, w).total;
+      if (t <= kMaxLds) {
+        lg = true;
+        waves = w;
+        lds = t;
+        break;
+      }
+    }
+  }
+  if (!lg) {
+    lds = whatif_group_lds_bytes(g.V, g.E, nb, dist64);
+    if (!lds) return hipErrorInvalidValue;
+  }
+  const uint32_t block = 64u * waves;
+  const uint32_t per_cu = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxLds / lds, 2048u / block));
   const uint64_t slots = (uint64_t)num_cus * per_cu;
   // work items of (source, chunk of links): ~8 per resident workgroup, so the tail is short
   uint64_t cps = (8u * slots + n_src - 1u) / n_src;
@@ -934,11 +1021,23 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
-  auto k = dist64 ? whatif_group_kernel<unsigned long long> : whatif_group_kernel<uint32_t>;
-  err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return err;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kGrpBlock), lds, s, g, links, n_links, sources, n_src, chunk, base_dist,
-                     base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr);
+#define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
+  do {                                                                                                         \
+    auto k = whatif_group_kernel<DT, LGV>;                                                                     \
+    err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                              (int)lds);                                                                       \
+    if (err != hipSuccess) return err;                                                                         \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
+                       base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr);                  \
+  } while (0)
+  if (dist64) {
+    if (lg) OPENR_GRP_LAUNCH(unsigned long long, true);
+    else OPENR_GRP_LAUNCH(unsigned long long, false);
+  } else {
+    if (lg) OPENR_GRP_LAUNCH(uint32_t, true);
+    else OPENR_GRP_LAUNCH(uint32_t, false);
+  }
+#undef OPENR_GRP_LAUNCH
   return hipGetLastError();
 }
 

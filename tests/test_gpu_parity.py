@@ -392,11 +392,16 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "incr", "solve"])
+@pytest.fixture(params=["group", "group-global", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
-    (default), per-unit incremental repair, or full re-solves."""
-    monkeypatch.setenv("OPENR_SPF_WHATIF", request.param)
+    (default; graph staged in LDS too, or read from global memory), per-unit incremental
+    repair, or full re-solves."""
+    mode = request.param
+    if mode == "group-global":
+        mode = "group"
+        monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "0")
+    monkeypatch.setenv("OPENR_SPF_WHATIF", mode)
     return request.param
 
 
