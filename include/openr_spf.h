@@ -39,22 +39,27 @@
  *   - There is no CPU fallback: if the HIP runtime or a device is unavailable,
  *     openr_spf_create fails with OPENR_SPF_ENODEV.
  *
- * Semantics (bit-exact with LinkState::runSpf for strictly positive metrics)
+ * Semantics (bit-exact with LinkState::runSpf, any metric values)
  *   dist[s][v]   u64 shortest distance (NodeSpfResult::metric), UINT64_MAX if v is not
  *                in the SpfResult (unreachable). dist[s][src] = 0.
  *   nh[s][v][b]  next-hop set of v as a bitset over the source's DISTINCT neighbours in
  *                CSR row order: bit i (byte i/8, bit i%8) <-> the i-th distinct `col`
  *                value of row src (openr_spf_neighbor_map). nh bits of src itself are 0.
  *   tight[s][w]  (OPENR_SPF_EMIT_TIGHT) bit e of the E-bit mask is set iff directed edge e
- *                u->v is on a shortest path: usable, dist[u]+w(e)==dist[v], and u may
- *                expand (u==src or !node_overloaded[u]). NodeSpfResult::pathLinks(v) is
- *                the tight in-edges of v ordered by (dist[u], name_rank[u]) then by
- *                position of e in row u.
+ *                u->v is in NodeSpfResult::pathLinks(v). For metrics in [1, 2^31-1] these
+ *                are the tight in-edges: usable, dist[u]+w(e)==dist[v], u may expand
+ *                (u==src or !node_overloaded[u]); pathLinks(v) orders them by
+ *                (dist[u], name_rank[u]) then by position of e in row u. In general
+ *                pathLinks(v) orders them by the pop index of u (openr_spf_solve_order)
+ *                then by row position.
  *   A directed edge is usable iff edge_up[e] and link_id[e] is not in the solve's
  *   ignore set. Overloaded nodes other than the source are reached but never expanded.
- *   Metrics of usable edges must lie in [1, 2^31-1] when OPENR_SPF_USE_LINK_METRIC is
- *   set (the i32 Adjacency.metric range); zero or wrapped-negative metrics make the
- *   reference's pop order history-dependent and are rejected with OPENR_SPF_ENOTSUP.
+ *   Usable metrics in [1, 2^31-1] (the positive i32 Adjacency.metric range) run on the
+ *   fast kernels. Zero or wrapped-negative metrics (an i32 < 0 stored as u64, sums wrap
+ *   mod 2^64 as in the reference) make the pop order history-dependent; those graphs,
+ *   next-hop sets wider than 256 and graphs beyond the LDS-resident layouts run on the
+ *   exact-order kernel, which replays the reference's heap process (slower, same
+ *   results). openr_spf_ksp2 needs metrics in [1, 2^31-1] (OPENR_SPF_ENOTSUP otherwise).
  */
 #ifndef OPENR_SPF_H
 #define OPENR_SPF_H
@@ -74,12 +79,13 @@ enum {
   OPENR_SPF_ENODEV = -19,   /* no usable GPU / HIP runtime */
   OPENR_SPF_EINVAL = -22,   /* bad argument (null, out of range, no graph set) */
   OPENR_SPF_E2BIG = -7,     /* graph too large for the engine (see openr_spf_limits) */
-  OPENR_SPF_ENOTSUP = -95,  /* metric outside [1, 2^31-1] on a usable edge */
+  OPENR_SPF_ENOTSUP = -95,  /* KSP2 on a graph with a metric outside [1, 2^31-1] */
 };
 
 enum {
   OPENR_SPF_USE_LINK_METRIC = 1u << 0, /* runSpf useLinkMetric; else every hop costs 1 */
   OPENR_SPF_EMIT_TIGHT = 1u << 1,      /* fill tight[] (pathLinks reconstruction)      */
+  OPENR_SPF_EMIT_ORDER = 1u << 2,      /* exact-order kernel (openr_spf_solve_order)  */
 };
 
 typedef struct openr_spf_ctx openr_spf_ctx;
@@ -138,6 +144,16 @@ int openr_spf_neighbor_map(const openr_spf_ctx* ctx, uint32_t src, uint32_t* out
 int openr_spf_solve(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n,
                     uint32_t flags, uint64_t* dist, uint8_t* nh, uint32_t nh_bytes,
                     uint64_t* tight);
+
+/* As openr_spf_solve_ignore (ignore_ptr may be NULL: no ignore sets), plus order [n][V]:
+   the index at which runSpf popped v from its queue (0 = the source), UINT32_MAX if v is
+   not in the SpfResult. Always runs the exact-order kernel; pathLinks(v) = the tight[]
+   in-edges of v sorted by order[u], then by row position (what LinkState needs when
+   metrics can be zero). */
+int openr_spf_solve_order(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n,
+                          uint32_t flags, const uint32_t* ignore_ptr,
+                          const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
+                          uint32_t nh_bytes, uint64_t* tight, uint32_t* order);
 
 /* As openr_spf_solve with a per-solve ignore set: solve i ignores the links
    ignore_links[ignore_ptr[i] .. ignore_ptr[i+1]) (ignore_ptr has n+1 entries). */

@@ -8,6 +8,7 @@
 #include "LinkState.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <sstream>
@@ -559,7 +560,7 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   for (uint32_t i = 0; i < V; ++i) m.id.emplace(m.names[i], i);
   m.nameRank.resize(V);
   for (uint32_t i = 0; i < V; ++i) m.nameRank[i] = i;
-  std::unordered_map<const Link*, uint32_t> linkIds;
+  auto& linkIds = m.linkIndex;
   // every link appears in the rows of its two ends: size the columns once
   const size_t maxE = 2 * allLinks_.size();
   linkIds.reserve(allLinks_.size());
@@ -580,6 +581,7 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
       if (ins.second) m.links.push_back(link);
       m.col.push_back(m.id.at(link->getOtherNodeName(name)));
       m.metric.push_back(link->getMetricFromNode(name));
+      if (link->isUp() && (m.metric.back() == 0 || m.metric.back() > 0x7FFFFFFFull)) m.metricsPositive = false;
       m.linkId.push_back(ins.first->second);
       m.edgeUp.push_back(link->isUp() ? 1 : 0);
       m.edgeOwner.push_back(u);
@@ -588,7 +590,10 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   }
   mirror_ = std::move(m);
   mirrorDirty_ = false;
-  ++mirrorGeneration_;
+  // process-wide: a graph uploaded by another LinkState (or by an earlier object at this
+  // address) never matches this mirror's generation
+  static std::atomic<uint64_t> generations{0};
+  mirrorGeneration_ = ++generations;
   return mirror_;
 }
 
@@ -634,12 +639,15 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
     std::vector<uint64_t> dist(n * V), tight(n * std::max<uint32_t>(tw, 1));
     std::vector<uint8_t> nh(n * V * nb);
     const uint32_t flags = (useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u) | (uint32_t)OPENR_SPF_EMIT_TIGHT;
+    // zero / wrapped metrics: pop order is history-dependent, take it from the exact kernel
+    const bool wantOrder = useLinkMetric && !m.metricsPositive;
+    std::vector<uint32_t> popIndex(wantOrder ? n * V : 0);
     bool anyIgnore = false;
     for (size_t k = 0; k < n; ++k) anyIgnore |= ignores[slot[k]] && !ignores[slot[k]]->empty();
+    std::vector<uint32_t> ptr, links;
     if (anyIgnore) {
-      std::unordered_map<const Link*, uint32_t> lid;
-      for (uint32_t l = 0; l < m.links.size(); ++l) lid.emplace(m.links[l].get(), l);
-      std::vector<uint32_t> ptr(n + 1, 0), links;
+      const auto& lid = m.linkIndex;
+      ptr.assign(n + 1, 0);
       for (size_t k = 0; k < n; ++k) {
         if (const LinkSet* ign = ignores[slot[k]]) {
           for (auto const& link : *ign) {
@@ -656,6 +664,13 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
         ptr[k + 1] = (uint32_t)links.size();
       }
       if (links.empty()) links.push_back(0);
+    }
+    if (wantOrder) {
+      SpfEngineHandle::check(openr_spf_solve_order(engine_->ctx(), ids.data(), (uint32_t)n, flags,
+                                                   anyIgnore ? ptr.data() : nullptr, anyIgnore ? links.data() : nullptr,
+                                                   dist.data(), nh.data(), nb, tight.data(), popIndex.data()),
+                             "openr_spf_solve_order");
+    } else if (anyIgnore) {
       SpfEngineHandle::check(openr_spf_solve_ignore(engine_->ctx(), ids.data(), (uint32_t)n, flags, ptr.data(),
                                                     links.data(), dist.data(), nh.data(), nb, tight.data()),
                              "openr_spf_solve_ignore");
@@ -665,7 +680,8 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
           "openr_spf_solve");
     }
     // materialise SpfResult: nextHops from the bitsets, pathLinks from tight edges
-    // ordered by the predecessor's settle order (dist, name) then row position.
+    // ordered by the predecessor's settle order ((dist, name), or the exact kernel's pop
+    // index) then row position.
     std::vector<uint32_t> nbrs(V ? V : 1);
     std::vector<uint32_t> order;
     for (size_t k = 0; k < n; ++k) {
@@ -689,8 +705,10 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
       order.clear();
       for (uint32_t e = 0; e < E; ++e)
         if ((t[e >> 6] >> (e & 63)) & 1ull) order.push_back(e);
+      const uint32_t* pop = wantOrder ? popIndex.data() + k * V : nullptr;
       std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
         const uint32_t ux = m.edgeOwner[x], uy = m.edgeOwner[y];
+        if (pop) return pop[ux] != pop[uy] ? pop[ux] < pop[uy] : x < y;
         if (d[ux] != d[uy]) return d[ux] < d[uy];
         if (m.nameRank[ux] != m.nameRank[uy]) return m.nameRank[ux] < m.nameRank[uy];
         return x < y;

@@ -308,6 +308,8 @@ class LinkState {
     std::vector<uint32_t> nameRank;
     std::vector<std::shared_ptr<Link>> links;  // link id -> Link
     std::vector<uint32_t> edgeOwner;
+    std::unordered_map<const Link*, uint32_t> linkIndex;  // Link -> link id (ignore sets)
+    bool metricsPositive = true;  // every usable metric in [1, 2^31-1]: fast kernels
   };
   const CsrMirror& csrMirror() const;
 

@@ -90,6 +90,9 @@ struct Device {
   DevBuf<PatchRec> precs;
   DevBuf<DeltaEdge> delta;
   DevBuf<uint32_t> alist, asrc, acount;
+  // exact-order kernel: per-solve slots when a slot does not fit LDS; pop-order rows
+  DevBuf<uint8_t> exscratch;
+  DevBuf<uint32_t> order;
 };
 
 // Launch counters live zeroed: each kernel's last workgroup resets what it used.
@@ -101,8 +104,8 @@ hipError_t reserve_counters(Device& d) {
 }
 
 void free_graph(DevGraph& g) {
-  void* ptrs[] = {g.row,   g.row2, g.row2t, g.ovl_bits, g.ellt, g.ellv, g.adj,    g.w,
-                   g.win,   g.rev,  g.lid,   g.nbr,      g.ovl,  g.cls,    g.cls_lvl, g.ledge, g.rank, g.erec};
+  void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
+                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -135,6 +138,9 @@ struct openr_spf_ctx {
   // delta edges of the most recent patch (openr_spf_refresh); invalid after set_graph
   std::vector<DeltaEdge> delta;
   bool delta_valid = false;
+  // the rows before or after the last patch came from a graph with zero / wrapped
+  // metrics: the delta filter's tight-edge reasoning does not hold, refresh every row
+  bool delta_all = false;
 };
 
 namespace {
@@ -143,6 +149,8 @@ constexpr uint32_t kDeepGraphLevels = 24;
 constexpr uint32_t kRoundsMaxDepth = 48;  // hop depth below which general metrics use the rounds kernel
 
 struct Plan {
+  bool exact = false;   // spf_exact.hip: the reference's heap process (metrics / sizes outside the fast kernels)
+  bool use_metric = true;
   bool bfs = true;
   bool rounds = false;  // general metrics: distance rounds + Kahn (shallow graphs), else fringe
   int family = kFamCode;
@@ -211,20 +219,26 @@ FrontierEstimate estimate_frontier(uint32_t V, const uint32_t* row_ptr, const ui
 
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   const bool use_metric = (flags & OPENR_SPF_USE_LINK_METRIC) != 0;
-  if (use_metric && !ctx->metric_ok)
-    return fail(OPENR_SPF_ENOTSUP,
-                "usable edge metric outside [1, 2^31-1]: the reference's (metric, name) pop order is "
-                "history-dependent for such metrics and the engine does not emulate it");
+  p->use_metric = use_metric;
+  // Outside the fast kernels' domain the exact-order kernel replays the reference's heap
+  // process instead of refusing the graph: zero or wrapped-negative usable metrics (pop
+  // order history-dependent), next-hop sets wider than 256, graphs larger
+  // than the LDS-resident layouts, and pop-order output requests.
+  auto exact = [p]() {
+    p->exact = true;
+    return OPENR_SPF_OK;
+  };
+  if ((flags & OPENR_SPF_EMIT_ORDER) || std::getenv("OPENR_SPF_FORCE_EXACT")) return exact();
+  if (use_metric && !ctx->metric_ok) return exact();
   p->nh_mode = nh_mode_for_bits(ctx->nh_bits);
-  if (p->nh_mode < 0) return fail(OPENR_SPF_E2BIG, "max distinct degree %u exceeds 256", ctx->nh_bits);
+  if (p->nh_mode < 0) return exact();
   if (!use_metric || ctx->w_min == ctx->w_max) {
     p->bfs = true;
     p->cost = use_metric ? std::max<uint32_t>(ctx->w_min, 1u) : 1u;
     p->family = family_override(ctx->family);
     for (int c = 0; c < num_classes(p->family); ++c)
       if ((ctx->cls_mask[p->family] >> c) & 1u)
-        if (!bfs_lds_bytes(p->family, ctx->V, ctx->L, has_ign, c))
-          return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident BFS kernel", ctx->V);
+        if (!bfs_lds_bytes(p->family, ctx->V, ctx->L, has_ign, c)) return exact();
   } else {
     p->bfs = false;
     p->delta = ctx->w_min;
@@ -237,11 +251,13 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
       if (!std::strcmp(e, "rounds")) p->rounds = ctx->devs[0].g.max_deg < 65535u;
     }
     if (p->rounds && !rounds_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64)) p->rounds = false;
-    if (!fringe_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64))
-      return fail(OPENR_SPF_E2BIG, "graph (V=%u) does not fit the LDS-resident general-metric kernel", ctx->V);
+    if (!fringe_lds_bytes(ctx->V, ctx->L, has_ign, p->nh_mode, p->dist64)) return exact();
   }
   return OPENR_SPF_OK;
 }
+
+// Bytes of exact-order slots (global memory) a device may hold at once.
+constexpr uint64_t kExactScratchBytes = uint64_t(2) << 30;
 
 // Tuning overrides (benchmarks only): OPENR_SPF_GROUP_LANES=1|2|4|..|64 lanes per
 // frontier node in the BFS kernel.
@@ -258,6 +274,21 @@ int group_lanes_override(int dflt) {
 // widest first.
 hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs a, hipStream_t s) {
   LaunchInfo info;
+  if (p.exact) {  // writes every dist / nh / tight word itself
+    const uint64_t slot = exact_slot_bytes(d.g.V, d.g.E, d.g.L, ctx->nh_bits);
+    uint64_t bytes = 0;
+    if (slot > kMaxLds || std::getenv("OPENR_SPF_EXACT_GLOBAL")) {
+      const uint64_t slots = std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)a.n, (uint64_t)d.num_cus * 8u,
+                                                                        kExactScratchBytes / std::max<uint64_t>(slot, 1)}));
+      bytes = slots * slot;
+      hipError_t err = d.exscratch.reserve(bytes);
+      if (err != hipSuccess) return err;
+    }
+    hipError_t err = reserve_counters(d);
+    if (err != hipSuccess) return err;
+    return launch_exact(d.g, a, d.g.w64, p.use_metric, ctx->nh_bits, d.exscratch.p, bytes, a.order,
+                        d.work.p + kExactCtr, d.num_cus, s);
+  }
   if (a.tight && !a.out_row) {
     hipError_t err = hipMemsetAsync(a.tight, 0, (size_t)a.n * ((d.g.E + 63u) / 64u) * 8u, s);
     if (err != hipSuccess) return err;
@@ -310,7 +341,8 @@ int check_solve_args(const openr_spf_ctx* ctx, const uint32_t* sources, uint32_t
 
 int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
                const uint32_t* ignore_ptr, const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
-               uint32_t nh_bytes, uint64_t* tight) {
+               uint32_t nh_bytes, uint64_t* tight, uint32_t* order = nullptr) {
+  if (order) flags |= OPENR_SPF_EMIT_ORDER;
   int rc = check_solve_args(ctx, sources, n, dist, nh, nh_bytes);
   if (rc) return rc;
   for (uint32_t i = 0; i < n; ++i)
@@ -338,6 +370,7 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     HIP_TRY(d.dist.reserve((size_t)m * V));
     if (nh) HIP_TRY(d.nh.reserve((size_t)m * V * nh_bytes));
     if (tight) HIP_TRY(d.tight.reserve((size_t)m * tw));
+    if (order) HIP_TRY(d.order.reserve((size_t)m * V));
     HIP_TRY(hipMemcpyAsync(d.src.p, sources + b, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
     SolveArgs a{};
     a.sources = d.src.p;
@@ -359,6 +392,7 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
     a.nh = nh ? d.nh.p : nullptr;
     a.nh_bytes = nh_bytes;
     a.tight = tight ? d.tight.p : nullptr;
+    a.order = order ? d.order.p : nullptr;
     a.nh_bits = ctx->nh_bits;
     HIP_TRY(d.ovf.reserve((size_t)m * ctx->nsl_max()));
     a.ovf_list = d.ovf.p;
@@ -374,6 +408,9 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
                              hipMemcpyDeviceToHost, d.stream));
     if (tight)
       HIP_TRY(hipMemcpyAsync(tight + (size_t)b * tw, d.tight.p, (size_t)m * tw * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, d.stream));
+    if (order)
+      HIP_TRY(hipMemcpyAsync(order + (size_t)b * V, d.order.p, (size_t)m * V * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, d.stream));
   }
   double kms = 0.0;
@@ -433,7 +470,11 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
   const char* mode = std::getenv("OPENR_SPF_WHATIF");
   const bool dist64 = use_link_metric && (uint64_t)V * ctx->w_max >= 0xFFFFFFFFull;
-  if (!mode || !std::strcmp(mode, "group")) {
+  // exact-order plans (metrics / widths outside the fast kernels): filter + re-solve; with
+  // zero or wrapped metrics the pop order depends on every relaxation, so every unit whose
+  // link is up is re-solved (no tight-edge filter)
+  const bool exact = base_plan.exact || ign_plan.exact;
+  if (!exact && (!mode || !std::strcmp(mode, "group"))) {
     // default: grouped repair (base rows staged once per (source, link chunk), fused filter)
     if (whatif_group_lds_bytes(V, ctx->E, nb, dist64)) {
       OPENR_TRY(d.wcount.reserve(1));
@@ -453,7 +494,8 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(d.wlink.reserve(units));
   OPENR_TRY(d.wunit.reserve(units));
   OPENR_TRY(d.wcount.reserve(1));
-  OPENR_TRY(launch_whatif_filter(d.g, d_links, n_links, d_sources, n_src, d.base_tight.p, d_changed, d.wsrc.p,
+  const uint64_t* filter_tight = (exact && !ctx->metric_ok && use_link_metric) ? nullptr : d.base_tight.p;
+  OPENR_TRY(launch_whatif_filter(d.g, d_links, n_links, d_sources, n_src, filter_tight, d_changed, d.wsrc.p,
                                  d.wlink.p, d.wunit.p, d.wcount.p, d.num_cus, s));
   uint32_t count = 0;
   OPENR_TRY(hipMemcpyAsync(&count, d.wcount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -462,7 +504,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   if (!count) return hipSuccess;
   // OPENR_SPF_WHATIF=incr: one wavefront per affected unit repairs it from the base rows it
   // re-reads (A set, distances inside A, dirty next hops); =solve re-solves every unit
-  if (!(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
+  if (!exact && !(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
     return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
                               !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);
   }
@@ -631,7 +673,7 @@ void openr_spf_limits(openr_spf_limits_t* out) {
     else hi = mid - 1;
   }
   out->max_nodes = lo;
-  out->max_nh_bits = 256;
+  out->max_nh_bits = 65535;  // wider than 256: the exact-order kernel
 }
 
 int openr_spf_create(const int* device_ids, int n_devices, openr_spf_ctx** out) {
@@ -695,6 +737,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
+    d.exscratch.release();
+    d.order.release();
     d.precs.release();
     d.delta.release();
     d.alist.release();
@@ -793,7 +837,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     row2t[u] = ovl[u] ? make_uint2(gr->row_ptr[u] | kNodeSink, gr->row_ptr[u]) : row2[u];
     if (ovl[u]) ovl_bits[u >> 5] |= 1u << (u & 31u);
   }
-  if (nh_bits > 256) return fail(OPENR_SPF_E2BIG, "distinct degree %u > 256", nh_bits);
+  // next-hop sets wider than 256 bits: only the exact-order kernel serves them (make_plan)
   // source class of every node (distinct degree -> next-hop width)
   std::vector<uint8_t> cls[kNumFamilies];
   uint32_t cls_mask[kNumFamilies] = {0, 0}, sliced_deg[kNumFamilies] = {0, 0};
@@ -802,7 +846,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     uint32_t nd = 0;
     for (uint32_t e = gr->row_ptr[u]; e < gr->row_ptr[u + 1]; ++e) nd = std::max<uint32_t>(nd, nbr[e] + 1u);
     for (int f = 0; f < kNumFamilies; ++f) {
-      const int c = src_class_for_degree(f, nd);
+      const int c = std::max(0, src_class_for_degree(f, std::min<uint32_t>(nd, 256u)));
       cls[f][u] = (uint8_t)c;
       cls_mask[f] |= 1u << c;
       if (c == sliced_class(f)) sliced_deg[f] = std::max(sliced_deg[f], nd);
@@ -844,6 +888,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
+    if (err == hipSuccess) err = up(&g.w64, gr->metric, E);
     if (err == hipSuccess) err = up(&g.win, win.data(), E);
     if (err == hipSuccess) err = up(&g.rev, rev.data(), E);
     if (err == hipSuccess) err = up(&g.lid, lid.data(), E);
@@ -973,6 +1018,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
                               ctx->rev[e]);
     rec(kPatchAdj, e, make_uint4(ctx->adj[e], 0, 0, 0));
     rec(kPatchW, e, make_uint4(ctx->w[e], 0, 0, 0));
+    rec(kPatchW64, e, make_uint4((uint32_t)ctx->metric[e], (uint32_t)(ctx->metric[e] >> 32), 0, 0));
     rec(kPatchWin, e, make_uint4(ctx->win[e], 0, 0, 0));
     rec(kPatchErec, e, ctx->erec[e]);
   }
@@ -1040,6 +1086,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
   }
   ctx->w_min = w_min;
   ctx->w_max = w_max;
+  ctx->delta_all = !ctx->metric_ok || !metric_ok;
   ctx->metric_ok = metric_ok;
   ctx->delta_valid = true;
   return OPENR_SPF_OK;
@@ -1062,7 +1109,11 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
   const uint32_t nd = (uint32_t)ctx->delta.size();
   uint32_t count = 0;
-  if (nd && n) {
+  if (ctx->delta_all && n) {
+    HIP_TRY(d.alist.reserve(n));
+    HIP_TRY(launch_iota(d.alist.p, n, d.num_cus, s));
+    count = n;
+  } else if (nd && n) {
     HIP_TRY(d.delta.reserve(nd));
     HIP_TRY(d.alist.reserve(n));
     HIP_TRY(d.asrc.reserve(n));
@@ -1078,7 +1129,7 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
   if (count) {
     if (d_tight) HIP_TRY(launch_zero_rows(d_tight, (ctx->E + 63u) / 64u, d.alist.p, count, d.num_cus, s));
     SolveArgs a{};
-    a.sources = d.asrc.p;
+    a.sources = ctx->delta_all ? d_sources : d.asrc.p;
     a.n = count;
     a.out_row = d.alist.p;
     a.dist = d_dist;
@@ -1177,6 +1228,13 @@ int openr_spf_neighbor_map(const openr_spf_ctx* ctx, uint32_t src, uint32_t* out
 int openr_spf_solve(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags, uint64_t* dist,
                     uint8_t* nh, uint32_t nh_bytes, uint64_t* tight) {
   return solve_host(ctx, sources, n, flags, nullptr, nullptr, dist, nh, nh_bytes, tight);
+}
+
+int openr_spf_solve_order(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
+                          const uint32_t* ignore_ptr, const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
+                          uint32_t nh_bytes, uint64_t* tight, uint32_t* order) {
+  if (n && !order) return fail(OPENR_SPF_EINVAL, "null order");
+  return solve_host(ctx, sources, n, flags, ignore_ptr, ignore_links, dist, nh, nh_bytes, tight, order);
 }
 
 int openr_spf_solve_ignore(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
@@ -1296,6 +1354,8 @@ int openr_spf_ksp2(openr_spf_ctx* ctx, const uint32_t* src, const uint32_t* dst,
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
   if (!ksp_lds_bytes(ctx->V, ctx->L, ctx->devs[0].g.max_deg))
     return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  if (!ctx->metric_ok)  // the tracer walks dist[u] + w == dist[v]: ambiguous under zero metrics
+    return fail(OPENR_SPF_ENOTSUP, "KSP2 needs usable metrics in [1, 2^31-1]");
   // distinct sources (the memoized SPF of each), pair -> base row
   std::vector<uint32_t> srcs, prow(n_pairs), row_of(ctx->V, UINT32_MAX);
   for (uint32_t i = 0; i < n_pairs; ++i) {
@@ -1349,6 +1409,8 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
   if (tok_cap < 1) return fail(OPENR_SPF_EINVAL, "tok_cap must be >= 1");
   if (!ksp_lds_bytes(ctx->V, ctx->L, ctx->devs[0].g.max_deg))
     return fail(OPENR_SPF_E2BIG, "too many links (%u) for the KSP tracer", ctx->L);
+  if (!ctx->metric_ok)  // the tracer walks dist[u] + w == dist[v]: ambiguous under zero metrics
+    return fail(OPENR_SPF_ENOTSUP, "KSP2 needs usable metrics in [1, 2^31-1]");
   Plan bp, ip;
   int rc = whatif_plans(ctx, OPENR_SPF_USE_LINK_METRIC, &bp, &ip);
   if (rc) return rc;

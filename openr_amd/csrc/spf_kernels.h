@@ -28,6 +28,7 @@ struct DevGraph {
                                //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
+  uint64_t* w64 = nullptr;     // [E] metric u->v as the caller gave it (exact-order kernel: 0 / wrapped values)
   uint32_t* win = nullptr;     // [E] metric of the reverse edge (col -> row owner)
   uint32_t* rev = nullptr;     // [E] index of the reverse edge
   uint32_t* lid = nullptr;     // [E] undirected link id
@@ -103,6 +104,7 @@ struct SolveArgs {
   // launcher then leaves zeroing those tight rows to the caller)
   const uint32_t* out_row;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
+  uint32_t* order;            // nullable [n][V]: pop index per node (exact-order kernel only)
 };
 // output row of solve sid (SolveArgs::out_row)
 __host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
@@ -113,6 +115,7 @@ constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch,
 constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
 constexpr uint32_t kFringeCtr = kCtrPerClass * (kMaxClasses - 1);  // BFS classes use < 7 blocks
 constexpr uint32_t kIncrCtr = kFringeCtr + 2;                        // incremental what-if
+constexpr uint32_t kExactCtr = kIncrCtr + 2;                         // exact-order kernel
 
 // Uniform-cost BFS kernel families (spf_capi.hip picks one per graph):
 //  * code (spf_bfs.hip): one packed LDS field per node = [next-hop bits | 3-bit level
@@ -191,6 +194,7 @@ uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64
 // one DevGraph array (structure — rows, columns, link ids — never changes).
 enum PatchArray : uint32_t {
   kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kPatchEllv,
+  kPatchW64,  // val.x = low, val.y = high word
   kNumPatchArrays
 };
 struct PatchRec {
@@ -241,6 +245,16 @@ hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg);
+
+// Exact-order kernel (spf_exact.hip): LinkState::runSpf's heap process replayed per solve
+// (one wavefront per solve) for graphs outside the fast kernels' domain — zero or
+// wrapped-negative metrics, graphs too large for their LDS layouts, next-hop sets wider
+// than 256. State in LDS when a slot fits (<= kMaxLds), else in `scratch` (slot bytes each).
+// tight = the edges left in pathLinks; a.order (nullable) = pop index per node.
+uint64_t exact_slot_bytes(uint32_t V, uint32_t E, uint32_t L, uint32_t nh_bits);
+hipError_t launch_exact(const DevGraph& g, const SolveArgs& a, const uint64_t* w64, bool use_metric, uint32_t nh_bits,
+                        uint8_t* scratch, uint64_t scratch_bytes, uint32_t* order_out, uint32_t* ctr, int num_cus,
+                        hipStream_t s);
 
 // LDS footprint of each kernel for a graph (0 if it cannot fit one workgroup per CU).
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);

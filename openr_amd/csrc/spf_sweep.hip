@@ -11,6 +11,7 @@
 // {link}) ignore set per solve) and reduced against the base rows by rows_compare.
 // Integer / byte work only: HBM-bound, coalesced row reads, one workgroup per unit.
 #include <algorithm>
+#include <cstdio>
 
 #include "spf_bfs_common.h"
 #include "spf_kernels.h"
@@ -38,8 +39,12 @@ __global__ __launch_bounds__(256) void whatif_filter(const uint2* ledge, uint32_
       changed[u] = 0;
       const uint2 ee = l < L ? ledge[l] : make_uint2(UINT32_MAX, UINT32_MAX);
       if (ee.x != UINT32_MAX) {
-        const uint64_t* trow = base_tight + (size_t)j * tight_words;
-        hit = ((trow[ee.x >> 6] >> (ee.x & 63u)) & 1ull) || ((trow[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
+        if (!base_tight) {
+          hit = true;  // exact-order plans: every unit is solved
+        } else {
+          const uint64_t* trow = base_tight + (size_t)j * tight_words;
+          hit = ((trow[ee.x >> 6] >> (ee.x & 63u)) & 1ull) || ((trow[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
+        }
       }
     }
     const unsigned long long m = __ballot(hit);
@@ -554,6 +559,7 @@ struct GrpWave {
   uint8_t* anh;
   uint32_t *ina, *dq, *nhm, *ctl;
   uint16_t *alist, *dlist;
+  unsigned long long* prof;  // tuning (OPENR_SPF_WHATIF_PROF): per-phase cycles and sizes, or null
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
@@ -625,6 +631,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     if (dt != INF && dh != INF && (uint64_t)dt + (c.unit ? 1u : g.w[e]) == (uint64_t)dh) bnode = head;
   }
   if (bnode == UINT32_MAX) return 0;
+  long long pt0 = c.prof ? (long long)__builtin_amdgcn_s_memtime() : 0, pt1 = 0, pt2 = 0, pt3 = 0;
   // (1) A by decremental propagation over the base tight DAG (base distances)
   if (lane == 0) {
     c.dq[bnode >> 5] |= 1u << (bnode & 31u);
@@ -663,6 +670,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     lds_fence();
   }
   const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
+  if (c.prof) pt1 = (long long)__builtin_amdgcn_s_memtime();
   // (2) new distances inside A: best entry from outside A, then relaxation within A
   for (uint32_t i = lane; i < na; i += 64u) {
     const uint32_t x = c.alist[i];
@@ -701,9 +709,11 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
   }
   // (3) next hops in increasing new distance over the dirty set
-  uint32_t nchanged = 0;
+  if (c.prof) pt2 = (long long)__builtin_amdgcn_s_memtime();
+  uint32_t nchanged = 0, buckets = 0;
   uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
   while (done < nd) {
+    ++buckets;
     D mn = INF;
     for (uint32_t i = done + lane; i < nd; i += 64u) {
       const D d = c.dist(c.dlist[i]);
@@ -792,6 +802,17 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     done += nm;
     nd = __builtin_amdgcn_readfirstlane(c.ctl[1]);
   }
+  if (c.prof && lane == 0) {
+    pt3 = (long long)__builtin_amdgcn_s_memtime();
+    atomicAdd(&c.prof[0], (unsigned long long)(pt1 - pt0));
+    atomicAdd(&c.prof[1], (unsigned long long)(pt2 - pt1));
+    atomicAdd(&c.prof[2], (unsigned long long)(pt3 - pt2));
+    atomicAdd(&c.prof[3], 1ull);
+    atomicAdd(&c.prof[4], (unsigned long long)na);
+    atomicAdd(&c.prof[5], (unsigned long long)nd);
+    atomicAdd(&c.prof[6], (unsigned long long)buckets);
+    atomicAdd(&c.prof[7], (unsigned long long)nchanged);
+  }
   return nchanged;
 }
 
@@ -801,8 +822,9 @@ template <typename D, bool LG>
 __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
-    uint32_t* changed, uint32_t* affected, uint32_t* ctr) {
+    uint32_t* changed, uint32_t* affected, uint32_t* ctr, unsigned long long* prof) {
   constexpr D INF = (D)~(D)0;
+  const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_item;
   const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
@@ -841,6 +863,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   }
   c.nb = nb;
   c.unit = unit != 0;
+  c.prof = prof;
   c.bdist = bdist;
   c.bnh = bnh;
   c.ctl = reinterpret_cast<uint32_t*>(wb);
@@ -909,6 +932,10 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     item = s_item;
   }
   if (lane == 0 && n_aff) atomicAdd(affected, n_aff);
+  if (prof && lane == 0) {
+    atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
+    atomicAdd(&prof[9], 1ull);
+  }
   bfs::retire_workgroup(ctr, nullptr);
 }
 
@@ -1021,6 +1048,14 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
+  // tuning aid: per-phase cycle sums and set sizes, printed after the launch
+  static unsigned long long* prof_buf = nullptr;
+  unsigned long long* prof = nullptr;
+  if (bfs::env_u32("OPENR_SPF_WHATIF_PROF", 0u, 0u, 1u)) {
+    if (!prof_buf && hipMalloc(&prof_buf, 16 * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
+    prof = prof_buf;
+    if (prof) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
+  }
 #define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
   do {                                                                                                         \
     auto k = whatif_group_kernel<DT, LGV>;                                                                     \
@@ -1028,7 +1063,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
-                       base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr);                  \
+                       base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr, prof);            \
   } while (0)
   if (dist64) {
     if (lg) OPENR_GRP_LAUNCH(unsigned long long, true);
@@ -1038,7 +1073,21 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     else OPENR_GRP_LAUNCH(uint32_t, false);
   }
 #undef OPENR_GRP_LAUNCH
-  return hipGetLastError();
+  err = hipGetLastError();
+  if (err == hipSuccess && prof) {
+    unsigned long long h[16];
+    if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess) {
+      const double u = h[3] ? (double)h[3] : 1.0;
+      std::fprintf(stderr,
+                   "whatif_group: lds_graph=%d waves=%u grid=%u chunk=%u units=%llu | cycles/unit: A %.0f dist %.0f "
+                   "nh %.0f | |A| %.2f dirty %.2f buckets %.2f changed %.2f | wave lifetime %.0f x %llu, repair "
+                   "share %.2f\n",
+                   (int)lg, waves, grid, chunk, h[3], h[0] / u, h[1] / u, h[2] / u, h[4] / u, h[5] / u, h[6] / u,
+                   h[7] / u, h[9] ? (double)h[8] / h[9] : 0.0, h[9],
+                   h[8] ? (double)(h[0] + h[1] + h[2]) / (double)h[8] : 0.0);
+    }
+  }
+  return err;
 }
 
 hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s) {

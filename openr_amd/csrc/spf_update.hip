@@ -41,6 +41,7 @@ __global__ __launch_bounds__(256) void patch_apply(DevGraph g, const PatchRec* r
     case kPatchRow2t: g.row2t[r.idx] = make_uint2(r.val.x, r.val.y); break;
     case kPatchOvl: g.ovl[r.idx] = (uint8_t)r.val.x; break;
     case kPatchOvlBits: g.ovl_bits[r.idx] = r.val.x; break;
+    case kPatchW64: g.w64[r.idx] = ((uint64_t)r.val.y << 32) | r.val.x; break;
     default: break;
   }
 }

@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libopenr_spf.so")
 
 USE_LINK_METRIC = 1
 EMIT_TIGHT = 2
+EMIT_ORDER = 4
 
 OK, EIO, ENOMEM, ENODEV, EINVAL, E2BIG, ENOTSUP = 0, -5, -12, -19, -22, -7, -95
 
@@ -34,6 +35,7 @@ EXPORTS = (
     "openr_spf_nh_bytes",
     "openr_spf_neighbor_map",
     "openr_spf_solve",
+    "openr_spf_solve_order",
     "openr_spf_solve_ignore",
     "openr_spf_solve_device",
     "openr_spf_whatif",
@@ -122,6 +124,7 @@ def load_library():
     l.openr_spf_nh_bytes.argtypes = [vp, P(u32)]
     l.openr_spf_neighbor_map.argtypes = [vp, u32, vp, u32, P(u32)]
     l.openr_spf_solve.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp]
+    l.openr_spf_solve_order.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
     l.openr_spf_solve_ignore.argtypes = [vp, vp, u32, u32, vp, vp, vp, vp, u32, vp]
     l.openr_spf_solve_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
     l.openr_spf_whatif.argtypes = [vp, vp, u32, vp, u32, u32, vp, P(ctypes.c_uint64)]
@@ -147,6 +150,15 @@ def _check(rc: int) -> None:
 
 def _p(a: Optional[np.ndarray]):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _ignore_arrays(ignore: Sequence[Sequence[int]], n: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-solve ignore sets -> (ignore_ptr[n+1], ignore_links) CSR arrays."""
+    ptr = np.zeros(n + 1, dtype=np.uint32)
+    ptr[1:] = np.cumsum([len(x) for x in ignore])
+    links = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in ignore])
+                                 if ptr[-1] else np.zeros(1, dtype=np.uint32), dtype=np.uint32)
+    return ptr, links
 
 
 class SpfEngine:
@@ -207,14 +219,29 @@ class SpfEngine:
         if ignore is None:
             rc = self._lib.openr_spf_solve(self._ctx, _p(src), n, flags, _p(dist), _p(nh), nb, _p(tight))
         else:
-            ptr = np.zeros(n + 1, dtype=np.uint32)
-            ptr[1:] = np.cumsum([len(x) for x in ignore])
-            links = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in ignore])
-                                         if ptr[-1] else np.zeros(1, dtype=np.uint32), dtype=np.uint32)
+            ptr, links = _ignore_arrays(ignore, n)
             rc = self._lib.openr_spf_solve_ignore(self._ctx, _p(src), n, flags, _p(ptr), _p(links), _p(dist),
                                                   _p(nh), nb, _p(tight))
         _check(rc)
         return dist, nh, tight
+
+    def solve_order(self, sources: Sequence[int], use_link_metric: bool = True, want_tight: bool = True,
+                    ignore: Optional[Sequence[Sequence[int]]] = None
+                    ) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray], np.ndarray]:
+        """Exact-order solve: (dist, nh, tight | None, order[n,V] u32 pop index, UINT32_MAX unreached)."""
+        g = self.g
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        n, V = int(src.shape[0]), g.num_nodes
+        dist = np.empty((n, V), dtype=np.uint64)
+        nh = np.empty((n, V, self.nh_bytes), dtype=np.uint8)
+        tw = (g.num_dir_edges + 63) // 64
+        tight = np.empty((n, max(tw, 1)), dtype=np.uint64) if want_tight else None
+        order = np.empty((n, V), dtype=np.uint32)
+        flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if want_tight else 0)
+        ptr, links = _ignore_arrays(ignore, n) if ignore is not None else (None, None)
+        _check(self._lib.openr_spf_solve_order(self._ctx, _p(src), n, flags, _p(ptr), _p(links), _p(dist), _p(nh),
+                                               self.nh_bytes, _p(tight), _p(order)))
+        return dist, nh, tight, order
 
     def solve_device(self, d_sources: int, n: int, d_dist: int, d_nh: int = 0, nh_bytes: int = 0,
                      use_link_metric: bool = True, stream: int = 0, device_index: int = 0,

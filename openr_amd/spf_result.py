@@ -38,8 +38,10 @@ def nh_names(g, src: int, nh_row: np.ndarray, nbrs: Sequence[int]) -> Set[str]:
     return out
 
 
-def tight_in_edges(g, dist: np.ndarray, tight: np.ndarray, owner: Optional[np.ndarray] = None) -> Dict[int, List[int]]:
-    """Per node v: tight in-edges (u->v) in the reference's pathLinks order."""
+def tight_in_edges(g, dist: np.ndarray, tight: np.ndarray, owner: Optional[np.ndarray] = None,
+                   pop: Optional[np.ndarray] = None) -> Dict[int, List[int]]:
+    """Per node v: tight in-edges (u->v) in the reference's pathLinks order: the settle
+    order of u ((dist, name), or the exact kernel's pop index `pop`), then row position."""
     if owner is None:
         owner = g.edge_owner()
     E = g.num_dir_edges
@@ -50,19 +52,20 @@ def tight_in_edges(g, dist: np.ndarray, tight: np.ndarray, owner: Optional[np.nd
         return per
     us = owner[edges].astype(np.int64)
     vs = g.col[edges].astype(np.int64)
-    du = dist[us]
-    rk = g.name_rank[us]
-    order = np.lexsort((edges, rk, du))  # settle order of u, then row position
+    if pop is not None:
+        order = np.lexsort((edges, pop[us]))
+    else:
+        order = np.lexsort((edges, g.name_rank[us], dist[us]))  # settle order of u, then row position
     for idx in order.tolist():
         per.setdefault(int(vs[idx]), []).append(int(edges[idx]))
     return per
 
 
 def materialize(g, src: int, dist: np.ndarray, nh: np.ndarray, nbrs: Sequence[int],
-                tight: Optional[np.ndarray] = None) -> Dict[str, NodeSpfResult]:
+                tight: Optional[np.ndarray] = None, pop: Optional[np.ndarray] = None) -> Dict[str, NodeSpfResult]:
     """Dense outputs of one solve -> SpfResult (name -> NodeSpfResult)."""
     owner = g.edge_owner()
-    pls = tight_in_edges(g, dist, tight, owner) if tight is not None else {}
+    pls = tight_in_edges(g, dist, tight, owner, pop) if tight is not None else {}
     res: Dict[str, NodeSpfResult] = {}
     for v in np.nonzero(dist != np.uint64(U64_MAX))[0].tolist():
         r = NodeSpfResult(int(dist[v]), nh_names(g, src, nh[v], nbrs))

@@ -520,8 +520,10 @@ TEST_GPU(DecisionTest_Grid_ShortestPath) {
 
 // Random topologies through the full adjacency-database path: every getSpfResult and
 // getKthPaths equals the oracle run on the same CSR mirror (pathLinks order included).
-TEST_GPU(LinkState_RandomOracleParity) {
-  std::mt19937_64 rng(7);
+// metric(rng) draws every directed metric of a trial
+template <typename MetricFn>
+static void randomOracleParity(uint64_t seed, MetricFn metric) {
+  std::mt19937_64 rng(seed);
   for (int trial = 0; trial < 6; ++trial) {
     const int V = 12 + trial * 9;
     LinkState ls(kArea);
@@ -534,16 +536,16 @@ TEST_GPU(LinkState_RandomOracleParity) {
       adjs[a].push_back(x);
       adjs[b].push_back(createAdjacency(std::to_string(a), ib, ia, wb));
     };
-    for (int v = 1; v < V; ++v) link((int)(rng() % v), v, 1 + rng() % 6, 1 + rng() % 6, false);
+    for (int v = 1; v < V; ++v) link((int)(rng() % v), v, metric(rng), metric(rng), false);
     for (int k = 0; k < V; ++k) {
       int a = rng() % V, b = rng() % V;
-      if (a != b) link(a, b, 1 + rng() % 6, 1 + rng() % 6, rng() % 10 == 0);
+      if (a != b) link(a, b, metric(rng), metric(rng), rng() % 10 == 0);
     }
     for (int k = 0; k < V / 4; ++k) {  // parallel links
       int a = rng() % V;
       if (!adjs[a].empty()) {
         int b = std::stoi(adjs[a][0].otherNodeName);
-        link(a, b, 1 + rng() % 6, 1 + rng() % 6, false);
+        link(a, b, metric(rng), metric(rng), false);
       }
     }
     for (int v = 0; v < V; ++v) {
@@ -601,6 +603,20 @@ TEST_GPU(LinkState_RandomOracleParity) {
       }
     }
   }
+}
+
+TEST_GPU(LinkState_RandomOracleParity) {
+  randomOracleParity(7, [](std::mt19937_64& r) { return (int)(1 + r() % 6); });
+}
+
+// Zero and negative i32 metrics (LinkState.cpp:151-152 stores them as u64, sums wrap):
+// the mirror routes these graphs to the exact-order kernel and rebuilds pathLinks from
+// its pop order (openr_spf_solve_order); results still equal the oracle's.
+TEST_GPU(LinkState_ZeroAndNegativeMetricOracleParity) {
+  randomOracleParity(11, [](std::mt19937_64& r) {
+    static const int kPool[] = {0, 0, 1, 2, 3, -1, -7};
+    return kPool[r() % 7];
+  });
 }
 
 int main(int argc, char** argv) { return run_tests(argc, argv); }

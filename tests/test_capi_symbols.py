@@ -40,7 +40,7 @@ def test_abi_version_and_limits():
     lib = engine.load_library()
     assert lib.openr_spf_abi_version() == 1
     lim = engine.limits()
-    assert lim.max_nh_bits == 256
+    assert lim.max_nh_bits == 65535  # > 256 distinct neighbours: the exact-order kernel
     assert lim.max_nodes >= 10000  # G100 must fit the LDS-resident kernels
 
 

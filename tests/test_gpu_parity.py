@@ -289,16 +289,6 @@ def test_empty_batch(eng):
     assert dist.shape == (0, 9)
 
 
-def test_zero_metric_rejected_loudly(eng):
-    g = T.grid_fast(3)
-    g.metric[0] = 0
-    eng.set_graph(g)
-    with pytest.raises(SpfError) as ei:
-        eng.solve([0], True)
-    assert ei.value.code == ENOTSUP
-    eng.solve([0], False)  # hop-count SPF ignores metrics
-
-
 def test_nh_bytes_too_small(eng):
     g = T.fabric(288 + 56)
     eng.set_graph(g)

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from openr_amd import topology as T
-from openr_amd.engine import EINVAL, ENOTSUP, SpfEngine, SpfError
+from openr_amd.engine import EINVAL, SpfEngine, SpfError
 from openr_amd.spf_result import tight_in_edges
 from oracle import Oracle
 from test_gpu_parity import random_graph
@@ -192,10 +192,14 @@ def test_patch_errors(eng):
     with pytest.raises(SpfError) as ei:
         eng.patch(nodes=[g.num_nodes], node_overloaded=[1])
     assert ei.value.code == EINVAL
-    eng.patch(edges=[0], metrics=[0])  # a zero metric is accepted by the mirror ...
-    with pytest.raises(SpfError) as ei:
-        eng.refresh([0, 1], d, n)  # ... and rejected loudly by the solve
-    assert ei.value.code == ENOTSUP
+    eng.patch(edges=[0], metrics=[0])  # a zero metric: every row re-solved by the exact kernel
+    assert eng.refresh([0, 1], d, n) == 2
+    check_rows(eng, eng.g, [0, 1], d, n, None)
+    eng.patch()  # empty patch after a zero-metric graph: rows re-solved again
+    assert eng.refresh([0, 1], d, n) == 2
+    eng.patch(edges=[0], metrics=[1])  # back to positive metrics: rows from the exact kernel refreshed
+    assert eng.refresh([0, 1], d, n) == 2
+    check_rows(eng, eng.g, [0, 1], d, n, None)
     eng.patch()  # empty patch: nothing to re-solve
     eng.patch(edges=[0], metrics=[1])
     assert eng.refresh([0, 1], d, n) >= 0
