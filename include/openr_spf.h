@@ -41,7 +41,9 @@
  *
  * Semantics (bit-exact with LinkState::runSpf, any metric values)
  *   dist[s][v]   u64 shortest distance (NodeSpfResult::metric), UINT64_MAX if v is not
- *                in the SpfResult (unreachable). dist[s][src] = 0.
+ *                in the SpfResult (unreachable). dist[s][src] = 0. (With wrapped metrics a
+ *                reached node's sum can itself be UINT64_MAX: openr_spf_solve_order's
+ *                order[] tells the two apart.)
  *   nh[s][v][b]  next-hop set of v as a bitset over the source's DISTINCT neighbours in
  *                CSR row order: bit i (byte i/8, bit i%8) <-> the i-th distinct `col`
  *                value of row src (openr_spf_neighbor_map). nh bits of src itself are 0.

@@ -694,8 +694,10 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
       const uint64_t* t = tight.data() + k * (size_t)std::max<uint32_t>(tw, 1);
       SpfResult& res = out[slot[k]];
       res.reserve(V);
+      const uint32_t* pop = wantOrder ? popIndex.data() + k * V : nullptr;
       for (uint32_t v = 0; v < V; ++v) {
-        if (d[v] == UINT64_MAX) continue;
+        // reached: popped (a wrapped sum can equal UINT64_MAX), else a finite distance
+        if (pop ? pop[v] == UINT32_MAX : d[v] == UINT64_MAX) continue;
         NodeSpfResult r(d[v]);
         const uint8_t* hv = h + (size_t)v * nb;
         for (uint32_t i = 0; i < nn; ++i)
@@ -705,7 +707,6 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
       order.clear();
       for (uint32_t e = 0; e < E; ++e)
         if ((t[e >> 6] >> (e & 63)) & 1ull) order.push_back(e);
-      const uint32_t* pop = wantOrder ? popIndex.data() + k * V : nullptr;
       std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
         const uint32_t ux = m.edgeOwner[x], uy = m.edgeOwner[y];
         if (pop) return pop[ux] != pop[uy] ? pop[ux] < pop[uy] : x < y;

@@ -547,6 +547,33 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
   return l;
 }
 
+// next-hop sets of the grouped repair as u32 words in registers (<= 256 bits)
+constexpr uint32_t kGrpNhWords = 8;
+
+// acc |= the nb-byte next-hop set at p (compile-time word indices: no scratch arrays)
+__device__ __forceinline__ void nh_or(uint32_t (&acc)[kGrpNhWords], const uint8_t* p, uint32_t nb) {
+#pragma unroll
+  for (uint32_t k = 0; k < kGrpNhWords; ++k) {
+    if (4u * k >= nb) break;
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; ++j)
+      if (4u * k + j < nb) w |= (uint32_t)p[4u * k + j] << (8u * j);
+    acc[k] |= w;
+  }
+}
+
+// min over the 8-lane group of the calling lane
+template <typename D>
+__device__ __forceinline__ D grp8_min(D x) {
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    const D y = __shfl_xor(x, o);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
 template <typename D, bool LG>
 struct GrpWave {
   const DevGraph* g;  // ledge / rev / adj of the unit's link (read once per unit)
@@ -560,6 +587,7 @@ struct GrpWave {
   uint32_t *ina, *dq, *nhm, *ctl;
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_WHATIF_PROF): per-phase cycles and sizes, or null
+  unsigned long long pacc[8];  // this wave's share of prof, added once when the wave retires
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
@@ -671,31 +699,40 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
   }
   const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
   if (c.prof) pt1 = (long long)__builtin_amdgcn_s_memtime();
-  // (2) new distances inside A: best entry from outside A, then relaxation within A
-  for (uint32_t i = lane; i < na; i += 64u) {
-    const uint32_t x = c.alist[i];
-    const uint2 r = c.gv.row(x);
+  // (2) new distances inside A: best entry from outside A, then relaxation within A; an
+  // 8-lane group per A node, a lane per in-edge (rows are short: one pass, then a min)
+  const uint32_t sub = lane & 7u;
+  for (uint32_t i0 = 0; i0 < na; i0 += 8u) {
+    const uint32_t i = i0 + (lane >> 3);
     D best = INF;
-    for (uint32_t e = r.x; e < r.y; ++e) {
-      const EdgeRec q = c.gv.rec(e);
-      if (!c.in_usable(q) || bit_of(c.ina, q.col)) continue;
-      const D du = c.bdist[q.col];
-      if (du == INF) continue;
-      const D cand = du + (D)c.wi(q);
-      best = cand < best ? cand : best;
+    uint32_t x = 0;
+    if (i < na) {
+      x = c.alist[i];
+      const uint2 r = c.gv.row(x);
+      for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
+        const EdgeRec q = c.gv.rec(e);
+        if (!c.in_usable(q) || bit_of(c.ina, q.col)) continue;
+        const D du = c.bdist[q.col];
+        if (du == INF) continue;
+        const D cand = du + (D)c.wi(q);
+        best = cand < best ? cand : best;
+      }
     }
-    c.adist[x] = best;
+    best = grp8_min(best);
+    if (i < na && sub == 0) c.adist[x] = best;
   }
   lds_fence();
   for (;;) {
     if (lane == 0) c.ctl[2] = 0;
     lds_fence();
-    for (uint32_t i = lane; i < na; i += 64u) {
+    for (uint32_t i0 = 0; i0 < na; i0 += 8u) {
+      const uint32_t i = i0 + (lane >> 3);
+      if (i >= na) continue;
       const uint32_t x = c.alist[i];
       const D dx = c.adist[x];
       if (dx == INF || !c.expands(x)) continue;
       const uint2 r = c.gv.row(x);
-      for (uint32_t e = r.x; e < r.y; ++e) {
+      for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
         const EdgeRec q = c.gv.rec(e);
         if (q.down || q.lid == c.link || !bit_of(c.ina, q.col)) continue;
         const D cand = dx + (D)c.w(q);
@@ -710,6 +747,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
   }
   // (3) next hops in increasing new distance over the dirty set
   if (c.prof) pt2 = (long long)__builtin_amdgcn_s_memtime();
+  const uint32_t nbw = (nb + 3u) / 4u;
   uint32_t nchanged = 0, buckets = 0;
   uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
   while (done < nd) {
@@ -738,20 +776,22 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
       c.dlist[done + i] = i < nm ? c.alist[i] : c.alist[V - 1u - (i - nm)];
     if (lane == 0) c.ctl[1] = nd;
     lds_fence();
+    // bucket members (all at distance mn: no member reads another's set) by 8-lane groups,
+    // a lane per in-edge; the group ORs its lanes' partial sets
     uint32_t cnt_changed = 0;
-    for (uint32_t i0 = 0; i0 < nm; i0 += 64u) {
-      const uint32_t i = i0 + lane;
-      bool counted = false;
-      if (i < nm) {
-        const uint32_t v = c.dlist[done + i];
-        uint8_t acc[32];
-        uint32_t acc1 = 0;
-        if (nb > 1)
-          for (uint32_t b = 0; b < nb; ++b) acc[b] = 0;
+    for (uint32_t i0 = 0; i0 < nm; i0 += 8u) {
+      const uint32_t i = i0 + (lane >> 3);
+      const bool act = i < nm;
+      uint32_t acc[kGrpNhWords];
+#pragma unroll
+      for (uint32_t k = 0; k < kGrpNhWords; ++k) acc[k] = 0;
+      uint32_t v = 0;
+      if (act) {
+        v = c.dlist[done + i];
         const D dv = c.dist(v);
         const uint2 r = c.gv.row(v);
         if (dv != INF)
-          for (uint32_t e = r.x; e < r.y; ++e) {
+          for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
             const EdgeRec q = c.gv.rec(e);
             if (!c.in_usable(q)) continue;
             const uint32_t u = q.col;
@@ -759,32 +799,41 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
             if (du == INF || (uint64_t)du + c.wi(q) != (uint64_t)dv) continue;
             if (u == c.src) {
               const uint32_t bit = c.gv.nbr_in(e);
-              if (nb == 1) acc1 |= 1u << bit;
-              else acc[bit >> 3] |= (uint8_t)(1u << (bit & 7u));
+#pragma unroll
+              for (uint32_t k = 0; k < kGrpNhWords; ++k)
+                if (bit >> 5 == k) acc[k] |= 1u << (bit & 31u);
             } else {
-              const uint8_t* hu = c.nh(u);
-              if (nb == 1) acc1 |= hu[0];
-              else
-                for (uint32_t b = 0; b < nb; ++b) acc[b] |= hu[b];
+              nh_or(acc, c.nh(u), nb);
             }
           }
-        const uint8_t* hv = c.nh(v);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kGrpNhWords; ++k) {
+        if (k >= nbw) break;
+        acc[k] |= __shfl_xor(acc[k], 1);
+        acc[k] |= __shfl_xor(acc[k], 2);
+        acc[k] |= __shfl_xor(acc[k], 4);
+      }
+      bool counted = false;
+      if (act) {
+        uint32_t cur[kGrpNhWords];
+#pragma unroll
+        for (uint32_t k = 0; k < kGrpNhWords; ++k) cur[k] = 0;
+        nh_or(cur, c.nh(v), nb);
         bool diff = false;
-        if (nb == 1) diff = (uint8_t)acc1 != hv[0];
-        else
-          for (uint32_t b = 0; b < nb; ++b) diff |= acc[b] != hv[b];
-        if (diff) {
+#pragma unroll
+        for (uint32_t k = 0; k < kGrpNhWords; ++k) diff |= acc[k] != cur[k];
+        if (diff && sub == 0) {
           uint8_t* o = c.anh + (size_t)v * nb;
-          if (nb == 1) o[0] = (uint8_t)acc1;
-          else
-            for (uint32_t b = 0; b < nb; ++b) o[b] = acc[b];
+          for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
           atomicOr(&c.nhm[v >> 5], 1u << (v & 31u));
         }
         const bool in_a = bit_of(c.ina, v);
-        counted = in_a || diff;
+        counted = sub == 0 && (in_a || diff);
         if (diff && !in_a && c.expands(v)) {
+          const D dv = c.dist(v);
           const uint2 ro = c.gv.row(v);
-          for (uint32_t e = ro.x; e < ro.y; ++e) {
+          for (uint32_t e = ro.x + sub; e < ro.y; e += 8u) {
             const EdgeRec q = c.gv.rec(e);
             const uint32_t y = q.col;
             if (q.down || q.lid == c.link || y == c.src) continue;
@@ -804,14 +853,14 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
   }
   if (c.prof && lane == 0) {
     pt3 = (long long)__builtin_amdgcn_s_memtime();
-    atomicAdd(&c.prof[0], (unsigned long long)(pt1 - pt0));
-    atomicAdd(&c.prof[1], (unsigned long long)(pt2 - pt1));
-    atomicAdd(&c.prof[2], (unsigned long long)(pt3 - pt2));
-    atomicAdd(&c.prof[3], 1ull);
-    atomicAdd(&c.prof[4], (unsigned long long)na);
-    atomicAdd(&c.prof[5], (unsigned long long)nd);
-    atomicAdd(&c.prof[6], (unsigned long long)buckets);
-    atomicAdd(&c.prof[7], (unsigned long long)nchanged);
+    c.pacc[0] += (unsigned long long)(pt1 - pt0);
+    c.pacc[1] += (unsigned long long)(pt2 - pt1);
+    c.pacc[2] += (unsigned long long)(pt3 - pt2);
+    c.pacc[3] += 1ull;
+    c.pacc[4] += na;
+    c.pacc[5] += nd;
+    c.pacc[6] += buckets;
+    c.pacc[7] += nchanged;
   }
   return nchanged;
 }
@@ -864,6 +913,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   c.nb = nb;
   c.unit = unit != 0;
   c.prof = prof;
+  for (int k = 0; k < 8; ++k) c.pacc[k] = 0;
   c.bdist = bdist;
   c.bnh = bnh;
   c.ctl = reinterpret_cast<uint32_t*>(wb);
@@ -933,6 +983,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   }
   if (lane == 0 && n_aff) atomicAdd(affected, n_aff);
   if (prof && lane == 0) {
+    for (int k = 0; k < 8; ++k) atomicAdd(&prof[k], c.pacc[k]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }

@@ -67,7 +67,8 @@ def materialize(g, src: int, dist: np.ndarray, nh: np.ndarray, nbrs: Sequence[in
     owner = g.edge_owner()
     pls = tight_in_edges(g, dist, tight, owner, pop) if tight is not None else {}
     res: Dict[str, NodeSpfResult] = {}
-    for v in np.nonzero(dist != np.uint64(U64_MAX))[0].tolist():
+    reached = (pop != 0xFFFFFFFF) if pop is not None else (dist != np.uint64(U64_MAX))  # wrapped sums may be U64_MAX
+    for v in np.nonzero(reached)[0].tolist():
         r = NodeSpfResult(int(dist[v]), nh_names(g, src, nh[v], nbrs))
         for e in pls.get(v, []):
             r.path_edges.append(e)

@@ -559,16 +559,19 @@ static void randomOracleParity(uint64_t seed, MetricFn metric) {
                     m.nameRank.data()};
     const uint32_t NV = og.num_nodes, NE = og.num_dir_edges;
     std::vector<uint64_t> dist(NV);
-    std::vector<uint32_t> plp(NV + 1), ple(NE + 1);
+    std::vector<uint32_t> plp(NV + 1), ple(NE + 1), order(NV);
+    std::vector<uint8_t> reached(NV);
     for (uint32_t s = 0; s < NV; ++s) {
       for (int useMetric = 0; useMetric < 2; ++useMetric) {
         auto const& res = ls.getSpfResult(m.names[s], useMetric != 0);
-        int64_t cnt = oracle_run_spf(&og, s, useMetric, nullptr, dist.data(), nullptr, 0, nullptr, plp.data(),
+        int64_t cnt = oracle_run_spf(&og, s, useMetric, nullptr, dist.data(), nullptr, 0, order.data(), plp.data(),
                                      ple.data());
         EXPECT_EQ((size_t)cnt, res.size());
+        std::fill(reached.begin(), reached.end(), 0);
+        for (int64_t i = 0; i < cnt; ++i) reached[order[i]] = 1;  // a wrapped dist may equal UINT64_MAX
         for (uint32_t v = 0; v < NV; ++v) {
           auto it = res.find(m.names[v]);
-          if (dist[v] == UINT64_MAX) {
+          if (!reached[v]) {
             EXPECT_TRUE(it == res.end());
             continue;
           }
