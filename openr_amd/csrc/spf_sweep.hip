@@ -131,14 +131,64 @@ __host__ __device__ inline IncrLayout incr_layout(uint32_t V, uint32_t nb, uint3
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ bool bit_of(const uint32_t* b, uint32_t i) { return (b[i >> 5] >> (i & 31u)) & 1u; }
 
+// DPP lane moves (VALU, no LDS round trip; ds_bpermute shuffles cost one each). An
+// invalid source lane (disabled by EXEC) yields x itself, neutral for min / or.
+template <int C, typename T>
+__device__ __forceinline__ T dppmv(T x) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
+  if constexpr (sizeof(T) == 4) {
+    return (T)__builtin_amdgcn_update_dpp((int)x, (int)x, C, 0xF, 0xF, false);
+  } else {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)x, (int)(uint32_t)x, C, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(x >> 32), (int)(uint32_t)(x >> 32), C,
+                                                              0xF, 0xF, false);
+    return (T)((uint64_t)lo | ((uint64_t)hi << 32));
+  }
+}
+constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowMirror = 0x140, kDppHalfMirror = 0x141;
+
+template <typename T>
+__device__ __forceinline__ T readlane_t(T x, int l) {
+  if constexpr (sizeof(T) == 4) {
+    return (T)__builtin_amdgcn_readlane((int)x, l);
+  } else {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return (T)((uint64_t)lo | ((uint64_t)hi << 32));
+  }
+}
+
+// min over the 8-lane group of the calling lane (every lane of the group gets it)
+template <typename D>
+__device__ __forceinline__ D grp8_min(D x) {
+  D y = dppmv<kDppQuadXor1>(x);
+  x = y < x ? y : x;
+  y = dppmv<kDppQuadXor2>(x);
+  x = y < x ? y : x;
+  y = dppmv<kDppHalfMirror>(x);
+  return y < x ? y : x;
+}
+
+// wave-wide minimum, uniform result: rows of 16 by DPP, then four lane reads
 template <typename D>
 __device__ __forceinline__ D wave_min_t(D x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const D y = __shfl_xor(x, o);
-    x = y < x ? y : x;
-  }
-  return x;
+  x = grp8_min(x);
+  const D y = dppmv<kDppRowMirror>(x);
+  x = y < x ? y : x;
+  const D a = readlane_t(x, 0), b = readlane_t(x, 16), c = readlane_t(x, 32), d = readlane_t(x, 48);
+  const D ab = a < b ? a : b, cd = c < d ? c : d;
+  return ab < cd ? ab : cd;
+}
+
+// OR over the lanes [0, n) of the wave (other lanes hold 0), uniform result
+__device__ __forceinline__ uint32_t wave_or_prefix(uint32_t x, uint32_t n) {
+  x |= dppmv<kDppQuadXor1>(x);
+  x |= dppmv<kDppQuadXor2>(x);
+  x |= dppmv<kDppHalfMirror>(x);
+  if (n <= 8u) return readlane_t(x, 0);
+  x |= dppmv<kDppRowMirror>(x);
+  if (n <= 16u) return readlane_t(x, 0);
+  return readlane_t(x, 0) | readlane_t(x, 16) | readlane_t(x, 32) | readlane_t(x, 48);
 }
 
 template <typename D>
@@ -509,10 +559,12 @@ struct GraphView<true> {  // compact LDS copy
   __device__ bool ovl(uint32_t x) const { return (ovlb[x >> 5] >> (x & 31u)) & 1u; }
 };
 
+constexpr uint32_t kGrpMaxChunk = 2048;  // links per work item
+
 struct GrpLayout {
   uint32_t grow, grec, gnbr, govl;                                  // LDS graph (LG only)
-  uint32_t bdist, bnh, btight, wave0, wstride;                      // wave w at wave0 + w * wstride
-  uint32_t w_ina, w_dq, w_nhm, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
+  uint32_t bdist, bnh, btight, btin, ulist, wave0, wstride;         // wave w at wave0 + w * wstride
+  uint32_t w_ina, w_dq, w_nhm, w_dec, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
   uint32_t total;
 };
 
@@ -533,10 +585,13 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
   l.bdist = take(off, dist_bytes * V);
   l.bnh = take(off, nb * V);
   l.btight = take(off, 8u * ((E + 63u) / 64u));
+  l.btin = take(off, 2u * (V + 1u));  // u16 base-tight in-degree per node
+  l.ulist = take(off, 4u * kGrpMaxChunk);  // the item's affected links: offset in the chunk << 16 | b
   uint32_t w = 16;  // wave control: [0] A count, [1] dirty count, [2] flag
   l.w_ina = take(w, 4u * vw);
   l.w_dq = take(w, 4u * vw);
   l.w_nhm = take(w, 4u * vw);
+  l.w_dec = take(w, 2u * (V + 1u));  // u16 per node: tight in-edges whose tail joined A
   l.w_adist = take(w, dist_bytes * V);
   l.w_anh = take(w, nb * V);
   l.w_alist = take(w, 2u * V);
@@ -548,33 +603,29 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
 }
 
 // next-hop sets of the grouped repair as u32 words in registers (<= 256 bits)
-constexpr uint32_t kGrpNhWords = 8;
+constexpr uint32_t kGrpNhWords = 8;  // W = 1 (sets <= 32 bits) or 8 (<= 256 bits): kernel variants
 
-// acc |= the nb-byte next-hop set at p (compile-time word indices: no scratch arrays)
-__device__ __forceinline__ void nh_or(uint32_t (&acc)[kGrpNhWords], const uint8_t* p, uint32_t nb) {
+// acc |= (sel ? a : b), nb-byte sets: both rows are loaded before the select, so an
+// overlay lookup costs one LDS round trip, not a bitmap read and then a row read
+template <uint32_t W>
+__device__ __forceinline__ void nh_or_sel(uint32_t (&acc)[W], const uint8_t* a, const uint8_t* b, bool sel,
+                                          uint32_t nb) {
 #pragma unroll
-  for (uint32_t k = 0; k < kGrpNhWords; ++k) {
+  for (uint32_t k = 0; k < W; ++k) {
     if (4u * k >= nb) break;
-    uint32_t w = 0;
+    uint32_t wa = 0, wb = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 4u; ++j)
-      if (4u * k + j < nb) w |= (uint32_t)p[4u * k + j] << (8u * j);
-    acc[k] |= w;
+      if (4u * k + j < nb) {
+        wa |= (uint32_t)a[4u * k + j] << (8u * j);
+        wb |= (uint32_t)b[4u * k + j] << (8u * j);
+      }
+    acc[k] |= sel ? wa : wb;
   }
 }
 
-// min over the 8-lane group of the calling lane
-template <typename D>
-__device__ __forceinline__ D grp8_min(D x) {
-#pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
-    const D y = __shfl_xor(x, o);
-    x = y < x ? y : x;
-  }
-  return x;
-}
 
-template <typename D, bool LG>
+template <typename D, bool LG, uint32_t W>
 struct GrpWave {
   const DevGraph* g;  // ledge / rev / adj of the unit's link (read once per unit)
   GraphView<LG> gv;
@@ -585,6 +636,9 @@ struct GrpWave {
   D* adist;
   uint8_t* anh;
   uint32_t *ina, *dq, *nhm, *ctl;
+  const uint64_t* btight;  // base-tight mask of the source (workgroup rows)
+  const uint16_t* tin;     // base-tight in-degree (workgroup rows)
+  uint16_t* dec;           // per unit: tight in-edges of v lost (tail in A, or the failed edge)
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_WHATIF_PROF): per-phase cycles and sizes, or null
   unsigned long long pacc[8];  // this wave's share of prof, added once when the wave retires
@@ -592,52 +646,20 @@ struct GrpWave {
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
   // distance after the repair of (2): A nodes from the overlay, the rest from the base
-  __device__ D dist(uint32_t u) const { return bit_of(ina, u) ? adist[u] : bdist[u]; }
-  __device__ const uint8_t* nh(uint32_t u) const {
-    return bit_of(nhm, u) ? anh + (size_t)u * nb : bnh + (size_t)u * nb;
+  __device__ D dist(uint32_t u) const {
+    const D a = adist[u], b = bdist[u];  // both loads issue with the bitmap read
+    return bit_of(ina, u) ? a : b;
+  }
+  __device__ void nh_or(uint32_t (&acc)[W], uint32_t u) const {
+    nh_or_sel(acc, anh + (size_t)u * nb, bnh + (size_t)u * nb, bit_of(nhm, u), nb);
   }
   // in-edge u -> v (the record of v -> u) usable, not the failed link, u may expand
   __device__ bool in_usable(const EdgeRec& r) const { return !r.down && r.lid != link && (r.col == src || !r.sink); }
 };
 
-// live tight in-edge of v from outside A (base distances; step (1) only), wave-parallel
-template <typename D, bool LG>
-__device__ bool grp_live_pred(const GrpWave<D, LG>& c, uint32_t v, uint32_t lane) {
-  constexpr D INF = (D)~(D)0;
-  const D dv = c.bdist[v];
-  const uint2 r = c.gv.row(v);
-  for (uint32_t e = r.x + lane; __any(e < r.y); e += 64u) {
-    bool ok = false;
-    if (e < r.y) {
-      const EdgeRec q = c.gv.rec(e);
-      if (c.in_usable(q) && !bit_of(c.ina, q.col)) {
-        const D du = c.bdist[q.col];
-        ok = du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv;
-      }
-    }
-    if (__any(ok)) return true;
-  }
-  return false;
-}
-
-template <typename D, bool LG>
-__device__ bool grp_live_pred_lane(const GrpWave<D, LG>& c, uint32_t v) {
-  constexpr D INF = (D)~(D)0;
-  const D dv = c.bdist[v];
-  const uint2 r = c.gv.row(v);
-  for (uint32_t e = r.x; e < r.y; ++e) {
-    const EdgeRec q = c.gv.rec(e);
-    if (!c.in_usable(q) || bit_of(c.ina, q.col)) continue;
-    const D du = c.bdist[q.col];
-    if (du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv) return true;
-  }
-  return false;
-}
-
 // One affected unit: returns the changed-node count (uniform across the wave).
-template <typename D, bool LG>
-__device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
-  const DevGraph& g = *c.g;
+template <typename D, bool LG, uint32_t W>
+__device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, uint32_t bnode) {
   constexpr D INF = (D)~(D)0;
   const uint32_t vw = (V + 31u) / 32u, nb = c.nb;
   for (uint32_t i = lane; i < vw; i += 64u) {
@@ -645,53 +667,40 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     c.dq[i] = 0;
     c.nhm[i] = 0;
   }
+  for (uint32_t i = lane; i < (V + 1u) / 2u; i += 64u) reinterpret_cast<uint32_t*>(c.dec)[i] = 0;
   if (lane == 0) c.ctl[0] = c.ctl[1] = 0;
   lds_fence();
-  // the tight direction a->b of the link (the caller checked one is tight)
-  const uint2 ee = g.ledge[c.link];
-  uint32_t bnode = UINT32_MAX;
-  for (int t = 0; t < 2; ++t) {
-    const uint32_t e = t ? ee.y : ee.x;
-    const uint32_t av = g.adj[e];
-    const uint32_t head = av & ~kEdgeDown, tail = g.adj[g.rev[e]] & ~kEdgeDown;
-    if ((av & kEdgeDown) || !c.expands(tail)) continue;
-    const D dt = c.bdist[tail], dh = c.bdist[head];
-    if (dt != INF && dh != INF && (uint64_t)dt + (c.unit ? 1u : g.w[e]) == (uint64_t)dh) bnode = head;
-  }
-  if (bnode == UINT32_MAX) return 0;
   long long pt0 = c.prof ? (long long)__builtin_amdgcn_s_memtime() : 0, pt1 = 0, pt2 = 0, pt3 = 0;
-  // (1) A by decremental propagation over the base tight DAG (base distances)
+  // (1) A by decremental propagation over the base tight DAG: v joins A when every one of
+  // its tight in-edges is lost (the failed edge a->b, or a tail already in A). dec[v]
+  // counts the lost ones; the lane whose increment reaches tin[v] appends v.
   if (lane == 0) {
     c.dq[bnode >> 5] |= 1u << (bnode & 31u);
     c.dlist[c.ctl[1]++] = (uint16_t)bnode;
-  }
-  if (!grp_live_pred(c, bnode, lane) && lane == 0) {
-    c.ina[bnode >> 5] |= 1u << (bnode & 31u);
-    c.alist[c.ctl[0]++] = (uint16_t)bnode;
+    if (c.tin[bnode] == 1u) {
+      c.ina[bnode >> 5] |= 1u << (bnode & 31u);
+      c.alist[c.ctl[0]++] = (uint16_t)bnode;
+    }
   }
   lds_fence();
-  // 8-lane groups: eight A members per wave pass (A only grows, so a successor tested by
-  // several groups is added once, by the bit's atomicOr; a pred that joins A later is
-  // itself processed later and re-tests its successors)
+  // 8-lane groups: eight A members per wave pass, a lane per out-edge (members appended
+  // during a pass are taken by the next)
   for (uint32_t idx0 = 0, na0; idx0 < (na0 = __builtin_amdgcn_readfirstlane(c.ctl[0]));
-       idx0 += min(8u, na0 - idx0)) {  // members appended during a pass are taken by the next
+       idx0 += min(8u, na0 - idx0)) {
     const uint32_t idx = idx0 + (lane >> 3), sub = lane & 7u;
     if (idx < na0) {
       const uint32_t x = c.alist[idx];
-      if (c.expands(x)) {
-        const D dx = c.bdist[x];
-        const uint2 r = c.gv.row(x);
-        for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
-          const EdgeRec q = c.gv.rec(e);
-          const uint32_t y = q.col;
-          if (!q.down && q.lid != c.link && !bit_of(c.ina, y) && c.bdist[y] != INF &&
-              (uint64_t)dx + c.w(q) == (uint64_t)c.bdist[y]) {
-            const uint32_t bit = 1u << (y & 31u);
-            if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
-            if (!grp_live_pred_lane(c, y)) {
-              if (!(atomicOr(&c.ina[y >> 5], bit) & bit)) c.alist[atomicAdd(&c.ctl[0], 1u)] = (uint16_t)y;
-            }
-          }
+      const uint2 r = c.gv.row(x);
+      for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
+        if (!((c.btight[e >> 6] >> (e & 63u)) & 1ull)) continue;  // base-tight x -> y (x expands)
+        const uint32_t y = c.gv.rec(e).col;
+        const uint32_t bit = 1u << (y & 31u);
+        if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
+        const uint32_t sh = 16u * (y & 1u);
+        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(c.dec) + (y >> 1), 1u << sh);
+        if (((old >> sh) & 0xFFFFu) + 1u == c.tin[y]) {
+          atomicOr(&c.ina[y >> 5], bit);
+          c.alist[atomicAdd(&c.ctl[0], 1u)] = (uint16_t)y;
         }
       }
     }
@@ -745,111 +754,144 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
     lds_fence();
     if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
   }
-  // (3) next hops in increasing new distance over the dirty set
+  // (3) next hops in increasing new distance over the dirty set. Buckets of equal distance
+  // (a successor appended while processing distance m lies strictly beyond m); one node
+  // at a time across the wave, a lane per edge of its row. The dirty list's first 64
+  // entries live in lanes (entry i in lane i), later ones are re-read from LDS.
   if (c.prof) pt2 = (long long)__builtin_amdgcn_s_memtime();
   const uint32_t nbw = (nb + 3u) / 4u;
   uint32_t nchanged = 0, buckets = 0;
-  uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), done = 0;
-  while (done < nd) {
-    ++buckets;
-    D mn = INF;
-    for (uint32_t i = done + lane; i < nd; i += 64u) {
-      const D d = c.dist(c.dlist[i]);
-      mn = d < mn ? d : mn;
+  uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), loaded = 0;
+  uint32_t ev = 0;
+  D ed = INF;
+  bool pend = false;
+  auto load_entries = [&]() {
+    const uint32_t hi = min(nd, 64u);
+    if (loaded < hi) {
+      if (lane >= loaded && lane < hi) {
+        ev = c.dlist[lane];
+        ed = c.dist(ev);
+        pend = true;
+      }
+      loaded = hi;
     }
-    mn = wave_min_t(mn);
-    uint32_t nm = 0, nr = 0;
-    for (uint32_t i0 = done; i0 < nd; i0 += 64u) {
+  };
+  // one dirty node v (wave-uniform) at new distance dv: pull its set over tight in-edges;
+  // if it changed and v keeps its base distance, its tight successors become dirty
+  auto process = [&](uint32_t v, D dv) {
+    const uint2 r = c.gv.row(v);
+    const uint32_t deg = r.y - r.x;
+    uint32_t cur[W], acc[W];
+#pragma unroll
+    for (uint32_t k = 0; k < W; ++k) cur[k] = acc[k] = 0;
+    c.nh_or(cur, v);
+    const bool in_a = bit_of(c.ina, v);
+    EdgeRec q{};
+    D du = INF;
+    for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+      const uint32_t e = e0 + lane;
+      du = INF;
+      if (e < r.y) {
+        q = c.gv.rec(e);
+        du = c.dist(q.col);
+        if (dv != INF && c.in_usable(q) && du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv) {
+          if (q.col == c.src) {
+            const uint32_t bit = c.gv.nbr_in(e);
+#pragma unroll
+            for (uint32_t k = 0; k < W; ++k)
+              if (bit >> 5 == k) acc[k] |= 1u << (bit & 31u);
+          } else {
+            c.nh_or(acc, q.col);
+          }
+        }
+      }
+    }
+    bool diff = false;
+#pragma unroll
+    for (uint32_t k = 0; k < W; ++k) {
+      if (W > 1 && k >= nbw) break;
+      acc[k] = wave_or_prefix(acc[k], min(deg, 64u));
+      diff |= acc[k] != __builtin_amdgcn_readfirstlane(cur[k]);
+    }
+    if (diff && lane == 0) {
+      uint8_t* o = c.anh + (size_t)v * nb;
+      for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
+      c.nhm[v >> 5] |= 1u << (v & 31u);
+    }
+    if (in_a || diff) ++nchanged;
+    if (!diff || in_a || dv == INF || !c.expands(v)) return;
+    for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+      const uint32_t e = e0 + lane;
+      if (deg > 64u) {  // rows longer than a wave: the first pass kept only its last chunk
+        du = INF;
+        if (e < r.y) {
+          q = c.gv.rec(e);
+          du = c.dist(q.col);
+        }
+      }
+      const uint32_t y = q.col;
+      bool fresh = false;
+      if (e < r.y && !q.down && q.lid != c.link && y != c.src && du != INF && (uint64_t)dv + c.w(q) == (uint64_t)du) {
+        const uint32_t bit = 1u << (y & 31u);
+        fresh = !(atomicOr(&c.dq[y >> 5], bit) & bit);
+      }
+      const unsigned long long m = __ballot(fresh);
+      if (fresh) {
+        const uint32_t pos = nd + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        c.dlist[pos] = (uint16_t)y;
+      }
+      nd += (uint32_t)__popcll(m);
+    }
+  };
+  load_entries();
+  bool first = true;
+  D last = 0;
+  for (;;) {
+    // bucket minimum over pending entries (lanes, then the LDS overflow beyond 64)
+    D mn = pend ? ed : INF;
+    bool anyp = __ballot(pend) != 0;
+    for (uint32_t i0 = 64; i0 < nd; i0 += 64u) {
       const uint32_t i = i0 + lane;
-      const bool live = i < nd;
-      const uint32_t v = live ? c.dlist[i] : 0u;
-      const bool in = live && c.dist(v) == mn;
-      const unsigned long long mi = __ballot(in), mr = __ballot(live && !in);
-      const unsigned long long lt = (1ull << lane) - 1ull;
-      if (in) c.alist[nm + (uint32_t)__popcll(mi & lt)] = (uint16_t)v;
-      if (live && !in) c.alist[V - 1u - (nr + (uint32_t)__popcll(mr & lt))] = (uint16_t)v;
-      nm += (uint32_t)__popcll(mi);
-      nr += (uint32_t)__popcll(mr);
+      if (i < nd) {
+        const D d = c.dist(c.dlist[i]);
+        const bool p = first || d > last;
+        mn = (p && d < mn) ? d : mn;
+        anyp |= __ballot(p) != 0;
+      }
+      anyp = __ballot(anyp) != 0;
     }
-    lds_fence();
-    for (uint32_t i = lane; i < nm + nr; i += 64u)
-      c.dlist[done + i] = i < nm ? c.alist[i] : c.alist[V - 1u - (i - nm)];
-    if (lane == 0) c.ctl[1] = nd;
-    lds_fence();
-    // bucket members (all at distance mn: no member reads another's set) by 8-lane groups,
-    // a lane per in-edge; the group ORs its lanes' partial sets
-    uint32_t cnt_changed = 0;
-    for (uint32_t i0 = 0; i0 < nm; i0 += 8u) {
-      const uint32_t i = i0 + (lane >> 3);
-      const bool act = i < nm;
-      uint32_t acc[kGrpNhWords];
-#pragma unroll
-      for (uint32_t k = 0; k < kGrpNhWords; ++k) acc[k] = 0;
+    if (!anyp) break;
+    mn = wave_min_t(mn);
+    ++buckets;
+    unsigned long long m = __ballot(pend && ed == mn);
+    const uint32_t nd0 = nd;
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      m &= m - 1ull;
+      process((uint32_t)__builtin_amdgcn_readlane((int)ev, k), mn);
+    }
+    for (uint32_t i0 = 64; i0 < nd0; i0 += 64u) {
+      const uint32_t i = i0 + lane;
       uint32_t v = 0;
-      if (act) {
-        v = c.dlist[done + i];
-        const D dv = c.dist(v);
-        const uint2 r = c.gv.row(v);
-        if (dv != INF)
-          for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
-            const EdgeRec q = c.gv.rec(e);
-            if (!c.in_usable(q)) continue;
-            const uint32_t u = q.col;
-            const D du = c.dist(u);
-            if (du == INF || (uint64_t)du + c.wi(q) != (uint64_t)dv) continue;
-            if (u == c.src) {
-              const uint32_t bit = c.gv.nbr_in(e);
-#pragma unroll
-              for (uint32_t k = 0; k < kGrpNhWords; ++k)
-                if (bit >> 5 == k) acc[k] |= 1u << (bit & 31u);
-            } else {
-              nh_or(acc, c.nh(u), nb);
-            }
-          }
+      bool hit = false;
+      if (i < nd0) {
+        v = c.dlist[i];
+        const D d = c.dist(v);
+        hit = (first || d > last) && d == mn;
       }
-#pragma unroll
-      for (uint32_t k = 0; k < kGrpNhWords; ++k) {
-        if (k >= nbw) break;
-        acc[k] |= __shfl_xor(acc[k], 1);
-        acc[k] |= __shfl_xor(acc[k], 2);
-        acc[k] |= __shfl_xor(acc[k], 4);
+      unsigned long long mo = __ballot(hit);
+      while (mo) {
+        const int k = __builtin_ctzll(mo);
+        mo &= mo - 1ull;
+        process((uint32_t)__builtin_amdgcn_readlane((int)v, k), mn);
       }
-      bool counted = false;
-      if (act) {
-        uint32_t cur[kGrpNhWords];
-#pragma unroll
-        for (uint32_t k = 0; k < kGrpNhWords; ++k) cur[k] = 0;
-        nh_or(cur, c.nh(v), nb);
-        bool diff = false;
-#pragma unroll
-        for (uint32_t k = 0; k < kGrpNhWords; ++k) diff |= acc[k] != cur[k];
-        if (diff && sub == 0) {
-          uint8_t* o = c.anh + (size_t)v * nb;
-          for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
-          atomicOr(&c.nhm[v >> 5], 1u << (v & 31u));
-        }
-        const bool in_a = bit_of(c.ina, v);
-        counted = sub == 0 && (in_a || diff);
-        if (diff && !in_a && c.expands(v)) {
-          const D dv = c.dist(v);
-          const uint2 ro = c.gv.row(v);
-          for (uint32_t e = ro.x + sub; e < ro.y; e += 8u) {
-            const EdgeRec q = c.gv.rec(e);
-            const uint32_t y = q.col;
-            if (q.down || q.lid == c.link || y == c.src) continue;
-            const D dy = c.dist(y);
-            if (dy == INF || (uint64_t)dv + c.w(q) != (uint64_t)dy) continue;
-            const uint32_t bit = 1u << (y & 31u);
-            if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
-          }
-        }
-      }
-      cnt_changed += (uint32_t)__popcll(__ballot(counted));
     }
-    nchanged += cnt_changed;
+    if (pend && ed == mn) pend = false;
+    first = false;
+    last = mn;
+    if (mn == INF) break;  // unreachable nodes expand nothing: this was the last bucket
     lds_fence();
-    done += nm;
-    nd = __builtin_amdgcn_readfirstlane(c.ctl[1]);
+    load_entries();
   }
   if (c.prof && lane == 0) {
     pt3 = (long long)__builtin_amdgcn_s_memtime();
@@ -867,7 +909,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG>& c, uint32_t lane, uint32_t V) {
 
 constexpr uint32_t kGrpMaxBlock = 512;
 
-template <typename D, bool LG>
+template <typename D, bool LG, uint32_t W>
 __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
@@ -885,8 +927,10 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   D* bdist = reinterpret_cast<D*>(base + lay.bdist);
   uint8_t* bnh = reinterpret_cast<uint8_t*>(base + lay.bnh);
   uint64_t* btight = reinterpret_cast<uint64_t*>(base + lay.btight);
+  uint32_t* ulist = reinterpret_cast<uint32_t*>(base + lay.ulist);
+  uint16_t* btin = reinterpret_cast<uint16_t*>(base + lay.btin);
   char* wb = base + lay.wave0 + wave * lay.wstride;
-  GrpWave<D, LG> c;
+  GrpWave<D, LG, W> c;
   c.g = &g;
   if constexpr (LG) {
     // stage the compact graph once per workgroup (a launch serves many items)
@@ -916,10 +960,13 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   for (int k = 0; k < 8; ++k) c.pacc[k] = 0;
   c.bdist = bdist;
   c.bnh = bnh;
+  c.btight = btight;
+  c.tin = btin;
   c.ctl = reinterpret_cast<uint32_t*>(wb);
   c.ina = reinterpret_cast<uint32_t*>(wb + lay.w_ina);
   c.dq = reinterpret_cast<uint32_t*>(wb + lay.w_dq);
   c.nhm = reinterpret_cast<uint32_t*>(wb + lay.w_nhm);
+  c.dec = reinterpret_cast<uint16_t*>(wb + lay.w_dec);
   c.adist = reinterpret_cast<D*>(wb + lay.w_adist);
   c.anh = reinterpret_cast<uint8_t*>(wb + lay.w_anh);
   c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
@@ -947,41 +994,60 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     }
     const uint64_t* trow = base_tight + (size_t)j * tw;
     for (uint32_t i = tid; i < tw; i += block) btight[i] = trow[i];
-    if (tid == 0) wctl[0] = 0;
+    for (uint32_t i = tid; i < (V + 1u) / 2u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
+    if (tid == 0) wctl[0] = wctl[1] = 0;  // [0] affected links listed, [1] next one to repair
     __syncthreads();
-    // waves take groups of 64 links dynamically; a lane per link for the fused filter
-    for (;;) {
-      uint32_t grp = 0;
-      if (lane == 0) grp = atomicAdd(&wctl[0], 1u);
-      grp = __builtin_amdgcn_readfirstlane(__shfl(grp, 0));
-      const uint32_t li = l0 + grp * 64u;
-      if (li >= l1) break;
-      const uint32_t i = li + lane;
+    for (uint32_t e = tid; e < E; e += block)  // base-tight in-degrees
+      if ((btight[e >> 6] >> (e & 63u)) & 1ull) {
+        const uint32_t v = c.gv.rec(e).col;
+        atomicAdd(reinterpret_cast<uint32_t*>(btin) + (v >> 1), 1u << (16u * (v & 1u)));
+      }
+    // fused filter, a thread per link: a link with no base-tight edge changes nothing;
+    // the others are listed with b, the head of their tight edge a->b (at most one
+    // direction of a link is tight), so a repair starts without dependent loads
+    for (uint32_t i0 = l0; i0 < l1; i0 += block) {
+      const uint32_t i = i0 + tid;
       bool hit = false;
-      uint32_t l = 0;
+      uint32_t bnode = 0;
       if (i < l1) {
-        l = links[i];
+        const uint32_t l = links[i];
         const uint2 ee = l < g.L ? g.ledge[l] : make_uint2(UINT32_MAX, UINT32_MAX);
-        if (ee.x != UINT32_MAX)
-          hit = ((btight[ee.x >> 6] >> (ee.x & 63u)) & 1ull) || ((btight[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
+        if (ee.x != UINT32_MAX) {
+          const bool tx = (btight[ee.x >> 6] >> (ee.x & 63u)) & 1ull;
+          hit = tx || ((btight[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
+          if (hit) bnode = g.adj[tx ? ee.x : ee.y] & ~kEdgeDown;
+        }
         if (!hit) changed[(size_t)i * n_src + j] = 0;
       }
-      unsigned long long m = __ballot(hit);
-      n_aff += (uint32_t)__popcll(m);
-      while (m) {
-        const uint32_t k = (uint32_t)__ffsll((long long)m) - 1u;
-        m &= m - 1ull;
-        c.link = __builtin_amdgcn_readfirstlane(__shfl(l, (int)k));
-        const uint32_t cnt = grp_repair(c, lane, V);
-        if (lane == 0) changed[(size_t)(li + k) * n_src + j] = cnt;
-      }
+      const unsigned long long m = __ballot(hit);
+      uint32_t basei = 0;
+      if (lane == 0 && m) basei = atomicAdd(&wctl[0], (uint32_t)__popcll(m));
+      basei = __builtin_amdgcn_readfirstlane(__shfl(basei, 0));
+      if (hit)
+        ulist[basei + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+            ((i - l0) << 16) | bnode;
+    }
+    __syncthreads();
+    const uint32_t n_hit = wctl[0];
+    n_aff += tid == 0 ? n_hit : 0u;
+    // waves take the listed units one at a time: the item ends within one repair of balance
+    for (;;) {
+      uint32_t idx = 0;
+      if (lane == 0) idx = atomicAdd(&wctl[1], 1u);
+      idx = __builtin_amdgcn_readfirstlane(__shfl(idx, 0));
+      if (idx >= n_hit) break;
+      const uint32_t ent = __builtin_amdgcn_readfirstlane(ulist[idx]);
+      const uint32_t i = l0 + (ent >> 16);
+      c.link = links[i];  // first needed in step (2): the load overlaps step (1)
+      const uint32_t cnt = grp_repair(c, lane, V, ent & 0xFFFFu);
+      if (lane == 0) changed[(size_t)i * n_src + j] = cnt;
     }
     __syncthreads();  // every wave is done with this item's shared rows and s_item
     if (tid == 0) s_item = gridDim.x + atomicAdd(&ctr[0], 1u);
     __syncthreads();
     item = s_item;
   }
-  if (lane == 0 && n_aff) atomicAdd(affected, n_aff);
+  if (tid == 0 && n_aff) atomicAdd(affected, n_aff);
   if (prof && lane == 0) {
     for (int k = 0; k < 8; ++k) atomicAdd(&prof[k], c.pacc[k]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
@@ -1095,7 +1161,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   uint64_t cps = (8u * slots + n_src - 1u) / n_src;
   cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
   uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
-  chunk = bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30);
+  chunk = std::min(bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30), kGrpMaxChunk);
   const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
@@ -1109,7 +1175,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   }
 #define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
   do {                                                                                                         \
-    auto k = whatif_group_kernel<DT, LGV>;                                                                     \
+    auto k = nb <= 4u ? whatif_group_kernel<DT, LGV, 1> : whatif_group_kernel<DT, LGV, kGrpNhWords>;                                                                     \
     err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \

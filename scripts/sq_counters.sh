@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counter passes (one rocprofv3 --pmc run each) for the default bench kernel.
-#   BENCH_ARGS="--topology grid100" bash scripts/sq_counters.sh
+#   BENCH_ARGS="--topology grid100" [KFILTER=kernel-name-substring] bash scripts/sq_counters.sh
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/sq"
@@ -14,13 +14,13 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WA
     python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
-python3 - "$OUT" <<'PY'
+python3 - "$OUT" "${KFILTER:-bfs_}" <<'PY'
 import csv, glob, sys, collections
 out = sys.argv[1]
 tot = collections.defaultdict(float); n = collections.Counter()
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "bfs_" not in r.get("Kernel_Name", ""): continue
+        if sys.argv[2] not in r.get("Kernel_Name", ""): continue
         tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
 for k in sorted(tot): print(f"{k:28s} {tot[k]/max(1,n[k]):.4g} per-dispatch-row (rows {n[k]})")
 PY
