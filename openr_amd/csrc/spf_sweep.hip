@@ -135,9 +135,9 @@ __device__ __forceinline__ bool bit_of(const uint32_t* b, uint32_t i) { return (
 // invalid source lane (disabled by EXEC) yields x itself, neutral for min / or.
 template <int C, typename T>
 __device__ __forceinline__ T dppmv(T x) {
-  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lanes");
-  if constexpr (sizeof(T) == 4) {
-    return (T)__builtin_amdgcn_update_dpp((int)x, (int)x, C, 0xF, 0xF, false);
+  static_assert(sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8, "16-, 32- or 64-bit lanes");
+  if constexpr (sizeof(T) <= 4) {
+    return (T)__builtin_amdgcn_update_dpp((int)(uint32_t)x, (int)(uint32_t)x, C, 0xF, 0xF, false);
   } else {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)x, (int)(uint32_t)x, C, 0xF, 0xF, false);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(x >> 32), (int)(uint32_t)(x >> 32), C,
@@ -145,12 +145,26 @@ __device__ __forceinline__ T dppmv(T x) {
     return (T)((uint64_t)lo | ((uint64_t)hi << 32));
   }
 }
+// LDS atomic min for the repair's distance types (16-bit: a CAS loop on the word)
+__device__ __forceinline__ void lds_atomic_min(uint16_t* p, uint16_t v) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(3));
+  const uint32_t sh = (reinterpret_cast<uintptr_t>(p) & 2u) * 8u;
+  uint32_t old = *w;
+  while (((old >> sh) & 0xFFFFu) > v) {
+    const uint32_t seen = atomicCAS(w, old, (old & ~(0xFFFFu << sh)) | ((uint32_t)v << sh));
+    if (seen == old) break;
+    old = seen;
+  }
+}
+__device__ __forceinline__ void lds_atomic_min(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+__device__ __forceinline__ void lds_atomic_min(unsigned long long* p, unsigned long long v) { atomicMin(p, v); }
+
 constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowMirror = 0x140, kDppHalfMirror = 0x141;
 
 template <typename T>
 __device__ __forceinline__ T readlane_t(T x, int l) {
-  if constexpr (sizeof(T) == 4) {
-    return (T)__builtin_amdgcn_readlane((int)x, l);
+  if constexpr (sizeof(T) <= 4) {
+    return (T)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
   } else {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -569,7 +583,7 @@ struct GrpLayout {
 };
 
 __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t nb, uint32_t dist_bytes, bool lg,
-                                                uint32_t waves) {
+                                                uint32_t waves, uint32_t chunk) {
   GrpLayout l;
   uint32_t off = 16;  // workgroup control: [0] next link group of the item
   auto take = [](uint32_t& o, uint32_t bytes) {
@@ -586,7 +600,7 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
   l.bnh = take(off, nb * V);
   l.btight = take(off, 8u * ((E + 63u) / 64u));
   l.btin = take(off, 2u * (V + 1u));  // u16 base-tight in-degree per node
-  l.ulist = take(off, 4u * kGrpMaxChunk);  // the item's affected links: offset in the chunk << 16 | b
+  l.ulist = take(off, 4u * chunk);  // the item's affected links: offset in the chunk << 16 | b
   uint32_t w = 16;  // wave control: [0] A count, [1] dirty count, [2] flag
   l.w_ina = take(w, 4u * vw);
   l.w_dq = take(w, 4u * vw);
@@ -650,6 +664,11 @@ struct GrpWave {
     const D a = adist[u], b = bdist[u];  // both loads issue with the bitmap read
     return bit_of(ina, u) ? a : b;
   }
+  __device__ D dist_a(uint32_t u, bool& in) const {
+    const D a = adist[u], b = bdist[u];
+    in = bit_of(ina, u);
+    return in ? a : b;
+  }
   __device__ void nh_or(uint32_t (&acc)[W], uint32_t u) const {
     nh_or_sel(acc, anh + (size_t)u * nb, bnh + (size_t)u * nb, bit_of(nhm, u), nb);
   }
@@ -708,8 +727,9 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   }
   const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
   if (c.prof) pt1 = (long long)__builtin_amdgcn_s_memtime();
-  // (2) new distances inside A: best entry from outside A, then relaxation within A; an
-  // 8-lane group per A node, a lane per in-edge (rows are short: one pass, then a min)
+  // (2) tentative distances inside A: the best entry from outside A (an 8-lane group per
+  // A node, a lane per in-edge, then a min). Relaxation within A happens in step (3),
+  // which settles A members in increasing distance together with the other dirty nodes.
   const uint32_t sub = lane & 7u;
   for (uint32_t i0 = 0; i0 < na; i0 += 8u) {
     const uint32_t i = i0 + (lane >> 3);
@@ -731,46 +751,27 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     if (i < na && sub == 0) c.adist[x] = best;
   }
   lds_fence();
-  for (;;) {
-    if (lane == 0) c.ctl[2] = 0;
-    lds_fence();
-    for (uint32_t i0 = 0; i0 < na; i0 += 8u) {
-      const uint32_t i = i0 + (lane >> 3);
-      if (i >= na) continue;
-      const uint32_t x = c.alist[i];
-      const D dx = c.adist[x];
-      if (dx == INF || !c.expands(x)) continue;
-      const uint2 r = c.gv.row(x);
-      for (uint32_t e = r.x + sub; e < r.y; e += 8u) {
-        const EdgeRec q = c.gv.rec(e);
-        if (q.down || q.lid == c.link || !bit_of(c.ina, q.col)) continue;
-        const D cand = dx + (D)c.w(q);
-        if (cand < c.adist[q.col]) {
-          atomicMin(&c.adist[q.col], cand);
-          c.ctl[2] = 1;
-        }
-      }
-    }
-    lds_fence();
-    if (!__builtin_amdgcn_readfirstlane(c.ctl[2])) break;
-  }
-  // (3) next hops in increasing new distance over the dirty set. Buckets of equal distance
-  // (a successor appended while processing distance m lies strictly beyond m); one node
-  // at a time across the wave, a lane per edge of its row. The dirty list's first 64
-  // entries live in lanes (entry i in lane i), later ones are re-read from LDS.
+  // (3) Dijkstra over the dirty set: buckets of equal (new) distance in increasing order. A
+  // bucket's A members are final (every node nearer was settled and relaxed its edges into
+  // A); settling a node pulls its next hops over tight in-edges, an A member relaxes its
+  // edges into A, and a non-A node whose set changed makes its tight successors dirty
+  // (both land strictly beyond the bucket). One node at a time across the wave, a lane
+  // per edge of its row. The dirty list's first 64 entries live in lanes (entry i in
+  // lane i), later ones are re-read from LDS.
   if (c.prof) pt2 = (long long)__builtin_amdgcn_s_memtime();
   const uint32_t nbw = (nb + 3u) / 4u;
   uint32_t nchanged = 0, buckets = 0;
   uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), loaded = 0;
   uint32_t ev = 0;
   D ed = INF;
-  bool pend = false;
+  bool pend = false, ea = false;  // ea: the lane's entry is in A (its distance may still drop)
   auto load_entries = [&]() {
+    if (pend && ea) ed = c.adist[ev];
     const uint32_t hi = min(nd, 64u);
     if (loaded < hi) {
       if (lane >= loaded && lane < hi) {
         ev = c.dlist[lane];
-        ed = c.dist(ev);
+        ed = c.dist_a(ev, ea);
         pend = true;
       }
       loaded = hi;
@@ -788,12 +789,18 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     const bool in_a = bit_of(c.ina, v);
     EdgeRec q{};
     D du = INF;
+    bool ua = false;
+    const bool relax = in_a && dv != INF && c.expands(v);
     for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
       const uint32_t e = e0 + lane;
       du = INF;
       if (e < r.y) {
         q = c.gv.rec(e);
-        du = c.dist(q.col);
+        du = c.dist_a(q.col, ua);
+        if (relax && ua && !q.down && q.lid != c.link) {  // v settled: relax v -> u inside A
+          const D cand = dv + (D)c.w(q);
+          if (cand < du) lds_atomic_min(&c.adist[q.col], cand);
+        }
         if (dv != INF && c.in_usable(q) && du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv) {
           if (q.col == c.src) {
             const uint32_t bit = c.gv.nbr_in(e);
@@ -921,7 +928,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   const uint32_t block = blockDim.x, waves = block >> 6;
   const uint32_t tw = (E + 63u) / 64u, vw = (V + 31u) / 32u;
-  const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves);
+  const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves, chunk);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* wctl = smem;
   D* bdist = reinterpret_cast<D*>(base + lay.bdist);
@@ -1117,13 +1124,13 @@ namespace {
 // LDS graph eligibility: ids / link ids / metrics fit the compact record, next-hop bits a byte
 bool grp_lds_graph_ok(const DevGraph& g, uint32_t w_max, uint32_t nh_bits) {
   return g.V <= 32767u && g.L <= 32767u && w_max <= 65535u && nh_bits <= 256u &&
-         bfs::env_u32("OPENR_SPF_WHATIF_LDSG", 1u, 0u, 1u);
+         bfs::env_u32("OPENR_SPF_WHATIF_LDSG", 0u, 0u, 1u);  // measured slower (fewer waves): opt-in
 }
 }  // namespace
 
 uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64) {
   if (V > 65535u || nb > 32u) return 0;
-  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u, false, 4).total;
+  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u, false, 4, kGrpMaxChunk).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -1134,34 +1141,38 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                                hipStream_t s) {
   hipError_t err = hipMemsetAsync(affected, 0, sizeof(uint32_t), s);
   if (err != hipSuccess || !n_links || !n_src) return err;
-  const uint32_t db = dist64 ? 8u : 4u;
-  // the LDS-graph variant with as many waves per workgroup (one workgroup per CU) as fit,
-  // else the global-graph variant at 4 waves per workgroup
+  // distances as u16 when every finite one fits (V * w_max < 0xFFFF): half the LDS rows,
+  // more workgroups per CU
+  const bool d16 = (uint64_t)g.V * (unit_cost ? 1u : w_max) < 0xFFFFull && !bfs::env_u32("OPENR_SPF_WHATIF_D32", 0u, 0u, 1u);
+  const uint32_t db = d16 ? 2u : dist64 ? 8u : 4u;
+  // the LDS-graph variant (opt-in) with as many waves per workgroup (one workgroup per
+  // CU) as fit, else the global-graph variant at OPENR_SPF_WHATIF_WAVES (3) per workgroup
   bool lg = false;
-  uint32_t waves = 4, lds = 0;
+  uint32_t waves = bfs::env_u32("OPENR_SPF_WHATIF_WAVES", 3u, 1u, kGrpMaxBlock / 64u);  // WAN: 3 -> 7.1, 4 -> 7.4, 5 -> 9.2 ms
+  auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch).total; };
   if (grp_lds_graph_ok(g, w_max, nh_bits)) {
     for (uint32_t w = kGrpMaxBlock / 64u; w >= 2u; --w) {
-      const uint32_t t = grp_layout(g.V, g.E, nb, db, true, w).total;
-      if (t <= kMaxLds) {
+      if (layout_bytes(true, w, kGrpMaxChunk) <= kMaxLds) {
         lg = true;
         waves = w;
-        lds = t;
         break;
       }
     }
   }
-  if (!lg) {
-    lds = whatif_group_lds_bytes(g.V, g.E, nb, dist64);
-    if (!lds) return hipErrorInvalidValue;
-  }
+  if (!lg && layout_bytes(false, waves, kGrpMaxChunk) > kMaxLds) waves = 4;
+  if (!lg && layout_bytes(false, waves, kGrpMaxChunk) > kMaxLds) return hipErrorInvalidValue;
   const uint32_t block = 64u * waves;
-  const uint32_t per_cu = std::max<uint32_t>(1u, std::min<uint32_t>(kMaxLds / lds, 2048u / block));
-  const uint64_t slots = (uint64_t)num_cus * per_cu;
+  auto slots_for = [&](uint32_t bytes) {
+    return (uint64_t)num_cus * std::max<uint32_t>(1u, std::min<uint32_t>(kMaxLds / bytes, 2048u / block));
+  };
   // work items of (source, chunk of links): ~8 per resident workgroup, so the tail is short
-  uint64_t cps = (8u * slots + n_src - 1u) / n_src;
+  const uint64_t slots0 = slots_for(layout_bytes(lg, waves, kGrpMaxChunk));
+  uint64_t cps = (8u * slots0 + n_src - 1u) / n_src;
   cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
   uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
   chunk = std::min(bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30), kGrpMaxChunk);
+  const uint32_t lds = layout_bytes(lg, waves, chunk);  // the list sized to the chunk
+  const uint64_t slots = slots_for(lds);
   const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
@@ -1182,7 +1193,10 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
                        base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr, prof);            \
   } while (0)
-  if (dist64) {
+  if (d16) {
+    if (lg) OPENR_GRP_LAUNCH(uint16_t, true);
+    else OPENR_GRP_LAUNCH(uint16_t, false);
+  } else if (dist64) {
     if (lg) OPENR_GRP_LAUNCH(unsigned long long, true);
     else OPENR_GRP_LAUNCH(unsigned long long, false);
   } else {

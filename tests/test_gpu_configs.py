@@ -94,15 +94,17 @@ def test_config3_grid100_all_sources(eng):
     pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
 
 
-@pytest.mark.parametrize("mode", ["group", "group-global", "incr", "solve"])
+@pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "incr", "solve"])
 def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
     """Per-link-failure sweep on the 1k-node WAN (U[1,64] asymmetric metrics): every one
     of the 3 000 links x 16 sources, changed-node counts vs oracle re-solves
-    runSpf(src, true, {link}); grouped repair (default), per-unit repair and re-solve modes."""
-    if mode == "group-global":
-        mode = "group"
-        monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "0")
-    monkeypatch.setenv("OPENR_SPF_WHATIF", mode)
+    runSpf(src, true, {link}); grouped repair (default: u16 distances, global graph; LDS
+    graph; u32 distances), per-unit repair and re-solve modes."""
+    if mode == "group-lds":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
+    if mode == "group-d32":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
+    monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     g = T.wan(1000, 3000, 64, seed=1)
     eng.set_graph(g)
     links = np.arange(g.num_links, dtype=np.uint32)

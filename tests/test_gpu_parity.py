@@ -382,16 +382,18 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "group-global", "incr", "solve"])
+@pytest.fixture(params=["group", "group-lds", "group-d32", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
-    (default; graph staged in LDS too, or read from global memory), per-unit incremental
-    repair, or full re-solves."""
+    (default: graph read from global memory, u16 distances when they fit; or the graph
+    staged in LDS too; or u32 / u64 distances), per-unit incremental repair, or full
+    re-solves."""
     mode = request.param
-    if mode == "group-global":
-        mode = "group"
-        monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "0")
-    monkeypatch.setenv("OPENR_SPF_WHATIF", mode)
+    if mode == "group-lds":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
+    if mode == "group-d32":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
+    monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     return request.param
 
 
