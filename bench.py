@@ -186,9 +186,12 @@ def whatif_main(args):
     torch.cuda.set_stream(stream)
     solved = [0]
 
+    kernel_ms = []
+
     def step():
         solved[0] = eng.whatif_device(links.data_ptr(), n_links, srcs.data_ptr(), V, changed.data_ptr(), use_metric,
                                       stream=stream.cuda_stream)
+        kernel_ms.append(eng.stats().last_kernel_ms)  # the repair kernel (HIP events in the engine)
 
     def barrier():
         if world > 1:
@@ -198,6 +201,7 @@ def whatif_main(args):
     for _ in range(args.warmup):
         step()
     barrier()
+    kernel_ms.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -210,18 +214,10 @@ def whatif_main(args):
     per_src = algorithmic_bytes(g, srcs_np) / V  # mean B(src)
     bytes_step = per_src * units
     bytes_solved = per_src * solved[0]
-    achieved = bytes_step / (elapsed / args.steps) / 1e9
-    traffic = None  # PMC HBM bytes per step of the dominant kernel (scripts: whatif profile in profiles/r01b)
-    tj_path = os.path.join(ROOT, "profiles", "r01b", "whatif_pmc_traffic.json")
-    if os.path.exists(tj_path):
-        try:
-            traffic = json.load(open(tj_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    physical = {"traffic_bytes": traffic,
-                "achieved_gbs": traffic / (elapsed / args.steps) / 1e9 if traffic else None}
-    if traffic:
-        physical["frac"] = physical["achieved_gbs"] / HBM_PEAK_GBS
+    kern_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else elapsed / args.steps
+    pmc = load_pmc("whatif")
+    traffic = pmc.get("hbm_bytes_per_launch") if (pmc and "whatif_group" in pmc.get("kernel", "")
+                                                  and world == 1) else None
     ucmp = None
     if rank == 0 and not args.no_ucmp:
         # config 4's "+ UCMP": the WAN's UCMP-weighted route DBs (RibPolicy
@@ -256,16 +252,13 @@ def whatif_main(args):
                            spf_solved_per_step=solved[0], use_link_metric=use_metric,
                            parallelism=f"link-sharded x{world}"),
             "solved_per_s": solved[0] * world * args.steps / elapsed,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "bytes_per_step": bytes_step,
-                         "note": "SURVEY.md 8d: B(src) credited per what-if unit (the formula is applied even "
-                                 "when the kernel exits early); units resolved by the tight-edge filter included. "
-                                 "Affected units are repaired incrementally from the base rows "
-                                 f"(openr_spf_whatif); affected units only: "
-                                 f"{bytes_solved / (elapsed / args.steps) / 1e9:.1f} GB/s. frac can exceed 1 because "
-                                 "the repair reads ~V*(8+nb) B per unit instead of solving; see physical",
-                         "physical": physical},
+            "roofline": dict(roofline_with_physical(
+                bytes_step, kern_s, traffic,
+                "dominant kernel whatif_group_kernel (grouped repair), HIP events around its launch; SURVEY.md 8d: "
+                "B(src) credited per what-if unit (link x source), units resolved by its fused tight-edge filter "
+                f"included (affected units only: {bytes_solved / kern_s / 1e9:.1f} GB/s credited). The repair reads "
+                "base rows staged once per (source, link chunk) in LDS instead of solving, so credited frac > 1; "
+                "its bound is LDS latency, not HBM (DESIGN.md 5.3)"), kernel_ms_mean=kern_s * 1e3),
         }
         if ucmp is not None:
             out["ucmp_routes"] = ucmp
@@ -275,6 +268,33 @@ def whatif_main(args):
     if world > 1:
         dist.destroy_process_group()
     eng.close()
+
+
+def load_pmc(name):
+    """profiles/r02/pmc_traffic_<name>.json (scripts/pmc_traffic.sh output), or None."""
+    path = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{name}.json")
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
+def roofline_with_physical(credited_bytes, seconds, traffic, note):
+    """HBM roofline of a launch / step: `credited_bytes` are SURVEY.md 8d's algorithmic bytes,
+    `traffic` the PMC-measured HBM bytes of the same launch (or None). Where the credited
+    fraction exceeds 1 (the kernel does not move the bytes the formula credits), the
+    reported achieved / frac are the physical ones, the credited ones kept."""
+    credited = credited_bytes / seconds / 1e9 if seconds > 0 else 0.0
+    phys = traffic / seconds / 1e9 if (traffic and seconds > 0) else None
+    r = {"bound": "hbm", "achieved": credited, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": credited / HBM_PEAK_GBS, "traffic": traffic, "credited_bytes": credited_bytes,
+         "credited_gbs": credited, "credited_frac": credited / HBM_PEAK_GBS,
+         "physical_gbs": phys, "physical_frac": phys / HBM_PEAK_GBS if phys is not None else None,
+         "seconds_per_launch": seconds, "note": note}
+    if credited / HBM_PEAK_GBS > 1.0 and phys is not None:
+        r["achieved"], r["frac"] = phys, phys / HBM_PEAK_GBS
+        r["note"] = note + "; credited frac > 1, so achieved / frac are the PMC-measured (physical) bytes"
+    return r
 
 
 def ksp2_cpu_baseline(g, seconds: float):
@@ -376,7 +396,11 @@ def ksp2_main(args):
                 "ksp2 bench result check failed"
     srcs_np = np.asarray(s_np, dtype=np.int64)
     per_pair = algorithmic_bytes(g, srcs_np) / max(nsrc, 1)  # B(src) per second SPF
-    achieved = per_pair * n_pairs * world / (elapsed / args.steps) / 1e9
+    step_s = elapsed / args.steps
+    pmc = load_pmc("ksp2")  # PMC_AGG summary: every engine kernel of a step, per pair
+    traffic = None
+    if pmc and pmc.get("hbm_bytes_per_step") and pmc.get("ksp_sources") and world == 1:
+        traffic = pmc["hbm_bytes_per_step"] / (pmc["ksp_sources"] * V) * n_pairs
     if rank == 0:
         out = {
             "metric": "KSP2 (getKthPaths k=1,2) all-pairs throughput, pairs/sec, fabric ~5k nodes",
@@ -386,10 +410,11 @@ def ksp2_main(args):
             "config": dict(cfg, workload="fabric5000-ksp2-all-pairs" if not args.ksp_sources else
                            f"fabric5000-ksp2-{n_src_total}-sources-x-all-dests", pairs_per_step=n_src_total * V,
                            tok_cap=tok_cap, sources_per_call=blk, parallelism=f"source-sharded x{world}"),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "note": "SURVEY.md 8d: B(src) per second SPF (one per pair); k=1 base SPFs and "
-                                 "traces not credited"},
+            "roofline": roofline_with_physical(
+                per_pair * n_pairs, step_s, traffic,
+                "per GPU, whole step (base SPFs, k=1 / k=2 traces, second SPFs): SURVEY.md 8d B(src) per second "
+                "SPF (one per pair), k=1 base SPFs and traces not credited; traffic = PMC HBM bytes of every engine "
+                "kernel per pair (profiles/r02/pmc_traffic_ksp2.json) x this step's pairs"),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ksp2_cpu_baseline(g, min(args.cpu_seconds, 10.0))

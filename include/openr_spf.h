@@ -117,7 +117,8 @@ typedef struct {
   uint64_t spf_runs;        /* logical SPFs solved (fb303 decision.spf_runs) */
   uint64_t batches;         /* solve calls */
   double last_batch_ms;     /* wall time of the last host-buffer solve (decision.spf_ms) */
-  double last_kernel_ms;    /* device time of the last solve's kernels */
+  double last_kernel_ms;    /* device time of the last solve's kernels (what-if sweep: its
+                               repair kernel alone, HIP events around that launch) */
 } openr_spf_stats_t;
 
 int openr_spf_abi_version(void);

@@ -478,13 +478,18 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     // default: grouped repair (base rows staged once per (source, link chunk), fused filter)
     if (whatif_group_lds_bytes(V, ctx->E, nb, dist64)) {
       OPENR_TRY(d.wcount.reserve(1));
+      OPENR_TRY(hipEventRecord(d.ev_begin, s));  // the repair kernel's own time -> stats.last_kernel_ms
       OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
                                     d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
                                     d_changed, d.wcount.p,
                                     d.work.p + kIncrCtr, d.num_cus, s));
+      OPENR_TRY(hipEventRecord(d.ev_end, s));
       uint32_t count = 0;
       OPENR_TRY(hipMemcpyAsync(&count, d.wcount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
       OPENR_TRY(hipStreamSynchronize(s));
+      float ms = 0.f;
+      OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
+      ctx->stats.last_kernel_ms = ms;
       *solved = count;
       return hipSuccess;
     }

@@ -33,15 +33,33 @@ def main():
     if "--topology" in bench_args:
         topo = bench_args[bench_args.index("--topology") + 1]
     res = {"topology": topo, "bench_args": " ".join(bench_args)}
+    if "--workload" in bench_args:
+        res["workload"] = bench_args[bench_args.index("--workload") + 1]
+    want = os.environ.get("PMC_KERNEL", "")  # pick this kernel instead of the dominant one
     kinds = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         for name, grid, v in per_dispatch(out_dir, ctr):
-            if "openr_spf" not in name:
+            if "openr_spf" not in name or want not in name:
                 continue
             k = kinds.setdefault(name, {"grid": grid, "FETCH_SIZE": [], "WRITE_SIZE": []})
             k[ctr].append(v)
     if not kinds:
         raise SystemExit("no openr_spf dispatches found")
+    # PMC_AGG=1: every engine kernel of a step (multi-kernel pipelines such as KSP2), per step
+    if os.environ.get("PMC_AGG") == "1":
+        steps = int(bench_args[bench_args.index("--steps") + 1]) + int(bench_args[bench_args.index("--warmup") + 1])
+        tot = 0.0
+        per = {}
+        for n, k in kinds.items():
+            b = 2.0 * sum(k["FETCH_SIZE"]) * 1024.0 + sum(k["WRITE_SIZE"]) * 1024.0
+            per[n] = b / steps
+            tot += b
+        res.update({"kernels": per, "steps_profiled": steps, "hbm_bytes_per_step": tot / steps,
+                    "correction": "FETCH_SIZE x2 (gfx950 counts 128-B requests at 64 B); WRITE_SIZE as counted"})
+        if "--ksp-sources" in bench_args:
+            res["ksp_sources"] = int(bench_args[bench_args.index("--ksp-sources") + 1])
+        print(json.dumps(res, indent=1))
+        return
     # dominant kernel = largest total fetch+write
     name = max(kinds, key=lambda n: sum(kinds[n]["FETCH_SIZE"]) + sum(kinds[n]["WRITE_SIZE"]))
     k = kinds[name]

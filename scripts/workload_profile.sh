@@ -20,6 +20,18 @@ for W in $WORKLOADS; do
     adjdb_fabric) ARGS="--workload adjdb --topology fabric --steps 5 --warmup 1" ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
+  # PMC HBM traffic first (what-if: its repair kernel; KSP2: every engine kernel of a step,
+  # on a 64-source sample), installed where bench.py reads it (profiles/r02/)
+  PMC=""
+  case $W in
+    whatif) PMC="PMC_KERNEL=whatif_group|--workload whatif --no-ucmp" ;;
+    ksp2)   PMC="PMC_AGG=1|--workload ksp2 --ksp-sources 64" ;;
+  esac
+  if [ -n "$PMC" ] && [ -z "${NO_PMC:-}" ]; then
+    env ${PMC%%|*} PMC_TAG="$TAG/$W/pmc" BENCH_ARGS="${PMC#*|}" bash "$R/scripts/pmc_traffic.sh"; stop $?
+    mkdir -p "$R/profiles/r02" && cp "$R/gpurun_out/pmc_$TAG/$W/pmc/pmc_traffic.json" "$R/profiles/r02/pmc_traffic_$W.json"
+    cp "$R/gpurun_out/pmc_$TAG/$W/pmc/pmc_traffic.json" "$OUT/pmc_traffic.json"
+  fi
   cd "$R" && timeout -k 10 400 python3 -u bench.py $ARGS > "$OUT/bench.log" 2>&1; stop $?
   grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json"
   cd /tmp
