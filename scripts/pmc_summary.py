@@ -35,6 +35,8 @@ def main():
     res = {"topology": topo, "bench_args": " ".join(bench_args)}
     if "--workload" in bench_args:
         res["workload"] = bench_args[bench_args.index("--workload") + 1]
+        # workloads with a fixed topology (bench.py: whatif = WAN, ksp2 = fabric)
+        res["topology"] = {"whatif": "wan", "ksp2": "fabric"}.get(res["workload"], topo)
     want = os.environ.get("PMC_KERNEL", "")  # pick this kernel instead of the dominant one
     kinds = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -74,7 +76,8 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 counts 128-B requests at 64 B); WRITE_SIZE as counted",
     })
     # n_sources of the launch: all V of the topology (bench default weak scaling, 1 rank)
-    res["n_sources"] = {"grid100": 10000, "fabric": 4992, "wan": 1000}.get(topo)
+    if "workload" not in res:
+        res["n_sources"] = {"grid100": 10000, "fabric": 4992, "wan": 1000}.get(topo)
     print(json.dumps(res, indent=1))
 
 
