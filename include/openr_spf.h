@@ -221,8 +221,10 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
      metric of directed edge e         Link::setMetricFromNode   (LinkState.cpp:195-204 getter)
      usability of link l (both edges)  Link::isUp: holds / adjacency overload (:233-236)
      overload of node x                LinkState::updateNodeOverloaded / isNodeOverloaded
-   The patch is also recorded as a delta for openr_spf_refresh (each call replaces the
-   previous delta). No solve may be in flight on the context's devices. */
+   The patch is also recorded as a delta for openr_spf_refresh: the first patch after a
+   refresh (or set_graph) starts a new delta, later patches with no refresh in between
+   merge into it (each edge keeps its state from before the first of them). No solve may
+   be in flight on the context's devices. */
 typedef struct {
   uint32_t n_edges;
   const uint32_t* edge_ids;         /* [n_edges] directed edge ids */
@@ -237,10 +239,11 @@ typedef struct {
 
 int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* patch);
 
-/* Incremental re-SPF after the most recent openr_spf_patch_graph: rows [n] (dist, and nh
-   / tight when non-NULL, laid out as openr_spf_solve writes them) hold the results of
-   sources[0..n) on the graph BEFORE that patch; on return they hold the results on the
-   patched graph, bit-exact with a fresh solve. Only rows the patch can change are
+/* Incremental re-SPF after openr_spf_patch_graph: rows [n] (dist, and nh / tight when
+   non-NULL, laid out as openr_spf_solve writes them) hold the results of sources[0..n)
+   on the graph before the delta (before the first patch since the last refresh); on
+   return they hold the results on the patched graph, bit-exact with a fresh solve. Every
+   refresh call of the same delta (e.g. one per batch of rows) sees the same delta. Only rows the patch can change are
    re-solved: row s is affected iff some changed directed edge u->v was tight for s
    before, or is usable with d_s(u) + w_new <= d_s(v) after (u expanding for s);
    *out_resolved (nullable) = rows re-solved (added to stats.spf_runs). Fails with

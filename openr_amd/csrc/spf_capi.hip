@@ -15,6 +15,7 @@
 #include <new>
 #include <string>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/openr_spf.h"
@@ -141,6 +142,10 @@ struct openr_spf_ctx {
   // the rows before or after the last patch came from a graph with zero / wrapped
   // metrics: the delta filter's tight-edge reasoning does not hold, refresh every row
   bool delta_all = false;
+  // no refresh since the last patch: the next patch merges into delta (rows may still be
+  // those of the graph before the earlier patch), keeping each edge's oldest state
+  bool refreshed = true;
+  std::unordered_map<uint32_t, uint32_t> delta_index;  // directed edge -> delta slot
 };
 
 namespace {
@@ -1063,21 +1068,48 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
   }
   if (w_min == UINT32_MAX) w_min = w_max = 1;
 
-  // 5) the delta edges of this patch (openr_spf_refresh)
-  ctx->delta.clear();
+  // 5) the delta edges of this patch (openr_spf_refresh). Patches with no refresh in
+  //    between accumulate: an edge keeps its state from before the first of them, so rows
+  //    of that older graph are still filtered correctly; edges back at that state drop out.
+  const bool merge = ctx->delta_valid && !ctx->refreshed;
+  if (!merge) {
+    ctx->delta.clear();
+    ctx->delta_index.clear();
+  }
   for (size_t k = 0; k < cand.size(); ++k) {
     uint32_t w1 = 0;
     const uint32_t f1 = state(cand[k], &w1);
     if (f1 == f0[k] && w1 == w0[k]) continue;
     const uint32_t e = cand[k];
+    const uint32_t new_flags = ((f1 & 1u) ? kDeltaUp1 : 0u) | ((f1 & 2u) ? kDeltaOvl1 : 0u);
+    auto it = ctx->delta_index.find(e);
+    if (it != ctx->delta_index.end()) {  // changed by an earlier, unrefreshed patch too
+      DeltaEdge& de = ctx->delta[it->second];
+      de.w1 = w1;
+      de.flags = (de.flags & (kDeltaUp0 | kDeltaOvl0)) | new_flags;
+      continue;
+    }
     DeltaEdge de{};
     de.u = ctx->owner[e];
     de.v = ctx->col[e];
     de.w0 = w0[k];
     de.w1 = w1;
-    de.flags = ((f0[k] & 1u) ? kDeltaUp0 : 0u) | ((f1 & 1u) ? kDeltaUp1 : 0u) | ((f0[k] & 2u) ? kDeltaOvl0 : 0u) |
-               ((f1 & 2u) ? kDeltaOvl1 : 0u);
+    de.flags = ((f0[k] & 1u) ? kDeltaUp0 : 0u) | ((f0[k] & 2u) ? kDeltaOvl0 : 0u) | new_flags;
+    de.pad0 = e;
+    ctx->delta_index.emplace(e, (uint32_t)ctx->delta.size());
     ctx->delta.push_back(de);
+  }
+  if (merge) {  // drop edges whose accumulated change cancelled out
+    size_t o = 0;
+    for (size_t k = 0; k < ctx->delta.size(); ++k) {
+      const DeltaEdge& de = ctx->delta[k];
+      const bool same = de.w0 == de.w1 && ((de.flags & kDeltaUp0) != 0) == ((de.flags & kDeltaUp1) != 0) &&
+                        ((de.flags & kDeltaOvl0) != 0) == ((de.flags & kDeltaOvl1) != 0);
+      if (!same) ctx->delta[o++] = de;
+    }
+    ctx->delta.resize(o);
+    ctx->delta_index.clear();
+    for (size_t k = 0; k < o; ++k) ctx->delta_index.emplace(ctx->delta[k].pad0, (uint32_t)k);
   }
 
   // 6) upload: one record list + one scatter kernel per replica
@@ -1091,9 +1123,10 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
   }
   ctx->w_min = w_min;
   ctx->w_max = w_max;
-  ctx->delta_all = !ctx->metric_ok || !metric_ok;
+  ctx->delta_all = (merge && ctx->delta_all) || !ctx->metric_ok || !metric_ok;
   ctx->metric_ok = metric_ok;
   ctx->delta_valid = true;
+  ctx->refreshed = false;
   return OPENR_SPF_OK;
 }
 
@@ -1151,6 +1184,7 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
     ctx->stats.batches += 1;
   }
   if (out_resolved) *out_resolved = count;
+  ctx->refreshed = true;  // the next patch starts a new delta
   return OPENR_SPF_OK;
 }
 

@@ -622,4 +622,43 @@ TEST_GPU(LinkState_ZeroAndNegativeMetricOracleParity) {
   });
 }
 
+// A hub with 300 distinct neighbours (next-hop sets wider than 256 bits): served by the
+// exact-order kernel; getSpfResult from the hub and from a leaf equals the oracle.
+TEST_GPU(LinkState_WideHubOracleParity) {
+  LinkState ls(kArea);
+  const int leaves = 300;
+  std::vector<thrift::Adjacency> hub;
+  for (int i = 1; i <= leaves; ++i) {
+    const std::string leaf = std::to_string(i), other = std::to_string(i % leaves + 1);
+    hub.push_back(createAdjacency(leaf, "h" + leaf, "u" + leaf, 1 + i % 3));
+    std::vector<thrift::Adjacency> adjs{createAdjacency("0", "u" + leaf, "h" + leaf, 2),
+                                        createAdjacency(other, "r" + leaf, "l" + other, 5)};
+    const std::string prev = std::to_string((i + leaves - 2) % leaves + 1);
+    adjs.push_back(createAdjacency(prev, "l" + leaf, "r" + prev, 5));
+    ls.updateAdjacencyDatabase(createAdjDb(leaf, adjs, i + 1));
+  }
+  ls.updateAdjacencyDatabase(createAdjDb("0", hub, 1));
+  auto const& m = ls.csrMirror();
+  oracle_graph og{(uint32_t)m.names.size(), (uint32_t)m.col.size(), (uint32_t)m.links.size(), m.rowPtr.data(),
+                  m.col.data(), m.metric.data(), m.linkId.data(), m.edgeUp.data(), m.overloaded.data(),
+                  m.nameRank.data()};
+  const uint32_t NV = og.num_nodes, NE = og.num_dir_edges;
+  std::vector<uint64_t> dist(NV);
+  std::vector<uint32_t> plp(NV + 1), ple(NE + 1);
+  for (const char* src : {"0", "1", "150"}) {
+    const uint32_t s = m.id.at(src);
+    auto const& res = ls.getSpfResult(src, true);
+    const int64_t cnt = oracle_run_spf(&og, s, 1, nullptr, dist.data(), nullptr, 0, nullptr, plp.data(), ple.data());
+    EXPECT_EQ((size_t)cnt, res.size());
+    bool same = true;
+    for (uint32_t v = 0; v < NV; ++v) {
+      auto it = res.find(m.names[v]);
+      same &= it != res.end() && it->second.metric() == dist[v] && it->second.pathLinks().size() == plp[v + 1] - plp[v];
+    }
+    EXPECT_TRUE(same);
+  }
+  auto const& r0 = ls.getSpfResult("0", true);
+  EXPECT_EQ(1u, r0.at("3").nextHops().size());  // direct neighbour 3 of the 300-wide hub
+}
+
 int main(int argc, char** argv) { return run_tests(argc, argv); }

@@ -204,3 +204,25 @@ def test_patch_errors(eng):
     eng.patch(edges=[0], metrics=[1])
     assert eng.refresh([0, 1], d, n) >= 0
     check_rows(eng, eng.g, [0, 1], d, n, None)
+
+
+def test_two_patches_one_refresh(eng, family):
+    """Patches with no refresh in between accumulate their delta: one refresh of the rows
+    of the original graph brings them to the twice-patched graph (edges changed and changed
+    back drop out; edges changed twice keep their original state)."""
+    g = random_graph(77, 120, 320, 9)
+    eng.set_graph(g)
+    srcs = list(range(g.num_nodes))
+    dist, nh, tight = eng.solve(srcs, True, want_tight=True)
+    rng = np.random.default_rng(77)
+    e = rng.choice(g.num_dir_edges, 6, replace=False)
+    eng.patch(edges=e, metrics=rng.integers(1, 10, 6).astype(np.uint64))
+    eng.patch(edges=e[:3], metrics=g.metric[e[:3]])  # three of them back to the original
+    lk = rng.choice(g.num_links, 2, replace=False)
+    eng.patch(links=lk, link_up=np.zeros(2, np.uint8))
+    eng.refresh(srcs, dist, nh, tight)
+    check_rows(eng, eng.g, srcs, dist, nh, tight, oracle_rows=range(0, len(srcs), 7))
+    # after a refresh the next patch starts a new delta
+    eng.patch(links=lk, link_up=np.ones(2, np.uint8))
+    eng.refresh(srcs, dist, nh, tight)
+    check_rows(eng, eng.g, srcs, dist, nh, tight, oracle_rows=range(0, len(srcs), 7))
