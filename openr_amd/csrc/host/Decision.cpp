@@ -4,6 +4,7 @@
 #include "Decision.h"
 
 #include <algorithm>
+#include <limits>
 #include <list>
 #include <stdexcept>
 #include <tuple>
@@ -266,7 +267,7 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
     hasBGP |= isBGP;
     hasNonBGP |= !isBGP;
     if (na.first == myNodeName) hasSelfPrependLabel &= e.prependLabel.has_value();
-    if (isBGP && !e.hasMv) missingMv = true;
+    if (isBGP && !e.mv.has_value()) missingMv = true;
   }
   if (hasBGP) {
     if (hasNonBGP && !enableBestRouteSelection_) {
@@ -308,14 +309,47 @@ BestRouteSelectionResult SpfSolver::selectBestRoutes(std::string const& myNodeNa
     ret.bestNodeArea = selectBestNodeArea(ret.allNodeAreas, myNodeName);
     ret.success = true;
   } else if (isBgp) {
-    // runBestPathSelectionBgp (metric vectors) is not mirrored: the route is skipped
-    counters_.skipped_unicast_route++;
-    return ret;
+    return runBestPathSelectionBgp(prefix, prefixEntries, als);
   } else {
     for (auto const& [na, _] : prefixEntries) ret.allNodeAreas.emplace(na);
     ret.bestNodeArea = *ret.allNodeAreas.begin();
     ret.success = true;
   }
+  return maybeFilterDrainedNodes(std::move(ret), als);
+}
+
+// Decision.cpp:806-848: the advertisers whose metric vector is best (ties broken by the
+// tie-breaker entities are multipath); an undecidable order skips the route
+BestRouteSelectionResult SpfSolver::runBestPathSelectionBgp(thrift::IpPrefix const& prefix,
+                                                            PrefixEntries const& prefixEntries,
+                                                            std::unordered_map<std::string, LinkState> const& als) {
+  using MetricVectorUtils::CompareResult;
+  (void)prefix;
+  BestRouteSelectionResult ret;
+  std::optional<thrift::MetricVector> bestVector;
+  for (auto const& [na, e] : prefixEntries) {
+    const CompareResult r =
+        bestVector ? MetricVectorUtils::compareMetricVectors(e.mv.value(), *bestVector) : CompareResult::WINNER;
+    switch (r) {
+      case CompareResult::WINNER:
+        ret.allNodeAreas.clear();
+        [[fallthrough]];
+      case CompareResult::TIE_WINNER:
+        bestVector = e.mv.value();
+        ret.bestNodeArea = na;
+        [[fallthrough]];
+      case CompareResult::TIE_LOOSER:
+        ret.allNodeAreas.emplace(na);
+        break;
+      case CompareResult::TIE:    // "Tie ordering prefix entries. Skipping route"
+      case CompareResult::ERROR:  // "Error ordering prefix entries. Skipping route"
+        counters_.skipped_unicast_route++;
+        return ret;
+      default:
+        break;
+    }
+  }
+  ret.success = true;
   return maybeFilterDrainedNodes(std::move(ret), als);
 }
 
@@ -637,4 +671,99 @@ std::vector<thrift::IpPrefix> RibPolicy::applyPolicy(std::map<thrift::IpPrefix, 
   return updated;
 }
 
+}  // namespace openr
+
+// ---------------------------------------------------------------------------
+// MetricVectorUtils (Util.cpp:1100-1246): entities compared in decreasing priority; a
+// loner (type present on one side only) decides by its CompareType; tie-breaker
+// entities give TIE_WINNER / TIE_LOOSER (multipath kept); the first decisive result wins.
+// ---------------------------------------------------------------------------
+namespace openr {
+namespace MetricVectorUtils {
+
+CompareResult operator!(CompareResult r) {
+  switch (r) {
+    case CompareResult::WINNER: return CompareResult::LOOSER;
+    case CompareResult::TIE_WINNER: return CompareResult::TIE_LOOSER;
+    case CompareResult::TIE: return CompareResult::TIE;
+    case CompareResult::TIE_LOOSER: return CompareResult::TIE_WINNER;
+    case CompareResult::LOOSER: return CompareResult::WINNER;
+    case CompareResult::ERROR: return CompareResult::ERROR;
+  }
+  return CompareResult::ERROR;
+}
+
+bool isDecisive(CompareResult r) {
+  return r == CompareResult::WINNER || r == CompareResult::LOOSER || r == CompareResult::ERROR;
+}
+
+bool isSorted(thrift::MetricVector const& mv) {
+  int64_t prior = std::numeric_limits<int64_t>::max();
+  for (auto const& e : mv.metrics) {
+    if (e.priority > prior) return false;
+    prior = e.priority;
+  }
+  return true;
+}
+
+CompareResult compareMetrics(std::vector<int64_t> const& l, std::vector<int64_t> const& r, bool tieBreaker) {
+  if (l.size() != r.size()) return CompareResult::ERROR;
+  for (size_t i = 0; i < l.size(); ++i) {
+    if (l[i] > r[i]) return tieBreaker ? CompareResult::TIE_WINNER : CompareResult::WINNER;
+    if (l[i] < r[i]) return tieBreaker ? CompareResult::TIE_LOOSER : CompareResult::LOOSER;
+  }
+  return CompareResult::TIE;
+}
+
+CompareResult resultForLoner(thrift::MetricEntity const& e) {
+  if (e.op == thrift::CompareType::WIN_IF_PRESENT)
+    return e.isBestPathTieBreaker ? CompareResult::TIE_WINNER : CompareResult::WINNER;
+  if (e.op == thrift::CompareType::WIN_IF_NOT_PRESENT)
+    return e.isBestPathTieBreaker ? CompareResult::TIE_LOOSER : CompareResult::LOOSER;
+  return CompareResult::TIE;  // IGNORE_IF_NOT_PRESENT
+}
+
+void maybeUpdate(CompareResult& target, CompareResult update) {
+  if (isDecisive(update) || target == CompareResult::TIE) target = update;
+}
+
+// Util.cpp:1143-1157: the reference sorts its (const) arguments in place by decreasing
+// priority (std::sort through a const_cast); the caller observes the sorted order, which
+// its own tests rely on (UtilTest.cpp:952-956 index the vectors after a comparison)
+void sortMetricVector(thrift::MetricVector const& mv) {
+  if (isSorted(mv)) return;
+  auto& m = const_cast<std::vector<thrift::MetricEntity>&>(mv.metrics);
+  std::sort(m.begin(), m.end(),
+            [](thrift::MetricEntity const& a, thrift::MetricEntity const& b) { return a.priority > b.priority; });
+}
+
+CompareResult compareMetricVectors(thrift::MetricVector const& lv, thrift::MetricVector const& rv) {
+  CompareResult result = CompareResult::TIE;
+  if (lv.version != rv.version) return CompareResult::ERROR;
+  sortMetricVector(lv);
+  sortMetricVector(rv);
+  auto const &l = lv.metrics, &r = rv.metrics;
+  auto li = l.begin(), ri = r.begin();
+  while (!isDecisive(result) && li != l.end() && ri != r.end()) {
+    if (li->type == ri->type) {
+      if (li->isBestPathTieBreaker != ri->isBestPathTieBreaker) maybeUpdate(result, CompareResult::ERROR);
+      else maybeUpdate(result, compareMetrics(li->metric, ri->metric, li->isBestPathTieBreaker));
+      ++li;
+      ++ri;
+    } else if (li->priority > ri->priority) {
+      maybeUpdate(result, resultForLoner(*li));
+      ++li;
+    } else if (li->priority < ri->priority) {
+      maybeUpdate(result, !resultForLoner(*ri));
+      ++ri;
+    } else {  // same priority, different types
+      maybeUpdate(result, CompareResult::ERROR);
+    }
+  }
+  while (!isDecisive(result) && li != l.end()) maybeUpdate(result, resultForLoner(*li++));
+  while (!isDecisive(result) && ri != r.end()) maybeUpdate(result, !resultForLoner(*ri++));
+  return result;
+}
+
+}  // namespace MetricVectorUtils
 }  // namespace openr

@@ -53,6 +53,20 @@ struct IpPrefix {
   std::string toString() const { return addr + "/" + std::to_string(prefixLength); }
 };
 
+// Lsdb.thrift:165-213 (deprecated BGP metric vectors, still honoured by the route build)
+enum class CompareType : int32_t { WIN_IF_PRESENT = 1, WIN_IF_NOT_PRESENT = 2, IGNORE_IF_NOT_PRESENT = 3 };
+struct MetricEntity {
+  int64_t type = 0;
+  int64_t priority = 0;
+  CompareType op = CompareType::WIN_IF_PRESENT;
+  bool isBestPathTieBreaker = false;
+  std::vector<int64_t> metric;
+};
+struct MetricVector {
+  int64_t version = 0;
+  std::vector<MetricEntity> metrics;  // expected sorted by decreasing priority
+};
+
 struct PrefixMetrics {  // Lsdb.thrift:228 (defaults 1, 0, 0, 0)
   int32_t version = 1;
   int32_t path_preference = 0;
@@ -65,7 +79,8 @@ struct PrefixEntry {  // Lsdb.thrift:269
   PrefixType type = PrefixType::LOOPBACK;
   PrefixForwardingType forwardingType = PrefixForwardingType::IP;
   PrefixForwardingAlgorithm forwardingAlgorithm = PrefixForwardingAlgorithm::SP_ECMP;
-  bool hasMv = false;  // deprecated BGP metric vector present
+  std::string data;                // opaque payload (BGP routes carry it to the RIB)
+  std::optional<MetricVector> mv;  // deprecated BGP metric vector
   std::optional<int64_t> minNexthop;
   std::optional<int32_t> prependLabel;
   PrefixMetrics metrics;
@@ -100,6 +115,19 @@ struct NextHopThrift {  // Network.thrift NextHopThrift
 }  // namespace thrift
 
 // Set semantics of the reference's unordered_set<NextHopThrift>, ordered for tests.
+// Util.h:505-540 MetricVectorUtils (metric vector comparison for BGP best paths)
+namespace MetricVectorUtils {
+enum class CompareResult { WINNER, TIE_WINNER, TIE, TIE_LOOSER, LOOSER, ERROR };
+CompareResult operator!(CompareResult r);
+bool isDecisive(CompareResult r);
+bool isSorted(thrift::MetricVector const& mv);
+void sortMetricVector(thrift::MetricVector const& mv);  // in place, as the reference
+CompareResult compareMetrics(std::vector<int64_t> const& l, std::vector<int64_t> const& r, bool tieBreaker);
+CompareResult resultForLoner(thrift::MetricEntity const& e);
+void maybeUpdate(CompareResult& target, CompareResult update);
+CompareResult compareMetricVectors(thrift::MetricVector const& l, thrift::MetricVector const& r);
+}  // namespace MetricVectorUtils
+
 using NextHopSet = std::set<thrift::NextHopThrift>;
 using PrefixEntries = std::unordered_map<NodeAndArea, thrift::PrefixEntry>;
 
@@ -195,6 +223,8 @@ class SpfSolver {
   BestRouteSelectionResult selectBestRoutes(std::string const& myNodeName, thrift::IpPrefix const& prefix,
                                             PrefixEntries const& prefixEntries, bool isBgp,
                                             std::unordered_map<std::string, LinkState> const& areaLinkStates);
+  BestRouteSelectionResult runBestPathSelectionBgp(thrift::IpPrefix const& prefix, PrefixEntries const& prefixEntries,
+                                                   std::unordered_map<std::string, LinkState> const& areaLinkStates);
   BestRouteSelectionResult maybeFilterDrainedNodes(
       BestRouteSelectionResult&& result, std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
   std::optional<int64_t> getMinNextHopThreshold(BestRouteSelectionResult const& nodes,

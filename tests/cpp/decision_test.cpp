@@ -1033,6 +1033,122 @@ thrift::BinaryAddress binAddr(const std::string& a) {
 }
 }  // namespace
 
+// UtilTest.cpp:911-972 MetricVectorUtilsTest.compareMetricVectors
+TEST_CPU(MetricVectorUtils_compareMetricVectors) {
+  using MetricVectorUtils::CompareResult;
+  using MetricVectorUtils::compareMetricVectors;
+  thrift::MetricVector l, r;
+  EXPECT_TRUE(CompareResult::TIE == compareMetricVectors(l, r));
+  l.version = 1;
+  r.version = 2;
+  EXPECT_TRUE(CompareResult::ERROR == compareMetricVectors(l, r));
+  r.version = 1;
+  const int64_t n = 5;
+  l.metrics.resize(n);
+  r.metrics.resize(n);
+  for (int64_t i = 0; i < n; ++i)
+    for (auto* v : {&l, &r}) v->metrics[i] = {i, i, thrift::CompareType::WIN_IF_PRESENT, false, {i}};
+  EXPECT_TRUE(CompareResult::TIE == compareMetricVectors(l, r));
+  r.metrics[n - 2].metric.front()--;
+  EXPECT_TRUE(CompareResult::WINNER == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::LOOSER == compareMetricVectors(r, l));
+  r.metrics[n - 2].isBestPathTieBreaker = true;
+  EXPECT_TRUE(CompareResult::ERROR == compareMetricVectors(l, r));
+  l.metrics[n - 2].isBestPathTieBreaker = true;
+  EXPECT_TRUE(CompareResult::TIE_WINNER == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::TIE_LOOSER == compareMetricVectors(r, l));
+  r.metrics.resize(n - 1);
+  EXPECT_TRUE(CompareResult::WINNER == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::LOOSER == compareMetricVectors(r, l));
+  l.metrics[0].type--;  // same priority, different type
+  EXPECT_TRUE(CompareResult::ERROR == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::ERROR == compareMetricVectors(r, l));
+  l.metrics[0].type++;
+  l.metrics[n - 1].op = thrift::CompareType::WIN_IF_NOT_PRESENT;
+  EXPECT_TRUE(CompareResult::LOOSER == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::WINNER == compareMetricVectors(r, l));
+  l.metrics[n - 1].op = thrift::CompareType::IGNORE_IF_NOT_PRESENT;
+  EXPECT_TRUE(CompareResult::TIE_WINNER == compareMetricVectors(l, r));
+  EXPECT_TRUE(CompareResult::TIE_LOOSER == compareMetricVectors(r, l));
+}
+
+// DecisionTest.cpp:715-897 BGPRedistribution.BasicOperation: BGP routes by metric vector
+TEST_GPU(BGPRedistribution_BasicOperation) {
+  SpfSolver solver("1", false, false);
+  std::unordered_map<std::string, LinkState> als;
+  als.emplace(kDefaultArea, LinkState(kDefaultArea));
+  auto& ls = als.at(kDefaultArea);
+  EXPECT_FALSE(ls.updateAdjacencyDatabase(createAdjDb("1", {adj12, adj13}, 0)).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("2", {adj21}, 0)).topologyChanged);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("3", {adj31}, 0)).topologyChanged);
+  PrefixState ps;
+  ps.updatePrefix("1", kDefaultArea, createPrefixEntry(addr1));
+  ps.updatePrefix("2", kDefaultArea, createPrefixEntry(addr2));
+  thrift::MetricVector mv1, mv2;
+  for (int64_t i = 0; i < 5; ++i) {
+    mv1.metrics.push_back({i, i, thrift::CompareType::WIN_IF_PRESENT, false, {i}});
+    mv2.metrics.push_back({i, i, thrift::CompareType::WIN_IF_PRESENT, false, {i}});
+  }
+  auto bgp = [](const thrift::MetricVector& mv, const std::string& data) {
+    auto e = createPrefixEntry(addr3);
+    e.type = thrift::PrefixType::BGP;
+    e.data = data;
+    e.mv = mv;
+    return e;
+  };
+  auto routeTo = [&](const std::string& node) -> std::optional<RibUnicastEntry> {
+    auto db = solver.buildRouteDb(node, als, ps);
+    auto it = db->unicastRoutes.find(addr3);
+    if (it == db->unicastRoutes.end()) return std::nullopt;
+    return it->second;
+  };
+  auto routes = [&](const std::string& node) { return solver.buildRouteDb(node, als, ps)->unicastRoutes.size(); };
+  // only node 1 advertises the BGP prefix: it is the best path
+  ps.updatePrefix("1", kDefaultArea, bgp(mv1, "data1"));
+  EXPECT_EQ(2u, routes("2"));
+  auto r = routeTo("2");
+  EXPECT_TRUE(r.has_value());
+  if (r) {
+    EXPECT_EQ(r->nexthops, NextHopSet({nhFromAdj(adj21, false, adj21.metric)}));
+    EXPECT_TRUE(r->bestPrefixEntry.type == thrift::PrefixType::BGP && r->bestPrefixEntry.data == "data1");
+    EXPECT_FALSE(r->doNotInstall);
+  }
+  // node 2 with the same metric vector: no best path, the route goes
+  ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));
+  EXPECT_EQ(1u, routes("1"));
+  // node 2's last metric lower: node 1 again
+  mv2.metrics[4].metric.front()--;
+  ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));
+  EXPECT_EQ(2u, routes("2"));
+  r = routeTo("2");
+  EXPECT_TRUE(r && r->bestPrefixEntry.data == "data1" && r->nexthops == NextHopSet({nhFromAdj(adj21, false, 10)}));
+  // node 2 better
+  mv2.metrics[4].metric.front() += 2;
+  ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));
+  EXPECT_EQ(2u, routes("1"));
+  r = routeTo("1");
+  EXPECT_TRUE(r && r->bestPrefixEntry.data == "data2" && r->nexthops == NextHopSet({nhFromAdj(adj12, false, 10)}));
+  // the last entity a tie breaker: multipath over both advertisers
+  mv1.metrics[4].isBestPathTieBreaker = true;
+  mv2.metrics[4].isBestPathTieBreaker = true;
+  ps.updatePrefix("1", kDefaultArea, bgp(mv1, "data1"));
+  ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));
+  EXPECT_EQ(1u, routes("1"));  // 1 and 2 advertise it themselves: no route
+  EXPECT_EQ(3u, routes("3"));
+  r = routeTo("3");
+  EXPECT_TRUE(r && r->bestPrefixEntry.data == "data2" && r->nexthops == NextHopSet({nhFromAdj(adj31, false, 10)}));
+  // disconnected: each node considers its own BGP route best and programs nothing
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("1", {}, 0)).topologyChanged);
+  EXPECT_FALSE(routeTo("1").has_value());
+  EXPECT_FALSE(routeTo("2").has_value());
+  // a BGP advertiser without a metric vector: the route is skipped
+  auto noMv = bgp(mv1, "data1");
+  noMv.mv.reset();
+  ps.updatePrefix("1", kDefaultArea, noMv);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("1", {adj12, adj13}, 0)).topologyChanged);
+  EXPECT_FALSE(routeTo("3").has_value());
+}
+
 TEST_CPU(RibPolicyTest_ApplyAction) {  // :180-236 only the first matching statement applies
   const auto stmt1 = policyStatement({pfx("fc01::/64")}, 1, {{"area1", 99}});
   const auto stmt2 = policyStatement({pfx("fc00::/64"), pfx("fc02::/64")}, 1, {{"area2", 99}});
