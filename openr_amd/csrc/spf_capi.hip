@@ -473,6 +473,37 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   a.ovf_list = d.ovf.p;
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
+  // re-solve the `count` units listed in wsrc / wlink / wunit (ignore set = the unit's
+  // link) and compare each row with its source's base row
+  auto resolve_units = [&](uint32_t count) -> hipError_t {
+    hipError_t e2;
+    const size_t row = (size_t)V * (8u + nb);
+    const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
+    if ((e2 = d.wdist.reserve((size_t)chunk * V)) != hipSuccess) return e2;
+    if ((e2 = d.wnh.reserve((size_t)chunk * V * nb)) != hipSuccess) return e2;
+    if ((e2 = d.wiota.reserve((size_t)chunk + 1u)) != hipSuccess) return e2;
+    if ((e2 = d.ovf.reserve((size_t)chunk * ctx->nsl_max())) != hipSuccess) return e2;
+    if ((e2 = launch_iota(d.wiota.p, chunk + 1u, d.num_cus, s)) != hipSuccess) return e2;
+    for (uint32_t off = 0; off < count; off += chunk) {
+      const uint32_t m = std::min(chunk, count - off);
+      SolveArgs b{};
+      b.sources = d.wsrc.p + off;
+      b.n = m;
+      b.ign_ptr = d.wiota.p;  // solve k ignores exactly wlink[off + k]
+      b.ign_links = d.wlink.p + off;
+      b.dist = d.wdist.p;
+      b.nh = d.wnh.p;
+      b.nh_bytes = nb;
+      b.nh_bits = ctx->nh_bits;
+      b.ovf_list = d.ovf.p;
+      b.work = d.work.p;
+      if ((e2 = launch(ctx, d, ign_plan, b, s)) != hipSuccess) return e2;
+      if ((e2 = launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
+                                    d_changed, d.num_cus, s)) != hipSuccess)
+        return e2;
+    }
+    return hipSuccess;
+  };
   const char* mode = std::getenv("OPENR_SPF_WHATIF");
   const bool dist64 = use_link_metric && (uint64_t)V * ctx->w_max >= 0xFFFFFFFFull;
   // exact-order plans (metrics / widths outside the fast kernels): filter + re-solve; with
@@ -481,21 +512,27 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   const bool exact = base_plan.exact || ign_plan.exact;
   if (!exact && (!mode || !std::strcmp(mode, "group"))) {
     // default: grouped repair (base rows staged once per (source, link chunk), fused filter)
-    if (whatif_group_lds_bytes(V, ctx->E, nb, dist64)) {
-      OPENR_TRY(d.wcount.reserve(1));
+    // (a unit with more dirty nodes than a wave's slots is re-solved after the launch)
+    if (whatif_group_lds_bytes(V, ctx->E, nb, dist64, d.g.max_deg)) {
+      const size_t units = (size_t)n_links * n_src;
+      OPENR_TRY(d.wcount.reserve(2));
+      OPENR_TRY(d.wsrc.reserve(units));
+      OPENR_TRY(d.wlink.reserve(units));
+      OPENR_TRY(d.wunit.reserve(units));
       OPENR_TRY(hipEventRecord(d.ev_begin, s));  // the repair kernel's own time -> stats.last_kernel_ms
       OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
                                     d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
-                                    d_changed, d.wcount.p,
-                                    d.work.p + kIncrCtr, d.num_cus, s));
+                                    d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
+                                    d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));
-      uint32_t count = 0;
-      OPENR_TRY(hipMemcpyAsync(&count, d.wcount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      uint32_t cnt[2] = {0, 0};  // affected units, units handed over
+      OPENR_TRY(hipMemcpyAsync(cnt, d.wcount.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
       OPENR_TRY(hipStreamSynchronize(s));
       float ms = 0.f;
       OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
       ctx->stats.last_kernel_ms = ms;
-      *solved = count;
+      if (cnt[1]) OPENR_TRY(resolve_units(cnt[1]));  // units past the slots: re-solved (few, large)
+      *solved = cnt[0];
       return hipSuccess;
     }
   }
@@ -518,30 +555,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
                               !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);
   }
-  const size_t row = (size_t)V * (8u + nb);
-  const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
-  OPENR_TRY(d.wdist.reserve((size_t)chunk * V));
-  OPENR_TRY(d.wnh.reserve((size_t)chunk * V * nb));
-  OPENR_TRY(d.wiota.reserve((size_t)chunk + 1u));
-  OPENR_TRY(d.ovf.reserve((size_t)chunk * ctx->nsl_max()));
-  OPENR_TRY(launch_iota(d.wiota.p, chunk + 1u, d.num_cus, s));
-  for (uint32_t off = 0; off < count; off += chunk) {
-    const uint32_t m = std::min(chunk, count - off);
-    SolveArgs b{};
-    b.sources = d.wsrc.p + off;
-    b.n = m;
-    b.ign_ptr = d.wiota.p;  // solve k ignores exactly wlink[off + k]
-    b.ign_links = d.wlink.p + off;
-    b.dist = d.wdist.p;
-    b.nh = d.wnh.p;
-    b.nh_bytes = nb;
-    b.nh_bits = ctx->nh_bits;
-    b.ovf_list = d.ovf.p;
-    b.work = d.work.p;
-    OPENR_TRY(launch(ctx, d, ign_plan, b, s));
-    OPENR_TRY(launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
-                                  d_changed, d.num_cus, s));
-  }
+  return resolve_units(count);
 #undef OPENR_TRY
   return hipSuccess;
 }

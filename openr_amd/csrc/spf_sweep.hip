@@ -574,16 +574,21 @@ struct GraphView<true> {  // compact LDS copy
 };
 
 constexpr uint32_t kGrpMaxChunk = 2048;  // links per work item
+constexpr uint32_t kGrpMaxCap = 255;     // dirty slots per wave (u8 slot index)
 
 struct GrpLayout {
   uint32_t grow, grec, gnbr, govl;                                  // LDS graph (LG only)
   uint32_t bdist, bnh, btight, btin, ulist, wave0, wstride;         // wave w at wave0 + w * wstride
-  uint32_t w_ina, w_dq, w_nhm, w_dec, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
+  uint32_t w_ina, w_dq, w_nhm, w_dec, w_didx, w_adist, w_anh, w_alist, w_dlist;  // offsets inside a wave block
   uint32_t total;
 };
 
+// Per-wave state is dense only where it is a bitmap or a byte per node; the overlays a
+// repair writes (new distances, next hops, the A and dirty lists) hold at most `cap`
+// dirty nodes (<= 255, indexed by didx[v] - 1); a unit with more is re-solved after
+// the launch (full SPF with the link ignored + row compare, spf_capi.hip).
 __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t nb, uint32_t dist_bytes, bool lg,
-                                                uint32_t waves, uint32_t chunk) {
+                                                uint32_t waves, uint32_t chunk, uint32_t cap) {
   GrpLayout l;
   uint32_t off = 16;  // workgroup control: [0] next link group of the item
   auto take = [](uint32_t& o, uint32_t bytes) {
@@ -599,17 +604,18 @@ __host__ __device__ inline GrpLayout grp_layout(uint32_t V, uint32_t E, uint32_t
   l.bdist = take(off, dist_bytes * V);
   l.bnh = take(off, nb * V);
   l.btight = take(off, 8u * ((E + 63u) / 64u));
-  l.btin = take(off, 2u * (V + 1u));  // u16 base-tight in-degree per node
+  l.btin = take(off, V + 4u);  // u8 base-tight in-degree per node (rows <= 255 edges)
   l.ulist = take(off, 4u * chunk);  // the item's affected links: offset in the chunk << 16 | b
   uint32_t w = 16;  // wave control: [0] A count, [1] dirty count, [2] flag
   l.w_ina = take(w, 4u * vw);
   l.w_dq = take(w, 4u * vw);
   l.w_nhm = take(w, 4u * vw);
-  l.w_dec = take(w, 2u * (V + 1u));  // u16 per node: tight in-edges whose tail joined A
-  l.w_adist = take(w, dist_bytes * V);
-  l.w_anh = take(w, nb * V);
-  l.w_alist = take(w, 2u * V);
-  l.w_dlist = take(w, 2u * V);
+  l.w_dec = take(w, V + 4u);   // u8 per node: tight in-edges whose tail joined A
+  l.w_didx = take(w, V + 4u);  // u8 per node: 1 + its slot in the dirty list, 0 = clean
+  l.w_adist = take(w, dist_bytes * cap);
+  l.w_anh = take(w, nb * cap);
+  l.w_alist = take(w, 2u * cap);
+  l.w_dlist = take(w, 2u * cap);
   l.wave0 = off;
   l.wstride = w;
   l.total = off + waves * w;
@@ -651,32 +657,48 @@ struct GrpWave {
   uint8_t* anh;
   uint32_t *ina, *dq, *nhm, *ctl;
   const uint64_t* btight;  // base-tight mask of the source (workgroup rows)
-  const uint16_t* tin;     // base-tight in-degree (workgroup rows)
-  uint16_t* dec;           // per unit: tight in-edges of v lost (tail in A, or the failed edge)
+  const uint8_t* tin;      // base-tight in-degree (workgroup rows)
+  uint8_t* dec;            // per unit: tight in-edges of v lost (tail in A, or the failed edge)
+  uint8_t* didx;           // per unit: 1 + v's dirty slot (adist / anh index), 0 = clean
+  uint32_t cap;            // dirty slots
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_WHATIF_PROF): per-phase cycles and sizes, or null
   unsigned long long pacc[8];  // this wave's share of prof, added once when the wave retires
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
-  // distance after the repair of (2): A nodes from the overlay, the rest from the base
+  // distance after step (2): A nodes from the overlay slot, the rest from the base (the
+  // bitmap, slot index and base value load together; only A nodes read the slot)
   __device__ D dist(uint32_t u) const {
-    const D a = adist[u], b = bdist[u];  // both loads issue with the bitmap read
-    return bit_of(ina, u) ? a : b;
+    bool in;
+    return dist_a(u, in);
   }
   __device__ D dist_a(uint32_t u, bool& in) const {
-    const D a = adist[u], b = bdist[u];
+    const uint32_t k = didx[u];
+    const D b = bdist[u];
     in = bit_of(ina, u);
-    return in ? a : b;
+    return in ? adist[k - 1u] : b;
   }
   __device__ void nh_or(uint32_t (&acc)[W], uint32_t u) const {
-    nh_or_sel(acc, anh + (size_t)u * nb, bnh + (size_t)u * nb, bit_of(nhm, u), nb);
+    const uint32_t k = didx[u];
+    const bool o = bit_of(nhm, u);
+    nh_or_sel(acc, anh + (size_t)(o ? k - 1u : 0u) * nb, bnh + (size_t)u * nb, o, nb);
+  }
+  // append v to the dirty list at slot pos (false: the unit outgrows the slots)
+  __device__ bool put_dirty(uint32_t v, uint32_t pos) const {
+    if (pos >= cap) return false;
+    dlist[pos] = (uint16_t)v;
+    didx[v] = (uint8_t)(pos + 1u);
+    return true;
   }
   // in-edge u -> v (the record of v -> u) usable, not the failed link, u may expand
   __device__ bool in_usable(const EdgeRec& r) const { return !r.down && r.lid != link && (r.col == src || !r.sink); }
 };
 
-// One affected unit: returns the changed-node count (uniform across the wave).
+constexpr uint32_t kGrpOverflow = UINT32_MAX;  // grp_repair: the unit outgrew the dirty slots
+
+// One affected unit: returns the changed-node count (uniform across the wave), or
+// kGrpOverflow.
 template <typename D, bool LG, uint32_t W>
 __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, uint32_t bnode) {
   constexpr D INF = (D)~(D)0;
@@ -686,8 +708,11 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     c.dq[i] = 0;
     c.nhm[i] = 0;
   }
-  for (uint32_t i = lane; i < (V + 1u) / 2u; i += 64u) reinterpret_cast<uint32_t*>(c.dec)[i] = 0;
-  if (lane == 0) c.ctl[0] = c.ctl[1] = 0;
+  for (uint32_t i = lane; i < (V + 4u) / 4u; i += 64u) {
+    reinterpret_cast<uint32_t*>(c.dec)[i] = 0;
+    reinterpret_cast<uint32_t*>(c.didx)[i] = 0;
+  }
+  if (lane == 0) c.ctl[0] = c.ctl[1] = c.ctl[2] = 0;  // [2]: the unit outgrew the dirty slots
   lds_fence();
   long long pt0 = c.prof ? (long long)__builtin_amdgcn_s_memtime() : 0, pt1 = 0, pt2 = 0, pt3 = 0;
   // (1) A by decremental propagation over the base tight DAG: v joins A when every one of
@@ -695,7 +720,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   // counts the lost ones; the lane whose increment reaches tin[v] appends v.
   if (lane == 0) {
     c.dq[bnode >> 5] |= 1u << (bnode & 31u);
-    c.dlist[c.ctl[1]++] = (uint16_t)bnode;
+    c.put_dirty(bnode, c.ctl[1]++);
     if (c.tin[bnode] == 1u) {
       c.ina[bnode >> 5] |= 1u << (bnode & 31u);
       c.alist[c.ctl[0]++] = (uint16_t)bnode;
@@ -704,7 +729,8 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   lds_fence();
   // 8-lane groups: eight A members per wave pass, a lane per out-edge (members appended
   // during a pass are taken by the next)
-  for (uint32_t idx0 = 0, na0; idx0 < (na0 = __builtin_amdgcn_readfirstlane(c.ctl[0]));
+  for (uint32_t idx0 = 0, na0; idx0 < (na0 = __builtin_amdgcn_readfirstlane(c.ctl[0])) &&
+                               !__builtin_amdgcn_readfirstlane(c.ctl[2]);
        idx0 += min(8u, na0 - idx0)) {
     const uint32_t idx = idx0 + (lane >> 3), sub = lane & 7u;
     if (idx < na0) {
@@ -714,17 +740,19 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
         if (!((c.btight[e >> 6] >> (e & 63u)) & 1ull)) continue;  // base-tight x -> y (x expands)
         const uint32_t y = c.gv.rec(e).col;
         const uint32_t bit = 1u << (y & 31u);
-        if (!(atomicOr(&c.dq[y >> 5], bit) & bit)) c.dlist[atomicAdd(&c.ctl[1], 1u)] = (uint16_t)y;
-        const uint32_t sh = 16u * (y & 1u);
-        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(c.dec) + (y >> 1), 1u << sh);
-        if (((old >> sh) & 0xFFFFu) + 1u == c.tin[y]) {
+        if (!(atomicOr(&c.dq[y >> 5], bit) & bit) && !c.put_dirty(y, atomicAdd(&c.ctl[1], 1u))) c.ctl[2] = 1;
+        const uint32_t sh = 8u * (y & 3u);
+        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(c.dec) + (y >> 2), 1u << sh);
+        if (((old >> sh) & 0xFFu) + 1u == c.tin[y]) {
           atomicOr(&c.ina[y >> 5], bit);
-          c.alist[atomicAdd(&c.ctl[0], 1u)] = (uint16_t)y;
+          const uint32_t pa = atomicAdd(&c.ctl[0], 1u);  // A is part of the dirty set: pa < cap
+          if (pa < c.cap) c.alist[pa] = (uint16_t)y;
         }
       }
     }
     lds_fence();
   }
+  if (__builtin_amdgcn_readfirstlane(c.ctl[2])) return kGrpOverflow;
   const uint32_t na = __builtin_amdgcn_readfirstlane(c.ctl[0]);
   if (c.prof) pt1 = (long long)__builtin_amdgcn_s_memtime();
   // (2) tentative distances inside A: the best entry from outside A (an 8-lane group per
@@ -748,7 +776,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       }
     }
     best = grp8_min(best);
-    if (i < na && sub == 0) c.adist[x] = best;
+    if (i < na && sub == 0) c.adist[c.didx[x] - 1u] = best;
   }
   lds_fence();
   // (3) Dijkstra over the dirty set: buckets of equal (new) distance in increasing order. A
@@ -766,7 +794,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   D ed = INF;
   bool pend = false, ea = false;  // ea: the lane's entry is in A (its distance may still drop)
   auto load_entries = [&]() {
-    if (pend && ea) ed = c.adist[ev];
+    if (pend && ea) ed = c.adist[lane];  // entry i sits in lane i and in slot i
     const uint32_t hi = min(nd, 64u);
     if (loaded < hi) {
       if (lane >= loaded && lane < hi) {
@@ -799,7 +827,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
         du = c.dist_a(q.col, ua);
         if (relax && ua && !q.down && q.lid != c.link) {  // v settled: relax v -> u inside A
           const D cand = dv + (D)c.w(q);
-          if (cand < du) lds_atomic_min(&c.adist[q.col], cand);
+          if (cand < du) lds_atomic_min(&c.adist[c.didx[q.col] - 1u], cand);
         }
         if (dv != INF && c.in_usable(q) && du != INF && (uint64_t)du + c.wi(q) == (uint64_t)dv) {
           if (q.col == c.src) {
@@ -821,7 +849,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       diff |= acc[k] != __builtin_amdgcn_readfirstlane(cur[k]);
     }
     if (diff && lane == 0) {
-      uint8_t* o = c.anh + (size_t)v * nb;
+      uint8_t* o = c.anh + (size_t)(c.didx[v] - 1u) * nb;
       for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
       c.nhm[v >> 5] |= 1u << (v & 31u);
     }
@@ -843,10 +871,8 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
         fresh = !(atomicOr(&c.dq[y >> 5], bit) & bit);
       }
       const unsigned long long m = __ballot(fresh);
-      if (fresh) {
-        const uint32_t pos = nd + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        c.dlist[pos] = (uint16_t)y;
-      }
+      if (fresh)  // past the slots: nd > cap aborts the unit after this node
+        c.put_dirty(y, nd + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)));
       nd += (uint32_t)__popcll(m);
     }
   };
@@ -876,6 +902,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       const int k = __builtin_ctzll(m);
       m &= m - 1ull;
       process((uint32_t)__builtin_amdgcn_readlane((int)ev, k), mn);
+      if (nd > c.cap) return kGrpOverflow;
     }
     for (uint32_t i0 = 64; i0 < nd0; i0 += 64u) {
       const uint32_t i = i0 + lane;
@@ -891,6 +918,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
         const int k = __builtin_ctzll(mo);
         mo &= mo - 1ull;
         process((uint32_t)__builtin_amdgcn_readlane((int)v, k), mn);
+        if (nd > c.cap) return kGrpOverflow;
       }
     }
     if (pend && ed == mn) pend = false;
@@ -920,7 +948,8 @@ template <typename D, bool LG, uint32_t W>
 __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
-    uint32_t* changed, uint32_t* affected, uint32_t* ctr, unsigned long long* prof) {
+    uint32_t cap, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
+    uint32_t* ctr, unsigned long long* prof) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -928,14 +957,14 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   const uint32_t block = blockDim.x, waves = block >> 6;
   const uint32_t tw = (E + 63u) / 64u, vw = (V + 31u) / 32u;
-  const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves, chunk);
+  const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves, chunk, cap);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* wctl = smem;
   D* bdist = reinterpret_cast<D*>(base + lay.bdist);
   uint8_t* bnh = reinterpret_cast<uint8_t*>(base + lay.bnh);
   uint64_t* btight = reinterpret_cast<uint64_t*>(base + lay.btight);
   uint32_t* ulist = reinterpret_cast<uint32_t*>(base + lay.ulist);
-  uint16_t* btin = reinterpret_cast<uint16_t*>(base + lay.btin);
+  uint8_t* btin = reinterpret_cast<uint8_t*>(base + lay.btin);
   char* wb = base + lay.wave0 + wave * lay.wstride;
   GrpWave<D, LG, W> c;
   c.g = &g;
@@ -973,7 +1002,9 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   c.ina = reinterpret_cast<uint32_t*>(wb + lay.w_ina);
   c.dq = reinterpret_cast<uint32_t*>(wb + lay.w_dq);
   c.nhm = reinterpret_cast<uint32_t*>(wb + lay.w_nhm);
-  c.dec = reinterpret_cast<uint16_t*>(wb + lay.w_dec);
+  c.dec = reinterpret_cast<uint8_t*>(wb + lay.w_dec);
+  c.didx = reinterpret_cast<uint8_t*>(wb + lay.w_didx);
+  c.cap = cap;
   c.adist = reinterpret_cast<D*>(wb + lay.w_adist);
   c.anh = reinterpret_cast<uint8_t*>(wb + lay.w_anh);
   c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
@@ -1001,13 +1032,13 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     }
     const uint64_t* trow = base_tight + (size_t)j * tw;
     for (uint32_t i = tid; i < tw; i += block) btight[i] = trow[i];
-    for (uint32_t i = tid; i < (V + 1u) / 2u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
+    for (uint32_t i = tid; i < (V + 4u) / 4u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
     if (tid == 0) wctl[0] = wctl[1] = 0;  // [0] affected links listed, [1] next one to repair
     __syncthreads();
     for (uint32_t e = tid; e < E; e += block)  // base-tight in-degrees
       if ((btight[e >> 6] >> (e & 63u)) & 1ull) {
         const uint32_t v = c.gv.rec(e).col;
-        atomicAdd(reinterpret_cast<uint32_t*>(btin) + (v >> 1), 1u << (16u * (v & 1u)));
+        atomicAdd(reinterpret_cast<uint32_t*>(btin) + (v >> 2), 1u << (8u * (v & 3u)));
       }
     // fused filter, a thread per link: a link with no base-tight edge changes nothing;
     // the others are listed with b, the head of their tight edge a->b (at most one
@@ -1047,7 +1078,16 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
       const uint32_t i = l0 + (ent >> 16);
       c.link = links[i];  // first needed in step (2): the load overlaps step (1)
       const uint32_t cnt = grp_repair(c, lane, V, ent & 0xFFFFu);
-      if (lane == 0) changed[(size_t)i * n_src + j] = cnt;
+      if (lane == 0) {
+        if (cnt != kGrpOverflow) {
+          changed[(size_t)i * n_src + j] = cnt;
+        } else {  // more dirty nodes than slots: re-solved after the launch (openr_spf_whatif)
+          const uint32_t k = atomicAdd(&affected[1], 1u);
+          ovf_src[k] = c.src;
+          ovf_link[k] = c.link;
+          ovf_unit[k] = i * n_src + j;
+        }
+      }
     }
     __syncthreads();  // every wave is done with this item's shared rows and s_item
     if (tid == 0) s_item = gridDim.x + atomicAdd(&ctr[0], 1u);
@@ -1128,18 +1168,18 @@ bool grp_lds_graph_ok(const DevGraph& g, uint32_t w_max, uint32_t nh_bits) {
 }
 }  // namespace
 
-uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64) {
-  if (V > 65535u || nb > 32u) return 0;
-  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u, false, 4, kGrpMaxChunk).total;
+uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64, uint32_t max_deg) {
+  if (V > 65535u || nb > 32u || max_deg > 255u) return 0;  // u16 ids, u8 in-degree counters
+  const uint32_t t = grp_layout(V, E, nb, dist64 ? 8u : 4u, false, 4, kGrpMaxChunk, kGrpMaxCap).total;
   return t <= kMaxLds ? t : 0;
 }
 
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
-                               uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ctr, int num_cus,
-                               hipStream_t s) {
-  hipError_t err = hipMemsetAsync(affected, 0, sizeof(uint32_t), s);
+                               uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
+                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s) {
+  hipError_t err = hipMemsetAsync(affected, 0, 2u * sizeof(uint32_t), s);  // [0] affected, [1] handed over
   if (err != hipSuccess || !n_links || !n_src) return err;
   // distances as u16 when every finite one fits (V * w_max < 0xFFFF): half the LDS rows,
   // more workgroups per CU
@@ -1148,8 +1188,9 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // the LDS-graph variant (opt-in) with as many waves per workgroup (one workgroup per
   // CU) as fit, else the global-graph variant at OPENR_SPF_WHATIF_WAVES (3) per workgroup
   bool lg = false;
-  uint32_t waves = bfs::env_u32("OPENR_SPF_WHATIF_WAVES", 3u, 1u, kGrpMaxBlock / 64u);  // WAN: 3 -> 7.1, 4 -> 7.4, 5 -> 9.2 ms
-  auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch).total; };
+  uint32_t waves = bfs::env_u32("OPENR_SPF_WHATIF_WAVES", 3u, 1u, kGrpMaxBlock / 64u);  // WAN: 3 / 4 / 8 -> 5.57 / 5.62 / 6.41 ms
+  const uint32_t cap = bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpMaxCap, 1u, kGrpMaxCap);  // tests force small caps
+  auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch, cap).total; };
   if (grp_lds_graph_ok(g, w_max, nh_bits)) {
     for (uint32_t w = kGrpMaxBlock / 64u; w >= 2u; --w) {
       if (layout_bytes(true, w, kGrpMaxChunk) <= kMaxLds) {
@@ -1191,7 +1232,8 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
-                       base_nh, base_tight, nb, (uint32_t)unit_cost, changed, affected, ctr, prof);            \
+                       base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed, affected, ovf_src, ovf_link,  \
+                       ovf_unit, ctr, prof);                                                                   \
   } while (0)
   if (d16) {
     if (lg) OPENR_GRP_LAUNCH(uint16_t, true);

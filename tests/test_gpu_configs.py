@@ -94,7 +94,7 @@ def test_config3_grid100_all_sources(eng):
     pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
 
 
-@pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "incr", "solve"])
+@pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "group-cap", "incr", "solve"])
 def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
     """Per-link-failure sweep on the 1k-node WAN (U[1,64] asymmetric metrics): every one
     of the 3 000 links x 16 sources, changed-node counts vs oracle re-solves
@@ -104,6 +104,8 @@ def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
         monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
+    if mode == "group-cap":  # 8 dirty slots per wave: larger units are re-solved
+        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "8")
     monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     g = T.wan(1000, 3000, 64, seed=1)
     eng.set_graph(g)

@@ -382,7 +382,7 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "group-lds", "group-d32", "incr", "solve"])
+@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
     (default: graph read from global memory, u16 distances when they fit; or the graph
@@ -393,6 +393,8 @@ def whatif_mode(request, monkeypatch):
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
         monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
+    if mode == "group-cap":  # 3 dirty slots per wave: most units are re-solved
+        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "3")
     monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     return request.param
 
