@@ -796,7 +796,12 @@ hipError_t launch_lvl_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
   const bool vis = SLICED || !Nh<MODE>::kSingle;
   const LvlShape sh = lvl_shape(g, has_ign, MODE, vis, env_u32("OPENR_SPF_BFS_WGS", kBfsTargetWgs, 1u, 16u));
   const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
-  const bool b128 = blk == 128u || (blk != 256u && sh.per_cu > 8u);
+  // 128-thread workgroups when the batch fills the GPU several times over (occupancy hides
+  // the level loop's latency: G100 0.863 vs 0.913 ms); 256 threads (four waves per solve,
+  // a wide level in one pass) when it fills it at most twice, as a strong-scaling shard
+  // does (G100 5 000 sources 0.518 vs 0.556 ms, 2 500: 0.357 vs 0.381 ms)
+  const bool small_batch = (uint64_t)a.n <= 2ull * (uint64_t)num_cus * sh.per_cu;
+  const bool b128 = blk == 128u || (blk != 256u && sh.per_cu > 8u && !small_batch);
 #define OPENR_LVL_MODE(BLK, E) \
   return launch_lvl_mode<MODE, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, num_cus, s, info)
   if (b128) {
