@@ -460,6 +460,202 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Lean level pass (the grid configuration): every transit row fits the 4 ELL slots, no
+// ignore set, no tight-edge output, one next-hop field per node inside one dword, u8
+// levels. Same semantics as bfs_lvl_kernel<MODE, *, u8, true, 2, false, false>
+// (LinkState::runSpf closed form for uniform cost, LinkState.cpp:808-882); the pass is
+// restated so that an edge slot costs ~11 vector instructions instead of ~30:
+//  * LDS is addressed through address-space-3 pointers: the level array sits at the
+//    constant byte offset 32, folded into the ds instruction;
+//  * a lane whose edge is not tight ORs its value into its own dummy word, which is all
+//    ones, so "first arrival" is one test of the returned field for every slot (a dummy
+//    field is never zero), and that test's compare mask is the slot's ballot;
+//  * the frontier queue is two halves of ring_cap / 2 entries, level L in half L & 1, so
+//    an append slot is base + mbcnt (no wrap mask); a level wider than a half flags the
+//    solve for the u16 full-order re-run of bfs_lvl_kernel, as a deeper-than-253 solve;
+//  * lanes past the frontier read the sentinel row ellv[V] (every slot V, lvl[V] = 0:
+//    never tight), so the pass has no divergent prologue.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds_or(lds_u32* p, uint32_t v) {
+  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add(lds_u32* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+struct LeanLayout {
+  uint32_t nh, ring, dummy, total;
+};
+// [0, 32) control, [32, 32 + V + 4) u8 levels, next-hop words, two queue halves, dummies
+__host__ __device__ inline LeanLayout lean_layout(uint32_t V, uint32_t nh_words, uint32_t ring_cap) {
+  LeanLayout l;
+  uint32_t off = 32u + ((V + 4u + 15u) & ~15u);
+  l.nh = off;
+  off += (4u * nh_words + 15u) & ~15u;
+  l.ring = off;
+  off += (2u * ring_cap + 15u) & ~15u;
+  l.dummy = off;
+  off += 4u * 64u;
+  l.total = off;
+  return l;
+}
+
+template <int MODE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_ell_kernel(
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+  using N = Nh<MODE>;
+  static_assert(N::kSingle, "single-dword next-hop fields only");
+  constexpr uint32_t kBits = 32u / N::kPer;
+  constexpr uint32_t kLog = kBits == 4 ? 3 : kBits == 8 ? 2 : kBits == 16 ? 1 : 0;  // log2 nodes per dword
+  constexpr uint32_t kShl = 5u - kLog;  // field shift = v << kShl (low 5 bits used by v_lshlrev / v_bfe)
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
+  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar loop bounds)
+  const uint32_t nh_words = N::words(V);
+  const LeanLayout lay = lean_layout(V, nh_words, ring_cap);
+  lds_u32* const ctl = (lds_u32*)(size_t)0u;  // [0..3] append counters, [4] overflow flag, [7] next unit
+  lds_u8* const lvl = (lds_u8*)(size_t)32u;
+  lds_u32* const lvl_w = (lds_u32*)(size_t)32u;
+  lds_u32* const nh = (lds_u32*)(size_t)lay.nh;
+  lds_u16* const ring = (lds_u16*)(size_t)lay.ring;
+  lds_u32* const my_dummy = (lds_u32*)(size_t)(lay.dummy + 4u * lane);
+  // generic views for the shared row writer
+  const uint8_t* lvl_g = reinterpret_cast<const uint8_t*>(reinterpret_cast<char*>(smem) + 32);
+  const uint32_t* nh_g = reinterpret_cast<const uint32_t*>(reinterpret_cast<char*>(smem) + lay.nh);
+  const uint32_t lvl_words = (V + 4u) / 4u;
+  const uint32_t half = ring_cap / 2u;
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  *my_dummy = 0xFFFFFFFFu;  // only ever ORed afterwards: its fields are never zero
+
+  for (uint32_t unit = blockIdx.x; unit < count;) {
+    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
+    const uint32_t src = a.sources[sid];
+    if (src < V) {  // block-uniform
+      for (uint32_t i = tid; i < lvl_words; i += BLOCK) lvl_w[i] = 0xFFFFFFFFu;
+      for (uint32_t i = tid; i < nh_words; i += BLOCK) nh[i] = 0;
+      if (tid < 5) ctl[tid] = 0;
+      __syncthreads();
+      if (tid == 0) {
+        lvl[src] = 0;
+        lvl[V] = 0;  // ELL sentinel: level 0 is never > L, so a sentinel slot is never tight
+      }
+      __syncthreads();
+      // level 0: the source expands even when overloaded; a directly connected node's
+      // next hop is the node itself (LinkState.cpp:867-872). Level 1 goes to half 1.
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
+          const uint32_t e = e0 + tid;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && v != src) {
+              const uint32_t sh = (v << kShl) & 31u;
+              fresh = ((lds_or(&nh[v >> kLog], (1u << g.nbr[e]) << sh) >> sh) & N::kMask) == 0u;
+              lvl[v] = 1;
+            }
+          }
+          const uint32_t slot = wave_append(fresh, reinterpret_cast<uint32_t*>(smem) + 1);
+          if (fresh) ring[half + slot] = (uint16_t)v;  // slot < deg(src) <= half (host-checked)
+        }
+      }
+      __syncthreads();
+
+      uint32_t cur = ctl[1], L = 1, reached = 1u + cur;
+      bool overflow = false;  // block-uniform
+      while (cur) {
+        if (L + 1u >= 0xFFu) {  // next level not representable in u8
+          overflow = true;
+          break;
+        }
+        // level L: entries [0, cur) of half L & 1; level L+1 appends to the other half,
+        // counted in ctl[(L + 1) & 3] (zeroed here: last read three barriers ago)
+        lds_u32* const cnt = &ctl[(L + 1u) & 3u];
+        if (tid == 0) ctl[(L + 2u) & 3u] = 0;
+        const uint32_t rd = (L & 1u) * half, wr = half - rd;
+        const uint8_t lnext = (uint8_t)(L + 1u);
+        for (uint32_t fb = wave * 64u; fb < cur; fb += BLOCK) {
+          const uint32_t idx = fb + lane;
+          const uint32_t q = ring[rd + idx];  // past the level: stale or unset, replaced below
+          const uint32_t u = idx < cur ? q : V;
+          const uint4 ell = g.ellv[u];  // ellv[V] = sentinel row
+          const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
+          const uint32_t vv[4] = {ell.x, ell.y, ell.z, ell.w};
+          // the four level reads issue together, then the four atomics
+          uint32_t lv[4], old[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lv[j] = lvl[vv[j]];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t v = vv[j];
+            const bool tight = lv[j] > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
+            old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, x << ((v << kShl) & 31u));
+          }
+          __builtin_amdgcn_sched_barrier(0);  // all four atomics in flight before their results are used
+          unsigned long long bj[4];
+          bool fresh[4];
+          uint32_t off[5];
+          off[0] = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // v's field was empty: this is the first arrival (a dummy field never is)
+            fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;
+            bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
+            off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+          }
+          const uint32_t total = off[4];
+          if (total) {  // wave-uniform
+            const uint32_t leader = (uint32_t)__builtin_amdgcn_readfirstlane(lane);
+            uint32_t wbase = 0;
+            if (lane == leader) wbase = lds_add(cnt, total);
+            const uint32_t bse = __builtin_amdgcn_readfirstlane(wbase);
+            if (bse + total <= half) {  // wave-uniform: the level fits its half so far
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (fresh[j]) {
+                  const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                  ring[wr + bse + off[j] + slot] = (uint16_t)vv[j];
+                  // only the appending arrival stores v's level; another arrival of this
+                  // level that reads it earlier sees "unset" (> L), i.e. tight, as it is
+                  lvl[vv[j]] = lnext;
+                }
+              }
+            } else if (lane == leader) {
+              ctl[4] = 1;  // the level outgrows its half
+            }
+          }
+        }
+        lds_barrier();
+        cur = *cnt;
+        reached += cur;
+        ++L;
+        if (ctl[4]) {  // uniform after the barrier
+          overflow = true;
+          break;
+        }
+        if (reached == V) break;  // every node reached: the newest level cannot expand tightly
+      }
+      if (overflow) {
+        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
+      } else {
+        write_rows<MODE, uint8_t, BLOCK, false>(a, sid, 0, V, lvl_g, nh_g, cost, nt != 0);
+      }
+    }
+    __syncthreads();  // every lane is done with this unit's LDS and ctl[7]
+    if (tid == 0) ctl[7] = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unit = ctl[7];
+  }
+  retire_workgroup(ctr, nullptr);
+}
+
 // Occupancy first (target workgroups per CU, 8 by default): the full-order u16 variant
 // when it fits the per-workgroup budget, else the u8 ring when a ring wide enough for the
 // estimated two-level frontier fits and the estimated depth stays under the u8 limit;
@@ -524,6 +720,24 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   return hipGetLastError();
 }
 
+template <int MODE, int BLOCK>
+hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr,
+                           uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
+  const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
+  auto k = bfs_ell_kernel<MODE, BLOCK>;
+  hipError_t err =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  if (info) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = "bfs_ell_kernel<halves,u8>";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, ctr, ovf_count, nt_stores());
+  return hipGetLastError();
+}
+
 template <int MODE, int BLOCK, int ELLM, bool SLICED>
 hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
                            uint32_t ring_cap, int num_cus, hipStream_t s, LaunchInfo* info) {
@@ -532,8 +746,19 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   if (!ring_cap)
     return launch_lvl_variant<MODE, BLOCK, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, false, blk,
                                                                           blk + 4, num_cus, s, info);
-  hipError_t err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap,
-                                                                                false, blk, blk + 4, num_cus, s, info);
+  hipError_t err;
+  if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
+    // lean pass: its queue halves must hold the widest sampled level (else the generic ring)
+    const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
+    if (!has_ign && !a.tight && ring_cap / 2u >= need1 && env_u32("OPENR_SPF_BFS_LEAN", 1u, 0u, 1u))
+      err = launch_lvl_lean<MODE, BLOCK>(g, a, cost, ring_cap, blk, blk + 4, num_cus, s, info);
+    else
+      err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, false,
+                                                                         blk, blk + 4, num_cus, s, info);
+  } else {
+    err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, false,
+                                                                       blk, blk + 4, num_cus, s, info);
+  }
   if (err != hipSuccess || (g.V <= ring_cap && g.V <= 254u)) return err;  // nothing can overflow
   return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true, blk + 2,
                                                                       blk + 4, num_cus, s, info);

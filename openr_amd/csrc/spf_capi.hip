@@ -179,9 +179,9 @@ int family_override(int dflt) {
 // (LinkState.cpp:831-838). depth picks the kernel family — the lvl kernels win on deep
 // graphs (grid G100: ~150 levels of ~70 nodes; 1.07 vs 1.92 ms), the code kernels on
 // shallow ones (fabric: 5 levels; 1.44 vs 1.95 ms) — and width2 (max |level L| +
-// |level L+1|) sizes the frontier ring.
+// |level L+1|) sizes the frontier ring (width1 = max |level L|: the lean pass's halves).
 struct FrontierEstimate {
-  uint32_t depth = 0, width2 = 0;
+  uint32_t depth = 0, width2 = 0, width1 = 0;
   int family() const { return depth >= kDeepGraphLevels ? kFamLvl : kFamCode; }
 };
 
@@ -218,6 +218,7 @@ FrontierEstimate estimate_frontier(uint32_t V, const uint32_t* row_ptr, const ui
     }
     est.depth = std::max<uint32_t>(est.depth, (uint32_t)width.size() - 1u);
     for (size_t l = 0; l + 1 < width.size(); ++l) est.width2 = std::max<uint32_t>(est.width2, width[l] + width[l + 1]);
+    for (uint32_t w : width) est.width1 = std::max(est.width1, w);
   }
   return est;
 }
@@ -891,6 +892,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     g.L = L;
     for (uint32_t u = 0; u < V; ++u) g.max_deg = std::max(g.max_deg, gr->row_ptr[u + 1] - gr->row_ptr[u]);
     g.est_width2 = est.width2;
+    g.est_width1 = est.width1;
     g.est_depth = est.depth;
     auto up = [&](auto** dst, const auto* srcp, size_t count) -> hipError_t {
       using T = std::remove_pointer_t<std::remove_pointer_t<decltype(dst)>>;
@@ -905,9 +907,9 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
     if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
     if (err == hipSuccess) {
-      std::vector<uint4> ellv(V);
+      std::vector<uint4> ellv(V + 1u, make_uint4(V, V, V, V));  // [V] = sentinel row (lean BFS pass)
       for (uint32_t u = 0; u < V; ++u) ellv[u] = ellv_of(ellt[u], V);
-      err = up(&g.ellv, ellv.data(), V);
+      err = up(&g.ellv, ellv.data(), V + 1u);
     }
     if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);

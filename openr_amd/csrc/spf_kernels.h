@@ -17,6 +17,7 @@ struct DevGraph {
   uint32_t V = 0, E = 0, L = 0;
   uint32_t max_deg = 0;        // largest row (source expansion must fit the frontier queue)
   uint32_t est_width2 = 0;     // sampled max |level L| + |level L+1| of a BFS (ring sizing)
+  uint32_t est_width1 = 0;     // sampled max |level L| (lean BFS pass: queue halves)
   uint32_t est_depth = 0;      // sampled max BFS depth (family choice, u8 level limit)
   uint32_t* row = nullptr;     // [V+1]
   uint2* row2 = nullptr;       // [V] (row[u], row[u+1]) in one 8-byte load
@@ -24,8 +25,9 @@ struct DevGraph {
                                //     (an overloaded node other than the source is never expanded)
   uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
   uint4* ellt = nullptr;       // [V] first 4 edges of each transit row (adj encoding, kEdgeDown-padded)
-  uint4* ellv = nullptr;       // [V] ellt with every down / padding slot replaced by the node id V (a
-                               //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests)
+  uint4* ellv = nullptr;       // [V+1] ellt with every down / padding slot replaced by the node id V (a
+                               //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests);
+                               //     ellv[V] = (V, V, V, V), the row of a lane past the frontier
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
   uint64_t* w64 = nullptr;     // [E] metric u->v as the caller gave it (exact-order kernel: 0 / wrapped values)
