@@ -14,6 +14,7 @@
 // One 256-thread workgroup per solve, persistent and dynamically scheduled; K=4 edges
 // per lane with their LDS reads, then their atomics, issued together.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "spf_bfs_common.h"
@@ -504,9 +505,10 @@ __host__ __device__ inline LeanLayout lean_layout(uint32_t V, uint32_t nh_words,
   return l;
 }
 
-template <int MODE, int BLOCK>
+template <int MODE, int BLOCK, bool PROF>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_ell_kernel(
-    DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+    DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt,
+    unsigned long long* prof) {
   using N = Nh<MODE>;
   static_assert(N::kSingle, "single-dword next-hop fields only");
   constexpr uint32_t kBits = 32u / N::kPer;
@@ -530,6 +532,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   const uint32_t half = ring_cap / 2u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   *my_dummy = 0xFFFFFFFFu;  // only ever ORed afterwards: its fields are never zero
+  // tuning (OPENR_SPF_BFS_PROF): wave 0's cycles per phase of its first pass of every
+  // level: [0] barrier -> queue entry, [1] ELL row load, [2] level / set reads, [3] atomics,
+  // [4] append, [5] drain + barrier, [6] levels, [7] solves. A stamp follows an asm use of
+  // the value the phase waits for, so it is taken once that value has arrived.
+  const bool pf = PROF && prof != nullptr && wave == 0;
+  unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long ts = 0;
+#define OPENR_LEAN_STAMP(i, dep)                             \
+  do {                                                       \
+    if (pf) {                                                \
+      asm volatile("" ::"v"(dep));                           \
+      const long long t = (long long)__builtin_amdgcn_s_memtime(); \
+      pacc[i] += (unsigned long long)(t - ts);               \
+      ts = t;                                                \
+    }                                                        \
+  } while (0)
 
   for (uint32_t unit = blockIdx.x; unit < count;) {
     const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
@@ -567,49 +585,65 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       }
       __syncthreads();
 
-      uint32_t cur = ctl[1], L = 1, reached = 1u + cur;
+      uint32_t cur = __builtin_amdgcn_readfirstlane(ctl[1]), L = 1, reached = 1u + cur;
       bool overflow = false;  // block-uniform
+      if (pf) {
+        ts = (long long)__builtin_amdgcn_s_memtime();
+        pacc[7] += 1;
+      }
+      // one lane per frontier node, its K = 4 ELL slots; NPP nodes per wave pass
+      // (4 lanes per node, one slot each, measured no faster on strong-scaling shards:
+      // the level then waits for every wave's shorter chain at the barrier instead)
+      constexpr uint32_t K = 4u, NPP = 64u, NPB = (uint32_t)BLOCK;
+      const uint32_t lnode = lane;
+      uint32_t q = ring[half + wave * NPP + lnode];  // first pass's queue entry of level 1
       while (cur) {
         if (L + 1u >= 0xFFu) {  // next level not representable in u8
           overflow = true;
           break;
         }
         // level L: entries [0, cur) of half L & 1; level L+1 appends to the other half,
-        // counted in ctl[(L + 1) & 3] (zeroed here: last read three barriers ago)
+        // counted in ctl[(L + 1) & 3] (zeroed here: last read three barriers ago); bit 31
+        // of that count flags a level that outgrew its half
         lds_u32* const cnt = &ctl[(L + 1u) & 3u];
         if (tid == 0) ctl[(L + 2u) & 3u] = 0;
         const uint32_t rd = (L & 1u) * half, wr = half - rd;
         const uint8_t lnext = (uint8_t)(L + 1u);
-        for (uint32_t fb = wave * 64u; fb < cur; fb += BLOCK) {
-          const uint32_t idx = fb + lane;
-          const uint32_t q = ring[rd + idx];  // past the level: stale or unset, replaced below
-          const uint32_t u = idx < cur ? q : V;
+        for (uint32_t fb = wave * NPP; fb < cur; fb += NPB) {
+          const uint32_t idx = fb + lnode;
+          if (fb != wave * NPP) q = ring[rd + idx];  // the first pass's entry was read with the count
+          const uint32_t u = idx < cur ? q : V;  // past the level: the sentinel row
+          const bool st = pf && fb == 0u;        // stamps: wave 0's first pass of the level
+          if (st) OPENR_LEAN_STAMP(0, u);
           const uint4 ell = g.ellv[u];  // ellv[V] = sentinel row
+          const uint32_t vv[K] = {ell.x, ell.y, ell.z, ell.w};
+          if (st) OPENR_LEAN_STAMP(1, vv[0]);
           const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
-          const uint32_t vv[4] = {ell.x, ell.y, ell.z, ell.w};
-          // the four level reads issue together, then the four atomics
-          uint32_t lv[4], old[4];
+          // the level reads issue together, then the atomics
+          uint32_t lv[K], old[K];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) lv[j] = lvl[vv[j]];
+          for (uint32_t j = 0; j < K; ++j) lv[j] = lvl[vv[j]];
+          if (st) OPENR_LEAN_STAMP(2, lv[0] + x);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (uint32_t j = 0; j < K; ++j) {
             const uint32_t v = vv[j];
             const bool tight = lv[j] > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
             old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, x << ((v << kShl) & 31u));
           }
-          __builtin_amdgcn_sched_barrier(0);  // all four atomics in flight before their results are used
-          unsigned long long bj[4];
-          bool fresh[4];
-          uint32_t off[5];
+          __builtin_amdgcn_sched_barrier(0);  // all atomics in flight before their results are used
+          if (st) OPENR_LEAN_STAMP(3, old[0]);
+          unsigned long long bj[K];
+          bool fresh[K];
+          uint32_t off[K + 1];
           off[0] = 0;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (uint32_t j = 0; j < K; ++j) {
             // v's field was empty: this is the first arrival (a dummy field never is)
             fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;
             bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
             off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
           }
-          const uint32_t total = off[4];
+          const uint32_t total = off[K];
           if (total) {  // wave-uniform
             const uint32_t leader = (uint32_t)__builtin_amdgcn_readfirstlane(lane);
             uint32_t wbase = 0;
@@ -617,7 +651,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             const uint32_t bse = __builtin_amdgcn_readfirstlane(wbase);
             if (bse + total <= half) {  // wave-uniform: the level fits its half so far
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
+              for (uint32_t j = 0; j < K; ++j) {
                 if (fresh[j]) {
                   const uint32_t slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
@@ -628,18 +662,26 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
                 }
               }
             } else if (lane == leader) {
-              ctl[4] = 1;  // the level outgrows its half
+              lds_or(cnt, 0x80000000u);  // the level outgrows its half
             }
           }
+          if (st) OPENR_LEAN_STAMP(4, total);
         }
         lds_barrier();
-        cur = *cnt;
-        reached += cur;
+        // the next level's count and its first pass's queue entry, read together
+        const uint32_t c = __builtin_amdgcn_readfirstlane(*cnt);
+        q = ring[wr + wave * NPP + lnode];
+        if (pf) {
+          OPENR_LEAN_STAMP(5, c);
+          pacc[6] += 1;
+        }
         ++L;
-        if (ctl[4]) {  // uniform after the barrier
+        if (c >> 31) {  // uniform after the barrier
           overflow = true;
           break;
         }
+        cur = c;
+        reached += cur;
         if (reached == V) break;  // every node reached: the newest level cannot expand tightly
       }
       if (overflow) {
@@ -653,6 +695,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
     __syncthreads();
     unit = ctl[7];
   }
+#undef OPENR_LEAN_STAMP
+  if (pf && lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&prof[i], pacc[i]);
   retire_workgroup(ctr, nullptr);
 }
 
@@ -725,7 +770,8 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
                            uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
   const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
-  auto k = bfs_ell_kernel<MODE, BLOCK>;
+  const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
+  auto k = want_prof ? bfs_ell_kernel<MODE, BLOCK, true> : bfs_ell_kernel<MODE, BLOCK, false>;
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
@@ -734,8 +780,28 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     info->grid = grid;
     info->kernel = "bfs_ell_kernel<halves,u8>";
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, ctr, ovf_count, nt_stores());
-  return hipGetLastError();
+  // tuning aid: per-phase cycle sums of the level loop, printed after the launch
+  static unsigned long long* prof_buf = nullptr;
+  unsigned long long* prof = nullptr;
+  if (want_prof) {
+    if (!prof_buf && hipMalloc(&prof_buf, 8 * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
+    prof = prof_buf;
+    if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, ctr, ovf_count, nt_stores(), prof);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && prof) {
+    unsigned long long h[8];
+    if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess) {
+      const double lv = h[6] ? (double)h[6] : 1.0;
+      std::fprintf(stderr,
+                   "bfs_ell: block=%d grid=%u n=%u solves=%llu levels/solve=%.1f | cycles/level: entry %.0f row %.0f "
+                   "reads %.0f atomics %.0f append %.0f barrier %.0f\n",
+                   BLOCK, grid, a.n, h[7], h[7] ? lv / (double)h[7] : 0.0, h[0] / lv, h[1] / lv, h[2] / lv, h[3] / lv,
+                   h[4] / lv, h[5] / lv);
+    }
+  }
+  return e;
 }
 
 template <int MODE, int BLOCK, int ELLM, bool SLICED>
