@@ -326,10 +326,15 @@ std::vector<std::shared_ptr<Link>> LinkState::orderedLinksFromNode(const std::st
 
 bool LinkState::updateNodeOverloaded(const std::string& nodeName, bool isOverloaded, LinkStateMetric holdUpTtl,
                                      LinkStateMetric holdDownTtl) {
-  markMirrorDirty();
   auto it = nodeOverloads_.find(nodeName);
-  if (it != nodeOverloads_.end()) return it->second.updateValue(isOverloaded, holdUpTtl, holdDownTtl);
+  if (it != nodeOverloads_.end()) {
+    // the mirror carries the effective (hold-aware) value: rebuild it only when that changed
+    const bool changed = it->second.updateValue(isOverloaded, holdUpTtl, holdDownTtl);
+    if (changed) markMirrorDirty();
+    return changed;
+  }
   nodeOverloads_.emplace(nodeName, HoldableValue<bool>{isOverloaded});
+  markMirrorDirty();
   return false;  // a new node is not a topology change
 }
 
@@ -404,7 +409,9 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
                                                               LinkStateMetric holdDownTtl) {
   LinkStateChange change;
   const std::string nodeName = db.thisNodeName;
-  markMirrorDirty();
+  // the CSR mirror changes only with the topology (addLink / removeLink mark it, and so
+  // does an effective metric / overload / up-down change below); a re-advertisement that
+  // changes nothing, or only labels and next-hop addresses, keeps mirror and device graph
 
   thrift::AdjacencyDatabase& stored = adjacencyDatabases_[nodeName];
   thrift::AdjacencyDatabase prior(std::move(stored));
@@ -463,6 +470,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
   if (change.topologyChanged) {
     spfResults_.clear();
     kthPathResults_.clear();
+    markMirrorDirty();
   }
   return change;
 }

@@ -312,6 +312,8 @@ class LinkState {
     bool metricsPositive = true;  // every usable metric in [1, 2^31-1]: fast kernels
   };
   const CsrMirror& csrMirror() const;
+  // process-wide id of the mirror csrMirror() last built (tests: a rebuild changes it)
+  uint64_t mirrorGeneration() const { return mirrorGeneration_; }
 
  private:
   const std::string area_;

@@ -332,6 +332,38 @@ TEST_CPU(LinkStateTest_HoldUpAndMirror) {
   EXPECT_EQ(4u, m2.metric[m2.rowPtr[m2.id.at("b")]]);
 }
 
+// The mirror (and so the device graph) is rebuilt only when the effective topology
+// changes: a re-advertised database, or one that changes only adjacency labels, keeps it
+// (ADVICE r1); a metric change or a new node rebuilds it.
+TEST_CPU(LinkStateTest_MirrorRebuiltOnlyOnTopologyChange) {
+  LinkState ls(kArea);
+  ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 1), 0, 0);
+  ls.updateAdjacencyDatabase(createAdjDb("b", {createAdjacency("a", "b/a", "a/b", 4)}, 2), 0, 0);
+  ls.csrMirror();
+  const uint64_t g0 = ls.mirrorGeneration();
+  auto ch = ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 1), 0, 0);
+  EXPECT_FALSE(ch.topologyChanged);
+  ls.csrMirror();
+  EXPECT_EQ(g0, ls.mirrorGeneration());
+  auto relabel = createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 1);
+  relabel.adjacencies[0].adjLabel = 777;
+  ch = ls.updateAdjacencyDatabase(relabel, 0, 0);
+  EXPECT_FALSE(ch.topologyChanged);
+  EXPECT_TRUE(ch.linkAttributesChanged);
+  ls.csrMirror();
+  EXPECT_EQ(g0, ls.mirrorGeneration());
+  ch = ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 9)}, 1), 0, 0);
+  EXPECT_TRUE(ch.topologyChanged);
+  auto const& m = ls.csrMirror();
+  EXPECT_TRUE(ls.mirrorGeneration() != g0);
+  EXPECT_EQ(9u, m.metric[m.rowPtr[m.id.at("a")]]);
+  const uint64_t g1 = ls.mirrorGeneration();
+  ls.updateAdjacencyDatabase(createAdjDb("c", {}, 3), 0, 0);  // isolated new node
+  auto const& m2 = ls.csrMirror();
+  EXPECT_TRUE(ls.mirrorGeneration() != g1);
+  EXPECT_EQ(3u, (unsigned)m2.names.size());
+}
+
 // ParallelAdjRingTopologyFixture adjacencies (DecisionTest.cpp:3146-3203)
 static LinkState parallelRing() {
   LinkState ls(kArea);
