@@ -1,4 +1,3 @@
-# ELL-row locality probe: G100 all-sources kernel time under node renumberings
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u scripts/perm_probe.py > gpurun_out/perm_probe.log 2>&1; rc=$?; grep order gpurun_out/perm_probe.log; exit $rc
+timeout -k 10 300 python -u scripts/sweep.py --topology grid100 --variants "XS=0;XS=1" --rounds 8 > gpurun_out/xs_sweep.log 2>&1; rc=$?; grep -E "variant|Error|error" gpurun_out/xs_sweep.log | cut -c1-120; exit $rc
