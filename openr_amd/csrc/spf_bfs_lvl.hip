@@ -816,7 +816,10 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
     // lean pass: its queue halves must hold the widest sampled level (else the generic ring)
     const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
-    if (!has_ign && !a.tight && ring_cap / 2u >= need1 && env_u32("OPENR_SPF_BFS_LEAN", 1u, 0u, 1u))
+    // (OPENR_SPF_LEAN_FORCE=1, tests: also when the halves are too small, so wide levels
+    // take the overflow -> u16 re-run path)
+    const bool fits = ring_cap / 2u >= need1 || env_u32("OPENR_SPF_LEAN_FORCE", 0u, 0u, 1u) != 0u;
+    if (!has_ign && !a.tight && fits && env_u32("OPENR_SPF_BFS_LEAN", 1u, 0u, 1u))
       err = launch_lvl_lean<MODE, BLOCK>(g, a, cost, ring_cap, blk, blk + 4, num_cus, s, info);
     else
       err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, false,

@@ -251,6 +251,40 @@ def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, full):
     check_against_oracle(eng, g, srcs, True, ignore=ignore)
 
 
+def test_lean_pass_depth_overflow(eng, monkeypatch, capfd, bfs_family):
+    """The lean ELL pass (graphs with <= 4 edges per row too big for the full-order queue,
+    sampled depth under the u8 limit): a 70 x 70 grid plus a separate 300-node chain whose
+    nodes no depth sample starts from. Chain sources run deeper than 253 levels: the lean
+    pass flags them at level 254 and the u16 full-order pass re-runs them. (With
+    OPENR_SPF_BFS_PROF the lean pass reports itself on stderr: proof that it ran.)"""
+    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    n, tail = 70, 300
+    names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)] + [f"z{i:03d}" for i in range(tail)]
+    links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
+    links += [(r * n + c, (r + 1) * n + c) for r in range(n - 1) for c in range(n)]
+    links += [(n * n + i, n * n + i + 1) for i in range(tail - 1)]
+    g = T.csr_from_links(names, np.array(links))
+    srcs = [0, n * n - 1, n * n, n * n + tail - 1, n * n + 10, 35 * n + 35]
+    dist, _ = check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
+    assert int(dist[2, n * n + tail - 1]) == tail - 1
+    assert ("bfs_ell:" in capfd.readouterr().err) == (bfs_family[0] == "lvl")
+
+
+def test_lean_pass_half_overflow(eng, monkeypatch, capfd, bfs_family):
+    """A level wider than a queue half in the lean pass (forced onto a graph whose sampled
+    width would otherwise keep it on the generic ring): the solve is flagged and re-run."""
+    monkeypatch.setenv("OPENR_SPF_LEAN_FORCE", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    chain, depth = 100, 11
+    names = [f"c{i:03d}" for i in range(chain)] + [f"t{i:05d}" for i in range(1, 2 ** (depth + 1) - 1)]
+    links = [(i, i + 1) for i in range(chain - 1)]
+    tid = lambda i: chain - 1 if i == 0 else chain - 1 + i  # heap index -> node id (root = last chain node)
+    links += [(tid(i), tid(c)) for i in range(2 ** depth - 1) for c in (2 * i + 1, 2 * i + 2)]
+    g = T.csr_from_links(names, np.array(links))
+    check_against_oracle(eng, g, [0, 50, chain - 1, chain + 5, len(names) - 1], True, check_pathlinks=False)
+    assert ("bfs_ell:" in capfd.readouterr().err) == (bfs_family[0] == "lvl")
+
+
 def test_ring_overflow_rerun_list(eng, monkeypatch):
     """A ring too small for the frontier (forced: levels of ~1000 nodes on a random
     expander) flags every solve; the full-order pass re-runs them from the list."""
