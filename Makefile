@@ -21,7 +21,7 @@ ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/%.o,$(ENGINE_SRCS))
 
 HOST := $(LIBDIR)/libopenr_decision.so
 HOST_SRCS := $(CSRC)/host/LinkState.cpp $(CSRC)/host/Decision.cpp $(CSRC)/host/AdjDbCodec.cpp $(CSRC)/host/adjdb_capi.cpp $(CSRC)/host/wan_gen.cpp
-HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h $(CSRC)/host/AdjDbCodec.h include/openr_spf.h include/openr_adjdb.h include/openr_topogen.h include/openr_routes.h
+HOST_HDRS := $(CSRC)/host/LinkState.h $(CSRC)/host/Decision.h $(CSRC)/host/HostParallel.h $(CSRC)/host/AdjDbCodec.h include/openr_spf.h include/openr_adjdb.h include/openr_topogen.h include/openr_routes.h
 CXX ?= g++
 CC ?= gcc
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
@@ -50,7 +50,7 @@ $(ENGINE): $(ENGINE_OBJS) $(ENGINE_SRCS) $(ENGINE_HDRS)
 $(HOST): $(HOST_SRCS) $(HOST_HDRS) $(ENGINE)
 	$(CXX) $(CXXFLAGS) -shared -o $@ $(HOST_SRCS) \
 	  -DOPENR_DECISION_BUILD_ID="\"$(call build_id,$(HOST_SRCS) $(HOST_HDRS))\"" \
-	  -L$(LIBDIR) -lopenr_spf -Wl,-rpath,'$$ORIGIN'
+	  -L$(LIBDIR) -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN'
 
 # C++ tests of the host mirror (oracle linked as the checker)
 $(CPPTEST): $(CPPTEST_SRCS) $(HOST)

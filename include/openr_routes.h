@@ -36,8 +36,9 @@ typedef struct {
   uint64_t weighted_nexthops; /* of them, weight > 1 (UCMP) */
   uint64_t checksum;          /* order-independent hash of (node, prefix, nexthop addr, ifName,
                                  neighbour, metric, weight) */
-  double ms_build;            /* SPF prefetch + route build, host wall time */
-  double ms_policy;           /* RibPolicy application */
+  double ms_build;            /* SPF prefetch + route build (+ tally, free), host wall time less ms_policy */
+  double ms_policy;           /* RibPolicy application: its thread time over the host workers
+                                 (OPENR_HOST_THREADS) — its share of the wall time */
 } openr_routes_stats_t;
 
 /* Route DBs of node_ids[0..n) (graph node ids). neighbor_weight (nullable) [V] by graph

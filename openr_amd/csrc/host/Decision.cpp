@@ -3,6 +3,8 @@
 // it reads come from the engine through LinkState (one batched prefetch per build).
 #include "Decision.h"
 
+#include "HostParallel.h"
+
 #include <algorithm>
 #include <limits>
 #include <list>
@@ -135,23 +137,81 @@ void SpfSolver::prefetch(const std::string& me, std::unordered_map<std::string, 
 std::vector<std::optional<DecisionRouteDb>> SpfSolver::buildRouteDbs(
     const std::vector<std::string>& nodes, std::unordered_map<std::string, LinkState> const& als,
     PrefixState const& prefixState) {
+  std::vector<std::optional<DecisionRouteDb>> out(nodes.size());
+  buildRouteDbs(nodes, als, prefixState, [&](size_t i, std::optional<DecisionRouteDb>& db) { out[i] = std::move(db); });
+  return out;
+}
+
+void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
+                              std::unordered_map<std::string, LinkState> const& als, PrefixState const& prefixState,
+                              const std::function<void(size_t, std::optional<DecisionRouteDb>&)>& sink) {
+  // KSP2 builds memoise k-th paths and run link-ignoring SPFs as they go (getKthPaths):
+  // those stay on this thread. Every other build only reads memoised SPFs once the
+  // prefetch below has run, so nodes are built by independent solver copies.
+  bool ksp2 = false;
+  for (auto const& [_, entries] : prefixState.prefixes()) {
+    for (auto const& [na, e] : entries) ksp2 |= e.forwardingAlgorithm == thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP;
+    if (ksp2) break;
+  }
+  const unsigned workers = ksp2 ? 1u : parallelWorkers(nodes.size(), 1);
+  auto known = [&](const std::string& n) {
+    for (auto const& [_, ls] : als)
+      if (ls.hasNode(n)) return true;
+    return false;
+  };
   for (auto const& [area, ls] : als) {  // one all-sources batch covers every node and its neighbours
     std::vector<std::string> present;
     for (auto const& n : nodes)
-      if (ls.hasNode(n)) present.push_back(n);
+      // a parallel build also memoises the self-only result of a node this area lacks but
+      // another has (createRouteForPrefix and the label routes read it in every area),
+      // which the sequential build adds on demand
+      if (ls.hasNode(n) || (workers > 1 && known(n))) present.push_back(n);
     if (computeLfaPaths_) {
       std::set<std::string> more(present.begin(), present.end());
       for (auto const& n : present)
-        for (auto const& link : ls.linksFromNode(n))
-          if (link->isUp()) more.insert(link->getOtherNodeName(n));
+        if (ls.hasNode(n))
+          for (auto const& link : ls.linksFromNode(n))
+            if (link->isUp()) more.insert(link->getOtherNodeName(n));
       present.assign(more.begin(), more.end());
     }
     ls.prefetchSpfResults(present, true);
   }
-  std::vector<std::optional<DecisionRouteDb>> out;
-  out.reserve(nodes.size());
-  for (auto const& n : nodes) out.push_back(buildRouteDb(n, als, prefixState));
-  return out;
+  if (workers <= 1) {
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      auto db = buildRouteDb(nodes[i], als, prefixState);
+      sink(i, db);
+    }
+    return;
+  }
+  std::vector<SpfSolver> solvers(workers, *this);  // config + static MPLS routes
+  for (auto& s : solvers) {
+    s.counters_ = DecisionCounters{};
+    s.bestRoutesCache_.clear();
+  }
+  // the sequential loop leaves the cache of the last node some area knows (an unknown
+  // node's build returns before touching it)
+  size_t last = nodes.size();
+  for (size_t i = nodes.size(); i-- > 0;)
+    if (known(nodes[i])) {
+      last = i;
+      break;
+    }
+  parallelFor(nodes.size(), 1, workers, [&](unsigned w, size_t i) {
+    auto db = solvers[w].buildRouteDb(nodes[i], als, prefixState);
+    if (i == last) bestRoutesCache_ = solvers[w].bestRoutesCache_;
+    sink(i, db);
+  });
+  for (auto const& s : solvers) {
+    auto const& c = s.counters_;
+    counters_.route_build_runs += c.route_build_runs;
+    counters_.get_route_for_prefix += c.get_route_for_prefix;
+    counters_.no_route_to_prefix += c.no_route_to_prefix;
+    counters_.skipped_unicast_route += c.skipped_unicast_route;
+    counters_.skipped_mpls_route += c.skipped_mpls_route;
+    counters_.duplicate_node_label += c.duplicate_node_label;
+    counters_.no_route_to_label += c.no_route_to_label;
+    counters_.incompatible_forwarding_type += c.incompatible_forwarding_type;
+  }
 }
 
 // Decision.cpp:568-734

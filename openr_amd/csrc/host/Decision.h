@@ -18,8 +18,10 @@
 // hold timers (Decision event plumbing), thrift serialization.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <optional>
 #include <set>
@@ -212,6 +214,14 @@ class SpfSolver {
       const std::vector<std::string>& nodes, std::unordered_map<std::string, LinkState> const& areaLinkStates,
       PrefixState const& prefixState);
 
+  // Streaming form: sink(i, db) runs on the host worker that built entry i (entries in no
+  // particular order; HostParallel.h) and the DB is destroyed there when the sink returns,
+  // so a consumer that applies policy or programs routes per node touches each DB while
+  // it is cache-hot and frees it into the allocating thread's arena.
+  void buildRouteDbs(const std::vector<std::string>& nodes,
+                     std::unordered_map<std::string, LinkState> const& areaLinkStates, PrefixState const& prefixState,
+                     const std::function<void(size_t, std::optional<DecisionRouteDb>&)>& sink);
+
   std::optional<RibUnicastEntry> createRouteForPrefix(const std::string& myNodeName,
                                                       std::unordered_map<std::string, LinkState> const& areaLinkStates,
                                                       PrefixState const& prefixState, thrift::IpPrefix const& prefix);
@@ -279,7 +289,7 @@ struct RibPolicyStatement {
 // fb303 decision.rib_policy.* counters (process-wide, like fb303::fbData)
 struct RibPolicyCounters {
   static RibPolicyCounters& get();
-  uint64_t invalidatedRoutes = 0;  // decision.rib_policy.invalidated_routes (RibPolicy.cpp:98-104)
+  std::atomic<uint64_t> invalidatedRoutes{0};  // decision.rib_policy.invalidated_routes (RibPolicy.cpp:98-104)
 };
 
 class RibPolicy {

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <sstream>
 
+#include "HostParallel.h"
 #include "../../../include/openr_spf.h"
 
 namespace openr {
@@ -689,10 +690,12 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
     }
     // materialise SpfResult: nextHops from the bitsets, pathLinks from tight edges
     // ordered by the predecessor's settle order ((dist, name), or the exact kernel's pop
-    // index) then row position.
-    std::vector<uint32_t> nbrs(V ? V : 1);
-    std::vector<uint32_t> order;
-    for (size_t k = 0; k < n; ++k) {
+    // index) then row position. Sources are independent: one host worker each.
+    const unsigned workers = parallelWorkers(n, 8);
+    std::vector<std::vector<uint32_t>> nbrsW(workers, std::vector<uint32_t>(V ? V : 1)), orderW(workers);
+    parallelFor(n, 8, workers, [&](unsigned w, size_t k) {
+      auto& nbrs = nbrsW[w];
+      auto& order = orderW[w];
       const uint32_t src = ids[k];
       uint32_t nn = 0;
       SpfEngineHandle::check(openr_spf_neighbor_map(engine_->ctx(), src, nbrs.data(), (uint32_t)nbrs.size(), &nn),
@@ -726,7 +729,7 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
         const uint32_t u = m.edgeOwner[e], v = m.col[e];
         res.at(m.names[v]).addPath(m.links[m.linkId[e]], m.names[u]);
       }
-    }
+    });
   }
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   SpfCounters::get().addSpfRun(ms, srcs.size());  // decision.spf_runs counts logical SPFs

@@ -2,6 +2,8 @@
 #include <cerrno>
 #include <chrono>
 #include <unordered_map>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -12,6 +14,7 @@
 #include "../../../include/openr_routes.h"
 #include "AdjDbCodec.h"
 #include "Decision.h"
+#include "HostParallel.h"
 
 struct openr_adjdb_batch {
   std::vector<openr::thrift::AdjacencyDatabase> dbs;
@@ -319,9 +322,7 @@ extern "C" int openr_routes_build(openr_adjdb_graph* g, const uint32_t* node_ids
     nodes.reserve(n);
     for (uint32_t i = 0; i < n; ++i) nodes.push_back(m.names[node_ids[i]]);
     openr::SpfSolver solver(nodes[0], (flags & OPENR_ROUTES_V4) != 0, (flags & OPENR_ROUTES_LFA) != 0);
-    const auto t0 = clock::now();
-    auto dbs = solver.buildRouteDbs(nodes, g->als, *g->prefixes);
-    const auto t1 = clock::now();
+    std::unique_ptr<openr::RibPolicy> policy;
     if (flags & OPENR_ROUTES_UCMP) {  // RibPolicy set_weight over every route (Decision.cpp applies it per rebuild)
       openr::RibPolicyStatement st;
       st.name = "ucmp";
@@ -330,33 +331,50 @@ extern "C" int openr_routes_build(openr_adjdb_graph* g, const uint32_t* node_ids
       if (neighbor_weight)
         for (uint32_t v = 0; v < V; ++v)
           if (neighbor_weight[v] > 0) st.neighborToWeight[m.names[v]] = neighbor_weight[v];
-      openr::RibPolicy policy({st});
-      for (auto& db : dbs)
-        if (db) policy.applyPolicy(db->unicastRoutes);
+      policy = std::make_unique<openr::RibPolicy>(std::vector<openr::RibPolicyStatement>{st});
     }
-    const auto t2 = clock::now();
-    uint64_t sum = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (!dbs[i]) continue;
+    // per node: build, policy, checksum, free — on the worker that built it (streaming
+    // buildRouteDbs), while the DB is cache-hot
+    std::vector<openr_routes_stats_t> per(n, openr_routes_stats_t{});
+    const auto t0 = clock::now();
+    solver.buildRouteDbs(nodes, g->als, *g->prefixes, [&](size_t i, std::optional<openr::DecisionRouteDb>& db) {
+      if (!db) return;
+      auto& o = per[i];
+      if (policy) {
+        const auto p0 = clock::now();
+        policy->applyPolicy(db->unicastRoutes);
+        o.ms_policy = std::chrono::duration<double, std::milli>(clock::now() - p0).count();
+      }
       const uint64_t hn = hashStr(0xcbf29ce484222325ULL, nodes[i]);
-      out->unicast_routes += dbs[i]->unicastRoutes.size();
-      out->mpls_routes += dbs[i]->mplsRoutes.size();
-      for (auto const& [p, route] : dbs[i]->unicastRoutes) {
+      o.unicast_routes = db->unicastRoutes.size();
+      o.mpls_routes = db->mplsRoutes.size();
+      for (auto const& [p, route] : db->unicastRoutes) {
         const uint64_t hp = hashStr(hn, p.addr) ^ (uint64_t)p.prefixLength;
         for (auto const& nh : route.nexthops) {
-          ++out->nexthops;
-          out->weighted_nexthops += nh.weight > 1;
+          ++o.nexthops;
+          o.weighted_nexthops += nh.weight > 1;
           uint64_t h = hashStr(hp, nh.address.addr);
           h = hashStr(h, nh.address.ifName.value_or(""));
           h = hashStr(h, nh.neighborNodeName.value_or(""));
           h = mix64(h ^ ((uint64_t)(uint32_t)nh.metric << 32) ^ (uint32_t)nh.weight);
-          sum += h;  // order-independent
+          o.checksum += h;  // order-independent
         }
       }
+    });
+    const double ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
+    double policyMs = 0;
+    for (auto const& o : per) {
+      out->unicast_routes += o.unicast_routes;
+      out->mpls_routes += o.mpls_routes;
+      out->nexthops += o.nexthops;
+      out->weighted_nexthops += o.weighted_nexthops;
+      out->checksum += o.checksum;
+      policyMs += o.ms_policy;
     }
-    out->checksum = sum;
-    out->ms_build = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    out->ms_policy = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    // the policy's share of the wall time: its thread time over the workers that ran
+    const unsigned workers = openr::parallelWorkers(n, 1);
+    out->ms_policy = policyMs / workers;
+    out->ms_build = ms - out->ms_policy;
     return 0;
   });
 }

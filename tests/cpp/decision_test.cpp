@@ -858,7 +858,7 @@ struct Wan {
   PrefixState ps;
   std::vector<std::string> names;
   std::vector<thrift::IpPrefix> prefix;
-  Wan(uint32_t n, uint32_t L, uint32_t par, uint64_t seed) {
+  Wan(uint32_t n, uint32_t L, uint32_t par, uint64_t seed, bool nodeLabels = false) {
     std::vector<uint32_t> ends(2 * (L + par)), muv(L + par), mvu(L + par);
     EXPECT_EQ(openr_topogen_wan(n, L, 64, seed, par, ends.data(), muv.data(), mvu.data()), 0);
     std::vector<std::vector<thrift::Adjacency>> adjs(n);
@@ -877,7 +877,7 @@ struct Wan {
     als.emplace(kDefaultArea, LinkState(kDefaultArea));
     for (uint32_t i = 0; i < n; ++i) {
       names.push_back(nm(i));
-      als.at(kDefaultArea).updateAdjacencyDatabase(createAdjDb(nm(i), adjs[i], 0));
+      als.at(kDefaultArea).updateAdjacencyDatabase(createAdjDb(nm(i), adjs[i], nodeLabels ? 100 + (int32_t)i : 0));
       prefix.push_back(pfx("fd00::" + std::to_string(i) + "/128"));
       ps.updatePrefix(nm(i), kDefaultArea, createPrefixEntry(prefix.back()));
     }
@@ -1011,6 +1011,72 @@ TEST_GPU(WanUcmpRoutes_vs_Oracle_Config4) {  // the config-4 WAN (1000 nodes, 30
   for (uint32_t i = 0; i < 1000; i += 63) sample.push_back(i);
   wanUcmpRoutes(w, sample, false);
   wanUcmpRoutes(w, sample, true);
+}
+
+// buildRouteDbs on host worker threads (HostParallel.h) against the one-thread loop: the
+// same route DBs (unicast + node-label MPLS routes, LFA on), counters and best-route
+// cache; an unknown node and a repeated node in the list.
+std::string flatten(const std::optional<DecisionRouteDb>& db) {
+  if (!db) return "none";
+  std::string s;
+  auto nhs = [&](const NextHopSet& set) {
+    for (auto const& nh : set)
+      s += nh.address.addr + "%" + nh.address.ifName.value_or("") + "@" + nh.neighborNodeName.value_or("") + "#" +
+           std::to_string(nh.metric) + "w" + std::to_string(nh.weight) +
+           (nh.mplsAction ? "a" + std::to_string((int)nh.mplsAction->action) : "") + ";";
+  };
+  for (auto const& [p, r] : db->unicastRoutes) {
+    s += p.toString() + "[" + r.bestArea + "]";
+    nhs(r.nexthops);
+    s += "\n";
+  }
+  for (auto const& [l, r] : db->mplsRoutes) {
+    s += std::to_string(l) + ":";
+    nhs(r.nexthops);
+    s += "\n";
+  }
+  return s;
+}
+
+TEST_GPU(BuildRouteDbs_HostThreads_MatchSequential) {
+  Wan w(300, 900, 10, 5, true);
+  std::vector<std::string> nodes;
+  for (uint32_t i = 0; i < 300; i += 2) nodes.push_back(w.names[i]);
+  nodes.push_back("not-a-node");
+  nodes.push_back(w.names[7]);
+  nodes.push_back("not-a-node-either");  // last entry unknown: the cache is the last known node's
+  auto run = [&](const char* threads) {
+    setenv("OPENR_HOST_THREADS", threads, 1);
+    Wan fresh(300, 900, 10, 5, true);  // cold SPF memo per run
+    SpfSolver solver(fresh.names[0], false, true);
+    auto dbs = solver.buildRouteDbs(nodes, fresh.als, fresh.ps);
+    std::vector<std::string> flat;
+    size_t mpls = 0;
+    for (auto const& db : dbs) {
+      flat.push_back(flatten(db));
+      if (db) mpls += db->mplsRoutes.size();
+    }
+    std::string cache;
+    for (auto const& [p, b] : solver.getBestRoutesCache()) {
+      cache += p.toString() + (b.success ? "+" : "-") + b.bestNodeArea.first + ":";
+      for (auto const& na : b.allNodeAreas) cache += na.first + ",";
+    }
+    auto const& c = solver.counters();
+    std::vector<uint64_t> cnt{c.route_build_runs,     c.get_route_for_prefix, c.no_route_to_prefix,
+                              c.skipped_unicast_route, c.skipped_mpls_route,   c.duplicate_node_label,
+                              c.no_route_to_label,     c.incompatible_forwarding_type};
+    return std::make_tuple(flat, cache, cnt, mpls);
+  };
+  const auto seq = run("1");
+  const auto par = run("6");
+  unsetenv("OPENR_HOST_THREADS");
+  EXPECT_EQ(std::get<0>(seq).size(), nodes.size());
+  EXPECT_TRUE(std::get<0>(seq) == std::get<0>(par));
+  EXPECT_TRUE(std::get<0>(seq)[nodes.size() - 3] == "none");
+  EXPECT_TRUE(!std::get<1>(seq).empty() && std::get<1>(seq) == std::get<1>(par));
+  EXPECT_TRUE(std::get<2>(seq) == std::get<2>(par));
+  EXPECT_EQ(std::get<2>(seq)[0], (uint64_t)nodes.size() - 2);
+  EXPECT_TRUE(std::get<3>(seq) > 0);  // node-label routes present
 }
 
 // --- RibPolicyTest.cpp:176-301 (RibPolicy.ApplyAction / ApplyPolicy) -----------------
