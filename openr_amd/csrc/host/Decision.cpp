@@ -224,6 +224,21 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   counters_.route_build_runs++;
   prefetch(myNodeName, als);
 
+  // KSP2 prefixes: every destination's first and second paths from here in one device
+  // launch per area (LinkState::prefetchKthPaths stages them; selectBestPathsKsp2's
+  // getKthPaths calls then take them in the order and with the counts of the reference)
+  std::unordered_map<std::string, std::vector<std::string>> ksp2Dests;
+  for (auto const& [_, entries] : prefixState.prefixes()) {
+    bool ksp2 = false;
+    for (auto const& [na, e] : entries) ksp2 |= e.forwardingAlgorithm == thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP;
+    if (ksp2)
+      for (auto const& [na, e] : entries) ksp2Dests[na.second].push_back(na.first);
+  }
+  for (auto const& [area, dests] : ksp2Dests) {
+    auto ls = als.find(area);
+    if (ls != als.end() && ls->second.hasNode(myNodeName)) ls->second.prefetchKthPaths(myNodeName, dests);
+  }
+
   DecisionRouteDb routeDb;
   bestRoutesCache_.clear();
   for (auto const& [prefix, _] : prefixState.prefixes())

@@ -349,8 +349,7 @@ LinkState::LinkStateChange LinkState::decrementHolds() {
   for (auto& link : allLinks_) change.topologyChanged |= link->decrementHolds();
   for (auto& kv : nodeOverloads_) change.topologyChanged |= kv.second.decrementTtl();
   if (change.topologyChanged) {
-    spfResults_.clear();
-    kthPathResults_.clear();
+    clearMemos();
     markMirrorDirty();
   }
   return change;
@@ -469,8 +468,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
     ++oi;
   }
   if (change.topologyChanged) {
-    spfResults_.clear();
-    kthPathResults_.clear();
+    clearMemos();
     markMirrorDirty();
   }
   return change;
@@ -483,8 +481,7 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string&
     removeNode(nodeName);
     adjacencyDatabases_.erase(it);
     ifIndex_.erase(nodeName);
-    spfResults_.clear();
-    kthPathResults_.clear();
+    clearMemos();
     markMirrorDirty();
     change.topologyChanged = true;
   }
@@ -512,6 +509,22 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(const std::string& sr
   const auto key = std::make_tuple(src, dest, k);
   auto it = kthPathResults_.find(key);
   if (it != kthPathResults_.end()) return it->second;
+  if (k <= 2) {  // prefetched: replay the memo and counter effects of the call sequence below
+    auto st = kthStaged_.find(std::make_pair(src, dest));
+    if (st != kthStaged_.end()) {
+      if (k == 1) {
+        getSpfResult(src, true);
+        return kthPathResults_.emplace(key, st->second.k1).first->second;
+      }
+      bool anyLink = false;
+      for (auto const& path : getKthPaths(src, dest, 1)) anyLink |= !path.empty();
+      if (anyLink) SpfCounters::get().addSpfRun(st->second.ms);  // runSpf(src, true, ignore)
+      else getSpfResult(src, true);
+      auto paths = std::move(st->second.k2);
+      kthStaged_.erase(st);
+      return kthPathResults_.emplace(key, std::move(paths)).first->second;
+    }
+  }
   LinkSet ignore;
   for (size_t i = 1; i < k; ++i)
     for (auto const& path : getKthPaths(src, dest, i))
@@ -606,6 +619,74 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   return mirror_;
 }
 
+// the engine holds this LinkState's current mirror (uploaded on first use after a rebuild)
+void LinkState::ensureEngineGraph() const {
+  const CsrMirror& m = csrMirror();
+  if (!engine_) engine_ = std::make_shared<SpfEngineHandle>();
+  if (engine_->owner == this && engine_->generation == mirrorGeneration_) return;
+  openr_spf_graph g{};
+  g.num_nodes = (uint32_t)m.names.size();
+  g.num_dir_edges = (uint32_t)m.col.size();
+  g.num_links = (uint32_t)m.links.size();
+  g.row_ptr = m.rowPtr.data();
+  g.col = m.col.data();
+  g.metric = m.metric.data();
+  g.link_id = m.linkId.data();
+  g.edge_up = m.edgeUp.data();
+  g.node_overloaded = m.overloaded.data();
+  g.name_rank = m.nameRank.data();
+  SpfEngineHandle::check(openr_spf_set_graph(engine_->ctx(), &g), "openr_spf_set_graph");
+  engine_->owner = this;
+  engine_->generation = mirrorGeneration_;
+}
+
+void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::string>& dests) const {
+  if (const char* e = std::getenv("OPENR_KSP2_PREFETCH"))  // 0: the call-by-call path (tests)
+    if (std::atoi(e) == 0) return;
+  const CsrMirror& m = csrMirror();
+  if (!m.metricsPositive) return;  // the device tracer needs metrics in [1, 2^31-1]
+  auto s = m.id.find(src);
+  if (s == m.id.end()) return;
+  std::vector<uint32_t> dst;
+  for (auto const& d : dests) {
+    auto it = m.id.find(d);
+    if (it == m.id.end() || d == src || kthPathResults_.count(std::make_tuple(src, d, size_t(2))) ||
+        kthStaged_.count(std::make_pair(src, d)))
+      continue;
+    dst.push_back(it->second);
+  }
+  std::sort(dst.begin(), dst.end());
+  dst.erase(std::unique(dst.begin(), dst.end()), dst.end());
+  if (dst.empty()) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  ensureEngineGraph();
+  const uint32_t n = (uint32_t)dst.size(), cap = 512;  // tokens per pair: [n_paths, (len, edges..)..]
+  std::vector<uint32_t> srcs(n, s->second), tok1((size_t)n * cap), tok2((size_t)n * cap);
+  for (uint32_t i = 0; i < n; ++i) tok1[(size_t)i * cap] = tok2[(size_t)i * cap] = 0xFFFFFFFFu;
+  const int rc = openr_spf_ksp2(engine_->ctx(), srcs.data(), dst.data(), n, cap, tok1.data(), tok2.data());
+  if (rc == OPENR_SPF_ENOTSUP) return;
+  if (rc != OPENR_SPF_E2BIG) SpfEngineHandle::check(rc, "openr_spf_ksp2");  // E2BIG: overflowed rows stay unmarked
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / n;
+  auto decode = [&](const uint32_t* row, std::vector<Path>& out) {
+    if (row[0] == 0xFFFFFFFFu) return false;
+    size_t at = 1;
+    for (uint32_t p = 0; p < row[0]; ++p) {
+      const uint32_t len = row[at++];
+      Path path;
+      path.reserve(len);
+      for (uint32_t j = 0; j < len; ++j) path.push_back(m.links[m.linkId[row[at++]]]);
+      out.push_back(std::move(path));
+    }
+    return true;
+  };
+  for (uint32_t i = 0; i < n; ++i) {
+    StagedKsp2 st;
+    st.ms = ms;
+    if (!decode(&tok1[(size_t)i * cap], st.k1) || !decode(&tok2[(size_t)i * cap], st.k2)) continue;
+    kthStaged_.emplace(std::make_pair(src, m.names[dst[i]]), std::move(st));
+  }
+}
+
 std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,
                                                          const std::vector<const LinkSet*>& ignores) const {
   const auto t0 = std::chrono::steady_clock::now();
@@ -624,23 +705,7 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
     }
   }
   if (!ids.empty()) {
-    if (!engine_) engine_ = std::make_shared<SpfEngineHandle>();
-    if (engine_->owner != this || engine_->generation != mirrorGeneration_) {
-      openr_spf_graph g{};
-      g.num_nodes = (uint32_t)m.names.size();
-      g.num_dir_edges = (uint32_t)m.col.size();
-      g.num_links = (uint32_t)m.links.size();
-      g.row_ptr = m.rowPtr.data();
-      g.col = m.col.data();
-      g.metric = m.metric.data();
-      g.link_id = m.linkId.data();
-      g.edge_up = m.edgeUp.data();
-      g.node_overloaded = m.overloaded.data();
-      g.name_rank = m.nameRank.data();
-      SpfEngineHandle::check(openr_spf_set_graph(engine_->ctx(), &g), "openr_spf_set_graph");
-      engine_->owner = this;
-      engine_->generation = mirrorGeneration_;
-    }
+    ensureEngineGraph();
     const uint32_t V = (uint32_t)m.names.size(), E = (uint32_t)m.col.size(), tw = (E + 63) / 64;
     uint32_t nb = 1;
     SpfEngineHandle::check(openr_spf_nh_bytes(engine_->ctx(), &nb), "openr_spf_nh_bytes");

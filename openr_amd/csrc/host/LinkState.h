@@ -258,6 +258,16 @@ class LinkState {
   std::vector<LinkState::Path> const& getKthPaths(const std::string& src, const std::string& dest,
                                                   size_t k) const;
 
+  // Batched KSP2 prefetch (new): getKthPaths(src, d, 1) and (src, d, 2) for every d in
+  // `dests`, traced on the device in one openr_spf_ksp2 launch instead of one ignore-set
+  // SPF per destination. Results are staged, not memoised: a later getKthPaths(src, d, k)
+  // takes its staged paths and records the logical SPF run the reference would have made
+  // then, so memo contents and decision.spf_runs match the call-by-call sequence however
+  // many destinations were prefetched. Graphs the device tracer refuses (a metric outside
+  // [1, 2^31-1], too many links) and pairs whose paths overflow the token rows are left to
+  // getKthPaths' own path.
+  void prefetchKthPaths(const std::string& src, const std::vector<std::string>& dests) const;
+
   class LinkStateChange {
    public:
     LinkStateChange() = default;
@@ -320,6 +330,17 @@ class LinkState {
   mutable std::unordered_map<std::pair<std::string, bool>, SpfResult> spfResults_;
   mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<LinkState::Path>>
       kthPathResults_;
+  struct StagedKsp2 {
+    std::vector<Path> k1, k2;
+    double ms = 0;  // this pair's share of the launch (decision.spf_ms)
+  };
+  mutable std::unordered_map<std::pair<std::string, std::string>, StagedKsp2> kthStaged_;
+  void clearMemos() const {
+    spfResults_.clear();
+    kthPathResults_.clear();
+    kthStaged_.clear();
+  }
+  void ensureEngineGraph() const;
 
   std::optional<Path> traceOnePath(std::string const& src, std::string const& dest, SpfResult const& result,
                                    LinkSet& linksToIgnore) const;

@@ -858,7 +858,7 @@ struct Wan {
   PrefixState ps;
   std::vector<std::string> names;
   std::vector<thrift::IpPrefix> prefix;
-  Wan(uint32_t n, uint32_t L, uint32_t par, uint64_t seed, bool nodeLabels = false) {
+  Wan(uint32_t n, uint32_t L, uint32_t par, uint64_t seed, bool nodeLabels = false, bool ksp2 = false) {
     std::vector<uint32_t> ends(2 * (L + par)), muv(L + par), mvu(L + par);
     EXPECT_EQ(openr_topogen_wan(n, L, 64, seed, par, ends.data(), muv.data(), mvu.data()), 0);
     std::vector<std::vector<thrift::Adjacency>> adjs(n);
@@ -879,7 +879,7 @@ struct Wan {
       names.push_back(nm(i));
       als.at(kDefaultArea).updateAdjacencyDatabase(createAdjDb(nm(i), adjs[i], nodeLabels ? 100 + (int32_t)i : 0));
       prefix.push_back(pfx("fd00::" + std::to_string(i) + "/128"));
-      ps.updatePrefix(nm(i), kDefaultArea, createPrefixEntry(prefix.back()));
+      ps.updatePrefix(nm(i), kDefaultArea, createPrefixEntry(prefix.back(), ksp2));
     }
   }
   RibPolicy policy() const {
@@ -1077,6 +1077,56 @@ TEST_GPU(BuildRouteDbs_HostThreads_MatchSequential) {
   EXPECT_TRUE(std::get<2>(seq) == std::get<2>(par));
   EXPECT_EQ(std::get<2>(seq)[0], (uint64_t)nodes.size() - 2);
   EXPECT_TRUE(std::get<3>(seq) > 0);  // node-label routes present
+}
+
+// KSP2 route DBs with the batched device prefetch (LinkState::prefetchKthPaths) against
+// the call-by-call getKthPaths path: same routes (SR-MPLS push labels, parallel links),
+// same decision.spf_runs, same memoised k-th paths afterwards.
+TEST_GPU(Ksp2RouteBuild_Prefetch_MatchesCallByCall) {
+  std::vector<uint32_t> picks{0, 17, 123, 250};
+  auto run = [&](const char* prefetch) {
+    setenv("OPENR_KSP2_PREFETCH", prefetch, 1);
+    Wan w(300, 900, 10, 9, true, true);
+    SpfSolver solver(w.names[0], false, false);
+    std::vector<std::string> nodes;
+    for (auto i : picks) nodes.push_back(w.names[i]);
+    const uint64_t runs0 = SpfCounters::get().spfRuns();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto dbs = solver.buildRouteDbs(nodes, w.als, w.ps);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const uint64_t runs = SpfCounters::get().spfRuns() - runs0;
+    std::vector<std::string> flat;
+    size_t routes = 0, pushes = 0;
+    for (auto const& db : dbs) {
+      flat.push_back(flatten(db));
+      if (!db) continue;
+      routes += db->unicastRoutes.size();
+      for (auto const& [p, r] : db->unicastRoutes)
+        for (auto const& nh : r.nexthops) pushes += nh.mplsAction && nh.mplsAction->pushLabels.has_value();
+    }
+    std::string memo;  // k-th paths memoised for a sample of pairs, as link strings
+    auto const& ls = w.als.at(kDefaultArea);
+    for (auto i : picks)
+      for (uint32_t d = 1; d < 300; d += 37)
+        for (size_t k = 1; k <= 2; ++k) {
+          for (auto const& path : ls.getKthPaths(w.names[i], w.names[d], k)) {
+            for (auto const& l : path) memo += l->toString() + ",";
+            memo += "|";
+          }
+          memo += "\n";
+        }
+    std::printf("  prefetch=%s: %zu routes, %zu push next hops, spf_runs %llu, %.1f ms\n", prefetch, routes, pushes,
+                (unsigned long long)runs, ms);
+    return std::make_tuple(flat, runs, memo, routes, pushes);
+  };
+  const auto off = run("0");
+  const auto on = run("1");
+  unsetenv("OPENR_KSP2_PREFETCH");
+  EXPECT_TRUE(std::get<0>(off) == std::get<0>(on));
+  EXPECT_EQ(std::get<1>(off), std::get<1>(on));
+  EXPECT_TRUE(std::get<2>(off) == std::get<2>(on));
+  EXPECT_EQ(std::get<3>(on), picks.size() * 299);
+  EXPECT_TRUE(std::get<4>(on) > 0);
 }
 
 // --- RibPolicyTest.cpp:176-301 (RibPolicy.ApplyAction / ApplyPolicy) -----------------
