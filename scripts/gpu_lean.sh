@@ -1,10 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-for ns in 0 1; do
-OPENR_SPF_NBR_NOSTORE=$ns timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/nbrprof3_$ns -o run --output-format csv -- python3 $R/bench.py --topology fabric --steps 5 --warmup 1 --no-cpu-baseline > $R/gpurun_out/nbrprof3.log 2>&1 || exit 1
-f=$(find $R/gpurun_out/nbrprof3_$ns -name "*kernel_stats.csv" | head -1); python3 -c "
-import csv,sys
-for r in csv.DictReader(open(sys.argv[1])): print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')" $f | grep nbr_nh
-done
+timeout -k 10 300 tests/cpp/build/decision_test gpu > gpurun_out/dec.log 2>&1 || { grep -E "FAIL|expected|Error|error" gpurun_out/dec.log | head -30; tail -5 gpurun_out/dec.log; exit 1; }
+grep -E "FAIL|tests,|prefetch=|HostThreads|Ksp2Route" gpurun_out/dec.log
+timeout -k 10 300 tests/cpp/build/linkstate_test gpu > gpurun_out/ls.log 2>&1 || { grep -E "FAIL" gpurun_out/ls.log | head; tail -5 gpurun_out/ls.log; exit 1; }
+grep -E "FAIL|tests," gpurun_out/ls.log
