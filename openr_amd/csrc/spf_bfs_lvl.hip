@@ -804,15 +804,286 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   return e;
 }
 
+// ---------------------------------------------------------------------------
+// Wave pass (graph in LDS): the lean pass with ONE wavefront per solve and the transit
+// rows staged in LDS. When every row has <= 4 edges and every neighbour id lies within
+// 127 of its row's node (a row-major grid: +-1, +-n), a row is four signed byte deltas
+// (`elld`, 4 bytes per node: a 100 x 100 grid in 40 KB), so one workgroup per CU stages
+// the whole graph once and its W wavefronts each own a solve slot [u8 levels | next-hop
+// words | two queue halves]. A solve's level loop then reads no global memory and has no
+// barrier: a wavefront's LDS operations complete in issue order, so the next level reads
+// the previous level's appends directly, and the append cursor is a scalar. Per level the
+// dependent chain is queue entry -> delta row + nh(u) -> levels -> atomics (four LDS round
+// trips, no L2 load, no ds_add, no s_barrier). Semantics as bfs_ell_kernel (closed form of
+// LinkState::runSpf for uniform cost, LinkState.cpp:808-882): a delta of 0 (no edge) or a
+// lane past the frontier resolves to a node whose level is <= L, never tight. A level
+// wider than a half or a solve deeper than 253 levels is listed for the u16 re-run.
+// ---------------------------------------------------------------------------
+struct WaveLayout {
+  uint32_t dummy, slot0, nh, q, per_slot, total;
+};
+// [0, 4V) delta rows, 64 all-ones dummy words, then W solve slots
+__host__ __device__ inline WaveLayout wave_layout(uint32_t V, uint32_t nh_words, uint32_t qhalf, uint32_t waves) {
+  WaveLayout l;
+  l.dummy = (4u * V + 15u) & ~15u;
+  l.slot0 = l.dummy + 256u;
+  l.nh = (V + 15u) & ~15u;  // within a slot: levels at 0
+  l.q = l.nh + ((4u * nh_words + 15u) & ~15u);
+  l.per_slot = l.q + ((4u * qhalf + 15u) & ~15u);
+  l.total = l.slot0 + waves * l.per_slot;
+  return l;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t qhalf,
+                                                       uint32_t waves, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
+  using N = Nh<MODE>;
+  static_assert(N::kSingle, "single-dword next-hop fields only");
+  constexpr uint32_t kBits = 32u / N::kPer;
+  constexpr uint32_t kLog = kBits == 4 ? 3 : kBits == 8 ? 2 : kBits == 16 ? 1 : 0;
+  constexpr uint32_t kShl = 5u - kLog;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
+  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nh_words = N::words(V);
+  const WaveLayout lay = wave_layout(V, nh_words, qhalf, waves);
+  const uint32_t slot = lay.slot0 + wave * lay.per_slot;
+  lds_u32* const rows = (lds_u32*)(size_t)0u;
+  lds_u8* const lvl = (lds_u8*)(size_t)slot;
+  lds_u32* const lvl_w = (lds_u32*)(size_t)slot;
+  lds_u32* const nh = (lds_u32*)(size_t)(slot + lay.nh);
+  lds_u16* const q = (lds_u16*)(size_t)(slot + lay.q);
+  lds_u32* const my_dummy = (lds_u32*)(size_t)(lay.dummy + 4u * lane);
+  for (uint32_t i = tid; i < V; i += blockDim.x) rows[i] = g.elld[i];
+  if (wave == 0) *my_dummy = 0xFFFFFFFFu;  // only ever ORed afterwards: its fields are never zero
+  __syncthreads();
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  const uint32_t lvl_words = (V + 3u) / 4u;
+  uint32_t unit = blockIdx.x * waves + wave;  // the first grid x W units are static, then dynamic
+  while (unit < count) {
+    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
+    const uint32_t src = a.sources[sid];
+    if (src < V) {  // wave-uniform
+      for (uint32_t i = lane; i < lvl_words; i += 64u) lvl_w[i] = 0xFFFFFFFFu;
+      for (uint32_t i = lane; i < nh_words; i += 64u) nh[i] = 0u;
+      if (lane == 0) lvl[src] = 0;
+      // level 0: the source expands even when overloaded (its full CSR row); a directly
+      // connected node's next hop is the node itself (LinkState.cpp:867-872)
+      uint32_t cur = 0;
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += 64u) {
+          const uint32_t e = e0 + lane;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && v != src) {
+              const uint32_t sh = (v << kShl) & 31u;
+              fresh = ((lds_or(&nh[v >> kLog], (1u << g.nbr[e]) << sh) >> sh) & N::kMask) == 0u;
+              lvl[v] = 1;
+            }
+          }
+          const unsigned long long b = __builtin_amdgcn_ballot_w64(fresh);
+          if (fresh)  // slot < deg(src) < qhalf (host-checked)
+            q[qhalf + cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+                (uint16_t)v;
+          cur += (uint32_t)__popcll(b);
+        }
+      }
+      uint32_t L = 1, reached = 1u + cur;
+      bool overflow = false;  // wave-uniform
+      while (cur) {
+        if (L + 1u >= 0xFFu) {  // next level not representable in u8
+          overflow = true;
+          break;
+        }
+        const uint32_t rd = (L & 1u) * qhalf, wr = qhalf - rd;
+        const uint8_t lnext = (uint8_t)(L + 1u);
+        uint32_t nxt = 0;  // scalar append cursor of level L+1
+        for (uint32_t fb = 0; fb < cur; fb += 64u) {
+          const uint32_t idx = fb + lane;
+          const bool live = idx < cur;
+          const uint32_t qe = q[rd + (live ? idx : 0u)];
+          const uint32_t u = live ? qe : src;               // past the level: the source (level 0)
+          const uint32_t r4 = rows[u];                      // issued with the nh(u) read below
+          const uint32_t d4 = live ? r4 : 0u;               // no slots: every slot resolves to u
+          const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
+          uint32_t vv[4], lv[4], old[4];
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) vv[j] = u + (uint32_t)__builtin_amdgcn_sbfe((int32_t)d4, 8u * j, 8u);
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) lv[j] = lvl[vv[j]];
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t v = vv[j];
+            const bool tight = lv[j] > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
+            old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, x << ((v << kShl) & 31u));
+          }
+          __builtin_amdgcn_sched_barrier(0);  // all atomics in flight before their results are used
+          unsigned long long bj[4];
+          bool fresh[4];
+          uint32_t off[5];
+          off[0] = 0;
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; ++j) {
+            fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;  // a dummy field never is
+            bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
+            off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+          }
+          const uint32_t total = off[4];
+          if (total) {  // wave-uniform
+            if (nxt + total <= qhalf) {
+#pragma unroll
+              for (uint32_t j = 0; j < 4u; ++j) {
+                if (fresh[j]) {
+                  const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                  q[wr + nxt + off[j] + k] = (uint16_t)vv[j];
+                  lvl[vv[j]] = lnext;  // only the appending arrival stores v's level
+                }
+              }
+            } else {
+              overflow = true;  // the level outgrows its half
+            }
+            nxt += total;
+          }
+        }
+        if (overflow) break;
+        ++L;
+        cur = nxt;
+        reached += cur;
+        if (reached == V) break;  // every node reached: the newest level cannot expand tightly
+      }
+      if (overflow) {
+        if (lane == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
+      } else {
+        // rows out: u64 distances from the levels, then the next-hop bytes
+        uint64_t* drow = a.dist + out_row_of(a, sid) * V;
+        if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0) {
+          ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
+          for (uint32_t i = lane; i < V / 4u; i += 64u) {
+            const uint32_t w = lvl_w[i];
+            uint64_t xd[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) {
+              const uint32_t l = (w >> (8u * k)) & 0xFFu;
+              xd[k] = l != 0xFFu ? (uint64_t)l * cost : ~0ull;
+            }
+            if (nt) {
+              __builtin_nontemporal_store(xd[0], &d2[2u * i].x);
+              __builtin_nontemporal_store(xd[1], &d2[2u * i].y);
+              __builtin_nontemporal_store(xd[2], &d2[2u * i + 1u].x);
+              __builtin_nontemporal_store(xd[3], &d2[2u * i + 1u].y);
+            } else {
+              d2[2u * i] = make_ulonglong2(xd[0], xd[1]);
+              d2[2u * i + 1u] = make_ulonglong2(xd[2], xd[3]);
+            }
+          }
+        } else {
+          for (uint32_t v = lane; v < V; v += 64u) {
+            const uint32_t l = lvl[v];
+            store_row<uint64_t>(&drow[v], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt != 0);
+          }
+        }
+        if (a.nh) {
+          const uint32_t nb = a.nh_bytes;
+          uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
+          const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
+          if (MODE == kNhNibble && nb == 1 && aligned4) {
+            uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+            for (uint32_t i = lane; i < V / 4u; i += 64u) {
+              const uint32_t h = (nh[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
+              store_row<uint32_t>(&nrow32[i],
+                                  (h & 0xFu) | ((h & 0xF0u) << 4) | ((h & 0xF00u) << 8) | ((h & 0xF000u) << 12),
+                                  nt != 0);
+            }
+          } else if (MODE == kNhByte && nb == 1 && aligned4) {
+            uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
+            for (uint32_t i = lane; i < V / 4u; i += 64u) store_row<uint32_t>(&nrow32[i], (uint32_t)nh[i], nt != 0);
+          } else {
+            for (uint32_t i = lane; i < V * nb; i += 64u) {
+              const uint32_t v = i / nb, j = i - v * nb;
+              const uint32_t f = __builtin_amdgcn_ubfe(nh[v >> kLog], v << kShl, kBits);
+              nrow[i] = 8u * j < kBits ? (uint8_t)(f >> (8u * j)) : (uint8_t)0;
+            }
+          }
+        }
+      }
+    }
+    uint32_t nx = 0;
+    if (lane == 0) nx = gridDim.x * waves + atomicAdd(&ctr[0], 1u);
+    unit = __builtin_amdgcn_readfirstlane(nx);
+  }
+  __syncthreads();  // no wave of this workgroup takes units any more
+  retire_workgroup(ctr, nullptr);
+}
+
+// Wavefronts per workgroup for the wave pass, 0 when it does not apply. One workgroup per
+// CU holds the delta rows plus up to W solve slots (W >= 4 by LDS), spread so every CU
+// gets work. Auto (OPENR_SPF_BFS_WAVE unset / 2): batches of at most three rounds of W
+// solves per CU — the strong-scaling shards, where a solve's latency is exposed (G100,
+// 1 250 sources: 0.165 vs 0.194 ms; 2 500: 0.273 vs 0.313; 5 000: 0.428 vs 0.460) —
+// while a full batch stays on the lean pass, whose two-wave workgroups keep 10 solves per
+// CU in flight (10 000 sources: 0.750 vs 0.804 ms). 1 = whenever it applies (tests), 0 =
+// never.
+uint32_t wave_pass_waves(const DevGraph& g, int mode, uint32_t qhalf, uint32_t n, int num_cus) {
+  const uint32_t knob = env_u32("OPENR_SPF_BFS_WAVE", 2u, 0u, 2u);
+  if (!g.elld || knob == 0u) return 0;
+  const WaveLayout one = wave_layout(g.V, nh_words_for(mode, g.V), qhalf, 0);
+  if (one.slot0 >= kMaxLds) return 0;
+  const uint32_t w = std::min<uint32_t>(8u, (kMaxLds - one.slot0) / one.per_slot);
+  if (w < env_u32("OPENR_SPF_WAVE_MIN", 4u, 1u, 8u)) return 0;
+  const uint64_t cus = (uint64_t)std::max(num_cus, 1);
+  if (knob == 2u && (uint64_t)n > 3ull * cus * w) return 0;
+  return (uint32_t)std::min<uint64_t>(w, std::max<uint64_t>(1, ((uint64_t)n + cus - 1) / cus));
+}
+
+template <int MODE>
+hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t qhalf, uint32_t waves,
+                           uint32_t* ctr, uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
+  const uint32_t lds = wave_layout(g.V, nh_words_for(MODE, g.V), qhalf, waves).total;
+  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cus, (a.n + waves - 1u) / waves));
+  auto k = bfs_wave_kernel<MODE>;
+  hipError_t err =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  if (info) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = "bfs_wave_kernel<lds-graph>";
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64u * waves), lds, s, g, a, cost, qhalf, waves, ctr, ovf_count, nt_stores());
+  if (env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u))  // tests: which pass ran
+    std::fprintf(stderr, "bfs_wave: grid=%u waves=%u n=%u qhalf=%u lds=%u\n", grid, waves, a.n, qhalf, lds);
+  return hipGetLastError();
+}
+
 template <int MODE, int BLOCK, int ELLM, bool SLICED>
 hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign,
                            uint32_t ring_cap, int num_cus, hipStream_t s, LaunchInfo* info) {
   // Counter block of the class: [0,1] first launch, [2,3] re-run launch, [4] listed units.
   uint32_t* blk = class_counters(a);
+  hipError_t err;
+  if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
+    const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
+    // wave pass (graph in LDS) for small batches when the delta rows fit with >= 4 solve
+    // slots per CU (OPENR_SPF_WAVE_QHALF, tests: a smaller half, so wide levels re-run)
+    const uint32_t qforce = env_u32("OPENR_SPF_WAVE_QHALF", 0u, 0u, 65535u);
+    const uint32_t qhalf = qforce ? (std::max<uint32_t>(qforce, g.max_deg + 1u) + 15u) & ~15u
+                                  : (std::max<uint32_t>(64u, need1) + 15u) & ~15u;
+    const uint32_t waves = (!has_ign && !a.tight) ? wave_pass_waves(g, MODE, qhalf, a.n, num_cus) : 0u;
+    if (waves) {
+      err = launch_lvl_wave<MODE>(g, a, cost, qhalf, waves, blk, blk + 4, num_cus, s, info);
+      if (err != hipSuccess || (g.V <= qhalf && g.V <= 254u)) return err;  // nothing can overflow
+      return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true,
+                                                                          blk + 2, blk + 4, num_cus, s, info);
+    }
+  }
   if (!ring_cap)
     return launch_lvl_variant<MODE, BLOCK, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, false, blk,
                                                                           blk + 4, num_cus, s, info);
-  hipError_t err;
   if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
     // lean pass: its queue halves must hold the widest sampled level (else the generic ring)
     const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);

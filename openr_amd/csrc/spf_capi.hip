@@ -106,7 +106,7 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
-                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64};
+                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -910,6 +910,21 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
       std::vector<uint4> ellv(V + 1u, make_uint4(V, V, V, V));  // [V] = sentinel row (lean BFS pass)
       for (uint32_t u = 0; u < V; ++u) ellv[u] = ellv_of(ellt[u], V);
       err = up(&g.ellv, ellv.data(), V + 1u);
+      // delta rows (wave pass): every row of <= 4 edges and every column within 127 ids of
+      // its row, down edges and overloaded rows included (a patch may bring them back)
+      bool delta_ok = true;
+      for (uint32_t u = 0; u < V && delta_ok; ++u) {
+        delta_ok = gr->row_ptr[u + 1] - gr->row_ptr[u] <= 4u;
+        for (uint32_t e = gr->row_ptr[u]; e < gr->row_ptr[u + 1] && delta_ok; ++e) {
+          const int32_t dlt = (int32_t)gr->col[e] - (int32_t)u;
+          delta_ok = dlt >= -127 && dlt <= 127;
+        }
+      }
+      if (err == hipSuccess && delta_ok) {
+        std::vector<uint32_t> elld(V);
+        for (uint32_t u = 0; u < V; ++u) elld[u] = elld_of(ellv[u], u, V);
+        err = up(&g.elld, elld.data(), V);
+      }
     }
     if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
@@ -1064,6 +1079,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     dirty_bits[u >> 5] = 1;
     rec(kPatchEllt, u, ctx->ellt[u]);
     rec(kPatchEllv, u, ellv_of(ctx->ellt[u], V));
+    rec(kPatchElld, u, make_uint4(elld_of(ellv_of(ctx->ellt[u], V), u, V), 0, 0, 0));
     rec(kPatchRow2t, u, make_uint4(ctx->row2t[u].x, ctx->row2t[u].y, 0, 0));
     rec(kPatchOvl, u, make_uint4(ctx->ovl[u], 0, 0, 0));
   }

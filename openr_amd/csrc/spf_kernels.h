@@ -28,6 +28,8 @@ struct DevGraph {
   uint4* ellv = nullptr;       // [V+1] ellt with every down / padding slot replaced by the node id V (a
                                //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests);
                                //     ellv[V] = (V, V, V, V), the row of a lane past the frontier
+  uint32_t* elld = nullptr;    // [V] ellv as four signed byte deltas (v - u; 0 = no edge), or null
+                               //     when a row has > 4 edges or a column > 127 ids away (wave pass)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
   uint64_t* w64 = nullptr;     // [E] metric u->v as the caller gave it (exact-order kernel: 0 / wrapped values)
@@ -53,6 +55,11 @@ constexpr uint32_t kBlock = 256;
 __host__ __device__ inline uint4 ellv_of(uint4 t, uint32_t V) {
   auto f = [V](uint32_t x) { return (x & kEdgeDown) ? V : x; };
   return make_uint4(f(t.x), f(t.y), f(t.z), f(t.w));
+}
+// elld row of an ellv row: the four slots as signed byte deltas v - u (0: V, no edge)
+__host__ __device__ inline uint32_t elld_of(uint4 r, uint32_t u, uint32_t V) {
+  auto d = [u, V](uint32_t x) -> uint32_t { return x >= V ? 0u : (uint32_t)(uint8_t)(int8_t)((int32_t)x - (int32_t)u); };
+  return d(r.x) | (d(r.y) << 8) | (d(r.z) << 16) | (d(r.w) << 24);
 }
 constexpr uint32_t kBfsEdgesPerLane = 4;  // edges a lane loads ahead per pass (register prefetch)
 constexpr uint32_t kBfsTargetWgs = 12;    // lvl BFS sizes its ring for this many workgroups per CU (G100: 8 -> 1.06 ms, 9..16 -> 1.02 ms)
@@ -198,6 +205,7 @@ uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64
 enum PatchArray : uint32_t {
   kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kPatchEllv,
   kPatchW64,  // val.x = low, val.y = high word
+  kPatchElld,
   kNumPatchArrays
 };
 struct PatchRec {

@@ -38,6 +38,9 @@ __global__ __launch_bounds__(256) void patch_apply(DevGraph g, const PatchRec* r
     case kPatchErec: g.erec[r.idx] = r.val; break;
     case kPatchEllt: g.ellt[r.idx] = r.val; break;
     case kPatchEllv: g.ellv[r.idx] = r.val; break;
+    case kPatchElld:
+      if (g.elld) g.elld[r.idx] = r.val.x;
+      break;
     case kPatchRow2t: g.row2t[r.idx] = make_uint2(r.val.x, r.val.y); break;
     case kPatchOvl: g.ovl[r.idx] = (uint8_t)r.val.x; break;
     case kPatchOvlBits: g.ovl_bits[r.idx] = r.val.x; break;

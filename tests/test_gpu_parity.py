@@ -251,6 +251,51 @@ def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, full):
     check_against_oracle(eng, g, srcs, True, ignore=ignore)
 
 
+@pytest.mark.parametrize("case", ["grid", "depth", "half", "overload-down"])
+def test_wave_pass(eng, monkeypatch, capfd, case):
+    """The wave pass (one wavefront per solve, delta-coded rows staged in LDS; picked for
+    small batches of graphs whose rows have <= 4 edges within 127 ids of their node),
+    forced on and checked against the oracle, including both re-run paths: a chain
+    deeper than 253 levels and a forced tiny queue half. OPENR_SPF_BFS_PROF makes the pass
+    report itself on stderr (proof that it ran)."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    n = 40
+    names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)]
+    links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
+    links += [(r * n + c, (r + 1) * n + c) for r in range(n - 1) for c in range(n)]
+    ovl = up = None
+    srcs = list(range(0, n * n, 7))
+    if case == "depth":
+        tail = 300
+        names += [f"z{i:03d}" for i in range(tail)]
+        links += [(n * n + i, n * n + i + 1) for i in range(tail - 1)]
+        srcs = [0, n * n - 1, n * n, n * n + tail - 1, n * n + 150, 20 * n + 20]
+    if case == "half":
+        monkeypatch.setenv("OPENR_SPF_WAVE_QHALF", "16")
+    if case == "overload-down":
+        rng = np.random.default_rng(3)
+        ovl = (rng.random(n * n) < 0.05).astype(np.uint8)
+        up = (rng.random(len(links)) > 0.05).astype(np.uint8)
+    g = T.csr_from_links(names, np.array(links), overloaded=ovl, link_up=up)
+    dist, _ = check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
+    if case == "depth":
+        assert int(dist[2, n * n + 299]) == 299
+    assert "bfs_wave:" in capfd.readouterr().err
+
+
+def test_wave_pass_not_applicable(eng, monkeypatch, capfd):
+    """A neighbour more than 127 ids away (here: a 200 x 200 grid, rows +-200) leaves the
+    wave pass off even when forced; the lean / generic passes serve the graph."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    g = T.grid_fast(200)
+    check_against_oracle(eng, g, [0, 199, 20100, 39999], True, check_pathlinks=False)
+    assert "bfs_wave:" not in capfd.readouterr().err
+
+
 def test_lean_pass_depth_overflow(eng, monkeypatch, capfd, bfs_family):
     """The lean ELL pass (graphs with <= 4 edges per row too big for the full-order queue,
     sampled depth under the u8 limit): a 70 x 70 grid plus a separate 300-node chain whose
@@ -258,6 +303,7 @@ def test_lean_pass_depth_overflow(eng, monkeypatch, capfd, bfs_family):
     pass flags them at level 254 and the u16 full-order pass re-runs them. (With
     OPENR_SPF_BFS_PROF the lean pass reports itself on stderr: proof that it ran.)"""
     monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")  # small batch: the wave pass would take it
     n, tail = 70, 300
     names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)] + [f"z{i:03d}" for i in range(tail)]
     links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
@@ -275,6 +321,7 @@ def test_lean_pass_half_overflow(eng, monkeypatch, capfd, bfs_family):
     width would otherwise keep it on the generic ring): the solve is flagged and re-run."""
     monkeypatch.setenv("OPENR_SPF_LEAN_FORCE", "1")
     monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")
     chain, depth = 100, 11
     names = [f"c{i:03d}" for i in range(chain)] + [f"t{i:05d}" for i in range(1, 2 ** (depth + 1) - 1)]
     links = [(i, i + 1) for i in range(chain - 1)]
