@@ -83,7 +83,7 @@ __host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has
     return o;
   };
   const uint32_t per = 32u / fb;
-  l.st = take(4u * ((V + per - 1u) / per));
+  l.st = take(4u * ((V + 1u + per - 1u) / per));  // + node V: a settled sentinel (lean edge loop)
   l.ring = take(2u * ring_cap);
   l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
   l.dummy = take(4u * 64u);  // per-lane sink for the no-op atomics of non-tight edges
@@ -166,7 +166,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
   uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
-  const uint32_t st_words = S::words(V);
+  const uint32_t st_words = S::words(V + 1u);
+  // lean edge loop (no ignore set, no tight-edge output, CSR rows): padding and down slots
+  // read the sentinel node V, whose code is "settled" (never tight, never empty), and a
+  // lane's no-op atomic goes to its own all-ones dummy word, so the returned field alone
+  // elects the appending arrival
+  constexpr bool kLeanT = !GENERIC && ELLM == 0;
+  const bool kLean = kLeanT && (nt & 2u) == 0u;  // (OPENR_SPF_CODE_LEAN=0: the generic loop, A/B)
+  nt &= 1u;
+  if (kLean && tid < 64) dummy[tid] = 0xFFFFFFFFu;
   const uint32_t ign_words = (g.L + 31u) / 32u;
   const uint32_t G = 1u << glog, ngroups = BLOCK >> glog, groups_per_wave = 64u >> glog;
   const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       __syncthreads();
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
+        atomicOr(&st[S::word(V)], kCodeSettledSink << S::shift(V));  // the sentinel
         atomicOr(&st[S::word(src)], level_code(0) << S::shift(src));
         if (own_dist) put(src, 0u);
       }
@@ -338,6 +347,56 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           OPENR_PROF_ADD(0, t0, t1);
           pc[7] += 1;
 #endif
+          if (kLeanT && kLean) {
+            for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
+              uint32_t vv[K], cw[K], old[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                const uint32_t e = e0 + j * G;
+                const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;  // masked: padding lanes issue no load
+                vv[j] = (raw & kEdgeDown) ? V : raw;                  // padding / down edge: the sentinel
+              }
+#pragma unroll
+              for (int j = 0; j < K; ++j) cw[j] = st[S::word(vv[j])];
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                const uint32_t c = (cw[j] >> S::shift(vv[j])) & kCodeMask;
+                const bool tight = c == 0u || c == cnext;  // first or equal-cost arrival (LinkState.cpp:857-873)
+                old[j] = atomicOr(tight ? &st[S::word(vv[j])] : &dummy[lane], xu << S::shift(vv[j]));
+              }
+              __builtin_amdgcn_sched_barrier(0);  // the K atomics in flight together
+              bool fresh[K];
+              unsigned long long bj[K];
+              uint32_t off[K + 1];
+              off[0] = 0;
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                fresh[j] = ((old[j] >> S::shift(vv[j])) & kCodeMask) == 0u;  // a dummy field never is
+                bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
+                off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+              }
+              const uint32_t total = off[K];
+              if (total) {  // wave-uniform
+                const int leader = __ffsll((long long)__ballot(1)) - 1;
+                uint32_t wbase = 0;
+                if ((int)lane == leader) wbase = atomicAdd(cnt, total);
+                const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
+                if (!RING || base + total - head <= ring_cap) {
+#pragma unroll
+                  for (int j = 0; j < K; ++j) {
+                    if (fresh[j]) {
+                      const uint32_t slot = base + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                      ring[RING ? (slot & rmask) : slot] = (uint16_t)vv[j];
+                    }
+                  }
+                } else if ((int)lane == leader) {
+                  ctl[4] = 1;  // two adjacent levels exceed the ring
+                }
+              }
+            }
+            continue;
+          }
           for (uint32_t e0 = (ELLM == 2 ? 0u : beg) + lane_g; __any(e0 < end); e0 += G * K) {
             uint32_t av[K], lv[K];
 #pragma unroll
@@ -552,7 +611,8 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
     info->kernel = RING ? "bfs_code_kernel<ring>" : "bfs_code_kernel<full>";
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
-                     (uint32_t)from_list, ctr, ovf_count, nt_stores());
+                     (uint32_t)from_list, ctr, ovf_count,
+                     nt_stores() | (env_u32("OPENR_SPF_CODE_LEAN", 1u, 0u, 1u) ? 0u : 2u));
   return hipGetLastError();
 }
 
