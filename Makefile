@@ -28,7 +28,7 @@ CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 CPPTEST := tests/cpp/build/linkstate_test
 DECTEST := tests/cpp/build/decision_test
 CPPTEST_SRCS := tests/cpp/linkstate_test.cpp tests/cpp/harness.h oracle/spf_oracle.c oracle/spf_oracle.h
-DECTEST_SRCS := tests/cpp/decision_test.cpp tests/cpp/harness.h oracle/spf_oracle.c oracle/spf_oracle.h
+DECTEST_SRCS := tests/cpp/decision_test.cpp tests/cpp/harness.h openr_amd/csrc/host/HostParallel.h oracle/spf_oracle.c oracle/spf_oracle.h
 
 # "<hash> <files>" of a file list (the same recipe as openr_amd/engine.py:source_hash)
 build_id = $$(cat $(1) | sha256sum | cut -c1-16) $(1)

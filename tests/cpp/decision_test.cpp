@@ -6,16 +6,19 @@
 // from the engine, so route-building tests are in the gpu group.
 //   decision_test cpu | gpu | all
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <cstdlib>
 #include <thread>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../include/openr_topogen.h"
 #include "../../openr_amd/csrc/host/Decision.h"
+#include "../../openr_amd/csrc/host/HostParallel.h"
 #include "../../oracle/spf_oracle.h"
 #include "harness.h"
 
@@ -1127,6 +1130,43 @@ TEST_GPU(Ksp2RouteBuild_Prefetch_MatchesCallByCall) {
   EXPECT_TRUE(std::get<2>(off) == std::get<2>(on));
   EXPECT_EQ(std::get<3>(on), picks.size() * 299);
   EXPECT_TRUE(std::get<4>(on) > 0);
+}
+
+// HostParallel.h: every item runs exactly once on some worker; an error reports the lowest
+// failing index, as the one-thread loop would; OPENR_HOST_THREADS bounds the workers.
+TEST_CPU(HostParallel_ParallelFor) {
+  const size_t n = 10007;
+  std::vector<std::atomic<int>> hits(n);
+  for (auto& h : hits) h = 0;
+  std::atomic<unsigned> maxWorker{0};
+  parallelFor(n, 7, 6, [&](unsigned w, size_t i) {
+    hits[i]++;
+    unsigned m = maxWorker.load();
+    while (w > m && !maxWorker.compare_exchange_weak(m, w)) {
+    }
+  });
+  bool once = true;
+  for (auto& h : hits) once &= h.load() == 1;
+  EXPECT_TRUE(once);
+  EXPECT_TRUE(maxWorker.load() < 6u);
+  for (unsigned workers : {1u, 4u}) {
+    std::string what;
+    try {
+      parallelFor(n, 3, workers, [&](unsigned, size_t i) {
+        if (i == 777 || i == 5000) throw std::runtime_error("item " + std::to_string(i));
+      });
+    } catch (const std::runtime_error& e) {
+      what = e.what();
+    }
+    EXPECT_TRUE(what == "item 777");
+  }
+  setenv("OPENR_HOST_THREADS", "3", 1);
+  EXPECT_EQ(hostThreads(), 3u);
+  EXPECT_EQ(parallelWorkers(100, 50), 2u);
+  setenv("OPENR_HOST_THREADS", "1", 1);
+  EXPECT_EQ(parallelWorkers(1000, 1), 1u);
+  unsetenv("OPENR_HOST_THREADS");
+  EXPECT_TRUE(hostThreads() >= 1u && hostThreads() <= 16u);
 }
 
 // --- RibPolicyTest.cpp:176-301 (RibPolicy.ApplyAction / ApplyPolicy) -----------------
