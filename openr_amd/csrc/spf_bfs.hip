@@ -31,8 +31,9 @@
 // barrier per level.
 //
 // Field widths by source class (distinct degree d of the source = next-hop set width):
-//   8 bits (d <= 5), 16 bits (d <= 13), 32 bits (d <= 24), and 32-bit fields holding
-//   24-bit slices of the set for d > 24 (one workgroup pass per (solve, slice)).
+//   8 bits (d <= 5), 16 bits (d <= 13), 32 bits (d <= 29), and 32-bit fields holding
+//   29-bit slices of the set for d > 29 (one workgroup pass per (solve, slice); the slices'
+//   chunks are merged into the next-hop bytes afterwards, slice_merge).
 //
 // No MFMA: min-plus relaxation is not a matrix contraction (DESIGN.md "Roofline").
 #include <algorithm>
@@ -53,8 +54,8 @@ template <int FB>
 struct State {
   static constexpr uint32_t kPer = 32u / FB;
   static constexpr uint32_t kFieldMask = FB == 32 ? 0xFFFFFFFFu : ((1u << (FB & 31)) - 1u);
-  static constexpr uint32_t kNhs = FB == 32 ? 8u : 3u;  // next-hop bits start here
-  static constexpr uint32_t kNhBits = FB - kNhs;         // 5 / 13 / 24
+  static constexpr uint32_t kNhs = 3u;           // next-hop bits start here
+  static constexpr uint32_t kNhBits = FB - kNhs;  // 5 / 13 / 29
   static constexpr uint32_t kNhMask = ((1u << kNhBits) - 1u) << kNhs;
   static __host__ __device__ uint32_t words(uint32_t V) { return (V + kPer - 1u) / kPer; }
   static __device__ __forceinline__ uint32_t word(uint32_t v) { return v / kPer; }
@@ -113,17 +114,9 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
     for (uint32_t v = tid; v < V; v += BLOCK)
       if ((S::field(st, v) & kCodeMask) == 0u) drow[v] = ~0ull;
   if (!nrow) return;
-  if (SLICED) {
-    const uint32_t j0 = 3u * slice, zero0 = 3u * a.nsl;
-    for (uint32_t v = tid; v < V; v += BLOCK) {
-      const uint32_t x = S::field(st, v) >> S::kNhs;
-      uint8_t* o = nrow + (size_t)v * nb;
-#pragma unroll
-      for (uint32_t jj = 0; jj < 3u; ++jj)
-        if (j0 + jj < nb) o[j0 + jj] = (uint8_t)(x >> (8u * jj));
-      if (slice == 0)
-        for (uint32_t j = zero0; j < nb; ++j) o[j] = 0;
-    }
+  if (SLICED) {  // the slice's 29-bit chunks, coalesced; slice_merge packs the bytes
+    uint32_t* trow = a.slice_tmp + ((size_t)sid * a.nsl + slice) * V;
+    for (uint32_t v = tid; v < V; v += BLOCK) store_row<uint32_t>(&trow[v], S::field(st, v) >> S::kNhs, nt);
     return;
   }
   if (FB == 8 && nb == 1 && ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0) {
@@ -146,7 +139,7 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
 //               levels exceed the ring is appended to a.ovf_list (count *ovf_count).
 // RING = false: full BFS order (capacity V, never overflows). from_list != 0: the
 //               units of a.ovf_list only (the re-run of what the ring variant flagged).
-// SLICED: one unit = (solve, 24-bit slice of the next-hop set).
+// SLICED: one unit = (solve, 29-bit slice of the next-hop set).
 // GENERIC = false: no ignore set and no tight-edge output (compile time), the
 // all-sources / prefetch case; GENERIC = true handles both at run time.
 template <int FB, int BLOCK, bool RING, int ELLM, bool GENERIC, bool SLICED>
@@ -648,6 +641,51 @@ hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, u
 #undef OPENR_BFS_SHAPE
 }
 
+// Sliced class, next-hop output: byte jj of node v's set is bits [8jj, 8jj + 8) of the
+// concatenated 29-bit slice chunks. A workgroup takes 256 nodes of one solve: each thread
+// reads its node's chunks (coalesced) and assembles its nb bytes in LDS, then the
+// workgroup stores the 256 * nb bytes of the row segment as coalesced dwords.
+__global__ __launch_bounds__(256) void slice_merge(SolveArgs a, uint32_t V) {
+  constexpr uint32_t kMaxNb = 40u;  // 11 slices x 29 bits; wider caller strides store directly
+  __shared__ uint32_t seg[256u * kMaxNb / 4u];
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  const uint32_t nsl = a.nsl, nb = a.nh_bytes, tiles = (V + 255u) / 256u;
+  uint8_t* segb = reinterpret_cast<uint8_t*>(seg);
+  for (uint64_t blk = blockIdx.x; blk < (uint64_t)count * tiles; blk += gridDim.x) {
+    const uint32_t k = (uint32_t)(blk / tiles), v0 = (uint32_t)(blk - (uint64_t)k * tiles) * 256u;
+    const uint32_t sid = a.perm ? a.perm[first + k] : k;
+    const uint32_t* t = a.slice_tmp + (size_t)sid * nsl * V;
+    const uint32_t nv = std::min<uint32_t>(256u, V - v0), v = v0 + threadIdx.x;
+    uint8_t* dst = a.nh + out_row_of(a, sid) * (size_t)V * nb + (size_t)v0 * nb;
+    const bool staged = nb <= kMaxNb;
+    if (threadIdx.x < nv) {
+      uint8_t* out = staged ? segb + threadIdx.x * nb : dst + (size_t)threadIdx.x * nb;
+      uint64_t acc = 0;
+      uint32_t have = 0, sl = 0;
+      for (uint32_t j = 0; j < nb; ++j) {
+        while (have < 8u && sl < nsl) {
+          acc |= (uint64_t)t[(size_t)sl * V + v] << have;
+          have += 29u;
+          ++sl;
+        }
+        out[j] = (uint8_t)acc;
+        acc >>= 8;
+        have = have >= 8u ? have - 8u : 0u;
+      }
+    }
+    if (!staged) continue;  // block-uniform
+    __syncthreads();
+    const uint32_t bytes = nv * nb;
+    if ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0) {
+      for (uint32_t i = threadIdx.x; i < bytes / 4u; i += 256u) reinterpret_cast<uint32_t*>(dst)[i] = seg[i];
+      for (uint32_t i = (bytes & ~3u) + threadIdx.x; i < bytes; i += 256u) dst[i] = segb[i];
+    } else {
+      for (uint32_t i = threadIdx.x; i < bytes; i += 256u) dst[i] = segb[i];
+    }
+    __syncthreads();
+  }
+}
+
 uint32_t field_bits(int cls) { return cls == kCls8 ? 8u : cls == kCls16 ? 16u : 32u; }
 }  // namespace
 
@@ -675,7 +713,15 @@ hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     case 8: return launch_bfs_fb<8, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
     case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
     default:
-      if (sliced) return launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+      if (sliced) {
+        if (a.nh && !a.slice_tmp) return hipErrorInvalidValue;
+        hipError_t err = launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
+        if (err != hipSuccess || !a.nh) return err;
+        const uint64_t items = (uint64_t)a.n * ((g.V + 255u) / 256u);  // upper bound: (solve, 256-node tile) pairs
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(items, 8192u);
+        hipLaunchKernelGGL(slice_merge, dim3(std::max(grid, 1u)), dim3(256), 0, s, a, g.V);
+        return hipGetLastError();
+      }
       return launch_bfs_fb<32, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   }
 }

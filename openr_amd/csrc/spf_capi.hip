@@ -75,6 +75,7 @@ struct Device {
   DevBuf<uint64_t> dist, tight;
   DevBuf<uint8_t> nh;
   DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
+  DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -314,6 +315,11 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     a.dist_only = 1;
     a.nsl = 1;
     mask = 1u << kCls8;
+  }
+  if (fam == kFamCode && ((mask >> kClsSliced) & 1u) && a.nh) {
+    hipError_t err = d.slicetmp.reserve((size_t)a.n * a.nsl * d.g.V);
+    if (err != hipSuccess) return err;
+    a.slice_tmp = d.slicetmp.p;
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
@@ -753,6 +759,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.tight.release();
     d.nh.release();
     d.ovf.release();
+    d.slicetmp.release();
     d.work.release();
     d.perm.release();
     d.part.release();

@@ -114,6 +114,9 @@ struct SolveArgs {
   const uint32_t* out_row;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
   uint32_t* order;            // nullable [n][V]: pop index per node (exact-order kernel only)
+  // code-family sliced class with next-hop output: [n][nsl][V] 29-bit chunks of the sets
+  // (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
+  uint32_t* slice_tmp;
 };
 // output row of solve sid (SolveArgs::out_row)
 __host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
@@ -136,8 +139,8 @@ enum BfsFamily : int { kFamCode = 0, kFamLvl = 1, kNumFamilies = 2 };
 
 // Source classes by distinct degree (next-hop bitset width).
 // code family: the per-node field holds the set plus a 3-bit level code in 8 bits
-// (d <= 5), 16 bits (d <= 13) or 32 bits (d <= 24); d > 24 solves in ceil(d / 24)
-// slices of 24 next-hop bits, one workgroup pass per slice.
+// (d <= 5), 16 bits (d <= 13) or 32 bits (d <= 29); d > 29 solves in ceil(d / 29)
+// slices of 29 next-hop bits, one workgroup pass per slice, merged into bytes afterwards.
 enum SrcClass : int { kCls8 = 0, kCls16 = 1, kCls32 = 2, kClsSliced = 3, kNumClasses = 4 };
 // lvl family: next-hop sets of 4 / 8 / 16 / 32 bits; d > 32 in 32-bit slices.
 enum LvlClass : int { kLvl4 = 0, kLvl8 = 1, kLvl16 = 2, kLvl32 = 3, kLvlSliced = 4, kNumLvlClasses = 5 };

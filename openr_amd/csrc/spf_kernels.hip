@@ -73,13 +73,13 @@ int src_class_for_degree(int family, uint32_t d) {
   }
   if (d <= 5) return kCls8;
   if (d <= 13) return kCls16;
-  if (d <= 24) return kCls32;
+  if (d <= 29) return kCls32;
   return kClsSliced;
 }
 
 int num_classes(int family) { return family == kFamLvl ? kNumLvlClasses : kNumClasses; }
 int sliced_class(int family) { return family == kFamLvl ? kLvlSliced : kClsSliced; }
-uint32_t slice_bits(int family) { return family == kFamLvl ? 32u : 24u; }
+uint32_t slice_bits(int family) { return family == kFamLvl ? 32u : 29u; }
 
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls) {
   return family == kFamLvl ? bfs_lvl_lds_bytes(V, L, has_ignore, cls) : bfs_code_lds_bytes(V, L, has_ignore, cls);
