@@ -177,6 +177,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   // a re-run launch with nothing flagged does no work
   const uint32_t units = from_list ? *ovf_count : count * nsl;
+  // nothing flagged: every workgroup leaves at once (no unit is taken, so the scheduling
+  // counters stay at rest and no workgroup needs to retire; saves the 256 retire atomics)
+  if (from_list && units == 0u) return;
 #ifdef OPENR_SPF_PROFILE
   // [0] load (ring + ELL/row), [1] field reads, [2] atomics, [3] append, [4] barrier,
   // [5] init + level 0, [6] write out, [7] passes, [8] levels, [9] solves
