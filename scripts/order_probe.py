@@ -1,18 +1,14 @@
 #!/usr/bin/env python3
-"""Does the order of sources in an all-sources launch matter? (tuning probe)
+"""All-sources G100 kernel time vs the order the batch lists its sources (tuning aid:
+tail balance of the dynamically scheduled solves). Orders: row-major, random, longest
+first (eccentricity descending), shortest first.
 
-Times one all-sources launch with the sources in id order and in descending
-eccentricity order (longest-processing-time first: the dynamically scheduled
-workgroups finish together instead of ending on a tail of deep solves). Rows are
-permuted back and checked equal.
-
-  python scripts/order_probe.py --topology grid100 --rounds 7
+  python scripts/order_probe.py [--reps 10]
 """
 import argparse
 import json
 import os
 import sys
-from collections import deque
 
 import numpy as np
 
@@ -20,75 +16,46 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def eccentricity(g):
-    """Exact hop eccentricity per node (host BFS from every node; probe only)."""
-    V = g.num_nodes
-    rp, col = g.row_ptr, g.col
-    ecc = np.zeros(V, np.int32)
-    for s in range(V):
-        lv = np.full(V, -1, np.int32)
-        lv[s] = 0
-        q = deque([s])
-        m = 0
-        while q:
-            u = q.popleft()
-            for e in range(rp[u], rp[u + 1]):
-                v = int(col[e])
-                if lv[v] < 0:
-                    lv[v] = lv[u] + 1
-                    m = lv[v]
-                    q.append(v)
-        ecc[s] = m
-    return ecc
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--topology", default="grid100")
-    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     import torch
 
-    from bench import build_topology
+    from openr_amd import topology as T
     from openr_amd.engine import SpfEngine
 
-    g, _ = build_topology(args.topology)
+    n = 100
+    g = T.grid_fast(n)
     V = g.num_nodes
-    if args.topology == "grid100":
-        n = 100
-        ecc = np.array([max(r, n - 1 - r) + max(c, n - 1 - c) for r in range(n) for c in range(n)])
-    else:
-        ecc = eccentricity(g)
-    eng = SpfEngine([0])
-    eng.set_graph(g)
-    nb = eng.nh_bytes
+    r, c = np.divmod(np.arange(V), n)
+    ecc = np.maximum(r, n - 1 - r) + np.maximum(c, n - 1 - c)
+    rng = np.random.default_rng(3)
+    orders = {"row-major": np.arange(V), "random": rng.permutation(V),
+              "longest-first": np.argsort(-ecc, kind="stable"), "shortest-first": np.argsort(ecc, kind="stable")}
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    orders = {"id": np.arange(V), "lpt": np.argsort(-ecc, kind="stable"), "spt": np.argsort(ecc, kind="stable"),
-              "rev": np.arange(V)[::-1].copy()}
-    srcs = {k: torch.tensor(v.astype(np.int32), device=dev) for k, v in orders.items()}
+    eng = SpfEngine([0])
+    eng.set_graph(g)
+    nb = eng.nh_bytes
     d_dist = torch.empty((V, V), dtype=torch.int64, device=dev)
     d_nh = torch.empty((V, V, nb), dtype=torch.uint8, device=dev)
-    times = {k: [] for k in orders}
-    rows = {}
-    for r in range(args.rounds):
-        for k in orders:
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record(stream)
-            eng.solve_device(srcs[k].data_ptr(), V, d_dist.data_ptr(), d_nh.data_ptr(), nb, True,
-                             stream=stream.cuda_stream)
-            ev1.record(stream)
-            torch.cuda.synchronize(dev)
-            if r:
-                times[k].append(ev0.elapsed_time(ev1))
-            if r == 0:
-                inv = np.empty(V, np.int64)
-                inv[orders[k]] = np.arange(V)
-                rows[k] = d_dist[torch.tensor(inv, device=dev)][:, :64].cpu().numpy()
-    for k in orders:
-        assert np.array_equal(rows[k], rows["id"]), k
-    print(json.dumps({k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for k, v in times.items()}))
+    for rnd in range(2):
+        for name, p in orders.items():
+            src = torch.from_numpy(np.ascontiguousarray(p, dtype=np.int32)).to(dev)
+            ts = []
+            for i in range(args.reps + 1):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                eng.solve_device(src.data_ptr(), V, d_dist.data_ptr(), d_nh.data_ptr(), nb, True,
+                                 stream=stream.cuda_stream)
+                b.record(stream)
+                torch.cuda.synchronize(dev)
+                if i:
+                    ts.append(a.elapsed_time(b))
+            print(json.dumps({"round": rnd, "order": name, "median_ms": float(np.median(ts)),
+                              "min_ms": float(np.min(ts))}), flush=True)
     eng.close()
 
 
