@@ -430,6 +430,24 @@ def test_source_classes_and_sliced_next_hops(eng, seed):
     check_against_oracle(eng, g, sub, True, ignore=ignore)
 
 
+def test_sliced_next_hops_wide_stride(eng, bfs_family):
+    """Sliced next-hop sets (29-bit code-family chunks merged into bytes, or 32-bit lvl
+    slices) into a caller stride wider than the set: the set's bytes as the oracle's, every
+    byte past them zero."""
+    g = hub_graph(4)
+    eng.set_graph(g)
+    o = Oracle(g)
+    nb = eng.nh_bytes
+    srcs = list(range(0, g.num_nodes, 3))
+    dist, nh, _ = eng.solve(srcs, True, nh_bytes=nb + 5)
+    assert nh.shape[-1] == nb + 5
+    for i, s in enumerate(srcs):
+        run = o.run_spf(int(s), True, None)
+        np.testing.assert_array_equal(dist[i], run.dist, err_msg=f"dist src={s}")
+        np.testing.assert_array_equal(nh[i][:, :nb], run.nh, err_msg=f"nh src={s}")
+    assert not nh[:, :, nb:].any()
+
+
 def test_source_classes_device_partition(eng):
     """solve_device partitions on the GPU: same results as the host-buffer solve."""
     import torch
