@@ -126,6 +126,10 @@ int openr_spf_abi_version(void);
    verify the library was built from the sources it ships with. */
 const char* openr_spf_build_id(void);
 const char* openr_spf_last_error(void);
+/* Diagnostics: "name;name;..." of the kernels the calling thread's last solve call
+   (openr_spf_solve*, _solve_device) enqueued, re-run launches included (tests assert
+   which kernel a configuration runs). */
+const char* openr_spf_last_kernels(void);
 void openr_spf_limits(openr_spf_limits_t* out);
 
 /* device_ids: n_devices HIP ordinals (NULL -> the current device). Sources of one

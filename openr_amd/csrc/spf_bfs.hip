@@ -606,6 +606,7 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
     info->grid = grid;
     info->kernel = RING ? "bfs_code_kernel<ring>" : "bfs_code_kernel<full>";
   }
+  note_launch(RING ? "bfs_code_kernel<ring>" : from_list ? "bfs_code_kernel<full>:rerun" : "bfs_code_kernel<full>");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
                      (uint32_t)from_list, ctr, ovf_count,
                      nt_stores() | (env_u32("OPENR_SPF_CODE_LEAN", 1u, 0u, 1u) ? 0u : 2u));

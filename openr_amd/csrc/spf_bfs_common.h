@@ -30,6 +30,24 @@
 namespace openr_spf {
 namespace bfs {
 
+// LDS through address-space-3 pointers: constant offsets fold into the ds instruction
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u128;
+__device__ __forceinline__ void lds_store4(uint32_t byte_addr, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  u32x4 v = {x, y, z, w};
+  *(lds_u128*)(size_t)byte_addr = v;
+}
+
+__device__ __forceinline__ uint32_t lds_or(lds_u32* p, uint32_t v) {
+  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add(lds_u32* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <typename T>
 __device__ __forceinline__ void store_row(T* p, const T& x, bool nt) {
   if (nt)

@@ -481,16 +481,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 //  * lanes past the frontier read the sentinel row ellv[V] (every slot V, lvl[V] = 0:
 //    never tight), so the pass has no divergent prologue.
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) uint16_t lds_u16;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
-__device__ __forceinline__ uint32_t lds_or(lds_u32* p, uint32_t v) {
-  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t lds_add(lds_u32* p, uint32_t v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 struct LeanLayout {
   uint32_t nh, ring, dummy, total;
 };
@@ -763,6 +753,7 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
     info->kernel = RING ? "bfs_lvl_kernel<ring,u8>" : "bfs_lvl_kernel<full,u16>";
   }
   const uint32_t flags = nt_stores() | (env_u32("OPENR_SPF_FRESH_LVL", 1u, 0u, 1u) << 1);
+  note_launch(RING ? "bfs_lvl_kernel<ring,u8>" : from_list ? "bfs_lvl_kernel<full,u16>:rerun" : "bfs_lvl_kernel<full,u16>");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
                      (uint32_t)from_list, ctr, ovf_count, flags);
   return hipGetLastError();
@@ -791,6 +782,7 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     prof = prof_buf;
     if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
   }
+  note_launch("bfs_ell_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, ctr, ovf_count, nt_stores(), prof);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && prof) {
@@ -1057,6 +1049,7 @@ hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     info->grid = grid;
     info->kernel = "bfs_wave_kernel<lds-graph>";
   }
+  note_launch("bfs_wave_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(64u * waves), lds, s, g, a, cost, qhalf, waves, ctr, ovf_count, nt_stores());
   if (env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u))  // tests: which pass ran
     std::fprintf(stderr, "bfs_wave: grid=%u waves=%u n=%u qhalf=%u lds=%u\n", grid, waves, a.n, qhalf, lds);
@@ -1069,6 +1062,20 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   // Counter block of the class: [0,1] first launch, [2,3] re-run launch, [4] listed units.
   uint32_t* blk = class_counters(a);
   hipError_t err;
+  if constexpr (ELLM == 2 && !SLICED && MODE == kNhNibble) {
+    // all-sources batches: a level pass, then next hops from neighbour level rows
+    // (spf_allsrc.hip); the rows it lists are re-run by the u16 full-order variant
+    if (const int pass = has_ign ? 0 : allsrc_pass(g, a)) {
+      const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
+      const uint32_t qforce = env_u32("OPENR_SPF_REACH_QHALF", 0u, 0u, 65535u);  // tests: force overflows
+      const uint32_t half = qforce ? (std::max<uint32_t>(qforce, g.max_deg + 1u) + 15u) & ~15u
+                                   : (std::max<uint32_t>(64u, need1) + 15u) & ~15u;
+      err = launch_allsrc(pass, g, a, cost, half, blk, num_cus, s, info);
+      if (err != hipSuccess) return err;
+      return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true,
+                                                                          blk + 2, blk + 4, num_cus, s, info);
+    }
+  }
   if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
     const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
     // wave pass (graph in LDS) for small batches when the delta rows fit with >= 4 solve
@@ -1350,6 +1357,7 @@ hipError_t launch_ell16(const DevGraph& g, const SolveArgs& a, uint64_t cost, ui
     info->grid = grid;
     info->kernel = "bfs_ell16_kernel";
   }
+  note_launch("bfs_ell16_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, blk, blk + 4, nt_stores());
   err = hipGetLastError();
   if (err != hipSuccess || (g.V <= ring_cap && g.V <= 253u)) return err;  // nothing can overflow

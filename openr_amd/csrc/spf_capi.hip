@@ -26,6 +26,7 @@ using namespace openr_spf;
 namespace {
 
 thread_local std::string g_last_error;
+thread_local std::string g_launch_trace;  // "kernel;kernel;..." of the last solve call
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -76,6 +77,9 @@ struct Device {
   DevBuf<uint8_t> nh;
   DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
+  // lvl-family reach pass (all-sources batches): u8 level rows, node -> row map, row flags
+  DevBuf<uint8_t> lvl8, rowok;
+  DevBuf<uint32_t> rowmap;
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -114,6 +118,16 @@ void free_graph(DevGraph& g) {
 }
 
 }  // namespace
+
+namespace openr_spf {
+void note_launch(const char* kernel) {
+  if (g_launch_trace.size() < 4096) {
+    g_launch_trace += kernel;
+    g_launch_trace += ';';
+  }
+}
+void clear_launch_trace() { g_launch_trace.clear(); }
+}  // namespace openr_spf
 
 struct openr_spf_ctx {
   std::vector<Device> devs;
@@ -321,6 +335,21 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     if (err != hipSuccess) return err;
     a.slice_tmp = d.slicetmp.p;
   }
+  // reach pass scratch (spf_bfs_lvl.hip: dist-level rows of a whole batch, then next hops
+  // from neighbour rows); only for batches that can hold every source's neighbours
+  a.lvl8 = nullptr;
+  a.rowmap = nullptr;
+  a.rowok = nullptr;
+  if (fam == kFamLvl && !a.tight && !a.ign_ptr && !a.out_row && __builtin_popcount(mask) == 1 &&
+      (a.n >= d.g.V || std::getenv("OPENR_SPF_BFS_REACH") || std::getenv("OPENR_SPF_BFS_MSBFS"))) {
+    hipError_t err = d.lvl8.reserve((size_t)a.n * reach_row_bytes(d.g.V));
+    if (err == hipSuccess) err = d.rowok.reserve(a.n);
+    if (err == hipSuccess) err = d.rowmap.reserve(d.g.V);
+    if (err != hipSuccess) return err;
+    a.lvl8 = d.lvl8.p;
+    a.rowok = d.rowok.p;
+    a.rowmap = d.rowmap.p;
+  }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
     return launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
@@ -354,6 +383,7 @@ int check_solve_args(const openr_spf_ctx* ctx, const uint32_t* sources, uint32_t
 int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags,
                const uint32_t* ignore_ptr, const uint32_t* ignore_links, uint64_t* dist, uint8_t* nh,
                uint32_t nh_bytes, uint64_t* tight, uint32_t* order = nullptr) {
+  clear_launch_trace();
   if (order) flags |= OPENR_SPF_EMIT_ORDER;
   int rc = check_solve_args(ctx, sources, n, dist, nh, nh_bytes);
   if (rc) return rc;
@@ -694,6 +724,8 @@ int openr_spf_abi_version(void) { return OPENR_SPF_ABI_VERSION; }
 
 const char* openr_spf_last_error(void) { return g_last_error.c_str(); }
 
+const char* openr_spf_last_kernels(void) { return g_launch_trace.c_str(); }
+
 void openr_spf_limits(openr_spf_limits_t* out) {
   if (!out) return;
   // Largest V whose LDS-resident BFS state (<= 8 next-hop bits, no ignore set) fits a CU.
@@ -760,6 +792,9 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.nh.release();
     d.ovf.release();
     d.slicetmp.release();
+    d.lvl8.release();
+    d.rowok.release();
+    d.rowmap.release();
     d.work.release();
     d.perm.release();
     d.part.release();
@@ -914,9 +949,14 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
     if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
     if (err == hipSuccess) {
-      std::vector<uint4> ellv(V + 1u, make_uint4(V, V, V, V));  // [V] = sentinel row (lean BFS pass)
+      // [V] = sentinel row (lean BFS pass); [V + 32k], k < 64: the reach pass's per-lane sentinels
+      std::vector<uint4> ellv(ellv_rows(V), make_uint4(V, V, V, V));
       for (uint32_t u = 0; u < V; ++u) ellv[u] = ellv_of(ellt[u], V);
-      err = up(&g.ellv, ellv.data(), V + 1u);
+      for (uint32_t k = 1; k < kReachSentinels; ++k) {
+        const uint32_t s = V + kReachSentinelStride * k;
+        ellv[s] = make_uint4(s, s, s, s);
+      }
+      err = up(&g.ellv, ellv.data(), ellv.size());
       // delta rows (wave pass): every row of <= 4 edges and every column within 127 ids of
       // its row, down edges and overloaded rows included (a patch may bring them back)
       bool delta_ok = true;
@@ -1325,6 +1365,7 @@ int openr_spf_solve_ignore(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t
 int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n,
                            uint32_t flags, const uint32_t* d_ignore_ptr, const uint32_t* d_ignore_links,
                            uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes, uint64_t* d_tight, void* stream) {
+  clear_launch_trace();
   int rc = check_solve_args(ctx, d_sources, n, d_dist, d_nh, nh_bytes);
   if (rc) return rc;
   if (device_index < 0 || device_index >= (int)ctx->devs.size())

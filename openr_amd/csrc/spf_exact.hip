@@ -247,6 +247,7 @@ hipError_t launch_exact(const DevGraph& g, const SolveArgs& a, const uint64_t* w
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)slot);
     if (err != hipSuccess) return err;
   }
+  note_launch("spf_exact_kernel");
   hipLaunchKernelGGL(spf_exact_kernel, dim3(grid), dim3(64), in_lds ? (uint32_t)slot : 0u, s, g, a, w64,
                      (uint32_t)use_metric, nbw, (uint32_t)in_lds, scratch, slot, order_out, ctr);
   return hipGetLastError();

@@ -234,6 +234,7 @@ hipError_t launch_fringe_t(const DevGraph& g, const SolveArgs& a, uint32_t delta
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
+  note_launch("fringe_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, a, delta, (uint32_t)has_ign, ctr);
   return hipGetLastError();
 }

@@ -25,9 +25,10 @@ struct DevGraph {
                                //     (an overloaded node other than the source is never expanded)
   uint32_t* ovl_bits = nullptr;  // [ceil(V/32)] overloaded bitmap (staged into LDS)
   uint4* ellt = nullptr;       // [V] first 4 edges of each transit row (adj encoding, kEdgeDown-padded)
-  uint4* ellv = nullptr;       // [V+1] ellt with every down / padding slot replaced by the node id V (a
+  uint4* ellv = nullptr;       // [ellv_rows(V)] ellt with every down / padding slot replaced by the node id V (a
                                //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests);
-                               //     ellv[V] = (V, V, V, V), the row of a lane past the frontier
+                               //     ellv[V] = (V, V, V, V), the row of a lane past the frontier;
+                               //     ellv[V + 32k] = four copies of V + 32k (reach pass sentinels)
   uint32_t* elld = nullptr;    // [V] ellv as four signed byte deltas (v - u; 0 = no edge), or null
                                //     when a row has > 4 edges or a column > 127 ids away (wave pass)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
@@ -78,6 +79,10 @@ struct LaunchInfo {
   uint32_t grid = 0;
   const char* kernel = "";
 };
+// Launch trace (openr_spf_last_kernels): every solve launcher records the kernel it
+// enqueued; the C-ABI clears the calling thread's trace at the start of each solve call.
+void note_launch(const char* kernel);
+void clear_launch_trace();
 
 struct SolveArgs {
   const uint32_t* sources;
@@ -117,7 +122,21 @@ struct SolveArgs {
   // code-family sliced class with next-hop output: [n][nsl][V] 29-bit chunks of the sets
   // (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
   uint32_t* slice_tmp;
+  // reach pass + next hops from neighbour level rows (spf_bfs_lvl.hip, all-sources batches
+  // on ELL-only graphs), all nullable (then the pass is not used): u8 level rows
+  // [n][reach_row_bytes(V)] (0xFF = unreached), node -> batch row map [V] (UINT32_MAX =
+  // not in the batch), per-row "level row valid" flags [n]
+  uint8_t* lvl8;
+  uint32_t* rowmap;
+  uint8_t* rowok;
 };
+// Row stride of SolveArgs::lvl8 (16-byte rows: the next-hop pass reads 16 levels per load)
+__host__ __device__ inline uint32_t reach_row_bytes(uint32_t V) { return (V + 15u) & ~15u; }
+// Reach pass sentinels: a lane past the frontier reads the ELL row of node V + 32 * lane,
+// four copies of its own id, whose visited bit lies in a dword of its own (DevGraph::ellv
+// holds these rows; every id >= V is pre-marked visited, so a sentinel slot never appends)
+constexpr uint32_t kReachSentinels = 64, kReachSentinelStride = 32;
+__host__ __device__ constexpr uint32_t ellv_rows(uint32_t V) { return V + kReachSentinelStride * (kReachSentinels - 1u) + 1u; }
 // output row of solve sid (SolveArgs::out_row)
 __host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
   return a.out_row ? (size_t)a.out_row[sid] : (size_t)sid;
@@ -274,6 +293,15 @@ hipError_t launch_exact(const DevGraph& g, const SolveArgs& a, const uint64_t* w
 uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
+
+// All-sources batches on uniform-cost graphs with rows of <= 4 edges (spf_allsrc.hip):
+// a level pass (2: bit-parallel multi-source BFS, 1: per-source reach pass; 0: neither
+// applies) writes u8 level rows, then every next-hop set is derived from the level rows of
+// the source's neighbours. Rows it cannot finish are appended to a.ovf_list (count in
+// blk[4]) for the caller's u16 full-order re-run. `half` = the reach pass's queue half.
+int allsrc_pass(const DevGraph& g, const SolveArgs& a);
+hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t half, uint32_t* blk,
+                         int num_cus, hipStream_t s, LaunchInfo* info);
 uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
 

@@ -245,6 +245,7 @@ hipError_t launch_rounds_t(const DevGraph& g, const SolveArgs& a, uint32_t lds, 
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
+  note_launch("rounds_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, a, (uint32_t)has_ign, ctr);
   return hipGetLastError();
 }

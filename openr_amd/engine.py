@@ -28,6 +28,7 @@ EXPORTS = (
     "openr_spf_abi_version",
     "openr_spf_build_id",
     "openr_spf_last_error",
+    "openr_spf_last_kernels",
     "openr_spf_limits",
     "openr_spf_create",
     "openr_spf_destroy",
@@ -115,6 +116,7 @@ def load_library():
     l.openr_spf_build_id.restype = ctypes.c_char_p
     check_build_id(l.openr_spf_build_id().decode(), LIB_PATH)
     l.openr_spf_last_error.restype = ctypes.c_char_p
+    l.openr_spf_last_kernels.restype = ctypes.c_char_p
     l.openr_spf_limits.argtypes = [P(SpfLimits)]
     l.openr_spf_limits.restype = None
     l.openr_spf_create.argtypes = [vp, ctypes.c_int, P(vp)]
@@ -136,7 +138,8 @@ def load_library():
     l.openr_spf_refresh_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, u32, vp, vp, P(u32)]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
     for name in EXPORTS:
-        if name not in ("openr_spf_last_error", "openr_spf_limits", "openr_spf_destroy", "openr_spf_build_id"):
+        if name not in ("openr_spf_last_error", "openr_spf_last_kernels", "openr_spf_limits", "openr_spf_destroy",
+                        "openr_spf_build_id"):
             getattr(l, name).restype = ctypes.c_int
     _lib = l
     return l
@@ -345,6 +348,10 @@ class SpfEngine:
                                                   vp(d_nh or None), nh_bytes or self.nh_bytes, vp(d_tight or None),
                                                   vp(stream or None), ctypes.byref(out)))
         return int(out.value)
+
+    def last_kernels(self) -> list:
+        """Kernels this thread's last solve call enqueued (openr_spf_last_kernels)."""
+        return [k for k in self._lib.openr_spf_last_kernels().decode().split(";") if k]
 
     def stats(self) -> SpfStats:
         s = SpfStats()

@@ -33,8 +33,11 @@ def eng():
     e.close()
 
 
-def all_sources_vs_oracle(eng, g, chunk, use_metric=True):
-    """Every source of g: engine dist + next-hop rows == oracle rows, chunk by chunk."""
+def all_sources_vs_oracle(eng, g, chunk, use_metric=True, expect_kernel=None, check_chunk=2500):
+    """Every source of g: engine dist + next-hop rows == oracle rows. The engine solves
+    `chunk` sources per call (one launch, as bench.py does at chunk = V); the rows are
+    compared against the oracle `check_chunk` at a time. expect_kernel: the kernel every
+    call must have run (openr_spf_last_kernels)."""
     eng.set_graph(g)
     o = Oracle(g)
     assert eng.nh_bytes == o.nh_bytes
@@ -42,11 +45,17 @@ def all_sources_vs_oracle(eng, g, chunk, use_metric=True):
     for lo in range(0, V, chunk):
         srcs = np.arange(lo, min(V, lo + chunk), dtype=np.uint32)
         dist, nh, _ = eng.solve(srcs, use_metric)
-        odist, onh = o.all_sources(srcs, use_metric, nthreads=16)
-        bad = np.nonzero(np.any(dist != odist, axis=1))[0]
-        assert bad.size == 0, f"dist differs for sources {srcs[bad[:8]].tolist()}"
-        bad = np.nonzero(np.any(nh != onh, axis=(1, 2)))[0]
-        assert bad.size == 0, f"next hops differ for sources {srcs[bad[:8]].tolist()}"
+        if expect_kernel is not None:
+            ran = eng.last_kernels()
+            assert expect_kernel in ran, ran
+        for clo in range(0, len(srcs), check_chunk):
+            sub = srcs[clo:clo + check_chunk]
+            odist, onh = o.all_sources(sub, use_metric, nthreads=16)
+            d, n = dist[clo:clo + check_chunk], nh[clo:clo + check_chunk]
+            bad = np.nonzero(np.any(d != odist, axis=1))[0]
+            assert bad.size == 0, f"dist differs for sources {sub[bad[:8]].tolist()}"
+            bad = np.nonzero(np.any(n != onh, axis=(1, 2)))[0]
+            assert bad.size == 0, f"next hops differ for sources {sub[bad[:8]].tolist()}"
 
 
 def pathlinks_vs_oracle(eng, g, sources, use_metric=True):
@@ -82,16 +91,40 @@ def test_config2_fabric5000_all_sources(eng, faithful):
     4 992 sources, ECMP next-hop sets up to 84 bits wide; both generator variants."""
     g = T.fabric(5000, faithful=faithful)
     assert g.num_nodes == 4992 and g.num_links == (56448 if not faithful else 32544)
-    all_sources_vs_oracle(eng, g, 1248)
+    # all 4 992 sources in one call, as bench.py launches them
+    all_sources_vs_oracle(eng, g, 4992, check_chunk=1248)
     pathlinks_vs_oracle(eng, g, [0, 287, 288, 959, 960, 4991])
 
 
 def test_config3_grid100_all_sources(eng):
-    """100x100 grid, all 10 000 sources (the headline workload; its multi-GPU sharding is
-    tests/test_gpu_multirank.py), plus pathLinks of a source sample."""
+    """100x100 grid, all 10 000 sources in ONE launch (the benchmarked configuration:
+    bench.py solves them in one call, which runs the multi-source pass msbfs_kernel and the
+    next-hop pass nh_from_levels_kernel), every row against the oracle; plus pathLinks of a
+    source sample."""
     g = T.grid_fast(100)
-    all_sources_vs_oracle(eng, g, 2500)
+    all_sources_vs_oracle(eng, g, 10000, expect_kernel="msbfs_kernel")
     pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
+
+
+@pytest.mark.parametrize("chunk,env,kernel", [
+    (10000, {"OPENR_SPF_BFS_MSBFS": "0"}, "bfs_reach_kernel"),
+    (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0"}, "bfs_ell_kernel"),
+    (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0", "OPENR_SPF_BFS_WAVE": "1"}, "bfs_wave_kernel"),
+    (1250, {}, "bfs_wave_kernel"),
+    (1250, {"OPENR_SPF_BFS_WAVE": "0"}, "bfs_ell_kernel"),
+    (1250, {"OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
+    (1250, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_kernel"),
+], ids=["full-batch-reach", "full-batch-lean", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
+        "shard1250-msbfs"])
+def test_config3_grid100_pass_variants(eng, monkeypatch, chunk, env, kernel):
+    """Config 3's other launch shapes, every row against the oracle: the full batch on the
+    reach pass and the round-2 lean and wave passes, and the 1 250-source shards of an
+    8-GPU strong-scaling run (per-GPU step: the wave pass by default; the lean pass; the
+    reach and multi-source passes, whose shard-boundary sources lack neighbour rows and
+    take the re-run)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    all_sources_vs_oracle(eng, T.grid_fast(100), chunk, expect_kernel=kernel)
 
 
 @pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "group-cap", "incr", "solve"])
