@@ -162,10 +162,10 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
   for (auto const& [area, ls] : als) {  // one all-sources batch covers every node and its neighbours
     std::vector<std::string> present;
     for (auto const& n : nodes)
-      // a parallel build also memoises the self-only result of a node this area lacks but
-      // another has (createRouteForPrefix and the label routes read it in every area),
-      // which the sequential build adds on demand
-      if (ls.hasNode(n) || (workers > 1 && known(n))) present.push_back(n);
+      // also the self-only result of a node this area lacks but another has
+      // (createRouteForPrefix and the label routes read it in every area): prefetched
+      // results count as SPF runs only when read, so counters equal the one-thread loop's
+      if (ls.hasNode(n) || known(n)) present.push_back(n);
     if (computeLfaPaths_) {
       std::set<std::string> more(present.begin(), present.end());
       for (auto const& n : present)
@@ -196,11 +196,16 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
       last = i;
       break;
     }
-  parallelFor(nodes.size(), 1, workers, [&](unsigned w, size_t i) {
-    auto db = solvers[w].buildRouteDb(nodes[i], als, prefixState);
-    if (i == last) bestRoutesCache_ = solvers[w].bestRoutesCache_;
-    sink(i, db);
-  });
+  {
+    // the workers only read memoised SPFs: a read the prefetch above missed throws
+    std::vector<std::unique_ptr<LinkState::MemoFreeze>> frozen;
+    for (auto const& [_, ls] : als) frozen.push_back(std::make_unique<LinkState::MemoFreeze>(ls));
+    parallelFor(nodes.size(), 1, workers, [&](unsigned w, size_t i) {
+      auto db = solvers[w].buildRouteDb(nodes[i], als, prefixState);
+      if (i == last) bestRoutesCache_ = solvers[w].bestRoutesCache_;
+      sink(i, db);
+    });
+  }
   for (auto const& s : solvers) {
     auto const& c = s.counters_;
     counters_.route_build_runs += c.route_build_runs;
@@ -416,9 +421,8 @@ BestRouteSelectionResult SpfSolver::runBestPathSelectionBgp(thrift::IpPrefix con
       case CompareResult::TIE_LOOSER:
         ret.allNodeAreas.emplace(na);
         break;
-      case CompareResult::TIE:    // "Tie ordering prefix entries. Skipping route"
-      case CompareResult::ERROR:  // "Error ordering prefix entries. Skipping route"
-        counters_.skipped_unicast_route++;
+      case CompareResult::TIE:    // "Tie ordering prefix entries. Skipping route" (logged, not counted:
+      case CompareResult::ERROR:  // Decision.cpp:830-837; createRouteForPrefix :503-505 adds nothing)
         return ret;
       default:
         break;

@@ -26,11 +26,24 @@ SpfCounters& SpfCounters::get() {
   return c;
 }
 void SpfCounters::addSpfRun(double ms, uint64_t runs) {
+  std::lock_guard<std::mutex> g(mu_);
   runs_ += runs;
   msSum_ += ms;
   samples_ += 1;
 }
-void SpfCounters::reset() { *this = SpfCounters(); }
+void SpfCounters::reset() {
+  std::lock_guard<std::mutex> g(mu_);
+  runs_ = samples_ = 0;
+  msSum_ = 0.0;
+}
+uint64_t SpfCounters::spfRuns() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return runs_;
+}
+double SpfCounters::spfMsAvg() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return samples_ ? msSum_ / (double)samples_ : 0.0;
+}
 
 // ---------------------------------------------------------------------------
 // HoldableValue (reference LinkState.cpp:54-125)
@@ -503,12 +516,20 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
   return best;
 }
 
+void LinkState::throwIfFrozen(const char* what, const std::string& key) const {
+  if (frozen_.v.load(std::memory_order_relaxed))
+    throw std::logic_error(std::string("LinkState::") + what + "(" + key +
+                           "): memo miss while the memo is frozen (a parallel route build read a result its "
+                           "prefetch did not cover)");
+}
+
 std::vector<LinkState::Path> const& LinkState::getKthPaths(const std::string& src, const std::string& dest,
                                                            size_t k) const {
   if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");  // CHECK_GE(k, 1)
   const auto key = std::make_tuple(src, dest, k);
   auto it = kthPathResults_.find(key);
   if (it != kthPathResults_.end()) return it->second;
+  throwIfFrozen("getKthPaths", src + "->" + dest);
   if (k <= 2) {  // prefetched: replay the memo and counter effects of the call sequence below
     auto st = kthStaged_.find(std::make_pair(src, dest));
     if (st != kthStaged_.end()) {
@@ -552,18 +573,36 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(const std::string& sr
 LinkState::SpfResult const& LinkState::getSpfResult(const std::string& nodeName, bool useLinkMetric) const {
   const auto key = std::make_pair(nodeName, useLinkMetric);
   auto it = spfResults_.find(key);
-  if (it == spfResults_.end()) it = spfResults_.emplace(key, runSpf(nodeName, useLinkMetric)).first;
-  return it->second;
+  if (it == spfResults_.end()) {  // LinkState.cpp:793-803: a miss runs the SPF
+    throwIfFrozen("getSpfResult", nodeName);
+    SpfResult res = runSpf(nodeName, useLinkMetric);
+    it = spfResults_.emplace(std::piecewise_construct, std::forward_as_tuple(key), std::forward_as_tuple()).first;
+    it->second.res = std::move(res);
+    it->second.counted.v.store(1, std::memory_order_relaxed);
+  } else if (!it->second.counted.v.exchange(1, std::memory_order_relaxed)) {
+    SpfCounters::get().addSpfRun(it->second.ms);  // prefetched: its run counts at this first read
+  }
+  return it->second.res;
 }
 
 void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric) const {
   std::vector<std::string> missing;
   for (auto const& n : nodes)
     if (!spfResults_.count(std::make_pair(n, useLinkMetric))) missing.push_back(n);
+  std::sort(missing.begin(), missing.end());
+  missing.erase(std::unique(missing.begin(), missing.end()), missing.end());
   if (missing.empty()) return;
-  auto results = runSpfBatch(missing, useLinkMetric, std::vector<const LinkSet*>(missing.size(), nullptr));
-  for (size_t i = 0; i < missing.size(); ++i)
-    spfResults_.emplace(std::make_pair(missing[i], useLinkMetric), std::move(results[i]));
+  throwIfFrozen("prefetchSpfResults", missing.front());
+  double ms = 0;
+  auto results = runSpfBatch(missing, useLinkMetric, std::vector<const LinkSet*>(missing.size(), nullptr), &ms);
+  for (size_t i = 0; i < missing.size(); ++i) {
+    auto it = spfResults_
+                  .emplace(std::piecewise_construct, std::forward_as_tuple(std::make_pair(missing[i], useLinkMetric)),
+                           std::forward_as_tuple())
+                  .first;
+    it->second.res = std::move(results[i]);
+    it->second.ms = ms / (double)missing.size();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -688,7 +727,8 @@ void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::
 }
 
 std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,
-                                                         const std::vector<const LinkSet*>& ignores) const {
+                                                         const std::vector<const LinkSet*>& ignores,
+                                                         double* msOut) const {
   const auto t0 = std::chrono::steady_clock::now();
   const CsrMirror& m = csrMirror();
   std::vector<SpfResult> out(srcs.size());
@@ -796,13 +836,14 @@ std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::
       }
     });
   }
-  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  SpfCounters::get().addSpfRun(ms, srcs.size());  // decision.spf_runs counts logical SPFs
+  *msOut = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return out;
 }
 
 LinkState::SpfResult LinkState::runSpf(const std::string& src, bool useLinkMetric, const LinkSet& linksToIgnore) const {
-  auto v = runSpfBatch({src}, useLinkMetric, {&linksToIgnore});
+  double ms = 0;
+  auto v = runSpfBatch({src}, useLinkMetric, {&linksToIgnore}, &ms);
+  SpfCounters::get().addSpfRun(ms);  // decision.spf_runs counts logical SPFs (LinkState.cpp:815, :880)
   return std::move(v[0]);
 }
 

@@ -13,11 +13,13 @@
 // BinaryAddress. In the real tree the generated types replace them.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -114,16 +116,29 @@ struct AdjacencyDatabase {
 
 // fb303-style counters of the SPF path: decision.spf_runs (COUNT) and decision.spf_ms
 // (AVG), as recorded by the reference at LinkState.cpp:815 and :880.
+// Thread-safe: route builds of many nodes run on host worker threads (SpfSolver::buildRouteDbs).
 struct SpfCounters {
   static SpfCounters& get();
   void addSpfRun(double ms, uint64_t runs = 1);
   void reset();
-  uint64_t spfRuns() const { return runs_; }
-  double spfMsAvg() const { return samples_ ? msSum_ / (double)samples_ : 0.0; }
+  uint64_t spfRuns() const;
+  double spfMsAvg() const;
 
  private:
+  mutable std::mutex mu_;
   uint64_t runs_ = 0, samples_ = 0;
   double msSum_ = 0.0;
+};
+
+// A flag that copies / moves by value (so structs holding it stay movable)
+struct RelaxedFlag {
+  std::atomic<int> v{0};
+  RelaxedFlag() = default;
+  RelaxedFlag(const RelaxedFlag& o) : v(o.v.load(std::memory_order_relaxed)) {}
+  RelaxedFlag& operator=(const RelaxedFlag& o) {
+    v.store(o.v.load(std::memory_order_relaxed), std::memory_order_relaxed);
+    return *this;
+  }
 };
 
 template <class T>
@@ -253,7 +268,24 @@ class LinkState {
 
   // Batched prefetch (new): one engine launch fills the memo for every node in
   // `nodes` (e.g. me + neighbours for LFA, or all nodes for all-sources route build).
+  // A prefetched result counts as an SPF run (decision.spf_runs / spf_ms) when it is first
+  // read, where the reference's memo miss would have run it: counters do not depend on
+  // what was prefetched, nor on how many threads read.
   void prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
+
+  // While a MemoFreeze is alive the SPF memos are read-only: several threads may read
+  // results the prefetch covered (getSpfResult / getKthPaths), and a read the prefetch did
+  // not cover throws std::logic_error instead of solving and inserting concurrently.
+  class MemoFreeze {
+   public:
+    explicit MemoFreeze(const LinkState& ls) : ls_(ls) { ls_.frozen_.v.fetch_add(1); }
+    ~MemoFreeze() { ls_.frozen_.v.fetch_sub(1); }
+    MemoFreeze(const MemoFreeze&) = delete;
+    MemoFreeze& operator=(const MemoFreeze&) = delete;
+
+   private:
+    const LinkState& ls_;
+  };
 
   std::vector<LinkState::Path> const& getKthPaths(const std::string& src, const std::string& dest,
                                                   size_t k) const;
@@ -327,7 +359,16 @@ class LinkState {
 
  private:
   const std::string area_;
-  mutable std::unordered_map<std::pair<std::string, bool>, SpfResult> spfResults_;
+  // memo entry: the result, and whether its logical SPF run has been counted (a prefetched
+  // entry is counted on its first read, with its share of the batch's time)
+  struct MemoEntry {
+    SpfResult res;
+    RelaxedFlag counted;
+    double ms = 0;
+  };
+  mutable std::unordered_map<std::pair<std::string, bool>, MemoEntry> spfResults_;
+  mutable RelaxedFlag frozen_;  // MemoFreeze depth
+  void throwIfFrozen(const char* what, const std::string& key) const;
   mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<LinkState::Path>>
       kthPathResults_;
   struct StagedKsp2 {
@@ -349,9 +390,11 @@ class LinkState {
   void removeNode(const std::string& nodeName);
   bool updateNodeOverloaded(const std::string& nodeName, bool isOverloaded, LinkStateMetric holdUpTtl,
                             LinkStateMetric holdDownTtl);
+  // one logical SPF (counted in decision.spf_runs)
   SpfResult runSpf(const std::string& src, bool useLinkMetric, const LinkSet& linksToIgnore = {}) const;
+  // a batch of SPFs, NOT counted (callers count when the reference would); *ms = wall time
   std::vector<SpfResult> runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,
-                                     const std::vector<const LinkSet*>& ignores) const;
+                                     const std::vector<const LinkSet*>& ignores, double* ms) const;
   std::shared_ptr<Link> maybeMakeLink(const std::string& nodeName, const thrift::Adjacency& adj) const;
   std::vector<std::shared_ptr<Link>> getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const;
   std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;

@@ -388,8 +388,8 @@ __global__ __launch_bounds__(64 * kNhlWaves) void nh_from_levels_kernel(DevGraph
 // rows, four u16 byte offsets into F per node (8 B: one ds_read_b64). Thread t owns nodes t + 512 i (consecutive lanes,
 // consecutive nodes: conflict-free banks) and keeps per node in registers its levels as 8
 // bit-planes (plane b holds bit j iff bit b of the level of (source j, node) is set); a
-// source's own bit is set in every plane (level 0xFF marks level 0: levels stop at 254), so
-// the visited word is the OR of the planes and takes no register. Planes 0-1 take a step's new bits where the level's low bits are set (the
+// source's own bit is set in every plane (level 0xFF marks level 0: levels stop at 254, so
+// 0xFF is free), and a visited word per node. Planes 0-1 take a step's new bits where the level's low bits are set (the
 // level loop is unrolled by 4, so that is compile-time), planes 2-7 under uniform masks.
 // A level ends with a barrier whose flag tells whether any node gained a bit; a batch
 // deeper than 254 levels is abandoned and its rows listed for the u16 full-order re-run.
@@ -455,8 +455,8 @@ struct MsUnroll {
 // chunk c + 1, then chunk c's arithmetic and frontier stores.
 constexpr uint32_t kMsChunk = 4;
 template <uint32_t NPT, uint32_t CUR, uint32_t NXT>
-__device__ __forceinline__ uint32_t ms_step(const MsBases& ab, uint32_t sink, uint32_t (&p)[8][NPT],
-                                            const uint32_t (&hm)[8]) {
+__device__ __forceinline__ uint32_t ms_step(const MsBases& ab, uint32_t sink, uint32_t (&vis)[NPT],
+                                            uint32_t (&p)[8][NPT], const uint32_t (&hm)[8]) {
   typedef __attribute__((address_space(3))) uint64_t lds_u64;
   static_assert(NPT % kMsChunk == 0, "whole chunks");
   constexpr uint32_t NC = NPT / kMsChunk;
@@ -484,9 +484,8 @@ __device__ __forceinline__ uint32_t ms_step(const MsBases& ab, uint32_t sink, ui
     for (uint32_t r = 0; r < kMsChunk; ++r) {
       constexpr uint32_t i0 = kMsChunk * c;
       const uint32_t i = i0 + r;
-      // visited = any plane bit (a source's own bit is set in every plane: level 0xFF marks it)
-      const uint32_t vis = (p[0][i] | p[1][i] | p[2][i]) | (p[3][i] | p[4][i] | p[5][i]) | (p[6][i] | p[7][i]);
-      const uint32_t nw = acc[r] & ~vis;
+      const uint32_t nw = acc[r] & ~vis[i];
+      vis[i] |= nw;
       ms_wr(ab.wb[NXT != 0u] + 4u * kMsThreads * i, ((sink >> i) & 1u) ? 0u : nw);
 #pragma unroll
       for (uint32_t b = 0; b < 8u; ++b) {
@@ -564,13 +563,13 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
     __syncthreads();
     // levels as bit-planes; a source's own bit reads level 0xFF (all planes), a node >= V
     // is "visited" for every source so it never gains a bit
-    uint32_t p[8][NPT];
+    uint32_t vis[NPT], p[8][NPT];
 #pragma unroll
     for (uint32_t i = 0; i < NPT; ++i) {
       const uint32_t v = tb + kMsThreads * i;
-      const uint32_t own = v < V ? ms_rd(4u * v) : ~0u;
+      vis[i] = v < V ? ms_rd(4u * v) : ~0u;
 #pragma unroll
-      for (uint32_t b = 0; b < 8u; ++b) p[b][i] = own;
+      for (uint32_t b = 0; b < 8u; ++b) p[b][i] = vis[i];
     }
     uint32_t L = 0;
     bool ovf = false;
@@ -595,9 +594,9 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
         break;
       }
       masks();
-      if (!level_end(ms_step<NPT, 0, Lay::kF1>(ab, sink, p, hm))) break;
+      if (!level_end(ms_step<NPT, 0, Lay::kF1>(ab, sink, vis, p, hm))) break;
       masks();
-      if (!level_end(ms_step<NPT, Lay::kF1, 0>(ab, sink, p, hm))) break;
+      if (!level_end(ms_step<NPT, Lay::kF1, 0>(ab, sink, vis, p, hm))) break;
     }
     if (ovf) {
       if (tid < nbk) {

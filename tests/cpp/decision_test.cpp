@@ -1269,9 +1269,12 @@ TEST_GPU(BGPRedistribution_BasicOperation) {
     EXPECT_TRUE(r->bestPrefixEntry.type == thrift::PrefixType::BGP && r->bestPrefixEntry.data == "data1");
     EXPECT_FALSE(r->doNotInstall);
   }
-  // node 2 with the same metric vector: no best path, the route goes
+  // node 2 with the same metric vector: no best path, the route goes; the tie is logged,
+  // not counted (Decision.cpp:830-837, createRouteForPrefix :503-505)
   ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));
+  const uint64_t skipped0 = solver.counters().skipped_unicast_route;
   EXPECT_EQ(1u, routes("1"));
+  EXPECT_EQ(skipped0, solver.counters().skipped_unicast_route);
   // node 2's last metric lower: node 1 again
   mv2.metrics[4].metric.front()--;
   ps.updatePrefix("2", kDefaultArea, bgp(mv2, "data2"));

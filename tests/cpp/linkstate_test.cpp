@@ -537,7 +537,7 @@ TEST_GPU(DecisionTest_Grid_ShortestPath) {
     for (int v = 0; v < n * n; ++v) all.push_back(std::to_string(v));
     SpfCounters::get().reset();
     ls.prefetchSpfResults(all);
-    EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());
+    EXPECT_EQ(0u, SpfCounters::get().spfRuns());  // prefetched runs count when first read
     bool ok = true;
     for (int a = 0; a < n * n; ++a)
       for (int b = 0; b < n * n; ++b) {
@@ -548,6 +548,35 @@ TEST_GPU(DecisionTest_Grid_ShortestPath) {
     EXPECT_TRUE(ok);
     EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());  // all served by the memo
   }
+}
+
+// The memo under LinkState::MemoFreeze (SpfSolver::buildRouteDbs' worker threads): reads
+// the prefetch covered are served, a miss throws instead of solving concurrently; prefetched
+// results count as SPF runs when first read (the reference's memo-miss accounting).
+TEST_GPU(LinkState_FrozenMemoMissThrows) {
+  LinkState ls(kArea);
+  ls.updateAdjacencyDatabase(
+      createAdjDb("1", {createAdjacency("2", "1/2", "2/1", 10), createAdjacency("3", "1/3", "3/1", 10)}, 1));
+  ls.updateAdjacencyDatabase(createAdjDb("2", {createAdjacency("1", "2/1", "1/2", 10)}, 2));
+  ls.updateAdjacencyDatabase(createAdjDb("3", {createAdjacency("1", "3/1", "1/3", 10)}, 3));
+  SpfCounters::get().reset();
+  ls.prefetchSpfResults({"1", "2"});
+  EXPECT_EQ(0u, SpfCounters::get().spfRuns());
+  {
+    LinkState::MemoFreeze freeze(ls);
+    EXPECT_EQ(10u, ls.getSpfResult("1").at("2").metric());
+    EXPECT_EQ(1u, SpfCounters::get().spfRuns());
+    ls.getSpfResult("1");  // a memo hit: no new run
+    EXPECT_EQ(1u, SpfCounters::get().spfRuns());
+    EXPECT_THROW(ls.getSpfResult("3"));
+    EXPECT_THROW(ls.getSpfResult("1", false));
+    EXPECT_THROW(ls.getKthPaths("1", "3", 1));
+    EXPECT_THROW(ls.prefetchSpfResults({"3"}));
+  }
+  EXPECT_EQ(20u, ls.getSpfResult("3").at("2").metric());  // unfrozen: a miss solves again
+  EXPECT_EQ(2u, SpfCounters::get().spfRuns());
+  ls.getSpfResult("2");
+  EXPECT_EQ(3u, SpfCounters::get().spfRuns());
 }
 
 // Random topologies through the full adjacency-database path: every getSpfResult and
