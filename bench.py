@@ -36,6 +36,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "all-sources SPF solves/sec + edge relax/s (% HBM roofline), 10k-node grid, 1-8 GPU"
+# The faithful-cost CPU model (oracle/spf_faithful.cpp) against the reference's own runSpf:
+# SURVEY.md section 6 times the shim-compiled reference at 15.3 ms per G100 solve (1 core, the
+# survey container); the faithful model takes 14.5 ms per G100 solve in this container
+# (1 core, 40 evenly spaced sources), so its figures stand for the reference within ~5 %.
+CPU_CALIBRATION = {"reference_ms_per_g100_solve": 15.3, "faithful_ms_per_g100_solve": 14.5,
+                   "faithful_over_reference": 14.5 / 15.3,
+                   "source": "SURVEY.md section 6 (reference, shim-compiled) vs oracle/spf_faithful.cpp, 1 core"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -44,6 +51,8 @@ def build_topology(name: str):
 
     if name == "grid100":
         return T.grid_fast(100), {"workload": "grid100-all-sources", "nodes": 10000, "links": 19800}
+    if name == "grid10":  # BASELINE config 1 (DecisionBenchmark 10x10 grid)
+        return T.grid_fast(10), {"workload": "grid10-all-sources", "nodes": 100, "links": 180}
     if name == "fabric":
         g = T.fabric(5000)
         return g, {"workload": "fabric5000-all-sources", "nodes": g.num_nodes, "links": g.num_links}
@@ -118,6 +127,10 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
     except Exception:
         cpu_model = "unknown"
     main = variants[f"faithful_{nthreads}threads"]
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        affinity = os.cpu_count() or 1
     return {
         "value": main["solves_per_s"],
         "unit": "solves/s",
@@ -125,8 +138,10 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
         "kind": "port",
         "cost_model": "faithful: reference data structures (oracle/spf_faithful.cpp)",
         "sample": f"{main['solves']} evenly spaced sources of {V}, runSpf with std::string-keyed LinkState "
-                  f"replicas, {nthreads} threads (this process's CPU share of the box), {main['seconds']:.1f}s; "
-                  f"{cpu_model}",
+                  f"replicas, {nthreads} threads, {main['seconds']:.1f}s; {cpu_model}",
+        "threads_note": f"{nthreads} threads = min(affinity {affinity}, 16): 16 is the host CPU share the GPU box "
+                        f"gives one GPU's job (worker pools are capped at 16 there), a cap, not the machine",
+        "calibration": CPU_CALIBRATION,
         "variants": variants,
     }
 
@@ -650,7 +665,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--topology", default="grid100", choices=["grid100", "fabric", "wan"])
+    ap.add_argument("--topology", default="grid100", choices=["grid100", "grid10", "fabric", "wan"])
     ap.add_argument("--no-metric", action="store_true", help="hop-count SPF (useLinkMetric=false)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -750,8 +765,9 @@ def all_sources_main(args):
     elapsed = max_over_ranks(elapsed, dev)  # the slowest rank's clock
 
     # correctness spot check (grid: Manhattan distances) outside the timed region
-    if args.topology == "grid100" and n_local:
-        n = 100
+    grid_n = {"grid100": 100, "grid10": 10}.get(args.topology)
+    if grid_n and n_local:
+        n = grid_n
         rows = [0, n_local - 1]
         host = d_dist[rows].cpu().numpy().view(np.uint64)
         a = np.arange(V)
@@ -775,13 +791,13 @@ def all_sources_main(args):
         barrier()
         gel = max_over_ranks(time.perf_counter() - tg, dev)
         # the gathered rows are the full all-sources result on every rank
-        if args.topology == "grid100":
+        if grid_n:
             full = gb.full_dist()
             r_chk = [0, V // 2, V - 1]
             host = full[r_chk].cpu().numpy().view(np.uint64)
             a = np.arange(V)
             for i, s in enumerate(r_chk):
-                exp = np.abs(s % 100 - a % 100) + np.abs(s // 100 - a // 100)
+                exp = np.abs(s % grid_n - a % grid_n) + np.abs(s // grid_n - a // grid_n)
                 assert np.array_equal(host[i].astype(np.int64), exp), "gathered result check failed"
         gather = {"ms_per_step": gel / args.steps * 1e3, "bytes_per_rank": int(V * V * (8 + nb)),
                   "gather_inclusive_value": V * args.steps / gel,
@@ -819,7 +835,7 @@ def all_sources_main(args):
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (reference benchmark grid generator, unit metrics)"
-                    if args.topology == "grid100" else "synthetic (benchmark generators)",
+                    if grid_n else "synthetic (benchmark generators)",
             "config": dict(cfg, **{"sources_per_step": solves_total // args.steps, "sources_per_rank": n_local,
                                    "use_link_metric": use_metric,
                                    "parallelism": (f"source-sharded x{world}" if strong else f"area-per-GPU x{world}")}),

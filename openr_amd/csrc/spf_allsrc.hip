@@ -246,6 +246,24 @@ __global__ void reach_map_fill_kernel(uint32_t* rowmap, const uint32_t* sources,
     if (sources[k] < V) rowmap[sources[k]] = k;
 }
 
+// Batch order of the multi-source BFS: when the call's sources are every node exactly once
+// (rowmap[sources[k]] == k for all k and n == V), position i takes the row of the i-th node
+// of the cluster order (DevGraph::corder), else row i.
+__global__ void ms_perm_count_kernel(const uint32_t* sources, uint32_t n, const uint32_t* rowmap, uint32_t V,
+                                     uint32_t* cnt) {
+  uint32_t c = 0;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+    c += (sources[k] < V && rowmap[sources[k]] == k) ? 1u : 0u;
+  c = __reduce_add_sync(~0ull, c);
+  if (__lane_id() == 0 && c) atomicAdd(cnt, c);
+}
+__global__ void ms_perm_fill_kernel(const uint32_t* corder, const uint32_t* rowmap, uint32_t n, uint32_t V,
+                                    const uint32_t* cnt, uint32_t* perm) {
+  const bool perm_all = corder && n == V && *cnt == n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    perm[i] = perm_all ? rowmap[corder[i]] : i;
+}
+
 // Four u8 levels per dword: bytes b of `ln` with ln_b + 1 == ls_b (mod 256) -> bit 7 of byte b
 __device__ __forceinline__ uint32_t swar_succ_eq(uint32_t ln, uint32_t ls) {
   const uint32_t inc = ((ln & 0x7F7F7F7Fu) + 0x01010101u) ^ (ln & 0x80808080u);  // per-byte +1, no carries
@@ -374,8 +392,9 @@ __global__ __launch_bounds__(64 * kNhlWaves) void nh_from_levels_kernel(DevGraph
 }
 
 // ---------------------------------------------------------------------------
-// Bit-parallel multi-source BFS (msbfs_kernel). Batch = 32 consecutive sources of the
-// call (bit j <-> sources[32 * batch + j]). Closed form of LinkState::runSpf for uniform
+// Bit-parallel multi-source BFS (msbfs_kernel). Batch b = 32 consecutive positions of the
+// batch order (bit j <-> row msperm[32 b + j]: for an all-sources call the compact
+// clusters of DevGraph::corder, deepest first; else the call's own order). Closed form of LinkState::runSpf for uniform
 // cost (LinkState.cpp:808-882), levels only: v is on level L+1 for source j iff bit j is
 // in no visited word of v so far and in the frontier word of some usable neighbour u on
 // level L that expands for j (u not overloaded, or u == the source itself: an overloaded
@@ -557,7 +576,7 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
     if (tid < 3u) ctl[tid] = 0u;
     __syncthreads();
     if (tid < nbk) {
-      const uint32_t src = a.sources[k0 + tid];
+      const uint32_t src = a.sources[a.msperm[k0 + tid]];
       if (src < V) lds_or((lds_u32*)(size_t)(4u * src), 1u << tid);
     }
     __syncthreads();
@@ -600,8 +619,9 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
     }
     if (ovf) {
       if (tid < nbk) {
-        a.rowok[k0 + tid] = 0u;
-        a.ovf_list[atomicAdd(ovf_count, 1u)] = k0 + tid;
+        const uint32_t k = a.msperm[k0 + tid];
+        a.rowok[k] = 0u;
+        a.ovf_list[atomicAdd(ovf_count, 1u)] = k;
       }
     } else {
       // rows out. Each node's planes are transposed in place (8 x 8 bit blocks): afterwards
@@ -639,7 +659,7 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
 #pragma unroll
       for (uint32_t j = 0; j < kMsBatch; ++j) {
         if (j >= nbk) continue;  // uniform
-        const size_t k = k0 + j;
+        const size_t k = a.msperm[k0 + j];
         uint8_t* lrow = a.lvl8 + k * rb;
         uint64_t* drow = a.dist + k * V;
 #pragma unroll
@@ -651,7 +671,10 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
           if (dist_here) store_row<uint64_t>(&drow[v], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt);
         }
       }
-      if (tid < nbk) a.rowok[k0 + tid] = a.sources[k0 + tid] < V ? 1u : 0u;
+      if (tid < nbk) {
+        const uint32_t k = a.msperm[k0 + tid];
+        a.rowok[k] = a.sources[k] < V ? 1u : 0u;
+      }
     }
     __syncthreads();  // every lane is done with this batch's LDS and next_unit
     if (tid == 0) *next_unit = gridDim.x + atomicAdd(&ctr[0], 1u);
@@ -685,10 +708,11 @@ hipError_t launch_msbfs_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost
 // sources, where every neighbour of a source is likely in the batch.
 int allsrc_pass(const DevGraph& g, const SolveArgs& a) {
   if (!a.lvl8 || !a.rowmap || !a.rowok || a.out_row || a.perm || a.tight || a.ign_ptr || g.max_deg > 4u) return 0;
-  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 2u, 0u, 2u);
-  if (ms != 0u && MsLayout<20>::bytes(g.V) <= kMaxLds && g.V <= MsLayout<20>::kMaxV && (ms == 1u || a.n >= g.V))
+  const bool ms_ok = a.msperm && a.mscnt;
+  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 0u, 0u, 2u);  // opt-in: slower than the wave pass on G100
+  if (ms != 0u && ms_ok && MsLayout<20>::bytes(g.V) <= kMaxLds && g.V <= MsLayout<20>::kMaxV && (ms == 1u || a.n >= g.V))
     return 2;
-  const uint32_t rk = env_u32("OPENR_SPF_BFS_REACH", 2u, 0u, 2u);
+  const uint32_t rk = env_u32("OPENR_SPF_BFS_REACH", 0u, 0u, 2u);  // opt-in, as above
   if (rk != 0u && (rk == 1u || a.n >= g.V)) return 1;
   return 0;
 }
@@ -706,6 +730,13 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
                      dim3(256), 0, s, a.rowmap, a.sources, a.n, g.V);
   hipError_t err;
   if (pass == 2) {
+    if (!a.msperm || !a.mscnt) return hipErrorInvalidValue;
+    const uint32_t pgrid = std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, 4u * (uint32_t)num_cus));
+    err = hipMemsetAsync(a.mscnt, 0, sizeof(uint32_t), s);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(ms_perm_count_kernel, dim3(pgrid), dim3(256), 0, s, a.sources, a.n, a.rowmap, g.V, a.mscnt);
+    hipLaunchKernelGGL(ms_perm_fill_kernel, dim3(pgrid), dim3(256), 0, s, g.corder, a.rowmap, a.n, g.V, a.mscnt,
+                       a.msperm);
     const uint32_t need = (g.V + kMsThreads - 1u) / kMsThreads;  // nodes per thread
     if (info) info->kernel = "msbfs_kernel";
     if (need <= 4u) err = launch_msbfs_npt<4>(g, a, cost, blk, num_cus, s, flags);

@@ -79,7 +79,7 @@ struct Device {
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
   // lvl-family reach pass (all-sources batches): u8 level rows, node -> row map, row flags
   DevBuf<uint8_t> lvl8, rowok;
-  DevBuf<uint32_t> rowmap;
+  DevBuf<uint32_t> rowmap, msperm, mscnt;
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -111,7 +111,8 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
-                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld};
+                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld,
+                   g.corder};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -238,6 +239,81 @@ FrontierEstimate estimate_frontier(uint32_t V, const uint32_t* row_ptr, const ui
   return est;
 }
 
+// Batch order of the multi-source BFS (spf_allsrc.hip) for all-sources calls: a batch of
+// 32 sources costs one dense pass per level of its deepest source, so sources are grouped
+// into compact clusters (BFS from the lowest unassigned node, taking the 32 nearest
+// unassigned nodes: the sources of a batch then reach every node within a few levels of
+// each other) and the clusters are ordered deepest-first (estimated depth: the BFS depth
+// from the cluster's seed plus the cluster's radius), so the dynamically scheduled batches
+// end together. A performance heuristic over the structural graph (every edge, any
+// state): results do not depend on it.
+std::vector<uint32_t> cluster_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col) {
+  constexpr uint32_t kC = 32;
+  std::vector<uint32_t> stamp(V, UINT32_MAX), lvl(V), q;
+  std::vector<uint8_t> taken(V, 0);
+  std::vector<std::pair<uint64_t, uint32_t>> key;  // (depth estimate, cluster) per cluster
+  std::vector<uint32_t> members;
+  std::vector<uint32_t> start;
+  q.reserve(V);
+  uint32_t nclusters = 0;
+  for (uint32_t s = 0; s < V; ++s) {
+    if (taken[s]) continue;
+    const uint32_t c = nclusters++;
+    start.push_back((uint32_t)members.size());
+    uint32_t got = 0, radius = 0;
+    q.clear();
+    q.push_back(s);
+    stamp[s] = c;
+    lvl[s] = 0;
+    for (size_t h = 0; h < q.size() && got < kC; ++h) {
+      const uint32_t u = q[h];
+      if (!taken[u]) {
+        taken[u] = 1;
+        members.push_back(u);
+        radius = lvl[u];
+        ++got;
+      }
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+        const uint32_t v = col[e];
+        if (stamp[v] == c) continue;
+        stamp[v] = c;
+        lvl[v] = lvl[u] + 1u;
+        q.push_back(v);
+      }
+    }
+    key.push_back({(uint64_t)radius, c});
+  }
+  start.push_back((uint32_t)members.size());
+  // depth of a full BFS from each seed (the cluster's first member)
+  std::vector<uint32_t> seen(V, UINT32_MAX);
+  for (uint32_t c = 0; c < nclusters; ++c) {
+    const uint32_t s = members[start[c]];
+    q.clear();
+    q.push_back(s);
+    seen[s] = c;
+    lvl[s] = 0;
+    uint32_t depth = 0;
+    for (size_t h = 0; h < q.size(); ++h) {
+      const uint32_t u = q[h];
+      depth = lvl[u];
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+        const uint32_t v = col[e];
+        if (seen[v] == c) continue;
+        seen[v] = c;
+        lvl[v] = lvl[u] + 1u;
+        q.push_back(v);
+      }
+    }
+    key[c].first += depth;
+  }
+  std::stable_sort(key.begin(), key.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  std::vector<uint32_t> order;
+  order.reserve(V);
+  for (auto const& kc : key)
+    for (uint32_t i = start[kc.second]; i < start[kc.second + 1]; ++i) order.push_back(members[i]);
+  return order;
+}
+
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   const bool use_metric = (flags & OPENR_SPF_USE_LINK_METRIC) != 0;
   p->use_metric = use_metric;
@@ -340,15 +416,21 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   a.lvl8 = nullptr;
   a.rowmap = nullptr;
   a.rowok = nullptr;
+  a.msperm = nullptr;
+  a.mscnt = nullptr;
   if (fam == kFamLvl && !a.tight && !a.ign_ptr && !a.out_row && __builtin_popcount(mask) == 1 &&
       (a.n >= d.g.V || std::getenv("OPENR_SPF_BFS_REACH") || std::getenv("OPENR_SPF_BFS_MSBFS"))) {
     hipError_t err = d.lvl8.reserve((size_t)a.n * reach_row_bytes(d.g.V));
     if (err == hipSuccess) err = d.rowok.reserve(a.n);
     if (err == hipSuccess) err = d.rowmap.reserve(d.g.V);
+    if (err == hipSuccess) err = d.msperm.reserve(a.n);
+    if (err == hipSuccess) err = d.mscnt.reserve(1);
     if (err != hipSuccess) return err;
     a.lvl8 = d.lvl8.p;
     a.rowok = d.rowok.p;
     a.rowmap = d.rowmap.p;
+    a.msperm = d.msperm.p;
+    a.mscnt = d.mscnt.p;
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
@@ -795,6 +877,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.lvl8.release();
     d.rowok.release();
     d.rowmap.release();
+    d.msperm.release();
+    d.mscnt.release();
     d.work.release();
     d.perm.release();
     d.part.release();
@@ -923,6 +1007,13 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (!cls_mask[f]) cls_mask[f] = 1u;  // no node: class 0
   const FrontierEstimate est = estimate_frontier(V, gr->row_ptr, adj.data(), ovl.data());
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
+  // multi-source BFS batch order (graphs it can serve: every row <= 4 edges, V <= 10 240)
+  std::vector<uint32_t> corder;
+  {
+    uint32_t md = 0;
+    for (uint32_t u = 0; u < V; ++u) md = std::max(md, gr->row_ptr[u + 1] - gr->row_ptr[u]);
+    if (V && V <= 10240u && md <= 4u) corder = cluster_order(V, gr->row_ptr, gr->col);
+  }
 
   for (Device& d : ctx->devs) {
     HIP_TRY(hipSetDevice(d.ordinal));
@@ -986,6 +1077,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.cls_lvl, cls[kFamLvl].data(), V);
     if (err == hipSuccess) err = up(&g.ledge, ledge.data(), L);
     if (err == hipSuccess) err = up(&g.rank, gr->name_rank, V);
+    if (err == hipSuccess && !corder.empty()) err = up(&g.corder, corder.data(), V);
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;

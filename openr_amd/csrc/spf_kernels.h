@@ -45,6 +45,8 @@ struct DevGraph {
   uint32_t* rank = nullptr;    // [V] name rank (pathLinks / pop-order tie-break)
   uint4* erec = nullptr;       // [E] packed edge e = u->col: {col | kEdgeDown | kNodeSink if col is
                                //     overloaded, win[e], lid[e], rev[e]} (one 16-byte load per edge)
+  uint32_t* corder = nullptr;  // [V] or null: nodes grouped into compact clusters of 32, the clusters
+                               //     deepest-first (multi-source BFS batches of all-sources calls)
 };
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
@@ -129,6 +131,10 @@ struct SolveArgs {
   uint8_t* lvl8;
   uint32_t* rowmap;
   uint8_t* rowok;
+  // multi-source BFS batch order: position i of the batch sequence is row msperm[i] (null:
+  // row i); mscnt = one scratch word (the permutation test)
+  uint32_t* msperm;
+  uint32_t* mscnt;
 };
 // Row stride of SolveArgs::lvl8 (16-byte rows: the next-hop pass reads 16 levels per load)
 __host__ __device__ inline uint32_t reach_row_bytes(uint32_t V) { return (V + 15u) & ~15u; }

@@ -165,12 +165,12 @@ def test_wider_nh_stride_zero_padded(eng):
 
 
 def test_grid100_full_batch_is_msbfs(eng, monkeypatch, level_pass):
-    """The benchmarked launch (all 10 000 G100 sources in one call, knobs at their
-    defaults) runs the multi-source pass; a sample of rows vs the oracle
+    """All 10 000 G100 sources in one call with the multi-source pass in auto mode run
+    it; a sample of rows vs the oracle
     (test_gpu_configs.py checks every row)."""
     if level_pass != "msbfs":
         pytest.skip("default configuration only")
-    monkeypatch.delenv("OPENR_SPF_BFS_MSBFS")
+    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "2")
     monkeypatch.delenv("OPENR_SPF_BFS_REACH")
     g = T.grid_fast(100)
     eng.set_graph(g)
