@@ -36,13 +36,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "all-sources SPF solves/sec + edge relax/s (% HBM roofline), 10k-node grid, 1-8 GPU"
-# The faithful-cost CPU model (oracle/spf_faithful.cpp) against the reference's own runSpf:
-# SURVEY.md section 6 times the shim-compiled reference at 15.3 ms per G100 solve (1 core, the
-# survey container); the faithful model takes 14.5 ms per G100 solve in this container
-# (1 core, 40 evenly spaced sources), so its figures stand for the reference within ~5 %.
-CPU_CALIBRATION = {"reference_ms_per_g100_solve": 15.3, "faithful_ms_per_g100_solve": 14.5,
-                   "faithful_over_reference": 14.5 / 15.3,
-                   "source": "SURVEY.md section 6 (reference, shim-compiled) vs oracle/spf_faithful.cpp, 1 core"}
+# The faithful-cost CPU model (oracle/spf_faithful.cpp) against the reference's own runSpf
+# (BASELINE.md "Calibration ratio"): SURVEY.md section 6 times the shim-compiled reference at
+# 15.3 ms per G100 solve (1 core, the survey container); the faithful model took 14.5 / 21.7 /
+# 31.5 ms per G100 solve in the build container across sessions (host load), 0.085 vs ~0.1 ms
+# on G10: its figures stand for the reference within a factor of about 2 either way.
+CPU_CALIBRATION = {"reference_ms_per_g100_solve": 15.3, "faithful_ms_per_g100_solve": [14.5, 21.7, 31.5],
+                   "faithful_over_reference_range": [0.95, 2.1],
+                   "reference_ms_per_g10_solve": 0.1, "faithful_ms_per_g10_solve": 0.085,
+                   "source": "SURVEY.md section 6 (reference, shim-compiled) vs oracle/spf_faithful.cpp, 1 core; "
+                             "BASELINE.md Calibration ratio"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -139,8 +142,11 @@ def cpu_baseline(g, seconds: float, use_metric: bool):
         "cost_model": "faithful: reference data structures (oracle/spf_faithful.cpp)",
         "sample": f"{main['solves']} evenly spaced sources of {V}, runSpf with std::string-keyed LinkState "
                   f"replicas, {nthreads} threads, {main['seconds']:.1f}s; {cpu_model}",
-        "threads_note": f"{nthreads} threads = min(affinity {affinity}, 16): 16 is the host CPU share the GPU box "
-                        f"gives one GPU's job (worker pools are capped at 16 there), a cap, not the machine",
+        "cores_cap": 16,
+        "affinity_cpus": affinity,
+        "threads_note": f"cores = {nthreads} = min(affinity {affinity}, 16), a CAP: the GPU box grants one GPU's job a "
+                        f"16-CPU share (its rules size worker pools to 16) although affinity lists {affinity} CPUs; "
+                        f"the faithful value stands for the reference within ~2x (calibration)",
         "calibration": CPU_CALIBRATION,
         "variants": variants,
     }
@@ -670,6 +676,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--gather", default="compact", choices=["compact", "full"],
+                    help="strong scaling exchange: compact = u8/u16 level rows + next hops (uniform-cost graphs), "
+                         "full = u64 dist + next hops")
     ap.add_argument("--no-ucmp", action="store_true", help="whatif: skip the UCMP route-build leg")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="strong (default, BASELINE config 3): the V sources of ONE topology are split over the "
@@ -777,9 +786,23 @@ def all_sources_main(args):
 
     gather = None
     if world > 1 and strong and not args.no_gather:
-        from openr_amd.shard import GatherBuffers
+        from openr_amd.shard import CompactGather, GatherBuffers
 
-        gb = GatherBuffers(d_dist[:n_local], d_nh[:n_local], V, world)
+        # compact form (default) on uniform-cost graphs: u8/u16 level rows + next-hop rows
+        # (dist = level x cost on the receiver); the full u64 form otherwise / --gather full
+        mets = np.unique(np.asarray(g.metric)[np.asarray(g.edge_up) != 0]) if use_metric else np.array([1])
+        cost = int(mets[0]) if mets.size == 1 else (1 if mets.size == 0 else 0)
+        form = "full"
+        if args.gather == "compact" and cost > 0:
+            fin = d_dist[:n_local][d_dist[:n_local] != -1]
+            mx = torch.tensor([float(fin.max().item()) if fin.numel() else 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            max_level = int(mx.item()) // cost
+            if max_level <= 65534:
+                gb = CompactGather(d_dist[:n_local], d_nh[:n_local], V, world, cost, max_level)
+                form = "levels-u8" if max_level <= 254 else "levels-u16"
+        if form == "full":
+            gb = GatherBuffers(d_dist[:n_local], d_nh[:n_local], V, world)
         for _ in range(max(1, args.warmup)):
             step()
             gb.allgather()
@@ -799,9 +822,17 @@ def all_sources_main(args):
             for i, s in enumerate(r_chk):
                 exp = np.abs(s % grid_n - a % grid_n) + np.abs(s // grid_n - a // grid_n)
                 assert np.array_equal(host[i].astype(np.int64), exp), "gathered result check failed"
-        gather = {"ms_per_step": gel / args.steps * 1e3, "bytes_per_rank": int(V * V * (8 + nb)),
+        m_rows = max(shard_range(V, r, world)[1] - shard_range(V, r, world)[0] for r in range(world))
+        full_bytes = int(m_rows * V * (8 + nb))
+        gather = {"form": form, "ms_per_step": gel / args.steps * 1e3,
+                  "bytes_per_rank": int(gb.bytes_per_rank) if form != "full" else full_bytes,
+                  "bytes_per_rank_full_form": full_bytes,
+                  "compute_only_value": None,  # filled below (= value)
                   "gather_inclusive_value": V * args.steps / gel,
-                  "collective": "all_gather_into_tensor (RCCL) of dist u64 + next-hop rows, solve included"}
+                  "collective": ("all_gather_into_tensor (RCCL) of " +
+                                 ("u8/u16 level rows (dist = level x cost on receipt, encoded on the device after "
+                                  "each solve) + next-hop rows" if form != "full" else "dist u64 + next-hop rows") +
+                                 ", solve included")}
 
     solves_total = (V if strong else V * world) * args.steps
     value = solves_total / elapsed
@@ -854,6 +885,7 @@ def all_sources_main(args):
             },
         }
         if gather is not None:
+            gather["compute_only_value"] = value
             out["gather"] = gather
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_seconds, use_metric)

@@ -325,10 +325,11 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
   // entries of reachable nodes only
   PrefixEntries prefixEntries = search->second;
   for (auto const& [area, ls] : als) {
-    auto const& mySpf = ls.getSpfResult(myNodeName);  // an unknown node's result holds only itself
+    // dense read of the memoised SPF (an unknown node's result holds only itself)
+    auto const mySpf = ls.getSpfView(myNodeName);
     for (auto it = prefixEntries.begin(); it != prefixEntries.end();) {
       const auto& [node, pArea] = it->first;
-      if (area != pArea || mySpf.count(node)) ++it;
+      if (area != pArea || mySpf.reached(node)) ++it;
       else it = prefixEntries.erase(it);
     }
   }
@@ -580,13 +581,12 @@ std::optional<RibUnicastEntry> SpfSolver::addBestPaths(std::string const& myNode
 
 // Decision.cpp:1094-1117
 std::pair<Metric, std::unordered_set<std::string>> SpfSolver::getMinCostNodes(
-    const LinkState::SpfResult& spf, const std::set<NodeAndArea>& dstNodeAreas) const {
+    const LinkState::SpfView& spf, const std::set<NodeAndArea>& dstNodeAreas) const {
   Metric shortest = std::numeric_limits<Metric>::max();
   std::unordered_set<std::string> nodes;
   for (auto const& [dst, _] : dstNodeAreas) {
-    auto it = spf.find(dst);
-    if (it == spf.end()) continue;
-    const Metric d = it->second.metric();
+    if (!spf.reached(dst)) continue;
+    const Metric d = spf.metric(dst);
     if (shortest >= d) {
       if (shortest > d) {
         shortest = d;
@@ -605,7 +605,9 @@ std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric
   std::unordered_map<std::pair<std::string, std::string>, Metric> nextHopNodes;
   Metric shortestMetric = std::numeric_limits<Metric>::max();
   for (auto const& [area, ls] : als) {
-    auto const& fromHere = ls.getSpfResult(me);
+    // dense reads of the memoised SPFs (LinkState::SpfView): same results as getSpfResult,
+    // no SpfResult map materialised per route build
+    auto const fromHere = ls.getSpfView(me);
     auto const mm = getMinCostNodes(fromHere, dstNodeAreas);
     if (shortestMetric < mm.first) continue;
     if (shortestMetric > mm.first) {
@@ -615,20 +617,20 @@ std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric
     if (mm.second.empty()) continue;
     for (auto const& dst : mm.second) {
       const std::string dstRef = perDestination ? dst : "";
-      for (auto const& nh : fromHere.at(dst).nextHops())
-        nextHopNodes[std::make_pair(nh, dstRef)] = shortestMetric - ls.getMetricFromAToB(me, nh).value();
+      // getMetricFromAToB(me, nh) reads the same (already counted) result: nh != me
+      for (auto const& nh : fromHere.nextHops(dst))
+        nextHopNodes[std::make_pair(nh, dstRef)] = shortestMetric - fromHere.metric(nh);
     }
     if (computeLfaPaths_) {
       for (auto const& link : ls.linksFromNode(me)) {
         if (!link->isUp()) continue;
         const auto& nbr = link->getOtherNodeName(me);
-        auto const& fromNbr = ls.getSpfResult(nbr);
-        const Metric nbrToHere = fromNbr.at(me).metric();
+        auto const fromNbr = ls.getSpfView(nbr);
+        const Metric nbrToHere = fromNbr.metric(me);
         for (auto const& [dst, dstArea] : dstNodeAreas) {
           if (area != dstArea) continue;
-          auto sp = fromNbr.find(dst);
-          if (sp == fromNbr.end()) continue;
-          const Metric dNbr = sp->second.metric();
+          if (!fromNbr.reached(dst)) continue;
+          const Metric dNbr = fromNbr.metric(dst);
           if (dNbr < shortestMetric + nbrToHere) {  // RFC 5286
             const auto key = std::make_pair(nbr, perDestination ? dst : std::string());
             auto it = nextHopNodes.find(key);

@@ -255,7 +255,7 @@ class SpfSolver {
                                               BestRouteSelectionResult const& best, PrefixEntries const& prefixEntries,
                                               PrefixState const& prefixState, bool isBgp, NextHopSet&& nextHops);
   std::pair<Metric, std::unordered_set<std::string>> getMinCostNodes(
-      const LinkState::SpfResult& spfResult, const std::set<NodeAndArea>& dstNodeAreas) const;
+      const LinkState::SpfView& spf, const std::set<NodeAndArea>& dstNodeAreas) const;
   std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric>> getNextHopsWithMetric(
       const std::string& myNodeName, const std::set<NodeAndArea>& dstNodeAreas, bool perDestination,
       std::unordered_map<std::string, LinkState> const& areaLinkStates) const;

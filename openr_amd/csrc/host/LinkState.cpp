@@ -344,7 +344,7 @@ bool LinkState::updateNodeOverloaded(const std::string& nodeName, bool isOverloa
   if (it != nodeOverloads_.end()) {
     // the mirror carries the effective (hold-aware) value: rebuild it only when that changed
     const bool changed = it->second.updateValue(isOverloaded, holdUpTtl, holdDownTtl);
-    if (changed) markMirrorDirty();
+    if (changed) attrNodes_.push_back(nodeName);  // attribute only: patched in place (applyAttrPatch)
     return changed;
   }
   nodeOverloads_.emplace(nodeName, HoldableValue<bool>{isOverloaded});
@@ -359,11 +359,21 @@ bool LinkState::isNodeOverloaded(const std::string& nodeName) const {
 
 LinkState::LinkStateChange LinkState::decrementHolds() {
   LinkStateChange change;
-  for (auto& link : allLinks_) change.topologyChanged |= link->decrementHolds();
-  for (auto& kv : nodeOverloads_) change.topologyChanged |= kv.second.decrementTtl();
+  std::vector<std::shared_ptr<Link>> links;
+  std::vector<std::string> nodes;
+  for (auto& link : allLinks_)
+    if (link->decrementHolds()) {
+      change.topologyChanged = true;
+      links.push_back(link);
+    }
+  for (auto& kv : nodeOverloads_)
+    if (kv.second.decrementTtl()) {
+      change.topologyChanged = true;
+      nodes.push_back(kv.first);
+    }
   if (change.topologyChanged) {
-    clearMemos();
-    markMirrorDirty();
+    clearMemos();  // LinkState.cpp:509-512
+    applyAttrPatch(links, nodes);  // held values only: the link structure is unchanged
   }
   return change;
 }
@@ -426,6 +436,8 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
   // does an effective metric / overload / up-down change below); a re-advertisement that
   // changes nothing, or only labels and next-hop addresses, keeps mirror and device graph
 
+  attrLinks_.clear();
+  attrNodes_.clear();
   thrift::AdjacencyDatabase& stored = adjacencyDatabases_[nodeName];
   thrift::AdjacencyDatabase prior(std::move(stored));
   stored = std::move(db);
@@ -459,12 +471,15 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
     // same link on both sides: update the object we already hold
     Link& cur = *oldLinks[oi];
     const Link& upd = *newLinks[ni];
+    bool attr = false;
     if (upd.getMetricFromNode(nodeName) != cur.getMetricFromNode(nodeName))
-      change.topologyChanged |= cur.setMetricFromNode(nodeName, upd.getMetricFromNode(nodeName), holdUpTtl,
-                                                      holdDownTtl);
+      attr |= cur.setMetricFromNode(nodeName, upd.getMetricFromNode(nodeName), holdUpTtl, holdDownTtl);
     if (upd.getOverloadFromNode(nodeName) != cur.getOverloadFromNode(nodeName))
-      change.topologyChanged |= cur.setOverloadFromNode(nodeName, upd.getOverloadFromNode(nodeName), holdUpTtl,
-                                                        holdDownTtl);
+      attr |= cur.setOverloadFromNode(nodeName, upd.getOverloadFromNode(nodeName), holdUpTtl, holdDownTtl);
+    if (attr) {
+      change.topologyChanged = true;
+      attrLinks_.push_back(oldLinks[oi]);
+    }
     if (upd.getAdjLabelFromNode(nodeName) != cur.getAdjLabelFromNode(nodeName)) {
       change.linkAttributesChanged = true;
       cur.setAdjLabelFromNode(nodeName, upd.getAdjLabelFromNode(nodeName));
@@ -481,9 +496,13 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
     ++oi;
   }
   if (change.topologyChanged) {
-    clearMemos();
-    markMirrorDirty();
+    clearMemos();  // LinkState.cpp:714-717
+    // links added / removed marked the mirror for a rebuild already; otherwise only
+    // attributes moved (metric, Link::isUp, node overload): patch in place
+    applyAttrPatch(attrLinks_, attrNodes_);
   }
+  attrLinks_.clear();
+  attrNodes_.clear();
   return change;
 }
 
@@ -575,14 +594,59 @@ LinkState::SpfResult const& LinkState::getSpfResult(const std::string& nodeName,
   auto it = spfResults_.find(key);
   if (it == spfResults_.end()) {  // LinkState.cpp:793-803: a miss runs the SPF
     throwIfFrozen("getSpfResult", nodeName);
-    SpfResult res = runSpf(nodeName, useLinkMetric);
-    it = spfResults_.emplace(std::piecewise_construct, std::forward_as_tuple(key), std::forward_as_tuple()).first;
-    it->second.res = std::move(res);
-    it->second.counted.v.store(1, std::memory_order_relaxed);
-  } else if (!it->second.counted.v.exchange(1, std::memory_order_relaxed)) {
-    SpfCounters::get().addSpfRun(it->second.ms);  // prefetched: its run counts at this first read
+    prefetchSpfResults({nodeName}, useLinkMetric);
+    it = spfResults_.find(key);
   }
-  return it->second.res;
+  if (!it->second.counted.v.exchange(1, std::memory_order_relaxed))
+    SpfCounters::get().addSpfRun(it->second.ms);  // its logical run counts at this first read
+  return materialize(it->second, useLinkMetric);
+}
+
+// The memo entry's SpfResult map, built from its dense row on first read (once, also when
+// several route-build workers read it together)
+const LinkState::SpfResult& LinkState::materialize(const MemoEntry& e, bool useLinkMetric) const {
+  if (e.row == UINT32_MAX) return e.res;
+  MemoEntry& me = const_cast<MemoEntry&>(e);
+  std::call_once(*me.once.f, [&]() {
+    const CsrMirror& m = mirror_;
+    const DenseRows& d = dense_[useLinkMetric ? 1 : 0];
+    const uint32_t V = (uint32_t)m.names.size(), src = d.src[e.row];
+    const uint64_t* dist = d.dist.data() + (size_t)e.row * V;
+    const uint8_t* h = d.nh.data() + (size_t)e.row * V * d.nb;
+    const std::vector<uint32_t>& nbrs = d.nbrs[e.row];
+    SpfResult res;
+    res.reserve(V);
+    for (uint32_t v = 0; v < V; ++v) {
+      if (dist[v] == UINT64_MAX) continue;
+      NodeSpfResult r(dist[v]);
+      const uint8_t* hv = h + (size_t)v * d.nb;
+      for (uint32_t i = 0; i < nbrs.size(); ++i)
+        if ((hv[i >> 3] >> (i & 7)) & 1u) r.addNextHop(m.names[nbrs[i]]);
+      res.emplace(m.names[v], std::move(r));
+    }
+    // pathLinks (LinkState.cpp:846-873): every usable in-edge u->v out of an expanding
+    // node u (not overloaded, or the source) with dist[u] + w == dist[v]; with metrics in
+    // [1, 2^31-1] these are exactly the links the reference's relaxations appended, and its
+    // (metric, name) pop order then row position orders them
+    std::vector<uint32_t> order;
+    const uint32_t E = (uint32_t)m.col.size();
+    for (uint32_t e2 = 0; e2 < E; ++e2) {
+      const uint32_t u = m.edgeOwner[e2], v = m.col[e2];
+      if (!m.edgeUp[e2] || dist[u] == UINT64_MAX || dist[v] == UINT64_MAX || u == v) continue;
+      if (m.overloaded[u] && u != src) continue;
+      const uint64_t w = useLinkMetric ? m.metric[e2] : 1u;
+      if (dist[u] + w == dist[v]) order.push_back(e2);
+    }
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+      const uint32_t ux = m.edgeOwner[x], uy = m.edgeOwner[y];
+      if (dist[ux] != dist[uy]) return dist[ux] < dist[uy];
+      if (m.nameRank[ux] != m.nameRank[uy]) return m.nameRank[ux] < m.nameRank[uy];
+      return x < y;
+    });
+    for (uint32_t e2 : order) res.at(m.names[m.col[e2]]).addPath(m.links[m.linkId[e2]], m.names[m.edgeOwner[e2]]);
+    me.res = std::move(res);
+  });
+  return e.res;
 }
 
 void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool useLinkMetric) const {
@@ -593,16 +657,137 @@ void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool u
   missing.erase(std::unique(missing.begin(), missing.end()), missing.end());
   if (missing.empty()) return;
   throwIfFrozen("prefetchSpfResults", missing.front());
-  double ms = 0;
-  auto results = runSpfBatch(missing, useLinkMetric, std::vector<const LinkSet*>(missing.size(), nullptr), &ms);
-  for (size_t i = 0; i < missing.size(); ++i) {
-    auto it = spfResults_
-                  .emplace(std::piecewise_construct, std::forward_as_tuple(std::make_pair(missing[i], useLinkMetric)),
-                           std::forward_as_tuple())
-                  .first;
-    it->second.res = std::move(results[i]);
-    it->second.ms = ms / (double)missing.size();
+  auto entry = [&](const std::string& n) -> MemoEntry& {
+    return spfResults_
+        .emplace(std::piecewise_construct, std::forward_as_tuple(std::make_pair(n, useLinkMetric)),
+                 std::forward_as_tuple())
+        .first->second;
+  };
+  if (!denseEligible(useLinkMetric)) {  // zero / wrapped metrics: exact pop order, materialised now
+    double ms = 0;
+    auto results = runSpfBatch(missing, useLinkMetric, std::vector<const LinkSet*>(missing.size(), nullptr), &ms);
+    for (size_t i = 0; i < missing.size(); ++i) {
+      MemoEntry& e = entry(missing[i]);
+      e.res = std::move(results[i]);
+      e.ms = ms / (double)missing.size();
+    }
+    return;
   }
+  const CsrMirror& m = csrMirror();
+  ensureEngineGraph();
+  DenseRows& d = dense_[useLinkMetric ? 1 : 0];
+  double rms = 0;
+  const size_t kept = d.src.size();
+  refreshDense(useLinkMetric, &rms);  // rows a patch left stale: only affected ones re-solved
+  const double keptMs = kept ? rms / (double)kept : 0.0;
+  std::vector<uint32_t> ids;
+  std::vector<const std::string*> idName;
+  for (auto const& n : missing) {
+    auto it = m.id.find(n);
+    if (it == m.id.end()) {  // unknown to the graph: the reference pops only the source itself
+      entry(n).res.emplace(n, NodeSpfResult(0));
+      continue;
+    }
+    auto sl = d.slot.find(it->second);
+    if (sl != d.slot.end()) {  // a row kept (and refreshed) across attribute changes
+      MemoEntry& e = entry(n);
+      e.row = sl->second;
+      e.ms = keptMs;
+      continue;
+    }
+    ids.push_back(it->second);
+    idName.push_back(&n);
+  }
+  if (ids.empty()) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t V = (uint32_t)m.names.size(), n = (uint32_t)ids.size();
+  uint32_t nb = 1;
+  SpfEngineHandle::check(openr_spf_nh_bytes(engine_->ctx(), &nb), "openr_spf_nh_bytes");
+  if (d.src.empty()) d.nb = nb;
+  const size_t r0 = d.src.size();
+  d.dist.resize((r0 + n) * (size_t)V);
+  d.nh.resize((r0 + n) * (size_t)V * d.nb);
+  SpfEngineHandle::check(openr_spf_solve(engine_->ctx(), ids.data(), n,
+                                         useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u,
+                                         d.dist.data() + r0 * V, d.nh.data() + r0 * V * d.nb, d.nb, nullptr),
+                         "openr_spf_solve");
+  d.nbrs.resize(r0 + n);
+  std::vector<uint32_t> buf(V ? V : 1);
+  for (uint32_t k = 0; k < n; ++k) {
+    uint32_t nn = 0;
+    SpfEngineHandle::check(openr_spf_neighbor_map(engine_->ctx(), ids[k], buf.data(), (uint32_t)buf.size(), &nn),
+                           "openr_spf_neighbor_map");
+    d.nbrs[r0 + k].assign(buf.begin(), buf.begin() + nn);
+    d.slot[ids[k]] = (uint32_t)(r0 + k);
+    d.src.push_back(ids[k]);
+  }
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / n;
+  for (uint32_t k = 0; k < n; ++k) {
+    MemoEntry& e = entry(*idName[k]);
+    e.row = (uint32_t)(r0 + k);
+    e.ms = ms;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SpfView: dense reads of a memo entry (route build fast path)
+// ---------------------------------------------------------------------------
+LinkState::SpfView LinkState::getSpfView(const std::string& nodeName, bool useLinkMetric) const {
+  const auto key = std::make_pair(nodeName, useLinkMetric);
+  auto it = spfResults_.find(key);
+  if (it == spfResults_.end()) {
+    throwIfFrozen("getSpfView", nodeName);
+    prefetchSpfResults({nodeName}, useLinkMetric);
+    it = spfResults_.find(key);
+  }
+  if (!it->second.counted.v.exchange(1, std::memory_order_relaxed)) SpfCounters::get().addSpfRun(it->second.ms);
+  SpfView v;
+  const MemoEntry& e = it->second;
+  if (e.row == UINT32_MAX) {
+    v.map_ = &e.res;
+    return v;
+  }
+  const DenseRows& d = dense_[useLinkMetric ? 1 : 0];
+  v.m_ = &mirror_;
+  const size_t V = mirror_.names.size();
+  v.dist_ = d.dist.data() + (size_t)e.row * V;
+  v.nh_ = d.nh.data() + (size_t)e.row * V * d.nb;
+  v.nb_ = d.nb;
+  v.nbrs_ = &d.nbrs[e.row];
+  return v;
+}
+
+int32_t LinkState::SpfView::id(const std::string& node) const {
+  auto it = m_->id.find(node);
+  if (it == m_->id.end() || dist_[it->second] == UINT64_MAX) return -1;
+  return (int32_t)it->second;
+}
+
+bool LinkState::SpfView::reached(const std::string& node) const {
+  if (map_) return map_->count(node) != 0;
+  return id(node) >= 0;
+}
+
+LinkStateMetric LinkState::SpfView::metric(const std::string& node) const {
+  if (map_) return map_->at(node).metric();
+  const int32_t v = id(node);
+  if (v < 0) throw std::out_of_range("SpfView::metric: " + node + " not reached");
+  return dist_[v];
+}
+
+std::vector<std::string> LinkState::SpfView::nextHops(const std::string& node) const {
+  std::vector<std::string> out;
+  if (map_) {
+    auto const& nh = map_->at(node).nextHops();
+    out.assign(nh.begin(), nh.end());
+    return out;
+  }
+  const int32_t v = id(node);
+  if (v < 0) throw std::out_of_range("SpfView::nextHops: " + node + " not reached");
+  const uint8_t* hv = nh_ + (size_t)v * nb_;
+  for (uint32_t i = 0; i < nbrs_->size(); ++i)
+    if ((hv[i >> 3] >> (i & 7)) & 1u) out.push_back(m_->names[(*nbrs_)[i]]);
+  return out;
 }
 
 // ---------------------------------------------------------------------------
@@ -626,6 +811,7 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   const size_t maxE = 2 * allLinks_.size();
   linkIds.reserve(allLinks_.size());
   m.links.reserve(allLinks_.size());
+  m.linkEdges.reserve(2 * allLinks_.size());
   m.col.reserve(maxE);
   m.metric.reserve(maxE);
   m.linkId.reserve(maxE);
@@ -640,6 +826,9 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
     for (auto const& link : linksFromNode(name)) {
       auto ins = linkIds.emplace(link.get(), (uint32_t)m.links.size());
       if (ins.second) m.links.push_back(link);
+      if (ins.second) m.linkEdges.insert(m.linkEdges.end(), {UINT32_MAX, UINT32_MAX});
+      m.linkEdges[2 * ins.first->second + (m.linkEdges[2 * ins.first->second] == UINT32_MAX ? 0 : 1)] =
+          (uint32_t)m.col.size();
       m.col.push_back(m.id.at(link->getOtherNodeName(name)));
       m.metric.push_back(link->getMetricFromNode(name));
       if (link->isUp() && (m.metric.back() == 0 || m.metric.back() > 0x7FFFFFFFull)) m.metricsPositive = false;
@@ -677,6 +866,115 @@ void LinkState::ensureEngineGraph() const {
   SpfEngineHandle::check(openr_spf_set_graph(engine_->ctx(), &g), "openr_spf_set_graph");
   engine_->owner = this;
   engine_->generation = mirrorGeneration_;
+  ++ustats_.graphUploads;
+  // rows the memo holds were solved on this same mirror; rows a patch left stale need the
+  // engine's delta, which the upload discards
+  for (auto& d : dense_)
+    if (d.stale) d.clear();
+}
+
+// ---------------------------------------------------------------------------
+// Attribute-only changes (round 3): the reference clears its memo and
+// re-runs every SPF it is asked for (LinkState.cpp:509-512, 714-717). Here the memo's
+// results are cleared the same way, but the engine's resident graph is patched in place
+// (openr_spf_patch_graph: no CSR rebuild, no upload) and the memo's dense rows stay: the
+// next read refreshes them (openr_spf_refresh: only rows the change can affect are
+// re-solved) instead of re-solving every source.
+// ---------------------------------------------------------------------------
+void LinkState::applyAttrPatch(const std::vector<std::shared_ptr<Link>>& links, const std::vector<std::string>& nodes) {
+  if (mirrorDirty_) return;  // the structure changed too: the mirror is rebuilt on next use
+  if (links.empty() && nodes.empty()) return;
+  CsrMirror& m = mirror_;
+  std::vector<uint32_t> eids, lids, nids;
+  std::vector<uint64_t> emet;
+  std::vector<uint8_t> lup, novl;
+  for (auto const& link : links) {
+    auto it = m.linkIndex.find(link.get());
+    if (it == m.linkIndex.end()) {  // not in the mirror (cannot happen for a same-structure update)
+      markMirrorDirty();
+      return;
+    }
+    const uint32_t lid = it->second;
+    const bool up = link->isUp();
+    lids.push_back(lid);
+    lup.push_back(up ? 1 : 0);
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t e = m.linkEdges[2 * lid + k];
+      if (e == UINT32_MAX) continue;
+      const uint64_t w = link->getMetricFromNode(m.names[m.edgeOwner[e]]);
+      m.metric[e] = w;
+      m.edgeUp[e] = up ? 1 : 0;
+      eids.push_back(e);
+      emet.push_back(w);
+    }
+  }
+  for (auto const& name : nodes) {
+    auto it = m.id.find(name);
+    if (it == m.id.end()) {
+      markMirrorDirty();
+      return;
+    }
+    nids.push_back(it->second);
+    novl.push_back(isNodeOverloaded(name) ? 1 : 0);
+    m.overloaded[it->second] = novl.back();
+  }
+  m.metricsPositive = true;
+  for (size_t e = 0; e < m.col.size(); ++e)
+    if (m.edgeUp[e] && (m.metric[e] == 0 || m.metric[e] > 0x7FFFFFFFull)) m.metricsPositive = false;
+  if (!engine_ || engine_->owner != this || engine_->generation != mirrorGeneration_) {
+    // the engine does not hold this graph: the next use uploads the patched mirror
+    dense_[0].clear();
+    dense_[1].clear();
+    return;
+  }
+  // stale rows must be refreshed against the delta they are stale for before a new patch
+  // starts the next one
+  for (int um = 0; um < 2; ++um)
+    if (dense_[um].stale) {
+      double ms = 0;
+      refreshDense(um != 0, &ms);
+    }
+  openr_spf_patch pt{};
+  pt.n_edges = (uint32_t)eids.size();
+  pt.edge_ids = eids.data();
+  pt.metric = emet.data();
+  pt.n_links = (uint32_t)lids.size();
+  pt.link_ids = lids.data();
+  pt.link_up = lup.data();
+  pt.n_nodes = (uint32_t)nids.size();
+  pt.node_ids = nids.data();
+  pt.node_overloaded = novl.data();
+  SpfEngineHandle::check(openr_spf_patch_graph(engine_->ctx(), &pt), "openr_spf_patch_graph");
+  ++ustats_.patches;
+  for (int um = 0; um < 2; ++um) {
+    if (dense_[um].src.empty()) continue;
+    if (um && !m.metricsPositive) dense_[um].clear();  // pathLinks then need the exact pop order
+    else dense_[um].stale = true;
+  }
+}
+
+bool LinkState::denseEligible(bool useLinkMetric) const {
+  if (const char* e = std::getenv("OPENR_DENSE_MEMO"))  // 0: the materialise-at-solve path (tests)
+    if (std::atoi(e) == 0) return false;
+  return !useLinkMetric || csrMirror().metricsPositive;
+}
+
+void LinkState::refreshDense(bool useLinkMetric, double* ms) const {
+  DenseRows& d = dense_[useLinkMetric ? 1 : 0];
+  *ms = 0;
+  if (!d.stale) return;
+  d.stale = false;
+  if (d.src.empty()) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t resolved = 0;
+  SpfEngineHandle::check(openr_spf_refresh(engine_->ctx(), d.src.data(), (uint32_t)d.src.size(),
+                                           useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u, d.dist.data(),
+                                           d.nh.data(), d.nb, nullptr, &resolved),
+                         "openr_spf_refresh");
+  ++ustats_.refreshes;
+  ustats_.rowsRefreshed += resolved;
+  ustats_.rowsKept += d.src.size();
+  *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::string>& dests) const {

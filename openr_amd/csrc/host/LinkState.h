@@ -20,6 +20,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -349,6 +350,7 @@ class LinkState {
     std::vector<uint8_t> edgeUp, overloaded;
     std::vector<uint32_t> nameRank;
     std::vector<std::shared_ptr<Link>> links;  // link id -> Link
+    std::vector<uint32_t> linkEdges;           // link id -> its two directed edge ids (2 per link)
     std::vector<uint32_t> edgeOwner;
     std::unordered_map<const Link*, uint32_t> linkIndex;  // Link -> link id (ignore sets)
     bool metricsPositive = true;  // every usable metric in [1, 2^31-1]: fast kernels
@@ -357,15 +359,89 @@ class LinkState {
   // process-wide id of the mirror csrMirror() last built (tests: a rebuild changes it)
   uint64_t mirrorGeneration() const { return mirrorGeneration_; }
 
+  // Dense view of a memoised SPF (route build fast path, round 3): the same result
+  // getSpfResult(node, useLinkMetric) holds — reached nodes, metrics, next hops — read from
+  // the memo's dense rows without materialising the SpfResult map. Counts the SPF run like
+  // getSpfResult (first read of the memo entry). Valid until the next topology change.
+  class SpfView {
+   public:
+    bool reached(const std::string& node) const;
+    // metric of a reached node (std::out_of_range otherwise, like SpfResult::at)
+    LinkStateMetric metric(const std::string& node) const;
+    // next hops of a reached node (std::out_of_range otherwise)
+    std::vector<std::string> nextHops(const std::string& node) const;
+
+   private:
+    friend class LinkState;
+    // the materialised SpfResult when the memo entry has no dense row (unknown source,
+    // zero / wrapped metrics): then every call reads it
+    const SpfResult* map_ = nullptr;
+    const CsrMirror* m_ = nullptr;
+    const uint64_t* dist_ = nullptr;
+    const uint8_t* nh_ = nullptr;
+    uint32_t nb_ = 1;
+    const std::vector<uint32_t>* nbrs_ = nullptr;
+    int32_t id(const std::string& node) const;
+  };
+  SpfView getSpfView(const std::string& nodeName, bool useLinkMetric = true) const;
+
+  // Incremental-update introspection (tests / benchmarks): attribute-only topology changes
+  // patch the engine's resident graph (openr_spf_patch_graph) and refresh the memo's dense
+  // rows (openr_spf_refresh) instead of re-uploading the graph and re-solving every row.
+  struct UpdateStats {
+    uint64_t graphUploads = 0;  // openr_spf_set_graph calls
+    uint64_t patches = 0;       // openr_spf_patch_graph calls
+    uint64_t refreshes = 0;     // openr_spf_refresh calls
+    uint64_t rowsRefreshed = 0; // rows those refreshes re-solved
+    uint64_t rowsKept = 0;      // dense rows carried across a change (not re-solved)
+  };
+  const UpdateStats& updateStats() const { return ustats_; }
+  size_t denseRows(bool useLinkMetric = true) const { return dense_[useLinkMetric ? 1 : 0].src.size(); }
+
  private:
   const std::string area_;
   // memo entry: the result, and whether its logical SPF run has been counted (a prefetched
   // entry is counted on its first read, with its share of the batch's time)
+  // A once-flag that copies as a fresh flag (memo entries stay copyable)
+  struct LazyOnce {
+    std::unique_ptr<std::once_flag> f = std::make_unique<std::once_flag>();
+    LazyOnce() = default;
+    LazyOnce(const LazyOnce&) : f(std::make_unique<std::once_flag>()) {}
+    LazyOnce& operator=(const LazyOnce&) {
+      f = std::make_unique<std::once_flag>();
+      return *this;
+    }
+  };
   struct MemoEntry {
     SpfResult res;
     RelaxedFlag counted;
     double ms = 0;
+    uint32_t row = UINT32_MAX;  // dense row of the result (materialised into res on first read), or none
+    LazyOnce once;
   };
+  // Dense memo rows per useLinkMetric (round 3): the results the memo holds as the engine
+  // writes them — u64 distance and next-hop bitset per (source, node) — host-resident. They
+  // outlive attribute-only topology changes (refreshed in place after the engine graph is
+  // patched) and are materialised into SpfResult maps only when read.
+  struct DenseRows {
+    uint32_t nb = 1;
+    std::unordered_map<uint32_t, uint32_t> slot;  // node id -> row
+    std::vector<uint32_t> src;                     // row -> node id
+    std::vector<uint64_t> dist;                    // rows x V
+    std::vector<uint8_t> nh;                       // rows x V x nb
+    std::vector<std::vector<uint32_t>> nbrs;       // row -> node id of next-hop bit i
+    bool stale = false;                            // rows predate a patch: refresh before any read
+    void clear() { *this = DenseRows{}; }
+  };
+  mutable DenseRows dense_[2];
+  mutable UpdateStats ustats_;
+  bool denseEligible(bool useLinkMetric) const;
+  void refreshDense(bool useLinkMetric, double* ms) const;
+  const SpfResult& materialize(const MemoEntry& e, bool useLinkMetric) const;
+  // attribute-only change: patch the mirror and the engine's graph in place
+  void applyAttrPatch(const std::vector<std::shared_ptr<Link>>& links, const std::vector<std::string>& nodes);
+  std::vector<std::shared_ptr<Link>> attrLinks_;  // links / nodes an update changed (attributes only)
+  std::vector<std::string> attrNodes_;
   mutable std::unordered_map<std::pair<std::string, bool>, MemoEntry> spfResults_;
   mutable RelaxedFlag frozen_;  // MemoFreeze depth
   void throwIfFrozen(const char* what, const std::string& key) const;
@@ -398,7 +474,11 @@ class LinkState {
   std::shared_ptr<Link> maybeMakeLink(const std::string& nodeName, const thrift::Adjacency& adj) const;
   std::vector<std::shared_ptr<Link>> getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const;
   std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;
-  void markMirrorDirty() { mirrorDirty_ = true; }
+  void markMirrorDirty() {
+    mirrorDirty_ = true;
+    dense_[0].clear();  // node ids change with the rebuilt mirror
+    dense_[1].clear();
+  }
 
   std::unordered_map<std::string, LinkSet> linkMap_;
   LinkSet allLinks_;

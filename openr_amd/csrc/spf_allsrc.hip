@@ -684,6 +684,260 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
   retire_workgroup(ctr, nullptr);
 }
 
+// ---------------------------------------------------------------------------
+// Tile-active multi-source BFS (msbfs_tile_kernel, round 3: the G100 all-sources path).
+//
+// Same closed form and bit-parallel state as msbfs_kernel, but a level no longer pulls over
+// every node. Nodes are renumbered (DevGraph::tord) so that 64 consecutive internal ids —
+// one wavefront slot — form a compact tile, and a level step only processes the tiles a
+// node of which may gain a bit: tile T can gain at step L only if a node of a tile in
+// N(T) (DevGraph::tmask) wrote a non-zero frontier word at step L-1. A processed tile whose
+// wave sees any non-zero frontier word ORs its tmask row into the next step's activity
+// bitmask (act[3][8] u32 in rotation, LDS); an empty bitmask ends the batch. For a
+// 32-source cluster on G100 a level touches ~37 of 157 tiles (scripts/tile_sim.py).
+//
+// Frontier words of skipped tiles are not rewritten: the buffer then holds a frontier of an
+// earlier level m <= L-1 of the same batch. Such bits are harmless: bit j of node x at level
+// m (x expands: sinks write 0) puts every neighbour of x on level <= m + 1 <= L for source
+// j, so the neighbour's visited word already holds j when it reads the stale word. Both
+// buffers are zeroed at the start of a batch.
+//
+// Thread t owns internal nodes p = t + 512 i (slot i = tile 8i + wave, lane = position in
+// the tile). A wave's active slots of a step are a bit mask in SGPRs; the pull row of the
+// next active slot is read while the current slot's frontier reads are in flight.
+// ---------------------------------------------------------------------------
+template <uint32_t NPT>
+struct MsTLayout {
+  static constexpr uint32_t kMaxV = kMsThreads * NPT;                // internal ids a workgroup owns
+  static constexpr uint32_t kF1 = (4u * (kMaxV + 4u) + 15u) & ~15u;  // byte offset of F[1]; F[x][kMaxV] = 0
+  static constexpr uint32_t kAct = 2u * kF1;                         // act[3][8] u32
+  static constexpr uint32_t kNext = kAct + 96u;                      // next batch
+  static constexpr uint32_t kEll = kAct + 128u;                      // pull rows, 8 B per internal id
+  __host__ __device__ static constexpr uint32_t bytes(uint32_t V) {
+    return kEll + 8u * ((V + kTileNodes - 1u) / kTileNodes) * kTileNodes;
+  }
+};
+
+template <uint32_t NPT>
+__global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, SolveArgs a, uint64_t cost,
+                                                                   uint32_t* ctr, uint32_t* ovf_count, uint32_t flags) {
+  using Lay = MsTLayout<NPT>;
+  typedef __attribute__((address_space(3))) uint64_t lds_u64;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
+  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  lds_u32* const act = (lds_u32*)(size_t)Lay::kAct;
+  lds_u32* const next_unit = (lds_u32*)(size_t)Lay::kNext;
+  const bool nt = (flags & 1u) != 0, dist_here = (flags & 2u) == 0;
+  const uint32_t rb = reach_row_bytes(V), vpad = g.ntiles * kTileNodes;
+  const uint32_t ebase = Lay::kEll + 8u * tid;  // this thread's first pull row
+  constexpr uint32_t kZero = 4u * Lay::kMaxV;   // byte offset of the zero word
+  // control words zero; pull rows in internal ids (a down edge or a missing slot reads the
+  // zero word); rows of padding ids (V <= p < vpad) read zero words only
+  for (uint32_t w = tid; w < 32u; w += kMsThreads) act[w] = 0u;
+  if (tid == 0) {
+    ms_wr(kZero, 0u);
+    ms_wr(Lay::kF1 + kZero, 0u);
+  }
+  uint32_t sink = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < NPT; ++i) {
+    const uint32_t p = tid + kMsThreads * i;
+    if (p < vpad) {
+      uint32_t o[4] = {kZero, kZero, kZero, kZero};
+      if (p < V) {
+        const uint32_t v = g.tord[p];
+        const uint2 r = g.row2[v];
+#pragma unroll
+        for (uint32_t c = 0; c < 4u; ++c) {
+          if (r.x + c < r.y) {
+            const uint32_t av = g.adj[r.x + c];
+            if (!(av & kEdgeDown)) o[c] = 4u * g.tinv[av];
+          }
+        }
+        if (g.ovl[v]) sink |= 1u << i;
+      }
+      *(lds_u64*)(size_t)(ebase + 8u * kMsThreads * i) =
+          (uint64_t)(o[0] | (o[1] << 16)) | ((uint64_t)(o[2] | (o[3] << 16)) << 32);
+    }
+  }
+  const uint32_t nbatch = (a.n + kMsBatch - 1u) / kMsBatch;
+  for (uint32_t unit = blockIdx.x; unit < nbatch;) {
+    const uint32_t k0 = unit * kMsBatch, nbk = min(kMsBatch, a.n - k0);
+    uint32_t tb = tid;
+    asm volatile("" : "+v"(tb));
+    // both frontier buffers zero over the owned ids, activity bitmasks zero
+#pragma unroll
+    for (uint32_t i = 0; i < NPT; ++i) {
+      ms_wr(4u * (tb + kMsThreads * i), 0u);
+      ms_wr(Lay::kF1 + 4u * (tb + kMsThreads * i), 0u);
+    }
+    if (tid < 24u) act[tid] = 0u;
+    __syncthreads();
+    // level 0: the sources' own bits in F[0]; their tiles' neighbourhoods are active at step 0
+    if (tid < nbk) {
+      const uint32_t src = a.sources[a.msperm[k0 + tid]];
+      if (src < V) {
+        const uint32_t ps = g.tinv[src];
+        lds_or((lds_u32*)(size_t)(4u * ps), 1u << tid);
+        const uint32_t* m = g.tmask + (size_t)(ps / kTileNodes) * kTileMaskWords;
+#pragma unroll
+        for (uint32_t k = 0; k < kTileMaskWords; ++k)
+          if (m[k]) lds_or(&act[k], m[k]);
+      }
+    }
+    __syncthreads();
+    uint32_t vis[NPT], p[8][NPT];
+#pragma unroll
+    for (uint32_t i = 0; i < NPT; ++i) {
+      const uint32_t q = tb + kMsThreads * i;
+      vis[i] = q < V ? ms_rd(4u * q) : ~0u;
+#pragma unroll
+      for (uint32_t b = 0; b < 8u; ++b) p[b][i] = vis[i];
+    }
+    uint32_t L = 0;
+    bool ovf = false;
+    for (;;) {
+      // this step's activity: bit (8i + wave) of act[L % 3] for slot i
+      const uint32_t cur_set = L % 3u;
+      uint32_t aw[5];
+#pragma unroll
+      for (uint32_t k = 0; k < 5u; ++k) aw[k] = __builtin_amdgcn_readfirstlane(act[8u * cur_set + k]);
+      uint32_t anyw = aw[0] | aw[1] | aw[2] | aw[3] | aw[4];
+#pragma unroll
+      for (uint32_t k = 5; k < kTileMaskWords; ++k) anyw |= __builtin_amdgcn_readfirstlane(act[8u * cur_set + k]);
+      if (anyw == 0u) break;  // uniform: every wave read the same words after the barrier
+      if (L + 2u > 254u) {  // levels must stay below 255 (u8 rows, 0xFF = unreached)
+        ovf = true;
+        break;
+      }
+      uint32_t A = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < NPT; ++i) A |= ((aw[i >> 2] >> (8u * (i & 3u) + wave)) & 1u) << i;
+      if (tid < 8u) act[8u * ((L + 2u) % 3u) + tid] = 0u;  // last read one step ago
+      lds_u32* const nact = act + 8u * ((L + 1u) % 3u);
+      uint32_t hm[8];
+#pragma unroll
+      for (uint32_t b = 0; b < 8u; ++b) hm[b] = (((L + 1u) >> b) & 1u) ? ~0u : 0u;
+      const uint32_t cur = (L & 1u) ? Lay::kF1 : 0u, nxt = (L & 1u) ? 0u : Lay::kF1;
+      uint32_t eaddr = ebase + 8u * kMsThreads * (A ? (uint32_t)__builtin_ctz(A) : 0u);
+      asm volatile("" : "+v"(eaddr));
+      uint64_t er = A ? *(const lds_u64*)(size_t)eaddr : 0ull;
+      MsUnroll<0, NPT>::run([&](auto ic) {
+        constexpr uint32_t i = decltype(ic)::value;
+        if ((A >> i) & 1u) {  // uniform
+          const uint32_t lo = (uint32_t)er, hi = (uint32_t)(er >> 32);
+          const uint32_t f = ms_rd(cur + (lo & 0xFFFFu)) | ms_rd(cur + (lo >> 16)) | ms_rd(cur + (hi & 0xFFFFu)) |
+                             ms_rd(cur + (hi >> 16));
+          const uint32_t rest = A & ~((2u << i) - 1u);
+          if (rest) {  // the next active slot's pull row, in flight with this slot's reads
+            uint32_t na = ebase + 8u * kMsThreads * (uint32_t)__builtin_ctz(rest);
+            asm volatile("" : "+v"(na));
+            er = *(const lds_u64*)(size_t)na;
+          }
+          const uint32_t nw = f & ~vis[i];
+          vis[i] |= nw;
+          const uint32_t fw = ((sink >> i) & 1u) ? 0u : nw;
+          ms_wr(nxt + 4u * (tb + kMsThreads * i), fw);
+#pragma unroll
+          for (uint32_t b = 0; b < 8u; ++b) p[b][i] |= nw & hm[b];
+          if (__builtin_amdgcn_ballot_w64(fw != 0u) != 0ull) {  // this tile emits: its neighbourhood is active next step
+            const uint32_t lane = __lane_id();
+            if (lane < kTileMaskWords) {
+              const uint32_t m = g.tmask[(size_t)(8u * i + wave) * kTileMaskWords + lane];
+              if (m) lds_or(&nact[lane], m);
+            }
+          }
+        }
+      });
+      lds_barrier();
+      ++L;
+    }
+    if (ovf) {
+      if (tid < nbk) {
+        const uint32_t k = a.msperm[k0 + tid];
+        a.rowok[k] = 0u;
+        a.ovf_list[atomicAdd(ovf_count, 1u)] = k;
+      }
+    } else {
+      // rows out: planes -> level bytes (as msbfs_kernel), stored at the node's own id
+#pragma unroll
+      for (uint32_t i = 0; i < NPT; ++i) {
+        uint32_t lw[8];
+#pragma unroll
+        for (uint32_t kb = 0; kb < 4u; ++kb) {
+          uint32_t lo = 0, hi = 0;
+#pragma unroll
+          for (uint32_t b = 0; b < 4u; ++b) {
+            lo |= ((p[b][i] >> (8u * kb)) & 0xFFu) << (8u * b);
+            hi |= ((p[b + 4u][i] >> (8u * kb)) & 0xFFu) << (8u * b);
+          }
+          uint64_t x = (uint64_t)lo | ((uint64_t)hi << 32);
+          uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+          x = x ^ t ^ (t << 7);
+          t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+          x = x ^ t ^ (t << 14);
+          t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+          x = x ^ t ^ (t << 28);
+          uint32_t w0 = (uint32_t)x, w1 = (uint32_t)(x >> 32);
+          w0 ^= ((swar_zero_hi(w0) | swar_zero_hi(~w0)) >> 7) * 0xFFu;
+          w1 ^= ((swar_zero_hi(w1) | swar_zero_hi(~w1)) >> 7) * 0xFFu;
+          lw[2u * kb] = w0;
+          lw[2u * kb + 1u] = w1;
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < 8u; ++c) p[c][i] = lw[c];
+      }
+      uint32_t orig[NPT];  // internal -> node id (the visited words' registers are free now)
+#pragma unroll
+      for (uint32_t i = 0; i < NPT; ++i) {
+        const uint32_t q = tb + kMsThreads * i;
+        orig[i] = q < V ? g.tord[q] : ~0u;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kMsBatch; ++j) {
+        if (j >= nbk) continue;  // uniform
+        const size_t k = a.msperm[k0 + j];
+        uint8_t* lrow = a.lvl8 + k * rb;
+        uint64_t* drow = a.dist + k * V;
+#pragma unroll
+        for (uint32_t i = 0; i < NPT; ++i) {
+          const uint32_t v = orig[i];
+          if (v >= V) continue;
+          const uint32_t l = (p[j >> 2][i] >> (8u * (j & 3u))) & 0xFFu;
+          lrow[v] = (uint8_t)l;
+          if (dist_here) store_row<uint64_t>(&drow[v], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt);
+        }
+      }
+      if (tid < nbk) {
+        const uint32_t k = a.msperm[k0 + tid];
+        a.rowok[k] = a.sources[k] < V ? 1u : 0u;
+      }
+    }
+    __syncthreads();  // every lane is done with this batch's LDS and next_unit
+    if (tid == 0) *next_unit = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unit = *next_unit;
+  }
+  retire_workgroup(ctr, nullptr);
+}
+
+template <uint32_t NPT>
+hipError_t launch_msbfs_tile_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t* blk, int num_cus,
+                                 hipStream_t s, uint32_t flags) {
+  using Lay = MsTLayout<NPT>;
+  auto k = msbfs_tile_kernel<NPT>;
+  const uint32_t lds = Lay::bytes(g.V);
+  hipError_t err =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  const uint32_t nbatch = (a.n + kMsBatch - 1u) / kMsBatch;
+  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(nbatch, (uint32_t)num_cus));
+  note_launch("msbfs_tile_kernel");
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMsThreads), lds, s, g, a, cost, blk, blk + 4, flags);
+  return hipGetLastError();
+}
+
 template <uint32_t NPT>
 hipError_t launch_msbfs_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t* blk, int num_cus,
                             hipStream_t s, uint32_t flags) {
@@ -706,11 +960,19 @@ hipError_t launch_msbfs_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost
 // Knobs: OPENR_SPF_BFS_MSBFS (0 off, 1 whenever it applies, 2 = auto) and
 // OPENR_SPF_BFS_REACH (0 off, 1 whenever it applies, 2 = auto); auto = batches of >= V
 // sources, where every neighbour of a source is likely in the batch.
+// the tile-active multi-source BFS serves the graph (tile order built, layout fits)
+bool ms_tile_ok(const DevGraph& g) {
+  return g.tord && g.tinv && g.tmask && g.ntiles <= 32u * kTileMaskWords &&
+         g.ntiles * kTileNodes <= MsTLayout<20>::kMaxV && MsTLayout<20>::bytes(g.V) <= kMaxLds &&
+         env_u32("OPENR_SPF_MSBFS_TILE", 1u, 0u, 1u) != 0u;
+}
+
 int allsrc_pass(const DevGraph& g, const SolveArgs& a) {
   if (!a.lvl8 || !a.rowmap || !a.rowok || a.out_row || a.perm || a.tight || a.ign_ptr || g.max_deg > 4u) return 0;
   const bool ms_ok = a.msperm && a.mscnt;
-  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 0u, 0u, 2u);  // opt-in: slower than the wave pass on G100
-  if (ms != 0u && ms_ok && MsLayout<20>::bytes(g.V) <= kMaxLds && g.V <= MsLayout<20>::kMaxV && (ms == 1u || a.n >= g.V))
+  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 2u, 0u, 2u);
+  if (ms != 0u && ms_ok && (ms_tile_ok(g) || (MsLayout<20>::bytes(g.V) <= kMaxLds && g.V <= MsLayout<20>::kMaxV)) &&
+      (ms == 1u || a.n >= g.V))
     return 2;
   const uint32_t rk = env_u32("OPENR_SPF_BFS_REACH", 0u, 0u, 2u);  // opt-in, as above
   if (rk != 0u && (rk == 1u || a.n >= g.V)) return 1;
@@ -737,13 +999,23 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
     hipLaunchKernelGGL(ms_perm_count_kernel, dim3(pgrid), dim3(256), 0, s, a.sources, a.n, a.rowmap, g.V, a.mscnt);
     hipLaunchKernelGGL(ms_perm_fill_kernel, dim3(pgrid), dim3(256), 0, s, g.corder, a.rowmap, a.n, g.V, a.mscnt,
                        a.msperm);
-    const uint32_t need = (g.V + kMsThreads - 1u) / kMsThreads;  // nodes per thread
-    if (info) info->kernel = "msbfs_kernel";
-    if (need <= 4u) err = launch_msbfs_npt<4>(g, a, cost, blk, num_cus, s, flags);
-    else if (need <= 8u) err = launch_msbfs_npt<8>(g, a, cost, blk, num_cus, s, flags);
-    else if (need <= 12u) err = launch_msbfs_npt<12>(g, a, cost, blk, num_cus, s, flags);
-    else if (need <= 16u) err = launch_msbfs_npt<16>(g, a, cost, blk, num_cus, s, flags);
-    else err = launch_msbfs_npt<20>(g, a, cost, blk, num_cus, s, flags);
+    if (ms_tile_ok(g)) {  // tile-active variant (OPENR_SPF_MSBFS_TILE=0: the dense pull)
+      const uint32_t need = (g.ntiles * kTileNodes + kMsThreads - 1u) / kMsThreads;  // internal ids per thread
+      if (info) info->kernel = "msbfs_tile_kernel";
+      if (need <= 4u) err = launch_msbfs_tile_npt<4>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 8u) err = launch_msbfs_tile_npt<8>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 12u) err = launch_msbfs_tile_npt<12>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 16u) err = launch_msbfs_tile_npt<16>(g, a, cost, blk, num_cus, s, flags);
+      else err = launch_msbfs_tile_npt<20>(g, a, cost, blk, num_cus, s, flags);
+    } else {
+      const uint32_t need = (g.V + kMsThreads - 1u) / kMsThreads;  // nodes per thread
+      if (info) info->kernel = "msbfs_kernel";
+      if (need <= 4u) err = launch_msbfs_npt<4>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 8u) err = launch_msbfs_npt<8>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 12u) err = launch_msbfs_npt<12>(g, a, cost, blk, num_cus, s, flags);
+      else if (need <= 16u) err = launch_msbfs_npt<16>(g, a, cost, blk, num_cus, s, flags);
+      else err = launch_msbfs_npt<20>(g, a, cost, blk, num_cus, s, flags);
+    }
   } else {
     constexpr int BLOCK = 128;
     // queue reads of lanes past a level's end land up to BLOCK entries past the halves

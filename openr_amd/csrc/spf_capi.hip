@@ -112,7 +112,7 @@ hipError_t reserve_counters(Device& d) {
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
                    g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld,
-                   g.corder};
+                   g.corder, g.tord, g.tinv, g.tmask};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -312,6 +312,71 @@ std::vector<uint32_t> cluster_order(uint32_t V, const uint32_t* row_ptr, const u
   for (auto const& kc : key)
     for (uint32_t i = start[kc.second]; i < start[kc.second + 1]; ++i) order.push_back(members[i]);
   return order;
+}
+
+// Tile order of the multi-source BFS (spf_allsrc.hip): 64 consecutive internal ids form a
+// tile, the unit whose activity a level tracks, so tiles should be compact (few tiles per
+// BFS level band). Seeds are taken in BFS order from a peripheral node (the farthest from
+// node 0, every component in turn); each unassigned seed grows a tile by BFS over
+// unassigned nodes until the tile holds 64 nodes (a seed whose region runs out leaves the
+// tile to the next seed). A performance heuristic over the structural graph: results do
+// not depend on it. Returns tord (internal -> node); tmask as DevGraph::tmask.
+void tile_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col, std::vector<uint32_t>& tord,
+                std::vector<uint32_t>& tmask) {
+  auto bfs_order = [&](uint32_t root, std::vector<uint32_t>& seen, uint32_t stamp, std::vector<uint32_t>& out) {
+    size_t h = out.size();
+    out.push_back(root);
+    seen[root] = stamp;
+    for (; h < out.size(); ++h) {
+      const uint32_t u = out[h];
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e)
+        if (seen[col[e]] != stamp) {
+          seen[col[e]] = stamp;
+          out.push_back(col[e]);
+        }
+    }
+  };
+  std::vector<uint32_t> seen(V, UINT32_MAX), seeds, tmp;
+  seeds.reserve(V);
+  for (uint32_t s = 0; s < V; ++s) {
+    if (seen[s] != UINT32_MAX) continue;
+    tmp.clear();
+    bfs_order(s, seen, 0u, tmp);  // the component of s; its last node is a peripheral root
+    const uint32_t root = tmp.back();
+    bfs_order(root, seen, 1u, seeds);
+  }
+  std::vector<uint8_t> taken(V, 0);
+  tord.clear();
+  tord.reserve(V);
+  std::vector<uint32_t> q;
+  for (uint32_t s : seeds) {
+    if (taken[s]) continue;
+    q.clear();
+    q.push_back(s);
+    taken[s] = 1;
+    tord.push_back(s);
+    for (size_t h = 0; h < q.size() && tord.size() % kTileNodes; ++h) {
+      const uint32_t u = q[h];
+      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1] && tord.size() % kTileNodes; ++e)
+        if (!taken[col[e]]) {
+          taken[col[e]] = 1;
+          tord.push_back(col[e]);
+          q.push_back(col[e]);
+        }
+    }
+  }
+  const uint32_t nt = (V + kTileNodes - 1u) / kTileNodes;
+  std::vector<uint32_t> tinv(V);
+  for (uint32_t p = 0; p < V; ++p) tinv[tord[p]] = p;
+  tmask.assign((size_t)nt * kTileMaskWords, 0u);
+  for (uint32_t u = 0; u < V; ++u) {
+    const uint32_t t = tinv[u] / kTileNodes;
+    tmask[(size_t)t * kTileMaskWords + t / 32u] |= 1u << (t & 31u);
+    for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
+      const uint32_t t2 = tinv[col[e]] / kTileNodes;
+      tmask[(size_t)t * kTileMaskWords + t2 / 32u] |= 1u << (t2 & 31u);
+    }
+  }
 }
 
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
@@ -1008,11 +1073,14 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   const FrontierEstimate est = estimate_frontier(V, gr->row_ptr, adj.data(), ovl.data());
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
   // multi-source BFS batch order (graphs it can serve: every row <= 4 edges, V <= 10 240)
-  std::vector<uint32_t> corder;
+  std::vector<uint32_t> corder, tord, tmask;
   {
     uint32_t md = 0;
     for (uint32_t u = 0; u < V; ++u) md = std::max(md, gr->row_ptr[u + 1] - gr->row_ptr[u]);
-    if (V && V <= 10240u && md <= 4u) corder = cluster_order(V, gr->row_ptr, gr->col);
+    if (V && V <= 10240u && md <= 4u) {
+      corder = cluster_order(V, gr->row_ptr, gr->col);
+      tile_order(V, gr->row_ptr, gr->col, tord, tmask);
+    }
   }
 
   for (Device& d : ctx->devs) {
@@ -1078,6 +1146,14 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.ledge, ledge.data(), L);
     if (err == hipSuccess) err = up(&g.rank, gr->name_rank, V);
     if (err == hipSuccess && !corder.empty()) err = up(&g.corder, corder.data(), V);
+    if (err == hipSuccess && !tord.empty()) {
+      std::vector<uint32_t> tinv(V);
+      for (uint32_t p = 0; p < V; ++p) tinv[tord[p]] = p;
+      err = up(&g.tord, tord.data(), V);
+      if (err == hipSuccess) err = up(&g.tinv, tinv.data(), V);
+      if (err == hipSuccess) err = up(&g.tmask, tmask.data(), tmask.size());
+      g.ntiles = (uint32_t)(tmask.size() / kTileMaskWords);
+    }
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;

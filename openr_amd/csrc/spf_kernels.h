@@ -47,7 +47,16 @@ struct DevGraph {
                                //     overloaded, win[e], lid[e], rev[e]} (one 16-byte load per edge)
   uint32_t* corder = nullptr;  // [V] or null: nodes grouped into compact clusters of 32, the clusters
                                //     deepest-first (multi-source BFS batches of all-sources calls)
+  // Tile order of the multi-source BFS (null when corder is): internal id p of node
+  // tord[p] (p < V; 64 consecutive internal ids = one tile of compact nodes), tinv = its
+  // inverse, tmask[t][8] = bitmask of the tiles holding a neighbour of a node of tile t
+  // (structural edges, any state; t itself included). ntiles = ceil(V / 64) <= 256.
+  uint32_t* tord = nullptr;
+  uint32_t* tinv = nullptr;
+  uint32_t* tmask = nullptr;
+  uint32_t ntiles = 0;
 };
+constexpr uint32_t kTileNodes = 64, kTileMaskWords = 8;
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
 // Sink flag of a transit row: ellt[u].x and row2t[u].x carry it when u is overloaded.

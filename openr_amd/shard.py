@@ -85,6 +85,101 @@ class GatherBuffers:
         return self._rows(1)
 
 
+class CompactGather:
+    """The config-3 exchange in level form: on a uniform-cost graph (every
+    usable edge costs ``cost``, or useLinkMetric=false) every finite distance of
+    LinkState::runSpf is level x cost, so a rank sends its rows as levels — u8 when every
+    finite level is <= 254, else u16 (all ones = unreached, i.e. UINT64_MAX) — plus its
+    next-hop rows, instead of u64 distances: 1 + B instead of 8 + B bytes per (source,
+    node). Receivers keep the gathered level rows and expand u64 distances on demand
+    (``full_dist``), bit-identical to the senders' rows.
+
+    ``dist_shard`` [n_r, V] int64 (UINT64_MAX viewed as -1) and ``nh_shard`` [n_r, V, B]
+    are this rank's engine rows (device tensors for RCCL, host tensors for gloo);
+    ``max_level`` bounds every finite level of the whole job (e.g. the largest finite
+    distance / cost, measured once outside any timed region).
+    """
+
+    def __init__(self, dist_shard, nh_shard, n_units: int, world: int, cost: int, max_level: int) -> None:
+        import torch
+
+        if cost < 1:
+            raise ValueError("cost must be >= 1")
+        if max_level > 65534:
+            raise ValueError("levels do not fit u16: use GatherBuffers")
+        self.cost = int(cost)
+        self.dtype = torch.uint8 if max_level <= 254 else torch.int16  # int16 holds u16 bit patterns
+        self.sentinel = 0xFF if self.dtype == torch.uint8 else -1  # all ones
+        self.dist_shard = dist_shard
+        self.sizes = shard_sizes(n_units, world)
+        self.m = max(self.sizes) if self.sizes else 0
+        self.world = world
+        V = dist_shard.shape[1]
+        dev = dist_shard.device
+        self.lv_send = torch.zeros((self.m, V), dtype=self.dtype, device=dev)
+        self.lv_full = torch.empty((world * self.m, V), dtype=self.dtype, device=dev)
+        self.nh = None
+        if nh_shard is not None:
+            tail = tuple(nh_shard.shape[1:])
+            send = nh_shard if nh_shard.shape[0] == self.m and nh_shard.is_contiguous() else torch.zeros(
+                (self.m,) + tail, dtype=nh_shard.dtype, device=dev)
+            self.nh = (nh_shard, send, torch.empty((world * self.m,) + tail, dtype=nh_shard.dtype, device=dev))
+        nb = 0
+        if nh_shard is not None:
+            nb = nh_shard.element_size()
+            for x in nh_shard.shape[2:]:
+                nb *= int(x)
+        self.bytes_per_rank = self.m * V * (self.lv_send.element_size() + nb)
+
+    def encode(self) -> None:
+        """This rank's u64 rows -> level rows (on the rows' device)."""
+        import torch
+
+        d = self.dist_shard
+        n = d.shape[0]
+        if n == 0:
+            return
+        lv = torch.div(d, self.cost, rounding_mode="floor")
+        lv = torch.where(d == -1, torch.full_like(lv, self.sentinel), lv)
+        self.lv_send[:n].copy_(lv.to(self.dtype))
+
+    def allgather(self) -> None:
+        import torch
+        import torch.distributed as dist
+
+        self.encode()
+        # byte views: u16 level rows travel as bytes (gloo has no 16-bit integer type)
+        dist.all_gather_into_tensor(self.lv_full.view(torch.uint8), self.lv_send.view(torch.uint8))
+        if self.nh is not None:
+            src, send, full = self.nh
+            if send is not src:
+                send[: src.shape[0]].copy_(src)
+            dist.all_gather_into_tensor(full, send)
+
+    def _rows(self, full):
+        import torch
+
+        return torch.cat([full[r * self.m: r * self.m + self.sizes[r]] for r in range(self.world)], dim=0)
+
+    def full_levels(self):
+        return self._rows(self.lv_full)
+
+    def full_dist(self):
+        """The gathered rows expanded to u64 distances (int64 view, UINT64_MAX = -1)."""
+        import torch
+
+        lv = self.full_levels()
+        unreached = lv == self.sentinel
+        d = lv.to(torch.int64)
+        if self.dtype != torch.uint8:
+            d = d & 0xFFFF
+        d = d * self.cost
+        return torch.where(unreached, torch.full_like(d, -1), d)
+
+    def full_nh(self):
+        return self._rows(self.nh[2]) if self.nh is not None else None
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """MAX of a host scalar over all ranks (bench timing: the slowest rank's clock);
     the identity without an initialised process group."""

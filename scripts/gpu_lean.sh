@@ -1,18 +1,25 @@
 # Scratch GPU experiment script: rewritten for each measurement and run as
 #   gpurun -- bash scripts/gpu_lean.sh
-# (its last contents: all-sources pass parity, then kernel times of the G100 launch)
+# (its last contents: tile-active multi-source BFS — parity of the all-sources passes,
+# then G100 batch latency of the tile / dense / lean passes and a kernel trace)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/msbfs2
+OUT=$R/gpurun_out/tile1
 mkdir -p $OUT
 cd $R
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_reach.py tests/test_gpu_configs.py -k "reach or msbfs or config3" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+timeout -k 10 400 python3 -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_reach.py tests/test_gpu_configs.py -k "reach or config3" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
-timeout -k 10 120 python3 scripts/batch_latency.py --sizes 10000 --reps 10 > $OUT/lat.log 2>&1 || { tail $OUT/lat.log; exit 1; }
-grep sources $OUT/lat.log
+timeout -k 10 400 python3 -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_cpp_host.py tests/test_gpu_multirank.py > $OUT/tests2.log 2>&1 || { tail -60 $OUT/tests2.log; exit 1; }
+tail -1 $OUT/tests2.log
+tests/cpp/build/linkstate_test gpu 2>&1 | grep -E "weighted|FAIL|failures"
+for cfg in "OPENR_SPF_MSBFS_TILE=1" "OPENR_SPF_MSBFS_TILE=0" "OPENR_SPF_BFS_MSBFS=0" "OPENR_SPF_REACH_DIST=2"; do
+  echo "== $cfg"
+  env $cfg timeout -k 10 120 python3 scripts/batch_latency.py --sizes 1250,2500,10000 --reps 10 > $OUT/lat.log 2>&1 || { tail $OUT/lat.log; exit 1; }
+  grep sources $OUT/lat.log
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/scripts/batch_latency.py --sizes 10000 --reps 10 > $OUT/trace.log 2>&1 || { tail $OUT/trace.log; exit 1; }
 f=$(find $OUT/trace -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats.csv
 python3 -c "
 import csv
-for r in csv.DictReader(open('$OUT/kernel_stats.csv')): print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')" | head -6
+for r in csv.DictReader(open('$OUT/kernel_stats.csv')): print(r['Name'][:70], r['Calls'], round(float(r['AverageNs'])/1e3,1), 'us')"

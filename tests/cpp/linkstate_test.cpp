@@ -5,6 +5,7 @@
 // oracle cross-checks (the oracle is linked here as the checker only).
 //   linkstate_test cpu   -> host-only tests (no GPU needed)
 //   linkstate_test gpu   -> tests that run SPF on the engine
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -332,9 +333,10 @@ TEST_CPU(LinkStateTest_HoldUpAndMirror) {
   EXPECT_EQ(4u, m2.metric[m2.rowPtr[m2.id.at("b")]]);
 }
 
-// The mirror (and so the device graph) is rebuilt only when the effective topology
-// changes: a re-advertised database, or one that changes only adjacency labels, keeps it
-// (ADVICE r1); a metric change or a new node rebuilds it.
+// The mirror (and so the device graph) is rebuilt only when the link structure changes: a
+// re-advertised database, or one that changes only adjacency labels, keeps it;
+// a metric change patches it in place (round 3: same generation, new metric); a new node
+// rebuilds it.
 TEST_CPU(LinkStateTest_MirrorRebuiltOnlyOnTopologyChange) {
   LinkState ls(kArea);
   ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 1), 0, 0);
@@ -355,8 +357,9 @@ TEST_CPU(LinkStateTest_MirrorRebuiltOnlyOnTopologyChange) {
   ch = ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 9)}, 1), 0, 0);
   EXPECT_TRUE(ch.topologyChanged);
   auto const& m = ls.csrMirror();
-  EXPECT_TRUE(ls.mirrorGeneration() != g0);
+  EXPECT_EQ(g0, ls.mirrorGeneration());  // patched in place
   EXPECT_EQ(9u, m.metric[m.rowPtr[m.id.at("a")]]);
+  EXPECT_EQ(4u, m.metric[m.rowPtr[m.id.at("b")]]);
   const uint64_t g1 = ls.mirrorGeneration();
   ls.updateAdjacencyDatabase(createAdjDb("c", {}, 3), 0, 0);  // isolated new node
   auto const& m2 = ls.csrMirror();
@@ -720,6 +723,180 @@ TEST_GPU(LinkState_WideHubOracleParity) {
   }
   auto const& r0 = ls.getSpfResult("0", true);
   EXPECT_EQ(1u, r0.at("3").nextHops().size());  // direct neighbour 3 of the 300-wide hub
+}
+
+// getSpfResult(names[s], useMetric) of every source in `srcs` equals the oracle run on the
+// current CSR mirror: reached set, metrics, next-hop names and pathLinks (link and previous
+// node, in order).
+static bool spfMatchesOracle(const LinkState& ls, const std::vector<uint32_t>& srcs, bool useMetric) {
+  auto const& m = ls.csrMirror();
+  oracle_graph og{(uint32_t)m.names.size(), (uint32_t)m.col.size(), (uint32_t)m.links.size(), m.rowPtr.data(),
+                  m.col.data(), m.metric.data(), m.linkId.data(), m.edgeUp.data(), m.overloaded.data(),
+                  m.nameRank.data()};
+  const uint32_t NV = og.num_nodes, NE = og.num_dir_edges;
+  std::vector<uint64_t> dist(NV);
+  std::vector<uint32_t> plp(NV + 1), ple(NE + 1);
+  bool ok = true;
+  for (uint32_t s : srcs) {
+    const uint32_t nb = (oracle_num_distinct_neighbors(&og, s) + 7) / 8 + 1;
+    std::vector<uint8_t> nh((size_t)NV * nb);
+    std::vector<uint32_t> nbr;  // distinct neighbours of s in row order = next-hop bit order
+    for (uint32_t e = m.rowPtr[s]; e < m.rowPtr[s + 1]; ++e)
+      if (std::find(nbr.begin(), nbr.end(), m.col[e]) == nbr.end()) nbr.push_back(m.col[e]);
+    auto const& res = ls.getSpfResult(m.names[s], useMetric);
+    const int64_t cnt = oracle_run_spf(&og, s, useMetric, nullptr, dist.data(), nh.data(), nb, nullptr, plp.data(),
+                                       ple.data());
+    ok &= (size_t)cnt == res.size();
+    for (uint32_t v = 0; v < NV && ok; ++v) {
+      auto it = res.find(m.names[v]);
+      if (dist[v] == UINT64_MAX) {
+        ok &= it == res.end();
+        continue;
+      }
+      if (it == res.end()) {
+        ok = false;
+        break;
+      }
+      ok &= dist[v] == it->second.metric();
+      std::unordered_set<std::string> want;
+      for (uint32_t i = 0; i < nbr.size(); ++i)
+        if ((nh[(size_t)v * nb + (i >> 3)] >> (i & 7)) & 1u) want.insert(m.names[nbr[i]]);
+      ok &= want == it->second.nextHops();
+      auto const& pls = it->second.pathLinks();
+      ok &= pls.size() == plp[v + 1] - plp[v];
+      for (uint32_t i = 0; ok && i < pls.size(); ++i) {
+        const uint32_t e = ple[plp[v] + i];
+        ok &= pls[i].link.get() == m.links[m.linkId[e]].get() && pls[i].prevNode == m.names[m.edgeOwner[e]];
+      }
+    }
+    if (!ok) std::printf("    oracle mismatch: source %s (useMetric %d)\n", m.names[s].c_str(), (int)useMetric);
+  }
+  return ok;
+}
+
+// n x n grid adjacency databases (DecisionTest.cpp:4207-4355 names / ifnames), metric w(i, j)
+template <typename W>
+static thrift::AdjacencyDatabase gridDb(int n, int i, int j, W w, bool overloaded = false) {
+  std::vector<thrift::Adjacency> adjs;
+  auto add = [&](int ii, int jj, const char* ifn, const char* oifn) {
+    if (ii < 0 || ii >= n || jj < 0 || jj >= n) return;
+    adjs.push_back(createAdjacency(std::to_string(ii * n + jj), ifn, oifn, w(i, j, ii, jj)));
+  };
+  add(i, j + 1, "0/1", "0/3");
+  add(i - 1, j, "0/2", "0/4");
+  add(i, j - 1, "0/3", "0/1");
+  add(i + 1, j, "0/4", "0/2");
+  auto db = createAdjDb(std::to_string(i * n + j), adjs, i * n + j + 1);
+  db.isOverloaded = overloaded;
+  return db;
+}
+
+// attribute-only updates — a node overload toggle (the BM_DecisionGrid /
+// BM_DecisionFabric update, RoutingBenchmarkUtils.cpp:407-479), a metric change, an
+// adjacency overload (Link::isUp), and held values released by decrementHolds — patch the
+// engine's resident graph instead of re-uploading it, keep the memo's dense rows and
+// refresh only the rows the change can affect; every result equals the oracle on the
+// updated graph, and decision.spf_runs counts each source read again as the reference's
+// cleared memo would (LinkState.cpp:714-717).
+TEST_GPU(LinkState_AttributeUpdatesPatchAndRefresh) {
+  const int n = 12;
+  for (int weighted = 0; weighted < 2; ++weighted) {
+    auto w = [weighted](int i, int j, int ii, int jj) { return weighted ? 1 + (i * 7 + j * 3 + ii + jj * 5) % 9 : 1; };
+    LinkState ls(kArea);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) ls.updateAdjacencyDatabase(gridDb(n, i, j, w));
+    std::vector<std::string> all;
+    std::vector<uint32_t> ids;
+    for (int v = 0; v < n * n; ++v) all.push_back(std::to_string(v));
+    ls.prefetchSpfResults(all);
+    ls.prefetchSpfResults(all, false);
+    auto const& m0 = ls.csrMirror();
+    for (auto const& a : all) ids.push_back(m0.id.at(a));
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, false));
+    const uint64_t gen = ls.mirrorGeneration(), uploads = ls.updateStats().graphUploads;
+    EXPECT_EQ((size_t)(n * n), ls.denseRows(true));
+    // 1) node overload on, then off (the benchmark's toggle)
+    const int x = 5 * n + 6, xi = x / n, xj = x % n;
+    for (int on = 1; on >= 0; --on) {
+      auto ch = ls.updateAdjacencyDatabase(gridDb(n, xi, xj, w, on != 0));
+      EXPECT_TRUE(ch.topologyChanged);
+      SpfCounters::get().reset();
+      ls.prefetchSpfResults(all);
+      EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+      EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());  // every source read once, counted once
+      EXPECT_TRUE(spfMatchesOracle(ls, ids, false));
+    }
+    EXPECT_EQ(gen, ls.mirrorGeneration());
+    EXPECT_EQ(uploads, ls.updateStats().graphUploads);  // patched, never re-uploaded
+    EXPECT_EQ(2u, (unsigned)ls.updateStats().patches);
+    // incremental: the refreshes re-solved fewer rows than they kept
+    EXPECT_TRUE(ls.updateStats().rowsRefreshed < ls.updateStats().rowsKept);
+    // 2) metric change of one adjacency, 3) adjacency overload (link down), then back up
+    auto w2 = [&](int i, int j, int ii, int jj) { return (i == 3 && j == 3 && jj == 4) ? 40 : w(i, j, ii, jj); };
+    ls.updateAdjacencyDatabase(gridDb(n, 3, 3, w2));
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    auto db = gridDb(n, 7, 2, w);
+    db.adjacencies[0].isOverloaded = true;
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db).topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, false));
+    db.adjacencies[0].isOverloaded = false;
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db).topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    // 4) a metric rise held down for two decrementHolds ticks (HoldableValue), released there
+    auto w3 = [&](int i, int j, int ii, int jj) { return (i == 9 && j == 9) ? 30 : w2(i, j, ii, jj); };
+    EXPECT_FALSE(ls.updateAdjacencyDatabase(gridDb(n, 9, 9, w3), 0, 2).topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    EXPECT_FALSE(ls.decrementHolds().topologyChanged);
+    EXPECT_TRUE(ls.decrementHolds().topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, false));
+    EXPECT_EQ(gen, ls.mirrorGeneration());
+    EXPECT_EQ(uploads, ls.updateStats().graphUploads);
+    // a structural change (a new link) rebuilds the mirror and uploads it
+    ls.updateAdjacencyDatabase(createAdjDb("extra", {createAdjacency("0", "x/0", "0/x", 1)}, 999));
+    auto db0 = gridDb(n, 0, 0, w);
+    db0.adjacencies.push_back(createAdjacency("extra", "0/x", "x/0", 1));
+    EXPECT_TRUE(ls.updateAdjacencyDatabase(db0).topologyChanged);
+    ids.clear();
+    auto const& m1 = ls.csrMirror();
+    for (uint32_t v = 0; v < m1.names.size(); ++v) ids.push_back(v);
+    EXPECT_TRUE(spfMatchesOracle(ls, ids, true));
+    EXPECT_TRUE(gen != ls.mirrorGeneration());
+    EXPECT_EQ(uploads + 1, ls.updateStats().graphUploads);
+    std::printf("    weighted=%d patches=%llu refreshes=%llu rows kept=%llu re-solved=%llu\n", weighted,
+                (unsigned long long)ls.updateStats().patches, (unsigned long long)ls.updateStats().refreshes,
+                (unsigned long long)ls.updateStats().rowsKept, (unsigned long long)ls.updateStats().rowsRefreshed);
+  }
+}
+
+// SpfView (the route build's dense read path) serves what getSpfResult does.
+TEST_GPU(LinkState_SpfViewMatchesSpfResult) {
+  const int n = 9;
+  LinkState ls(kArea);
+  auto w = [](int i, int j, int ii, int jj) { return 1 + (i + 2 * j + ii * jj) % 5; };
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) ls.updateAdjacencyDatabase(gridDb(n, i, j, w, i * n + j == 40));
+  bool ok = true;
+  for (int useMetric = 0; useMetric < 2; ++useMetric)
+    for (int s = 0; s < n * n; s += 4) {
+      auto const v = ls.getSpfView(std::to_string(s), useMetric != 0);
+      auto const& r = ls.getSpfResult(std::to_string(s), useMetric != 0);
+      for (int d = 0; d < n * n; ++d) {
+        const std::string dn = std::to_string(d);
+        auto it = r.find(dn);
+        ok &= v.reached(dn) == (it != r.end());
+        if (it == r.end()) continue;
+        ok &= v.metric(dn) == it->second.metric();
+        auto nh = v.nextHops(dn);
+        ok &= std::unordered_set<std::string>(nh.begin(), nh.end()) == it->second.nextHops();
+      }
+    }
+  EXPECT_TRUE(ok);
+  auto const u = ls.getSpfView("no-such-node");
+  EXPECT_TRUE(u.reached("no-such-node"));
+  EXPECT_FALSE(u.reached("0"));
 }
 
 int main(int argc, char** argv) { return run_tests(argc, argv); }

@@ -5,8 +5,8 @@ all pairs across GPUs) run one process per GPU, each holding a CSR replica and s
 contiguous block of units (shard.py), with the result shards all-gathered. The 1-GPU
 box cannot host two RCCL ranks on one device, so here both ranks put the ENGINE on
 cuda:0 and exchange their shards over gloo (host tensors); the per-rank code path —
-shard_range, SpfEngine.solve / ksp2 on the rank's block, GatherBuffers — is the one
-bench.py runs over RCCL. The gathered rows must equal the oracle's, bit for bit.
+shard_range, SpfEngine.solve / ksp2 on the rank's block, GatherBuffers and the compact
+level-row CompactGather — is the one bench.py runs over RCCL. The gathered rows must equal the oracle's, bit for bit.
 """
 import os
 import socket
@@ -44,8 +44,11 @@ def _rank_main(rank, world, port, gname, out_dir):
     eng.set_graph(g)
     lo, hi = shard.shard_range(V, rank, world)
     d, nh, _ = eng.solve(np.arange(lo, hi, dtype=np.uint32), True)
-    full_d, full_nh = shard.allgather_results(torch.from_numpy(d.view(np.int64).copy()), torch.from_numpy(nh.copy()),
-                                              V, world)
+    d_t, nh_t = torch.from_numpy(d.view(np.int64).copy()), torch.from_numpy(nh.copy())
+    full_d, full_nh = shard.allgather_results(d_t, nh_t, V, world)
+    # the compact exchange bench.py runs by default (u8 level rows + next hops; unit metrics)
+    cg = shard.CompactGather(d_t, nh_t, V, world, cost=1, max_level=254)
+    cg.allgather()
     # KSP2 pairs sharded the same way (config 5): this rank's sources x a destination sample
     ks = np.arange(lo, hi, max(1, (hi - lo) // 5), dtype=np.uint32)
     dst = np.arange(0, V, 7, dtype=np.uint32)
@@ -56,6 +59,8 @@ def _rank_main(rank, world, port, gname, out_dir):
     if rank == 0:
         np.save(os.path.join(out_dir, "dist.npy"), full_d.numpy())
         np.save(os.path.join(out_dir, "nh.npy"), full_nh.numpy())
+        np.save(os.path.join(out_dir, "cdist.npy"), cg.full_dist().numpy())
+        np.save(os.path.join(out_dir, "cnh.npy"), cg.full_nh().numpy())
     eng.close()
     dist.destroy_process_group()
 
@@ -75,6 +80,8 @@ def test_engine_ranks_shard_and_allgather(tmp_path, gname, world):
     d, nh = o.all_sources(np.arange(V, dtype=np.uint32), True, nthreads=8)
     np.testing.assert_array_equal(np.load(tmp_path / "dist.npy").view(np.uint64), d)
     np.testing.assert_array_equal(np.load(tmp_path / "nh.npy"), nh)
+    np.testing.assert_array_equal(np.load(tmp_path / "cdist.npy").view(np.uint64), d)
+    np.testing.assert_array_equal(np.load(tmp_path / "cnh.npy"), nh)
     dst = np.arange(0, V, 7, dtype=np.uint32)
     for r in range(world):
         ks = np.load(tmp_path / f"ksp_src_{r}.npy")

@@ -29,14 +29,16 @@ def eng():
     e.close()
 
 
-PASS_KERNEL = {"msbfs": "msbfs_kernel", "reach": "bfs_reach_kernel"}
+PASS_KERNEL = {"msbfs": "msbfs_tile_kernel", "msbfs_dense": "msbfs_kernel", "reach": "bfs_reach_kernel"}
 
 
-@pytest.fixture(autouse=True, params=["msbfs", "reach"])
+@pytest.fixture(autouse=True, params=["msbfs", "msbfs_dense", "reach"])
 def level_pass(request, monkeypatch):
-    """Every test runs on both level passes (forced: also on batches smaller than V)."""
+    """Every test runs on every level pass (forced: also on batches smaller than V):
+    the tile-active multi-source BFS, the dense-pull one and the per-source reach pass."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
-    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "1" if request.param == "msbfs" else "0")
+    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "0" if request.param == "reach" else "1")
+    monkeypatch.setenv("OPENR_SPF_MSBFS_TILE", "0" if request.param == "msbfs_dense" else "1")
     monkeypatch.setenv("OPENR_SPF_BFS_REACH", "1")
     return request.param
 
@@ -168,8 +170,8 @@ def test_grid100_full_batch_is_msbfs(eng, monkeypatch, level_pass):
     """All 10 000 G100 sources in one call with the multi-source pass in auto mode run
     it; a sample of rows vs the oracle
     (test_gpu_configs.py checks every row)."""
-    if level_pass != "msbfs":
-        pytest.skip("default configuration only")
+    if level_pass == "reach":
+        pytest.skip("multi-source passes")
     monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "2")
     monkeypatch.delenv("OPENR_SPF_BFS_REACH")
     g = T.grid_fast(100)
@@ -177,7 +179,7 @@ def test_grid100_full_batch_is_msbfs(eng, monkeypatch, level_pass):
     src = np.arange(10000, dtype=np.uint32)
     dist, nh, _ = eng.solve(src, True)
     ran = eng.last_kernels()
-    assert "msbfs_kernel" in ran and "nh_from_levels_kernel" in ran, ran
+    assert PASS_KERNEL[level_pass] in ran and "nh_from_levels_kernel" in ran, ran
     o = Oracle(g)
     pick = np.array([0, 99, 4950, 5050, 9900, 9999, 1234, 7777], dtype=np.uint32)
     od, on = o.all_sources(pick, True, nthreads=8)

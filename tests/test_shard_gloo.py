@@ -1,6 +1,6 @@
 """Multi-rank sharding on CPU (gloo): contiguous source blocks per rank, the result
-all-gather of uneven shards (shard.py), and the max-over-ranks timing reduction the
-bench uses. The per-rank solve here is the CPU oracle standing in for the GPU engine
+all-gather of uneven shards (shard.py) in full (u64) and compact (level-row) form, and
+the max-over-ranks timing reduction the bench uses. The per-rank solve here is the CPU oracle standing in for the GPU engine
 (test infrastructure only); the GPU path runs the same shard.py code over RCCL.
 """
 import os
@@ -35,10 +35,22 @@ def _worker(rank, world, port, n, out_dir):
     nh_t = torch.from_numpy(nh.copy())
     full_d, full_nh = shard.allgather_results(d_t, nh_t, V, world)
     t = shard.max_over_ranks(float(rank + 1))
+    # the compact (level-row) form of the same exchange: u8 levels, and u16 levels of a
+    # cost-7 copy of the grid (7 x level: the receiver expands level x cost)
+    cg = shard.CompactGather(d_t, nh_t, V, world, cost=1, max_level=2 * (n - 1))
+    cg.allgather()
+    d7 = torch.where(d_t == -1, d_t, d_t * 7)
+    cg16 = shard.CompactGather(d7, None, V, world, cost=7, max_level=300)
+    cg16.allgather()
     if rank == 0:
         np.save(os.path.join(out_dir, "dist.npy"), full_d.numpy())
         np.save(os.path.join(out_dir, "nh.npy"), full_nh.numpy())
         np.save(os.path.join(out_dir, "tmax.npy"), np.array([t]))
+        np.save(os.path.join(out_dir, "cdist.npy"), cg.full_dist().numpy())
+        np.save(os.path.join(out_dir, "cnh.npy"), cg.full_nh().numpy())
+        np.save(os.path.join(out_dir, "cdist7.npy"), cg16.full_dist().numpy())
+        np.save(os.path.join(out_dir, "cbytes.npy"), np.array([cg.bytes_per_rank, cg16.bytes_per_rank,
+                                                               str(cg.lv_full.dtype) == "torch.uint8"]))
     dist.destroy_process_group()
 
 
@@ -54,6 +66,14 @@ def test_sharded_all_sources_allgather(tmp_path, world, n):
     np.testing.assert_array_equal(np.load(tmp_path / "dist.npy").view(np.uint64), d)
     np.testing.assert_array_equal(np.load(tmp_path / "nh.npy"), nh)
     assert float(np.load(tmp_path / "tmax.npy")[0]) == float(world)
+    # compact gather: identical rows from u8 / u16 level rows, 1 + B (2 + 0) bytes per entry
+    np.testing.assert_array_equal(np.load(tmp_path / "cdist.npy").view(np.uint64), d)
+    np.testing.assert_array_equal(np.load(tmp_path / "cnh.npy"), nh)
+    d7 = np.where(d == np.uint64(2**64 - 1), d, d * np.uint64(7))
+    np.testing.assert_array_equal(np.load(tmp_path / "cdist7.npy").view(np.uint64), d7)
+    m = max(shard.shard_sizes(V, world))
+    b8, b16, is_u8 = np.load(tmp_path / "cbytes.npy").tolist()
+    assert is_u8 and b8 == m * V * (1 + nh.shape[2]) and b16 == m * V * 2
 
 
 def test_shard_ranges_cover_exactly():
