@@ -105,6 +105,7 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
   const uint32_t nb = a.nh_bytes;
   uint8_t* nrow = a.nh ? a.nh + out_row_of(a, sid) * V * nb : nullptr;
   if (GENERIC && a.lvl16) {  // u16 level row (dist-only, never sliced)
+    if (a.lvl_tag) return;  // tagged rows: unreached nodes stay unwritten
     uint16_t* lrow = a.lvl16 + out_row_of(a, sid) * V;
     for (uint32_t v = tid; v < V; v += BLOCK)
       if ((S::field(st, v) & kCodeMask) == 0u) lrow[v] = 0xFFFFu;
@@ -198,8 +199,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
       uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       uint16_t* lrow = (GENERIC && a.lvl16) ? a.lvl16 + out_row_of(a, sid) * V : nullptr;
       // settle node u on level l (distance l * cost): u64 distance or u16 level row
+      const uint32_t ltag = (GENERIC && lrow) ? a.lvl_tag << a.lvl_shift : 0u;
       auto put = [&](uint32_t u, uint32_t l) {
-        if (GENERIC && lrow) lrow[u] = (uint16_t)l;
+        if (GENERIC && lrow) lrow[u] = (uint16_t)(ltag | l);
         else drow[u] = (uint64_t)l * cost;
       };
       for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;

@@ -89,6 +89,8 @@ struct Device {
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
   DevBuf<uint16_t> krows16;  // KSP2 second SPFs on the code family: u16 level rows
+  uint32_t ktag = 0;         // tagged krows16: tag of the last chunk (0 = rows zeroed)
+  size_t ktag_rows = 0;      // entries of krows16 zeroed for tagging
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
@@ -779,13 +781,28 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
   const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
-  // uniform-cost second SPFs on the code family are distance-only: u16 level rows
+  // uniform-cost second SPFs on the code family are distance-only: u16 level rows, tagged
+  // (SolveArgs::lvl_tag: a solve writes only the nodes it settles — it stops at the pair's
+  // target — and the trace reads other entries as unreached) when levels leave >= 2 tag bits
   const bool rows16 = ign_plan.bfs && ign_plan.family == kFamCode;
+  uint32_t lshift = 1;
+  while ((1u << lshift) < V) ++lshift;  // levels < V <= 2^lshift
+  const uint32_t tag_max = lshift <= 14u ? (1u << (16u - lshift)) - 1u : 0u;
+  const char* tag_env = std::getenv("OPENR_SPF_KSP_TAG");  // 0: untagged rows, unreached fill (A/B)
+  const bool tagged = rows16 && tag_max && !(tag_env && std::atoi(tag_env) == 0);
   const size_t row_bytes = (size_t)V * (rows16 ? 2u : 8u);
-  const uint32_t chunk =
+  uint32_t chunk =
       (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / (row_bytes + 4u * ign_cap)));
+  if (const char* e = std::getenv("OPENR_SPF_KSP_CHUNK"))  // pairs per chunk (tests: many chunks, tag wrap)
+    if (std::atoi(e) > 0) chunk = std::min<uint32_t>(chunk, (uint32_t)std::atoi(e));
   if (rows16) OPENR_TRY(d.krows16.reserve((size_t)chunk * V));
   else OPENR_TRY(d.krows.reserve((size_t)chunk * V));
+  uint32_t& tag = d.ktag;  // the tag of the last chunk written into krows16 (0: rows all zero)
+  if (tagged && d.ktag_rows < (size_t)chunk * V) {  // fresh or grown buffer: no valid tag in it
+    OPENR_TRY(hipMemsetAsync(d.krows16.p, 0, (size_t)chunk * V * sizeof(uint16_t), s));
+    d.ktag_rows = (size_t)chunk * V;
+    tag = 0;
+  }
   OPENR_TRY(d.kign.reserve((size_t)chunk * ign_cap));
   OPENR_TRY(d.kend.reserve(chunk));
   OPENR_TRY(d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V));
@@ -824,6 +841,14 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.ign_links = d.kign.p;
     b.dist = rows16 ? nullptr : d.krows.p;
     b.lvl16 = rows16 ? d.krows16.p : nullptr;
+    if (tagged) {
+      if (tag == tag_max) {  // every tag used since the rows were zeroed: zero them again
+        OPENR_TRY(hipMemsetAsync(d.krows16.p, 0, d.ktag_rows * sizeof(uint16_t), s));
+        tag = 0;
+      }
+      b.lvl_tag = ++tag;
+      b.lvl_shift = lshift;
+    }
     b.nh_bits = ctx->nh_bits;
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
@@ -833,10 +858,12 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, nullptr, nullptr,
-                               rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u));
+                               rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u,
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, s, kst ? kst + nst : nullptr, rlist2,
-                               rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u));
+                               rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u,
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);
@@ -1087,6 +1114,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     HIP_TRY(hipSetDevice(d.ordinal));
     HIP_TRY(hipStreamSynchronize(d.stream));
     free_graph(d.g);
+    d.ktag_rows = 0;  // tagged KSP2 rows of another graph (another level width): zero before reuse
     DevGraph g;
     g.V = V;
     g.E = E;

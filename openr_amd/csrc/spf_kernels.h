@@ -124,6 +124,11 @@ struct SolveArgs {
   // [n][V] here instead of u64 distance rows (0xFFFF = unreached; dist = level * cost;
   // levels stay below V <= 65535). KSP2 second SPFs: 4x fewer bytes per pair row.
   uint16_t* lvl16;
+  // lvl16 rows in tagged form when lvl_tag != 0 (KSP2 second SPFs, round 3): a node's entry
+  // is (lvl_tag << lvl_shift) | level, written only when the node is settled; the unreached
+  // fill is skipped, so a row costs the bytes of the nodes the (target-bounded) solve
+  // reached, and an entry with another tag reads as unreached. Levels < V < 2^lvl_shift.
+  uint32_t lvl_tag, lvl_shift;
   // nullable: solve sid writes its dist / nh / tight rows at row out_row[sid] instead of
   // sid (openr_spf_refresh re-solves a scattered subset of resident rows in place; the
   // launcher then leaves zeroing those tight rows to the caller)
@@ -285,8 +290,9 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* retry_list = nullptr, uint32_t* retry_count = nullptr,
                             uint32_t* work_ctr = nullptr,  // zeroed dynamic-scheduling counter (required)
                             const uint16_t* rows16 = nullptr,  // kind 2: u16 level rows (SolveArgs::lvl16)
-                            uint64_t lcost = 0);  // instead of `rows`: dist = level * lcost; non-zero lcost
+                            uint64_t lcost = 0,   // instead of `rows`: dist = level * lcost; non-zero lcost
                                                   // also marks a uniform-cost graph (rank by name / edge)
+                            uint32_t ltag = 0);   // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);

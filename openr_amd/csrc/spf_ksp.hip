@@ -110,6 +110,7 @@ struct KspState {
   bool use16;
   const uint16_t* l16;  // non-null: the pair's row is u16 levels (0xFFFF unreached), dist = level * lcost
   uint64_t lcost;       // non-zero: every usable edge costs lcost (uniform-cost graph)
+  uint32_t ltag, lshift;  // ltag != 0: l16 entries are ltag << lshift | level, other tags unreached
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -122,6 +123,7 @@ __device__ __forceinline__ uint64_t dist_of(const KspState& st, uint32_t u) {
   }
   if (st.l16) {
     const uint32_t l = st.l16[u];
+    if (st.ltag) return (l >> st.lshift) != st.ltag ? kNoKey : (uint64_t)(l & ((1u << st.lshift) - 1u)) * st.lcost;
     return l == 0xFFFFu ? kNoKey : (uint64_t)l * st.lcost;
   }
   return st.drow[u];
@@ -500,7 +502,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t frames, uint32_t arena, const uint32_t* list,
                                                           const uint32_t* list_count, uint32_t* retry_list,
                                                           uint32_t* retry_count, uint32_t* work_ctr,
-                                                          const uint16_t* rows16, uint64_t lcost) {
+                                                          const uint16_t* rows16, uint64_t lcost,
+                                                          uint32_t ltag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, use_d16 != 0);
@@ -547,6 +550,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     st.drow = rows + (size_t)(KIND == 1 ? row : k) * V;
     st.l16 = (KIND == 2 && rows16) ? rows16 + (size_t)k * V : nullptr;
     st.lcost = lcost;
+    st.ltag = ltag >> 8;
+    st.lshift = ltag & 0xFFu;
     st.use16 = false;
     const uint64_t ddst = dst < V ? dist_of(st, dst) : kNoKey;
     if (d16 && !st.l16 && ddst < 0xFFFFull) {
@@ -684,7 +689,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* ign_end, uint32_t ign_cap, uint32_t* tok, uint32_t tok_cap, uint32_t* status,
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
                             const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
-                            uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost) {
+                            uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost,
+                            uint32_t ltag) {
   if (!n) return hipSuccess;
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
@@ -701,7 +707,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                      ign_cap, tok, tok_cap, status, qbuf,
                      bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16() ? 1u : 0u,
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
-                     lcost);
+                     lcost, ltag);
   return hipGetLastError();
 }
 

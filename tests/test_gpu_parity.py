@@ -716,6 +716,22 @@ def test_ksp2_device_capacity_tiers(eng, tier, monkeypatch):
     check_ksp2_against_oracle(eng, g, [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 30)])
 
 
+@pytest.mark.parametrize("tag", ["1", "0"], ids=["tagged", "filled"])
+def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
+    """KSP2 second-SPF level rows (code family, uniform cost): tagged — a solve writes only
+    the nodes it settles (it stops at the pair's target) as tag << shift | level, and an
+    entry with another chunk's tag reads as unreached — or filled (unreached = 0xFFFF).
+    Chunks of 7 pairs: on the 300-node graph (9 level bits, tags 1..127) the tags wrap and
+    the rows are zeroed again mid-call; results equal the oracle either way."""
+    monkeypatch.setenv("OPENR_SPF_KSP_TAG", tag)
+    monkeypatch.setenv("OPENR_SPF_KSP_CHUNK", "7")
+    g = random_graph(9, 300, 620, 1, p_ovl=0.05, p_down=0.05, p_par=0.1)
+    rng = np.random.default_rng(11)
+    check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (1400, 2))])
+    g = T.fabric(288 + 56)
+    check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
+
+
 @pytest.mark.parametrize("ring", [None, "256"])
 def test_ell16_kernel_opt_in(eng, monkeypatch, ring):
     """The opt-in single-u16-state ELL kernel (OPENR_SPF_ELL16=1, spf_bfs_lvl.hip) on grids,
