@@ -648,6 +648,54 @@ def adjdb_main(args):
     eng.close()
 
 
+def routes_main(args):
+    """SURVEY.md §8f rank 1 / VERDICT r2 f1: SpfSolver::buildRouteDbs for EVERY node of the
+    topology (G100: the getRouteMap-scale grid workload of DecisionTest.cpp:4289-4355 at
+    n = 100), through the route-build C-ABI (include/openr_routes.h): one all-sources SPF
+    batch on the GPU engine, its rows kept dense in the LinkState memo, then the per-node
+    route builds on host worker threads reading them through LinkState::SpfView (no
+    SpfResult map materialised). Each node's DB is tallied and freed as it is built
+    (streaming form), so host memory stays at the dense rows. value = unicast routes/s;
+    peak_rss_mb = this process's peak resident set (getrusage)."""
+    import resource
+
+    import torch
+
+    from openr_amd import adjdb
+
+    torch.cuda.set_device(0)
+    g, cfg = build_topology(args.topology)
+    batch = adjdb.AdjDbBatch.from_columns(adjdb.columns_for_graph(g))
+    rb = adjdb.RouteBuilder(batch, "0")
+    ids = np.arange(rb.num_nodes)
+    flags = adjdb.ROUTES_LFA if args.lfa else 0
+    rb.build(ids[:8], flags)  # warm-up (engine context, prefixes)
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
+    times, st = [], None
+    for _ in range(max(1, args.steps)):
+        t0 = time.perf_counter()
+        st = rb.build(ids, flags)
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
+    out = {
+        "metric": "route DBs of every node (SpfSolver::buildRouteDbs, GPU SPF + host route build), unicast routes/s",
+        "value": st.unicast_routes / dt, "unit": "routes/s", "n_gpus": 1, "steps": len(times), "warmup": 1,
+        "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u64", "data": "synthetic (benchmark generators, one prefix per node)",
+        "config": dict(cfg, workload=cfg["workload"].replace("all-sources", "route-dbs-all-nodes"), lfa=bool(args.lfa),
+                       host_threads=int(os.environ.get("OPENR_HOST_THREADS", "0")) or None),
+        "unicast_routes": int(st.unicast_routes), "mpls_routes": int(st.mpls_routes), "nexthops": int(st.nexthops),
+        "checksum": f"{st.checksum:016x}", "ms_spf_and_route_build": st.ms_build,
+        "peak_rss_mb": rss, "rss_before_build_mb": rss0,
+        "roofline": None,
+        "note": "host route build over dense SPF rows (LinkState::SpfView); the device solve is the config-2/3 kernel",
+    }
+    print(json.dumps(out), flush=True)
+    rb.close()
+    batch.close()
+
+
 def relaunch_distributed(n: int) -> int:
     """`bench.py --gpus N` started without torch.distributed.run: launch N ranks (one
     process per GPU) under torch.distributed.run as a CHILD process and return its exit
@@ -690,7 +738,9 @@ def main():
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
                     help="ksp2: sources per device call within a step (token rows are reused)")
-    ap.add_argument("--workload", default="all-sources", choices=["all-sources", "whatif", "ksp2", "update", "adjdb"],
+    ap.add_argument("--lfa", action="store_true", help="routes: SpfSolver computeLfaPaths")
+    ap.add_argument("--workload", default="all-sources",
+                    choices=["all-sources", "whatif", "ksp2", "update", "adjdb", "routes"],
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
                          "(BASELINE config 4)")
     args = ap.parse_args()
@@ -707,6 +757,8 @@ def main():
         return update_main(args)
     if args.workload == "adjdb":
         return adjdb_main(args)
+    if args.workload == "routes":
+        return routes_main(args)
     return all_sources_main(args)
 
 

@@ -264,6 +264,74 @@ __global__ void ms_perm_fill_kernel(const uint32_t* corder, const uint32_t* rowm
     perm[i] = perm_all ? rowmap[corder[i]] : i;
 }
 
+// ---------------------------------------------------------------------------
+// Extended batch of a partial all-sources call (tile-active multi-source pass, round 3:
+// strong-scaling shards, LFA prefetches). The next-hop derivation needs the level rows of
+// every usable, non-overloaded neighbour of a source; a batch that lacks some gets them as
+// halo rows (levels only), appended after the call's rows: xsrc = [sources | halo]. The
+// batch sequence follows the cluster order restricted to the extended batch (xslot[crank of
+// a source] = its row; duplicates and invalid sources go last), so 32-source batches stay
+// compact. Results do not depend on the order.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kExtPending = 0xFFFFFFFEu;
+__global__ void ms_ext_clear_kernel(uint32_t* rowmap, uint32_t* slot, uint32_t V, uint32_t* xcount) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < V; i += gridDim.x * blockDim.x) {
+    rowmap[i] = ~0u;
+    slot[i] = ~0u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) xcount[threadIdx.x] = 0;  // [0] halo rows, [1] tail rows
+}
+__global__ void ms_ext_fill_kernel(const uint32_t* sources, uint32_t n, uint32_t V, const uint32_t* crank,
+                                   uint32_t* rowmap, uint32_t* slot, uint32_t* xsrc, uint32_t* xdup, uint32_t* xcount) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const uint32_t s = sources[k];
+    xsrc[k] = s;
+    if (s < V) rowmap[s] = k;  // a duplicate's row holds the same results: any one serves
+    if (s >= V || atomicCAS(&slot[crank[s]], ~0u, k) != ~0u) xdup[atomicAdd(&xcount[1], 1u)] = k;
+  }
+}
+__global__ void ms_ext_halo_kernel(DevGraph g, const uint32_t* sources, uint32_t n, uint32_t* rowmap,
+                                   uint32_t* slot, uint32_t* xsrc, uint32_t* xcount) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const uint32_t s = sources[k];
+    if (s >= g.V) continue;
+    const uint2 r = g.row2[s];
+    for (uint32_t e = r.x; e < r.y; ++e) {
+      const uint32_t av = g.adj[e];
+      if (av & kEdgeDown) continue;
+      const uint32_t x = av;
+      if (x == s || g.ovl[x]) continue;  // an overloaded neighbour is a next hop by id, no row
+      if (atomicCAS(&rowmap[x], ~0u, kExtPending) != ~0u) continue;  // has a row, or another thread adds it
+      const uint32_t row = n + atomicAdd(&xcount[0], 1u);
+      xsrc[row] = x;
+      rowmap[x] = row;
+      slot[g.crank[x]] = row;  // x is no call source: its slot is free
+    }
+  }
+}
+// one workgroup: msperm = the occupied slots in cluster order, then the tail rows
+__global__ __launch_bounds__(1024) void ms_ext_order_kernel(const uint32_t* slot, uint32_t V, const uint32_t* xdup,
+                                                            const uint32_t* xcount, uint32_t* perm) {
+  __shared__ uint32_t cnt[1024];
+  const uint32_t tid = threadIdx.x, per = (V + 1023u) / 1024u;
+  const uint32_t lo = min(V, tid * per), hi = min(V, lo + per);
+  uint32_t c = 0;
+  for (uint32_t i = lo; i < hi; ++i) c += slot[i] != ~0u ? 1u : 0u;
+  cnt[tid] = c;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024u; d <<= 1) {  // inclusive scan
+    const uint32_t x = tid >= d ? cnt[tid - d] : 0u;
+    __syncthreads();
+    cnt[tid] += x;
+    __syncthreads();
+  }
+  uint32_t o = cnt[tid] - c;
+  for (uint32_t i = lo; i < hi; ++i)
+    if (slot[i] != ~0u) perm[o++] = slot[i];
+  const uint32_t placed = cnt[1023], tail = xcount[1];
+  for (uint32_t j = tid; j < tail; j += 1024u) perm[placed + j] = xdup[j];
+}
+
 // Four u8 levels per dword: bytes b of `ln` with ln_b + 1 == ls_b (mod 256) -> bit 7 of byte b
 __device__ __forceinline__ uint32_t swar_succ_eq(uint32_t ln, uint32_t ls) {
   const uint32_t inc = ((ln & 0x7F7F7F7Fu) + 0x01010101u) ^ (ln & 0x80808080u);  // per-byte +1, no carries
@@ -706,38 +774,56 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_kernel(DevGraph g, SolveA
 // the tile). A wave's active slots of a step are a bit mask in SGPRs; the pull row of the
 // next active slot is read while the current slot's frontier reads are in flight.
 // ---------------------------------------------------------------------------
-template <uint32_t NPT>
+// LDS layout (bytes) for vpad = ntiles * 64 internal ids: F[0] and F[1] frontier words
+// (vpad + 4 each; word vpad is a zero word padding slots read), act[3][8] activity words,
+// the next batch, the tiles' neighbour lists (u8 tile ids, kTileList per tile), pull rows.
 struct MsTLayout {
-  static constexpr uint32_t kMaxV = kMsThreads * NPT;                // internal ids a workgroup owns
-  static constexpr uint32_t kF1 = (4u * (kMaxV + 4u) + 15u) & ~15u;  // byte offset of F[1]; F[x][kMaxV] = 0
-  static constexpr uint32_t kAct = 2u * kF1;                         // act[3][8] u32
-  static constexpr uint32_t kNext = kAct + 96u;                      // next batch
-  static constexpr uint32_t kEll = kAct + 128u;                      // pull rows, 8 B per internal id
-  __host__ __device__ static constexpr uint32_t bytes(uint32_t V) {
-    return kEll + 8u * ((V + kTileNodes - 1u) / kTileNodes) * kTileNodes;
+  uint32_t f1, act, next, tl, ell, total;
+  __host__ __device__ explicit MsTLayout(uint32_t ntiles) {
+    const uint32_t vpad = ntiles * kTileNodes;
+    f1 = (4u * (vpad + 4u) + 15u) & ~15u;
+    act = 2u * f1;
+    next = act + 96u;
+    tl = act + 128u;
+    ell = tl + ((ntiles * kTileList + 15u) & ~15u);
+    total = ell + 8u * vpad;
   }
 };
 
+// The tile kernel's arguments, compact (fewer kernel-argument SGPRs than DevGraph + SolveArgs)
+struct MsTileArgs {
+  const uint32_t *tord, *tinv, *adj, *tmask, *sources, *msperm, *xcount;
+  const uint2* row2;
+  const uint8_t *ovl, *tlist;
+  uint8_t *lvl8, *rowok;
+  uint64_t* dist;
+  uint32_t* ovf_list;
+  uint32_t V, ntiles, n;
+};
+
 template <uint32_t NPT>
-__global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, SolveArgs a, uint64_t cost,
+__global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(MsTileArgs t, uint64_t cost,
                                                                    uint32_t* ctr, uint32_t* ovf_count, uint32_t flags) {
-  using Lay = MsTLayout<NPT>;
   typedef __attribute__((address_space(3))) uint64_t lds_u64;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
-  const uint32_t V = g.V, tid = threadIdx.x;
+  const uint32_t V = t.V, tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  lds_u32* const act = (lds_u32*)(size_t)Lay::kAct;
-  lds_u32* const next_unit = (lds_u32*)(size_t)Lay::kNext;
+  const MsTLayout lay(t.ntiles);
+  lds_u32* const act = (lds_u32*)(size_t)lay.act;
+  lds_u32* const next_unit = (lds_u32*)(size_t)lay.next;
   const bool nt = (flags & 1u) != 0, dist_here = (flags & 2u) == 0;
-  const uint32_t rb = reach_row_bytes(V), vpad = g.ntiles * kTileNodes;
-  const uint32_t ebase = Lay::kEll + 8u * tid;  // this thread's first pull row
-  constexpr uint32_t kZero = 4u * Lay::kMaxV;   // byte offset of the zero word
-  // control words zero; pull rows in internal ids (a down edge or a missing slot reads the
-  // zero word); rows of padding ids (V <= p < vpad) read zero words only
+  const uint32_t rb = reach_row_bytes(V), vpad = t.ntiles * kTileNodes;
+  const uint32_t ebase = lay.ell + 8u * tid;  // this thread's first pull row
+  const uint32_t kZero = 4u * vpad;           // byte offset of the zero word
+  const uint32_t F1 = lay.f1;
+  // control words zero, neighbour lists staged; pull rows in internal ids (a down edge or a
+  // missing slot reads the zero word); rows of padding ids (V <= p < vpad) read zero words
   for (uint32_t w = tid; w < 32u; w += kMsThreads) act[w] = 0u;
+  for (uint32_t w = tid; w < (t.ntiles * kTileList + 3u) / 4u; w += kMsThreads)
+    *(lds_u32*)(size_t)(lay.tl + 4u * w) = reinterpret_cast<const uint32_t*>(t.tlist)[w];
   if (tid == 0) {
     ms_wr(kZero, 0u);
-    ms_wr(Lay::kF1 + kZero, 0u);
+    ms_wr(F1 + kZero, 0u);
   }
   uint32_t sink = 0;
 #pragma unroll
@@ -746,54 +832,60 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
     if (p < vpad) {
       uint32_t o[4] = {kZero, kZero, kZero, kZero};
       if (p < V) {
-        const uint32_t v = g.tord[p];
-        const uint2 r = g.row2[v];
+        const uint32_t v = t.tord[p];
+        const uint2 r = t.row2[v];
 #pragma unroll
         for (uint32_t c = 0; c < 4u; ++c) {
           if (r.x + c < r.y) {
-            const uint32_t av = g.adj[r.x + c];
-            if (!(av & kEdgeDown)) o[c] = 4u * g.tinv[av];
+            const uint32_t av = t.adj[r.x + c];
+            if (!(av & kEdgeDown)) o[c] = 4u * t.tinv[av];
           }
         }
-        if (g.ovl[v]) sink |= 1u << i;
+        if (t.ovl[v]) sink |= 1u << i;
       }
       *(lds_u64*)(size_t)(ebase + 8u * kMsThreads * i) =
           (uint64_t)(o[0] | (o[1] << 16)) | ((uint64_t)(o[2] | (o[3] << 16)) << 32);
     }
   }
-  const uint32_t nbatch = (a.n + kMsBatch - 1u) / kMsBatch;
+  // rows: the call's, then (extended batch) the halo rows
+  const uint32_t ntot = t.xcount ? t.n + t.xcount[0] : t.n;
+  const uint32_t nbatch = (ntot + kMsBatch - 1u) / kMsBatch;
   for (uint32_t unit = blockIdx.x; unit < nbatch;) {
-    const uint32_t k0 = unit * kMsBatch, nbk = min(kMsBatch, a.n - k0);
+    const uint32_t k0 = unit * kMsBatch, nbk = min(kMsBatch, ntot - k0);
     uint32_t tb = tid;
     asm volatile("" : "+v"(tb));
     // both frontier buffers zero over the owned ids, activity bitmasks zero
 #pragma unroll
     for (uint32_t i = 0; i < NPT; ++i) {
-      ms_wr(4u * (tb + kMsThreads * i), 0u);
-      ms_wr(Lay::kF1 + 4u * (tb + kMsThreads * i), 0u);
+      if (tb + kMsThreads * i < vpad) {
+        ms_wr(4u * (tb + kMsThreads * i), 0u);
+        ms_wr(F1 + 4u * (tb + kMsThreads * i), 0u);
+      }
     }
     if (tid < 24u) act[tid] = 0u;
     __syncthreads();
     // level 0: the sources' own bits in F[0]; their tiles' neighbourhoods are active at step 0
     if (tid < nbk) {
-      const uint32_t src = a.sources[a.msperm[k0 + tid]];
+      const uint32_t src = t.sources[t.msperm[k0 + tid]];
       if (src < V) {
-        const uint32_t ps = g.tinv[src];
+        const uint32_t ps = t.tinv[src];
         lds_or((lds_u32*)(size_t)(4u * ps), 1u << tid);
-        const uint32_t* m = g.tmask + (size_t)(ps / kTileNodes) * kTileMaskWords;
+        const uint32_t* m = t.tmask + (size_t)(ps / kTileNodes) * kTileMaskWords;
 #pragma unroll
         for (uint32_t k = 0; k < kTileMaskWords; ++k)
           if (m[k]) lds_or(&act[k], m[k]);
       }
     }
     __syncthreads();
-    uint32_t vis[NPT], p[8][NPT];
+    // levels as bit-planes; the visited word of a node is the OR of its planes (every level
+    // >= 1 has a bit set, level 0 is all ones); a node >= V is visited for every source
+    uint32_t p[8][NPT];
 #pragma unroll
     for (uint32_t i = 0; i < NPT; ++i) {
       const uint32_t q = tb + kMsThreads * i;
-      vis[i] = q < V ? ms_rd(4u * q) : ~0u;
+      const uint32_t v0 = q < V ? ms_rd(4u * q) : ~0u;
 #pragma unroll
-      for (uint32_t b = 0; b < 8u; ++b) p[b][i] = vis[i];
+      for (uint32_t b = 0; b < 8u; ++b) p[b][i] = v0;
     }
     uint32_t L = 0;
     bool ovf = false;
@@ -819,7 +911,7 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
       uint32_t hm[8];
 #pragma unroll
       for (uint32_t b = 0; b < 8u; ++b) hm[b] = (((L + 1u) >> b) & 1u) ? ~0u : 0u;
-      const uint32_t cur = (L & 1u) ? Lay::kF1 : 0u, nxt = (L & 1u) ? 0u : Lay::kF1;
+      const uint32_t cur = (L & 1u) ? F1 : 0u, nxt = (L & 1u) ? 0u : F1;
       uint32_t eaddr = ebase + 8u * kMsThreads * (A ? (uint32_t)__builtin_ctz(A) : 0u);
       asm volatile("" : "+v"(eaddr));
       uint64_t er = A ? *(const lds_u64*)(size_t)eaddr : 0ull;
@@ -829,24 +921,28 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
           const uint32_t lo = (uint32_t)er, hi = (uint32_t)(er >> 32);
           const uint32_t f = ms_rd(cur + (lo & 0xFFFFu)) | ms_rd(cur + (lo >> 16)) | ms_rd(cur + (hi & 0xFFFFu)) |
                              ms_rd(cur + (hi >> 16));
+          // the tile's neighbour list (lane j < kTileList: its j-th tile, itself included),
+          // read behind the frontier words: used if the tile emits
+          const uint32_t lane = __lane_id();
+          uint32_t lt = lay.tl + kTileList * (8u * i + wave);
+          asm volatile("" : "+s"(lt));  // per slot, not hoisted out of the level loop
+          const uint32_t nbt = lane < kTileList ? *(const lds_u8*)(size_t)(lt + lane) : 0xFFu;
           const uint32_t rest = A & ~((2u << i) - 1u);
           if (rest) {  // the next active slot's pull row, in flight with this slot's reads
             uint32_t na = ebase + 8u * kMsThreads * (uint32_t)__builtin_ctz(rest);
             asm volatile("" : "+v"(na));
             er = *(const lds_u64*)(size_t)na;
           }
-          const uint32_t nw = f & ~vis[i];
-          vis[i] |= nw;
+          const uint32_t vis = p[0][i] | p[1][i] | p[2][i] | p[3][i] | p[4][i] | p[5][i] | p[6][i] | p[7][i];
+          const uint32_t nw = f & ~vis;
           const uint32_t fw = ((sink >> i) & 1u) ? 0u : nw;
           ms_wr(nxt + 4u * (tb + kMsThreads * i), fw);
 #pragma unroll
           for (uint32_t b = 0; b < 8u; ++b) p[b][i] |= nw & hm[b];
           if (__builtin_amdgcn_ballot_w64(fw != 0u) != 0ull) {  // this tile emits: its neighbourhood is active next step
-            const uint32_t lane = __lane_id();
-            if (lane < kTileMaskWords) {
-              const uint32_t m = g.tmask[(size_t)(8u * i + wave) * kTileMaskWords + lane];
-              if (m) lds_or(&nact[lane], m);
-            }
+            if (nbt < 0xFEu) lds_or(&nact[nbt >> 5], 1u << (nbt & 31u));
+            // a tile with more than kTileList neighbour tiles (list head 0xFE) marks every tile
+            if (__builtin_amdgcn_readfirstlane(nbt) == 0xFEu && lane < kTileMaskWords) lds_or(&nact[lane], ~0u);
           }
         }
       });
@@ -855,9 +951,10 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
     }
     if (ovf) {
       if (tid < nbk) {
-        const uint32_t k = a.msperm[k0 + tid];
-        a.rowok[k] = 0u;
-        a.ovf_list[atomicAdd(ovf_count, 1u)] = k;
+        const uint32_t k = t.msperm[k0 + tid];
+        t.rowok[k] = 0u;
+        // a halo row is no call row: the sources that need it are listed by the next-hop pass
+        if (k < t.n) t.ovf_list[atomicAdd(ovf_count, 1u)] = k;
       }
     } else {
       // rows out: planes -> level bytes (as msbfs_kernel), stored at the node's own id
@@ -892,14 +989,14 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
 #pragma unroll
       for (uint32_t i = 0; i < NPT; ++i) {
         const uint32_t q = tb + kMsThreads * i;
-        orig[i] = q < V ? g.tord[q] : ~0u;
+        orig[i] = q < V ? t.tord[q] : ~0u;
       }
 #pragma unroll
       for (uint32_t j = 0; j < kMsBatch; ++j) {
         if (j >= nbk) continue;  // uniform
-        const size_t k = a.msperm[k0 + j];
-        uint8_t* lrow = a.lvl8 + k * rb;
-        uint64_t* drow = a.dist + k * V;
+        const size_t k = t.msperm[k0 + j];
+        uint8_t* lrow = t.lvl8 + k * rb;
+        uint64_t* drow = t.dist + k * V;
 #pragma unroll
         for (uint32_t i = 0; i < NPT; ++i) {
           const uint32_t v = orig[i];
@@ -910,8 +1007,8 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
         }
       }
       if (tid < nbk) {
-        const uint32_t k = a.msperm[k0 + tid];
-        a.rowok[k] = a.sources[k] < V ? 1u : 0u;
+        const uint32_t k = t.msperm[k0 + tid];
+        t.rowok[k] = t.sources[k] < V ? 1u : 0u;
       }
     }
     __syncthreads();  // every lane is done with this batch's LDS and next_unit
@@ -925,16 +1022,34 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(DevGraph g, S
 template <uint32_t NPT>
 hipError_t launch_msbfs_tile_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t* blk, int num_cus,
                                  hipStream_t s, uint32_t flags) {
-  using Lay = MsTLayout<NPT>;
   auto k = msbfs_tile_kernel<NPT>;
-  const uint32_t lds = Lay::bytes(g.V);
+  const uint32_t lds = MsTLayout(g.ntiles).total;
+  MsTileArgs t;
+  t.tord = g.tord;
+  t.tinv = g.tinv;
+  t.adj = g.adj;
+  t.tmask = g.tmask;
+  t.sources = a.sources;
+  t.msperm = a.msperm;
+  t.xcount = a.xcount;
+  t.row2 = g.row2;
+  t.ovl = g.ovl;
+  t.tlist = g.tlist;
+  t.lvl8 = a.lvl8;
+  t.rowok = a.rowok;
+  t.dist = a.dist;
+  t.ovf_list = a.ovf_list;
+  t.V = g.V;
+  t.ntiles = g.ntiles;
+  t.n = a.n;
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
-  const uint32_t nbatch = (a.n + kMsBatch - 1u) / kMsBatch;
+  // an extended batch holds at most the halo bound more rows (ms_ext_rows)
+  const uint32_t nbatch = ((a.xcount ? ms_ext_rows(g, a.n) : a.n) + kMsBatch - 1u) / kMsBatch;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(nbatch, (uint32_t)num_cus));
   note_launch("msbfs_tile_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kMsThreads), lds, s, g, a, cost, blk, blk + 4, flags);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMsThreads), lds, s, t, cost, blk, blk + 4, flags);
   return hipGetLastError();
 }
 
@@ -960,10 +1075,16 @@ hipError_t launch_msbfs_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost
 // Knobs: OPENR_SPF_BFS_MSBFS (0 off, 1 whenever it applies, 2 = auto) and
 // OPENR_SPF_BFS_REACH (0 off, 1 whenever it applies, 2 = auto); auto = batches of >= V
 // sources, where every neighbour of a source is likely in the batch.
+// rows of an extended batch of n sources: the call's plus at most one halo row per
+// usable neighbour slot, and never more halo rows than nodes outside the call
+uint32_t ms_ext_rows(const DevGraph& g, uint32_t n) {
+  return n + std::min<uint32_t>(g.V, (uint32_t)std::min<uint64_t>((uint64_t)n * g.max_deg, 0xFFFFFFFFu));
+}
+
 // the tile-active multi-source BFS serves the graph (tile order built, layout fits)
 bool ms_tile_ok(const DevGraph& g) {
-  return g.tord && g.tinv && g.tmask && g.ntiles <= 32u * kTileMaskWords &&
-         g.ntiles * kTileNodes <= MsTLayout<20>::kMaxV && MsTLayout<20>::bytes(g.V) <= kMaxLds &&
+  return g.tord && g.tinv && g.tmask && g.tlist && g.ntiles <= 32u * kTileMaskWords &&
+         g.ntiles * kTileNodes <= 20u * kMsThreads && MsTLayout(g.ntiles).total <= kMaxLds &&
          env_u32("OPENR_SPF_MSBFS_TILE", 1u, 0u, 1u) != 0u;
 }
 
@@ -985,28 +1106,52 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
   const bool dist2 = env_u32("OPENR_SPF_REACH_DIST", 1u, 1u, 2u) == 2u;
   const uint32_t flags = nt_stores() | (dist2 ? 2u : 0u);
   const uint32_t mgrid = std::max<uint32_t>(1u, std::min<uint32_t>((g.V + 255u) / 256u, 4u * (uint32_t)num_cus));
-  note_launch("reach_map");
-  hipLaunchKernelGGL(reach_map_clear_kernel, dim3(mgrid), dim3(256), 0, s, a.rowmap, g.V);
-  hipLaunchKernelGGL(reach_map_fill_kernel,
-                     dim3(std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, 4u * (uint32_t)num_cus))),
-                     dim3(256), 0, s, a.rowmap, a.sources, a.n, g.V);
+  const uint32_t ngrid = std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, 4u * (uint32_t)num_cus));
+  // a partial batch on the tile-active pass: extended with halo rows (ms_ext_*)
+  const bool ext = pass == 2 && ms_tile_ok(g) && a.n < g.V && a.xsrc && a.xcount && a.xslot && a.xdup && g.crank &&
+                   env_u32("OPENR_SPF_MSBFS_HALO", 1u, 0u, 1u);
   hipError_t err;
-  if (pass == 2) {
+  if (ext) {
+    note_launch("ms_ext");
+    hipLaunchKernelGGL(ms_ext_clear_kernel, dim3(mgrid), dim3(256), 0, s, a.rowmap, a.xslot, g.V, a.xcount);
+    hipLaunchKernelGGL(ms_ext_fill_kernel, dim3(ngrid), dim3(256), 0, s, a.sources, a.n, g.V, g.crank, a.rowmap,
+                       a.xslot, a.xsrc, a.xdup, a.xcount);
+    hipLaunchKernelGGL(ms_ext_halo_kernel, dim3(ngrid), dim3(256), 0, s, g, a.sources, a.n, a.rowmap, a.xslot, a.xsrc,
+                       a.xcount);
+    hipLaunchKernelGGL(ms_ext_order_kernel, dim3(1), dim3(1024), 0, s, a.xslot, g.V, a.xdup, a.xcount, a.msperm);
+  } else {
+    note_launch("reach_map");
+    hipLaunchKernelGGL(reach_map_clear_kernel, dim3(mgrid), dim3(256), 0, s, a.rowmap, g.V);
+    hipLaunchKernelGGL(reach_map_fill_kernel, dim3(ngrid), dim3(256), 0, s, a.rowmap, a.sources, a.n, g.V);
+  }
+  if (ext) {
+    SolveArgs b = a;  // the multi-source pass solves [sources | halo]; the next-hop pass the call's rows
+    b.sources = a.xsrc;
+    if (info) info->kernel = "msbfs_tile_kernel";
+    const uint32_t need = (g.ntiles * kTileNodes + kMsThreads - 1u) / kMsThreads;
+    if (need <= 4u) err = launch_msbfs_tile_npt<4>(g, b, cost, blk, num_cus, s, flags);
+    else if (need <= 8u) err = launch_msbfs_tile_npt<8>(g, b, cost, blk, num_cus, s, flags);
+    else if (need <= 12u) err = launch_msbfs_tile_npt<12>(g, b, cost, blk, num_cus, s, flags);
+    else if (need <= 16u) err = launch_msbfs_tile_npt<16>(g, b, cost, blk, num_cus, s, flags);
+    else err = launch_msbfs_tile_npt<20>(g, b, cost, blk, num_cus, s, flags);
+  } else if (pass == 2) {
     if (!a.msperm || !a.mscnt) return hipErrorInvalidValue;
-    const uint32_t pgrid = std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, 4u * (uint32_t)num_cus));
+    const uint32_t pgrid = ngrid;
     err = hipMemsetAsync(a.mscnt, 0, sizeof(uint32_t), s);
     if (err != hipSuccess) return err;
     hipLaunchKernelGGL(ms_perm_count_kernel, dim3(pgrid), dim3(256), 0, s, a.sources, a.n, a.rowmap, g.V, a.mscnt);
     hipLaunchKernelGGL(ms_perm_fill_kernel, dim3(pgrid), dim3(256), 0, s, g.corder, a.rowmap, a.n, g.V, a.mscnt,
                        a.msperm);
+    SolveArgs b = a;
+    b.xcount = nullptr;  // every neighbour row is in the call
     if (ms_tile_ok(g)) {  // tile-active variant (OPENR_SPF_MSBFS_TILE=0: the dense pull)
       const uint32_t need = (g.ntiles * kTileNodes + kMsThreads - 1u) / kMsThreads;  // internal ids per thread
       if (info) info->kernel = "msbfs_tile_kernel";
-      if (need <= 4u) err = launch_msbfs_tile_npt<4>(g, a, cost, blk, num_cus, s, flags);
-      else if (need <= 8u) err = launch_msbfs_tile_npt<8>(g, a, cost, blk, num_cus, s, flags);
-      else if (need <= 12u) err = launch_msbfs_tile_npt<12>(g, a, cost, blk, num_cus, s, flags);
-      else if (need <= 16u) err = launch_msbfs_tile_npt<16>(g, a, cost, blk, num_cus, s, flags);
-      else err = launch_msbfs_tile_npt<20>(g, a, cost, blk, num_cus, s, flags);
+      if (need <= 4u) err = launch_msbfs_tile_npt<4>(g, b, cost, blk, num_cus, s, flags);
+      else if (need <= 8u) err = launch_msbfs_tile_npt<8>(g, b, cost, blk, num_cus, s, flags);
+      else if (need <= 12u) err = launch_msbfs_tile_npt<12>(g, b, cost, blk, num_cus, s, flags);
+      else if (need <= 16u) err = launch_msbfs_tile_npt<16>(g, b, cost, blk, num_cus, s, flags);
+      else err = launch_msbfs_tile_npt<20>(g, b, cost, blk, num_cus, s, flags);
     } else {
       const uint32_t need = (g.V + kMsThreads - 1u) / kMsThreads;  // nodes per thread
       if (info) info->kernel = "msbfs_kernel";

@@ -331,7 +331,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
             }
             if (lane_g == 0) {
               if (own_dist) {  // u settled on level L
-                if (GENERIC && lrow) lrow[u] = (uint16_t)L;
+                if (GENERIC && lrow) lrow[u] = (uint16_t)(ltag | L);
                 else drow[u] = dL;
               }
               if (sink) atomicOr(&st[S::word(u)], kCodeSettledSink << S::shift(u));

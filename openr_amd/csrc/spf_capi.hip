@@ -80,6 +80,7 @@ struct Device {
   // lvl-family reach pass (all-sources batches): u8 level rows, node -> row map, row flags
   DevBuf<uint8_t> lvl8, rowok;
   DevBuf<uint32_t> rowmap, msperm, mscnt;
+  DevBuf<uint32_t> xsrc, xcount, xslot, xdup;  // extended (halo) batches of the multi-source pass
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -97,7 +98,7 @@ struct Device {
   // host-form refresh rows
   DevBuf<PatchRec> precs;
   DevBuf<DeltaEdge> delta;
-  DevBuf<uint32_t> alist, asrc, acount;
+  DevBuf<uint32_t> alist, asrc, acount, alist2, asrc2;  // refresh: listed rows (first / exact stage)
   // exact-order kernel: per-solve slots when a slot does not fit LDS; pop-order rows
   DevBuf<uint8_t> exscratch;
   DevBuf<uint32_t> order;
@@ -114,7 +115,7 @@ hipError_t reserve_counters(Device& d) {
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
                    g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld,
-                   g.corder, g.tord, g.tinv, g.tmask};
+                   g.corder, g.tord, g.tinv, g.tmask, g.crank, g.tlist};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -381,6 +382,9 @@ void tile_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col, std::v
   }
 }
 
+// Bytes of exact-order slots (global memory) a device may hold at once.
+constexpr uint64_t kExactScratchBytes = uint64_t(2) << 30;
+
 int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   const bool use_metric = (flags & OPENR_SPF_USE_LINK_METRIC) != 0;
   p->use_metric = use_metric;
@@ -388,7 +392,12 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   // process instead of refusing the graph: zero or wrapped-negative usable metrics (pop
   // order history-dependent), next-hop sets wider than 256, graphs larger
   // than the LDS-resident layouts, and pop-order output requests.
-  auto exact = [p]() {
+  auto exact = [p, ctx]() -> int {
+    // one exact-order slot per solve, addressed with u32 offsets (spf_exact.hip ex_layout)
+    const uint64_t slot = exact_slot_bytes(ctx->V, ctx->E, ctx->L, ctx->nh_bits);
+    if (slot > 0xFFFFFFFFull || slot > kExactScratchBytes)
+      return fail(OPENR_SPF_E2BIG, "graph too large for the exact-order kernel (%llu bytes per solve)",
+                  (unsigned long long)slot);
     p->exact = true;
     return OPENR_SPF_OK;
   };
@@ -420,8 +429,6 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
   return OPENR_SPF_OK;
 }
 
-// Bytes of exact-order slots (global memory) a device may hold at once.
-constexpr uint64_t kExactScratchBytes = uint64_t(2) << 30;
 
 // Tuning overrides (benchmarks only): OPENR_SPF_GROUP_LANES=1|2|4|..|64 lanes per
 // frontier node in the BFS kernel.
@@ -485,19 +492,35 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   a.rowok = nullptr;
   a.msperm = nullptr;
   a.mscnt = nullptr;
+  a.xsrc = a.xcount = a.xslot = a.xdup = nullptr;
   if (fam == kFamLvl && !a.tight && !a.ign_ptr && !a.out_row && __builtin_popcount(mask) == 1 &&
-      (a.n >= d.g.V || std::getenv("OPENR_SPF_BFS_REACH") || std::getenv("OPENR_SPF_BFS_MSBFS"))) {
-    hipError_t err = d.lvl8.reserve((size_t)a.n * reach_row_bytes(d.g.V));
-    if (err == hipSuccess) err = d.rowok.reserve(a.n);
+      (a.n >= d.g.V || ms_tile_ok(d.g) || std::getenv("OPENR_SPF_BFS_REACH") || std::getenv("OPENR_SPF_BFS_MSBFS"))) {
+    // a partial batch on the tile-active pass is extended with halo rows (ms_ext_rows)
+    const bool ext = a.n < d.g.V && ms_tile_ok(d.g) && d.g.crank;
+    const uint32_t rows = ext ? ms_ext_rows(d.g, a.n) : a.n;
+    hipError_t err = d.lvl8.reserve((size_t)rows * reach_row_bytes(d.g.V));
+    if (err == hipSuccess) err = d.rowok.reserve(rows);
     if (err == hipSuccess) err = d.rowmap.reserve(d.g.V);
-    if (err == hipSuccess) err = d.msperm.reserve(a.n);
+    if (err == hipSuccess) err = d.msperm.reserve(rows);
     if (err == hipSuccess) err = d.mscnt.reserve(1);
+    if (ext) {
+      if (err == hipSuccess) err = d.xsrc.reserve(rows);
+      if (err == hipSuccess) err = d.xcount.reserve(2);
+      if (err == hipSuccess) err = d.xslot.reserve(d.g.V);
+      if (err == hipSuccess) err = d.xdup.reserve(std::max<uint32_t>(a.n, 1u));
+    }
     if (err != hipSuccess) return err;
     a.lvl8 = d.lvl8.p;
     a.rowok = d.rowok.p;
     a.rowmap = d.rowmap.p;
     a.msperm = d.msperm.p;
     a.mscnt = d.mscnt.p;
+    if (ext) {
+      a.xsrc = d.xsrc.p;
+      a.xcount = d.xcount.p;
+      a.xslot = d.xslot.p;
+      a.xdup = d.xdup.p;
+    }
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
@@ -971,6 +994,10 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.rowmap.release();
     d.msperm.release();
     d.mscnt.release();
+    d.xsrc.release();
+    d.xcount.release();
+    d.xslot.release();
+    d.xdup.release();
     d.work.release();
     d.perm.release();
     d.part.release();
@@ -986,6 +1013,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.delta.release();
     d.alist.release();
     d.asrc.release();
+    d.alist2.release();
+    d.asrc2.release();
     d.acount.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
@@ -1181,6 +1210,23 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
       if (err == hipSuccess) err = up(&g.tinv, tinv.data(), V);
       if (err == hipSuccess) err = up(&g.tmask, tmask.data(), tmask.size());
       g.ntiles = (uint32_t)(tmask.size() / kTileMaskWords);
+      std::vector<uint32_t> crank(V);
+      for (uint32_t i = 0; i < V; ++i) crank[corder[i]] = i;
+      if (err == hipSuccess) err = up(&g.crank, crank.data(), V);
+      // neighbour lists (u8 ids; at most 256 tiles by the caller's check)
+      std::vector<uint8_t> tlist((size_t)g.ntiles * kTileList + 4u, 0xFFu);
+      for (uint32_t t = 0; t < g.ntiles && g.ntiles <= 255u; ++t) {
+        uint32_t c = 0;
+        for (uint32_t t2 = 0; t2 < g.ntiles; ++t2) {
+          if (!((tmask[(size_t)t * kTileMaskWords + t2 / 32u] >> (t2 & 31u)) & 1u)) continue;
+          if (c == kTileList) {
+            tlist[(size_t)t * kTileList] = 0xFEu;
+            break;
+          }
+          tlist[(size_t)t * kTileList + c++] = (uint8_t)t2;
+        }
+      }
+      if (err == hipSuccess) err = up(&g.tlist, tlist.data(), tlist.size());
     }
     d.g = g;
     if (err != hipSuccess) {
@@ -1430,14 +1476,30 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
     HIP_TRY(d.delta.reserve(nd));
     HIP_TRY(d.alist.reserve(n));
     HIP_TRY(d.asrc.reserve(n));
-    HIP_TRY(d.acount.reserve(1));
+    HIP_TRY(d.acount.reserve(2));
     HIP_TRY(hipMemcpyAsync(d.delta.p, ctx->delta.data(), nd * sizeof(DeltaEdge), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(d.acount.p, 0, sizeof(uint32_t), s));
     HIP_TRY(launch_refresh_filter(d.delta.p, nd, d_sources, n, ctx->V, d_dist,
                                   (flags & OPENR_SPF_USE_LINK_METRIC) == 0, d.alist.p, d.asrc.p, d.acount.p,
                                   d.num_cus, s));
-    HIP_TRY(hipMemcpyAsync(&count, d.acount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));  // the affected-row count sizes the re-solve
+    // exact second stage (spf_update.hip) when next-hop rows are kept and no tight rows are:
+    // of the listed rows, only those the change really moves are re-solved
+    const char* ex = std::getenv("OPENR_SPF_REFRESH_EXACT");  // 0: first stage only (A/B)
+    if (d_nh && !d_tight && nh_bytes <= 32u && !(ex && std::atoi(ex) == 0)) {
+      HIP_TRY(d.alist2.reserve(n));
+      HIP_TRY(d.asrc2.reserve(n));
+      HIP_TRY(hipMemsetAsync(d.acount.p + 1, 0, sizeof(uint32_t), s));
+      HIP_TRY(launch_refresh_exact(d.g, d.delta.p, nd, ctx->V, d_dist, d_nh, nh_bytes,
+                                   (flags & OPENR_SPF_USE_LINK_METRIC) == 0, d.alist.p, d.asrc.p, d.acount.p, n,
+                                   d.alist2.p, d.asrc2.p, d.acount.p + 1, d.num_cus, s));
+      HIP_TRY(hipMemcpyAsync(&count, d.acount.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      std::swap(d.alist, d.alist2);  // the exact list is the one re-solved
+      std::swap(d.asrc, d.asrc2);
+    } else {
+      HIP_TRY(hipMemcpyAsync(&count, d.acount.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));  // the affected-row count sizes the re-solve
+    }
   }
   if (count) {
     if (d_tight) HIP_TRY(launch_zero_rows(d_tight, (ctx->E + 63u) / 64u, d.alist.p, count, d.num_cus, s));

@@ -35,6 +35,7 @@ namespace {
 
 struct ExLayout {
   uint32_t key, state, order, queue, nh, plep, recep, ign, total;
+  uint64_t total64;  // the slot's bytes; the u32 offsets above hold only when it is <= UINT32_MAX
 };
 
 // per-solve state, offsets from the slot base; nbw = next-hop words per node
@@ -55,6 +56,7 @@ __host__ __device__ inline ExLayout ex_layout(uint32_t V, uint32_t E, uint32_t L
   l.recep = take(4ull * E);  // epoch + 1 at which edge e was appended to pathLinks(col)
   l.ign = take(4ull * ((L + 31u) / 32u));
   l.total = (uint32_t)std::min<uint64_t>(off, 0xFFFFFFFFull);
+  l.total64 = off;
   return l;
 }
 
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(64) void spf_exact_kernel(DevGraph g, SolveArgs a, 
 
 uint64_t exact_slot_bytes(uint32_t V, uint32_t E, uint32_t L, uint32_t nh_bits) {
   const uint32_t nbw = std::max<uint32_t>(1u, (nh_bits + 31u) / 32u);
-  return ex_layout(V, E, L, nbw).total;
+  return ex_layout(V, E, L, nbw).total64;  // > UINT32_MAX: the layout does not fit (make_plan refuses)
 }
 
 hipError_t launch_exact(const DevGraph& g, const SolveArgs& a, const uint64_t* w64, bool use_metric, uint32_t nh_bits, uint8_t* scratch, uint64_t scratch_bytes, uint32_t* order_out,
@@ -234,6 +236,7 @@ hipError_t launch_exact(const DevGraph& g, const SolveArgs& a, const uint64_t* w
   if (!a.n) return hipSuccess;
   const uint32_t nbw = std::max<uint32_t>(1u, (nh_bits + 31u) / 32u);
   const uint64_t slot = exact_slot_bytes(g.V, g.E, g.L, nh_bits);
+  if (slot > 0xFFFFFFFFull) return hipErrorInvalidValue;  // u32 slot offsets (make_plan refuses such graphs)
   const bool in_lds = slot <= kMaxLds && !bfs::env_u32("OPENR_SPF_EXACT_GLOBAL", 0u, 0u, 1u);
   uint32_t grid;
   if (in_lds) {

@@ -54,9 +54,12 @@ struct DevGraph {
   uint32_t* tord = nullptr;
   uint32_t* tinv = nullptr;
   uint32_t* tmask = nullptr;
+  uint8_t* tlist = nullptr;    // [ntiles][kTileList] the tiles of tmask[t] (t included) as u8 ids, 0xFF
+                               //     padded; list head 0xFE: more than kTileList (every tile counts)
   uint32_t ntiles = 0;
+  uint32_t* crank = nullptr;   // [V] or null: position of each node in corder
 };
-constexpr uint32_t kTileNodes = 64, kTileMaskWords = 8;
+constexpr uint32_t kTileNodes = 64, kTileMaskWords = 8, kTileList = 12;
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
 // Sink flag of a transit row: ellt[u].x and row2t[u].x carry it when u is overloaded.
@@ -149,6 +152,14 @@ struct SolveArgs {
   // row i); mscnt = one scratch word (the permutation test)
   uint32_t* msperm;
   uint32_t* mscnt;
+  // batches that do not hold every source's neighbours (tile-active multi-source pass): the
+  // extended batch xsrc = sources followed by the halo (usable, non-overloaded neighbours of
+  // sources the batch lacks; level rows only, for the next-hop pass), *xcount halo rows;
+  // xslot [V] scratch (cluster-order placement), xdup [n] scratch (duplicate rows)
+  uint32_t* xsrc;
+  uint32_t* xcount;
+  uint32_t* xslot;
+  uint32_t* xdup;
 };
 // Row stride of SolveArgs::lvl8 (16-byte rows: the next-hop pass reads 16 levels per load)
 __host__ __device__ inline uint32_t reach_row_bytes(uint32_t V) { return (V + 15u) & ~15u; }
@@ -267,6 +278,13 @@ constexpr uint32_t kDeltaUp0 = 1u, kDeltaUp1 = 2u, kDeltaOvl0 = 4u, kDeltaOvl1 =
 hipError_t launch_refresh_filter(const DeltaEdge* delta, uint32_t n_delta, const uint32_t* sources, uint32_t n,
                                  uint32_t V, const uint64_t* dist, bool unit_cost, uint32_t* alist, uint32_t* asrc,
                                  uint32_t* count, int num_cus, hipStream_t s);
+// Exact second stage: of the *count_in rows the filter listed, those whose dist or next-hop
+// rows the change really moves (needs the next-hop rows; nb <= 32); n_max bounds *count_in.
+hipError_t launch_refresh_exact(const DevGraph& g, const DeltaEdge* delta, uint32_t n_delta, uint32_t V,
+                                const uint64_t* dist, const uint8_t* nh, uint32_t nb, bool unit_cost,
+                                const uint32_t* alist_in, const uint32_t* asrc_in, const uint32_t* count_in,
+                                uint32_t n_max, uint32_t* alist, uint32_t* asrc, uint32_t* count, int num_cus,
+                                hipStream_t s);
 // rows[alist[k]][0 .. words) = 0 for k < n
 hipError_t launch_zero_rows(uint64_t* rows, uint32_t words, const uint32_t* alist, uint32_t n, int num_cus,
                             hipStream_t s);
@@ -321,6 +339,9 @@ uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 // the source's neighbours. Rows it cannot finish are appended to a.ovf_list (count in
 // blk[4]) for the caller's u16 full-order re-run. `half` = the reach pass's queue half.
 int allsrc_pass(const DevGraph& g, const SolveArgs& a);
+// the tile-active multi-source pass serves g; rows of its extended batch of n sources (halo)
+bool ms_tile_ok(const DevGraph& g);
+uint32_t ms_ext_rows(const DevGraph& g, uint32_t n);
 hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t half, uint32_t* blk,
                          int num_cus, hipStream_t s, LaunchInfo* info);
 uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);

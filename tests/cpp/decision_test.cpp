@@ -733,44 +733,64 @@ TEST_GPU(LoopFreeAlternatePaths) {
 // --- GridTopologyFixture.ShortestPathTest (DecisionTest.cpp:4206-4355) ------------
 static int gridDistance(int a, int b, int n) { return std::abs(a % n - b % n) + std::abs(a / n - b / n); }
 
+// createGrid (DecisionTest.cpp:4240-4265): n x n grid, unit metrics, adjacency labels
+// 100001 + neighbour, node labels node + 1, one prefix per node
+static void createGrid(LinkState& ls, PrefixState& ps, int n) {
+  auto addAdj = [&](int i, int j, const std::string& ifName, std::vector<thrift::Adjacency>& adjs,
+                    const std::string& otherIf) {  // :4208-4233
+    if (i < 0 || i >= n || j < 0 || j >= n) return;
+    const int nb = i * n + j;
+    adjs.push_back(createAdjacency(std::to_string(nb), ifName, otherIf, "fe80::" + std::to_string(nb),
+                                   "192.168." + std::to_string(nb / 256) + "." + std::to_string(nb % 256), 1,
+                                   100001 + nb));
+  };
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      const int node = i * n + j;
+      std::vector<thrift::Adjacency> adjs;
+      addAdj(i, j + 1, "0/1", adjs, "0/3");
+      addAdj(i - 1, j, "0/2", adjs, "0/4");
+      addAdj(i, j - 1, "0/3", adjs, "0/1");
+      addAdj(i + 1, j, "0/4", adjs, "0/2");
+      ls.updateAdjacencyDatabase(createAdjDb(std::to_string(node), adjs, node + 1));
+      ps.updatePrefix(std::to_string(node), kDefaultArea, createPrefixEntry(pfx("fc00::" + std::to_string(node) + "/128")));
+    }
+}
+
+// GridTopologyFixture over the reference's whole Range(2, 17, 2) (DecisionTest.cpp:4289-4290):
+// the route count 2n^4 + 3n^2 - 4n, and — stronger than the reference's four sampled pairs —
+// every (src, dst) unicast route: metric = grid distance, next hops = exactly the
+// neighbours one hop closer to dst.
 TEST_GPU(GridTopology_ShortestPathTest) {
-  for (int n = 2; n <= 8; n += 2) {
+  for (int n = 2; n <= 16; n += 2) {
     std::unordered_map<std::string, LinkState> als;
     als.emplace(kDefaultArea, LinkState(kDefaultArea));
-    auto& ls = als.at(kDefaultArea);
     PrefixState ps;
-    auto addAdj = [&](int i, int j, const std::string& ifName, std::vector<thrift::Adjacency>& adjs,
-                      const std::string& otherIf) {  // :4208-4233
-      if (i < 0 || i >= n || j < 0 || j >= n) return;
-      const int nb = i * n + j;
-      adjs.push_back(createAdjacency(std::to_string(nb), ifName, otherIf, "fe80::" + std::to_string(nb),
-                                     "192.168." + std::to_string(nb / 256) + "." + std::to_string(nb % 256), 1,
-                                     100001 + nb));
-    };
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) {  // createGrid :4240-4265
-        const int node = i * n + j;
-        std::vector<thrift::Adjacency> adjs;
-        addAdj(i, j + 1, "0/1", adjs, "0/3");
-        addAdj(i - 1, j, "0/2", adjs, "0/4");
-        addAdj(i, j - 1, "0/3", adjs, "0/1");
-        addAdj(i + 1, j, "0/4", adjs, "0/2");
-        ls.updateAdjacencyDatabase(createAdjDb(std::to_string(node), adjs, node + 1));
-        ps.updatePrefix(std::to_string(node), kDefaultArea, createPrefixEntry(pfx("fc00::" + std::to_string(node) + "/128")));
-      }
+    createGrid(als.at(kDefaultArea), ps, n);
     SpfSolver solver("1", false, false);
     std::vector<std::string> all;
     for (int i = 0; i < n * n; ++i) all.push_back(std::to_string(i));
     auto m = getRouteMap(solver, all, als, ps);
     EXPECT_EQ((long)m.size(), 2L * n * n * n * n + 3L * n * n - 4L * n);
-    auto metricOf = [&](int src, int dst) {
-      auto const& nhs = m[{std::to_string(src), "fc00::" + std::to_string(dst) + "/128"}];
-      return nhs.empty() ? -1 : nhs.begin()->metric;
-    };
-    EXPECT_EQ(metricOf(0, n * n - 1), gridDistance(0, n * n - 1, n));
-    EXPECT_EQ(metricOf(n - 1, n * (n - 1)), gridDistance(n - 1, n * (n - 1), n));
-    for (int k = 1; k < n * n; k += 3) EXPECT_EQ(metricOf(k, (k * 7) % (n * n) == k ? 0 : (k * 7) % (n * n)),
-                                                 gridDistance(k, (k * 7) % (n * n) == k ? 0 : (k * 7) % (n * n), n));
+    bool ok = true;
+    for (int src = 0; src < n * n; ++src)
+      for (int dst = 0; dst < n * n; ++dst) {
+        if (src == dst) continue;
+        auto const& nhs = m[{std::to_string(src), "fc00::" + std::to_string(dst) + "/128"}];
+        std::set<std::string> got, want;
+        for (auto const& nh : nhs) {
+          ok &= nh.metric == gridDistance(src, dst, n);
+          got.insert(nh.neighborNodeName.value_or(""));
+        }
+        const int si = src / n, sj = src % n;
+        const int cand[4][2] = {{si, sj + 1}, {si - 1, sj}, {si, sj - 1}, {si + 1, sj}};
+        for (auto const& c : cand)
+          if (c[0] >= 0 && c[0] < n && c[1] >= 0 && c[1] < n &&
+              gridDistance(c[0] * n + c[1], dst, n) == gridDistance(src, dst, n) - 1)
+            want.insert(std::to_string(c[0] * n + c[1]));
+        ok &= got == want;
+      }
+    EXPECT_TRUE(ok);
   }
 }
 
@@ -1014,6 +1034,46 @@ TEST_GPU(WanUcmpRoutes_vs_Oracle_Config4) {  // the config-4 WAN (1000 nodes, 30
   for (uint32_t i = 0; i < 1000; i += 63) sample.push_back(i);
   wanUcmpRoutes(w, sample, false);
   wanUcmpRoutes(w, sample, true);
+}
+
+// GridTopology.StressTest (DecisionTest.cpp:4358-4372): 99 x 99 grid, LFA on, the route
+// DB of node "523" — timed, and every unicast route checked against routes rebuilt from
+// oracle SPF runs (shortest next hops + RFC 5286 alternates), plus the label routes.
+TEST_GPU(GridTopology_StressTest) {
+  std::unordered_map<std::string, LinkState> als;
+  als.emplace(kDefaultArea, LinkState(kDefaultArea));
+  PrefixState ps;
+  const auto t0 = std::chrono::steady_clock::now();
+  createGrid(als.at(kDefaultArea), ps, 99);
+  const auto t1 = std::chrono::steady_clock::now();
+  SpfSolver solver("1", false, true);
+  SpfCounters::get().reset();
+  auto db = solver.buildRouteDb("523", als, ps);
+  const auto t2 = std::chrono::steady_clock::now();
+  EXPECT_TRUE(db.has_value());
+  if (!db) return;
+  EXPECT_EQ(99u * 99u - 1u, (unsigned)db->unicastRoutes.size());
+  EXPECT_EQ(99u * 99u + 4u, (unsigned)db->mplsRoutes.size());  // node labels + 523's four adjacency labels
+  EXPECT_EQ(5u, (unsigned)SpfCounters::get().spfRuns());       // 523 and its four LFA neighbours
+  auto const& m = als.at(kDefaultArea).csrMirror();
+  OracleRows o(m);
+  RibPolicyStatement none;  // a policy that matches no route: applyAction leaves next hops as they are
+  none.name = "none";
+  none.prefixes = {pfx("fd99::1/128")};
+  const RibPolicy pol({none});
+  const uint32_t me = m.id.at("523");
+  bool ok = true;
+  size_t alternates = 0;
+  for (auto const& [p, route] : db->unicastRoutes) {
+    const std::string ps6 = p.toString();  // fc00::<node>/128
+    const uint32_t dst = m.id.at(ps6.substr(6, ps6.size() - 10));
+    ok &= route.nexthops == expectedRoute(o, me, dst, true, pol, p);
+    for (auto const& nh : route.nexthops) alternates += nh.metric != route.nexthops.begin()->metric;
+  }
+  EXPECT_TRUE(ok);
+  std::printf("  99x99 grid: createGrid %.1f ms, buildRouteDb(\"523\") with LFA %.1f ms, %zu routes, %zu alternates\n",
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(t2 - t1).count(), db->unicastRoutes.size(), alternates);
 }
 
 // buildRouteDbs on host worker threads (HostParallel.h) against the one-thread loop: the

@@ -65,12 +65,16 @@ def check_rows(eng, g, sources, dist, nh, tight, use_metric=True, oracle_rows=No
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("max_metric", [1, 9])
-def test_random_patches_match_oracle(eng, family, seed, max_metric):
+@pytest.mark.parametrize("with_tight", [True, False], ids=["tight", "exact"])
+def test_random_patches_match_oracle(eng, family, seed, max_metric, with_tight):
+    """Rows with tight-edge rows refresh through the first-stage filter; rows without
+    through the exact second stage too (only rows whose dist / next hops move are
+    re-solved, spf_update.hip refresh_exact)."""
     g = random_graph(200 + seed, 80 + 20 * seed, 200 + 40 * seed, max_metric)
     eng.set_graph(g)
     srcs = list(range(g.num_nodes))
     rng = np.random.default_rng(seed)
-    dist, nh, tight = eng.solve(srcs, True, want_tight=True)
+    dist, nh, tight = eng.solve(srcs, True, want_tight=with_tight)
     for step in range(4):
         p = random_patch(g, rng, max_metric=max_metric if step % 2 else 1)
         eng.patch(**p)
@@ -129,6 +133,30 @@ def test_fabric_rsw_overload_toggle(eng):
     n_rsw = sum(1 for nm in g.names if nm.startswith("3-"))
     assert 0 < n <= g.num_nodes - n_rsw + 1
     check_rows(eng, eng.g, srcs, dist, nh, tight, oracle_rows=range(0, g.num_nodes, 37))
+
+
+def test_fabric_rsw_overload_exact_filter(eng, monkeypatch):
+    """Without tight rows the exact second stage re-solves only the rows the RSW toggle
+    really moves (the pod's FSWs lose the RSW as a next hop towards the pod's other-plane
+    FSWs; SSWs keep theirs through the other RSWs): far fewer than the first stage lists,
+    and every row equals a fresh solve."""
+    g = T.fabric(1200)
+    eng.set_graph(g)
+    srcs = np.arange(g.num_nodes, dtype=np.uint32)
+    dist, nh, _ = eng.solve(srcs, True)
+    rsw = [i for i, nm in enumerate(g.names) if nm.startswith("3-")][7]
+    counts = []
+    for exact in ("0", "1"):
+        monkeypatch.setenv("OPENR_SPF_REFRESH_EXACT", exact)
+        d, n = dist.copy(), nh.copy()
+        eng.patch(nodes=[rsw], node_overloaded=[1])
+        counts.append(eng.refresh(srcs, d, n))
+        check_rows(eng, eng.g, srcs, d, n, None, oracle_rows=range(0, g.num_nodes, 37))
+        eng.patch(nodes=[rsw], node_overloaded=[0])
+        eng.refresh(srcs, d, n)
+        np.testing.assert_array_equal(d, dist)
+        np.testing.assert_array_equal(n, nh)
+    assert 0 < counts[1] < counts[0] // 4, counts
 
 
 def test_uniform_to_general_metric_switches_kernel(eng):
