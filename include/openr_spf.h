@@ -252,7 +252,11 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* patch);
    before, or is usable with d_s(u) + w_new <= d_s(v) after (u expanding for s);
    *out_resolved (nullable) = rows re-solved (added to stats.spf_runs). Fails with
    OPENR_SPF_EINVAL when no patch followed the last set_graph. The host form splits the
-   rows across devices like openr_spf_solve; the device form synchronizes `stream` once. */
+   rows across devices like openr_spf_solve; the device form synchronizes `stream` once.
+   Multi-device callers of the device form: the delta is per context, and any refresh
+   ends its merging, so refresh the rows held on EVERY device before the next patch (a
+   device whose rows skipped a delta would be refreshed against the later delta only and
+   stay stale; the host LinkState mirror does this). */
 int openr_spf_refresh(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t flags, uint64_t* dist,
                       uint8_t* nh, uint32_t nh_bytes, uint64_t* tight, uint32_t* out_resolved);
 int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_sources, uint32_t n,

@@ -447,12 +447,36 @@ __global__ __launch_bounds__(64 * kNhlWaves) void nh_from_levels_kernel(DevGraph
           }
         }
       }
-      if (want_dist) {
-        const uint32_t lw[4] = {ls.x, ls.y, ls.z, ls.w};
+    }
+    if (want_dist) {
+      // distance row from the level row (just read: L2), four nodes per lane and step so a
+      // wavefront's stores cover whole lines
+      const uint32_t* lw = reinterpret_cast<const uint32_t*>(a.lvl8 + (size_t)k * rb);
+      if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0) {
+        ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
+        for (uint32_t i = lane; i < V / 4u; i += 64u) {
+          const uint32_t w = lw[i];
+          uint64_t xd[4];
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; ++j) {
-          const uint32_t l = (lw[j >> 2] >> (8u * (j & 3u))) & 0xFFu;
-          if (v0 + j < V) store_row<uint64_t>(&drow[v0 + j], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt);
+          for (uint32_t j = 0; j < 4u; ++j) {
+            const uint32_t l = (w >> (8u * j)) & 0xFFu;
+            xd[j] = l != 0xFFu ? (uint64_t)l * cost : ~0ull;
+          }
+          if (nt) {
+            __builtin_nontemporal_store(xd[0], &d2[2u * i].x);
+            __builtin_nontemporal_store(xd[1], &d2[2u * i].y);
+            __builtin_nontemporal_store(xd[2], &d2[2u * i + 1u].x);
+            __builtin_nontemporal_store(xd[3], &d2[2u * i + 1u].y);
+          } else {
+            d2[2u * i] = make_ulonglong2(xd[0], xd[1]);
+            d2[2u * i + 1u] = make_ulonglong2(xd[2], xd[3]);
+          }
+        }
+      } else {
+        const uint8_t* lb = a.lvl8 + (size_t)k * rb;
+        for (uint32_t v = lane; v < V; v += 64u) {
+          const uint32_t l = lb[v];
+          store_row<uint64_t>(&drow[v], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt);
         }
       }
     }
@@ -801,9 +825,26 @@ struct MsTileArgs {
   uint32_t V, ntiles, n;
 };
 
-template <uint32_t NPT>
+template <uint32_t NPT, bool PROF>
 __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(MsTileArgs t, uint64_t cost,
-                                                                   uint32_t* ctr, uint32_t* ovf_count, uint32_t flags) {
+                                                                   uint32_t* ctr, uint32_t* ovf_count, uint32_t flags,
+                                                                   unsigned long long* prof) {
+  // tuning (OPENR_SPF_MS_PROF=1): wave 0's cycles per phase of every level step — [0] level
+  // start (activity words, chunk mask), [1] a chunk's frontier reads, [2] its arithmetic and
+  // frontier stores, [3] its emission marks, [4] the barrier — and [5] steps, [6] active
+  // chunks, [7] batches. A stamp follows an asm use of the value the phase waits for.
+  const bool pf = PROF && prof != nullptr && threadIdx.x < 64u;
+  unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long ts = 0;
+#define OPENR_MS_STAMP(i, dep)                                     \
+  do {                                                             \
+    if (pf) {                                                      \
+      asm volatile("" ::"v"(dep));                                 \
+      const long long tnow = (long long)__builtin_amdgcn_s_memtime(); \
+      pacc[i] += (unsigned long long)(tnow - ts);                  \
+      ts = tnow;                                                   \
+    }                                                              \
+  } while (0)
   typedef __attribute__((address_space(3))) uint64_t lds_u64;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
   const uint32_t V = t.V, tid = threadIdx.x;
@@ -889,8 +930,13 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(MsTileArgs t,
     }
     uint32_t L = 0;
     bool ovf = false;
+    if (pf) {
+      ts = (long long)__builtin_amdgcn_s_memtime();
+      pacc[7] += 1;
+    }
     for (;;) {
-      // this step's activity: bit (8i + wave) of act[L % 3] for slot i
+      // this step's activity: bit (8i + wave) of act[L % 3] for slot i; slots go in chunks
+      // of kMsChunk (tile order makes a chunk's tiles neighbours: tile_order in spf_capi)
       const uint32_t cur_set = L % 3u;
       uint32_t aw[5];
 #pragma unroll
@@ -903,50 +949,89 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(MsTileArgs t,
         ovf = true;
         break;
       }
-      uint32_t A = 0;
+      constexpr uint32_t NC = NPT / kMsChunk;
+      // chunk c of this wave holds tiles 32c + 8r + wave (r < 4): bits wave + 8r of word c
+      uint32_t C = 0;  // active chunks
 #pragma unroll
-      for (uint32_t i = 0; i < NPT; ++i) A |= ((aw[i >> 2] >> (8u * (i & 3u) + wave)) & 1u) << i;
+      for (uint32_t c = 0; c < NC; ++c) C |= ((aw[c] & (0x01010101u << wave)) != 0u ? 1u : 0u) << c;
+      if (pf) {
+        pacc[5] += 1;
+        pacc[6] += (unsigned long long)__builtin_popcount(C);
+      }
+      OPENR_MS_STAMP(0, C);
       if (tid < 8u) act[8u * ((L + 2u) % 3u) + tid] = 0u;  // last read one step ago
       lds_u32* const nact = act + 8u * ((L + 1u) % 3u);
       uint32_t hm[8];
 #pragma unroll
       for (uint32_t b = 0; b < 8u; ++b) hm[b] = (((L + 1u) >> b) & 1u) ? ~0u : 0u;
       const uint32_t cur = (L & 1u) ? F1 : 0u, nxt = (L & 1u) ? 0u : F1;
-      uint32_t eaddr = ebase + 8u * kMsThreads * (A ? (uint32_t)__builtin_ctz(A) : 0u);
-      asm volatile("" : "+v"(eaddr));
-      uint64_t er = A ? *(const lds_u64*)(size_t)eaddr : 0ull;
-      MsUnroll<0, NPT>::run([&](auto ic) {
-        constexpr uint32_t i = decltype(ic)::value;
-        if ((A >> i) & 1u) {  // uniform
-          const uint32_t lo = (uint32_t)er, hi = (uint32_t)(er >> 32);
-          const uint32_t f = ms_rd(cur + (lo & 0xFFFFu)) | ms_rd(cur + (lo >> 16)) | ms_rd(cur + (hi & 0xFFFFu)) |
-                             ms_rd(cur + (hi >> 16));
-          // the tile's neighbour list (lane j < kTileList: its j-th tile, itself included),
-          // read behind the frontier words: used if the tile emits
-          const uint32_t lane = __lane_id();
-          uint32_t lt = lay.tl + kTileList * (8u * i + wave);
-          asm volatile("" : "+s"(lt));  // per slot, not hoisted out of the level loop
-          const uint32_t nbt = lane < kTileList ? *(const lds_u8*)(size_t)(lt + lane) : 0xFFu;
-          const uint32_t rest = A & ~((2u << i) - 1u);
-          if (rest) {  // the next active slot's pull row, in flight with this slot's reads
-            uint32_t na = ebase + 8u * kMsThreads * (uint32_t)__builtin_ctz(rest);
-            asm volatile("" : "+v"(na));
-            er = *(const lds_u64*)(size_t)na;
-          }
-          const uint32_t vis = p[0][i] | p[1][i] | p[2][i] | p[3][i] | p[4][i] | p[5][i] | p[6][i] | p[7][i];
-          const uint32_t nw = f & ~vis;
-          const uint32_t fw = ((sink >> i) & 1u) ? 0u : nw;
-          ms_wr(nxt + 4u * (tb + kMsThreads * i), fw);
+      // pull rows of the first active chunk (a slot past the last tile has none: it reads zero
+      // words and writes nothing)
+      const uint32_t zrow = kZero | (kZero << 16);
+      const uint64_t zer = (uint64_t)zrow | ((uint64_t)zrow << 32);
+      uint64_t er[kMsChunk];
+      {
+        const uint32_t c0 = C ? (uint32_t)__builtin_ctz(C) : 0u;
+        uint32_t eaddr = ebase + 8u * kMsThreads * kMsChunk * c0;
+        asm volatile("" : "+v"(eaddr));
 #pragma unroll
-          for (uint32_t b = 0; b < 8u; ++b) p[b][i] |= nw & hm[b];
-          if (__builtin_amdgcn_ballot_w64(fw != 0u) != 0ull) {  // this tile emits: its neighbourhood is active next step
+        for (uint32_t r = 0; r < kMsChunk; ++r)
+          er[r] = (C && 8u * (kMsChunk * c0 + r) + wave < t.ntiles) ? *(const lds_u64*)(size_t)(eaddr + 8u * kMsThreads * r)
+                                                                 : zer;
+      }
+      MsUnroll<0, NC>::run([&](auto ic) {
+        constexpr uint32_t c = decltype(ic)::value;
+        if ((C >> c) & 1u) {  // uniform
+          uint32_t f[kMsChunk];
+#pragma unroll
+          for (uint32_t r = 0; r < kMsChunk; ++r) {
+            const uint32_t lo = (uint32_t)er[r], hi = (uint32_t)(er[r] >> 32);
+            f[r] = ms_rd(cur + (lo & 0xFFFFu)) | ms_rd(cur + (lo >> 16)) | ms_rd(cur + (hi & 0xFFFFu)) |
+                   ms_rd(cur + (hi >> 16));
+          }
+          OPENR_MS_STAMP(1, f[0] | f[1] | f[2] | f[3]);
+          const uint32_t rest = C & ~((2u << c) - 1u);
+          if (rest) {  // the next active chunk's pull rows, in flight with this chunk's reads
+            const uint32_t c1 = (uint32_t)__builtin_ctz(rest);
+            uint32_t na = ebase + 8u * kMsThreads * kMsChunk * c1;
+            asm volatile("" : "+v"(na));
+#pragma unroll
+            for (uint32_t r = 0; r < kMsChunk; ++r)
+              er[r] = 8u * (kMsChunk * c1 + r) + wave < t.ntiles ? *(const lds_u64*)(size_t)(na + 8u * kMsThreads * r) : zer;
+          }
+          uint32_t em = 0;  // slots of the chunk that emit (a non-zero frontier word)
+#pragma unroll
+          for (uint32_t r = 0; r < kMsChunk; ++r) {
+            constexpr uint32_t i0 = kMsChunk * c;
+            const uint32_t i = i0 + r;
+            if (8u * i + wave >= t.ntiles) continue;  // uniform: a slot past the last tile
+            const uint32_t vis = p[0][i] | p[1][i] | p[2][i] | p[3][i] | p[4][i] | p[5][i] | p[6][i] | p[7][i];
+            const uint32_t nw = f[r] & ~vis;
+            const uint32_t fw = ((sink >> i) & 1u) ? 0u : nw;
+            ms_wr(nxt + 4u * (tb + kMsThreads * i), fw);
+#pragma unroll
+            for (uint32_t b = 0; b < 8u; ++b) {
+              p[b][i] |= nw & hm[b];
+              asm volatile("" : "+v"(p[b][i]));  // updated here: not sunk past the barrier with nw live
+            }
+            em |= (__builtin_amdgcn_ballot_w64(fw != 0u) != 0ull ? 1u : 0u) << r;
+          }
+          OPENR_MS_STAMP(2, em);
+          // emitting tiles mark their neighbourhoods (lists: lane j < kTileList holds the
+          // j-th tile, the tile itself included) active for the next step
+          const uint32_t lane = __lane_id();
+          for (uint32_t m = em; m; m &= m - 1u) {
+            const uint32_t tile = 8u * (kMsChunk * c + (uint32_t)__builtin_ctz(m)) + wave;
+            const uint32_t nbt = lane < kTileList ? *(const lds_u8*)(size_t)(lay.tl + kTileList * tile + lane) : 0xFFu;
             if (nbt < 0xFEu) lds_or(&nact[nbt >> 5], 1u << (nbt & 31u));
-            // a tile with more than kTileList neighbour tiles (list head 0xFE) marks every tile
+            // more than kTileList neighbour tiles (list head 0xFE): every tile
             if (__builtin_amdgcn_readfirstlane(nbt) == 0xFEu && lane < kTileMaskWords) lds_or(&nact[lane], ~0u);
           }
+          OPENR_MS_STAMP(3, em);
         }
       });
       lds_barrier();
+      OPENR_MS_STAMP(4, L);
       ++L;
     }
     if (ovf) {
@@ -1016,13 +1101,17 @@ __global__ __launch_bounds__(kMsThreads, 1) void msbfs_tile_kernel(MsTileArgs t,
     __syncthreads();
     unit = *next_unit;
   }
+#undef OPENR_MS_STAMP
+  if (pf && __lane_id() == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&prof[i], pacc[i]);
   retire_workgroup(ctr, nullptr);
 }
 
 template <uint32_t NPT>
 hipError_t launch_msbfs_tile_npt(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t* blk, int num_cus,
                                  hipStream_t s, uint32_t flags) {
-  auto k = msbfs_tile_kernel<NPT>;
+  const bool want_prof = env_u32("OPENR_SPF_MS_PROF", 0u, 0u, 1u) != 0;
+  auto k = want_prof ? msbfs_tile_kernel<NPT, true> : msbfs_tile_kernel<NPT, false>;
   const uint32_t lds = MsTLayout(g.ntiles).total;
   MsTileArgs t;
   t.tord = g.tord;
@@ -1048,9 +1137,29 @@ hipError_t launch_msbfs_tile_npt(const DevGraph& g, const SolveArgs& a, uint64_t
   // an extended batch holds at most the halo bound more rows (ms_ext_rows)
   const uint32_t nbatch = ((a.xcount ? ms_ext_rows(g, a.n) : a.n) + kMsBatch - 1u) / kMsBatch;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>(nbatch, (uint32_t)num_cus));
+  static unsigned long long* prof_buf = nullptr;  // tuning aid: per-phase cycle sums, printed
+  unsigned long long* prof = nullptr;
+  if (want_prof) {
+    if (!prof_buf && hipMalloc(&prof_buf, 8 * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
+    prof = prof_buf;
+    if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
+  }
   note_launch("msbfs_tile_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kMsThreads), lds, s, t, cost, blk, blk + 4, flags);
-  return hipGetLastError();
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kMsThreads), lds, s, t, cost, blk, blk + 4, flags, prof);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && prof) {
+    unsigned long long h[8];
+    if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+      const double st = h[5] ? (double)h[5] : 1.0, ch = h[6] ? (double)h[6] : 1.0;
+      std::fprintf(stderr,
+                   "msbfs_tile: grid=%u batches(wave0)=%llu steps/batch=%.1f active chunks/step=%.2f | cycles/step: "
+                   "start %.0f barrier %.0f | cycles/chunk: reads %.0f compute %.0f marks %.0f\n",
+                   grid, h[7], h[7] ? st / (double)h[7] : 0.0, ch / st, h[0] / st, h[4] / st, h[1] / ch, h[2] / ch,
+                   h[3] / ch);
+    }
+  }
+  return e;
 }
 
 template <uint32_t NPT>
@@ -1088,10 +1197,30 @@ bool ms_tile_ok(const DevGraph& g) {
          env_u32("OPENR_SPF_MSBFS_TILE", 1u, 0u, 1u) != 0u;
 }
 
+// wave-reach knob: 0 off, 1 whenever it applies, 2 auto
+static uint32_t wreach_knob() { return env_u32("OPENR_SPF_BFS_WREACH", 0u, 0u, 2u); }
+
+// queue half: the widest sampled level with a quarter's margin (OPENR_SPF_REACH_QHALF, tests:
+// a smaller half, so wide levels take the u16 re-run)
+uint32_t allsrc_qhalf(const DevGraph& g) {
+  const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
+  const uint32_t qforce = env_u32("OPENR_SPF_REACH_QHALF", 0u, 0u, 65535u);
+  return qforce ? (std::max<uint32_t>(qforce, g.max_deg + 1u) + 15u) & ~15u : (std::max<uint32_t>(64u, need1) + 15u) & ~15u;
+}
+
+bool allsrc_ext_ok(const DevGraph& g) {
+  return g.crank && (ms_tile_ok(g) || (g.elld && wreach_knob() != 0u)) && env_u32("OPENR_SPF_MSBFS_HALO", 1u, 0u, 1u);
+}
+
 int allsrc_pass(const DevGraph& g, const SolveArgs& a) {
   if (!a.lvl8 || !a.rowmap || !a.rowok || a.out_row || a.perm || a.tight || a.ign_ptr || g.max_deg > 4u) return 0;
+  // the wave-reach pass: a full batch, or a partial one extended with halo rows
+  const uint32_t wr = wreach_knob();
+  if (wr != 0u && wreach_lds_bytes(g, allsrc_qhalf(g)) &&
+      (a.n >= g.V || (a.xsrc && a.xcount && a.xslot && a.xdup && g.crank)))
+    return 3;
   const bool ms_ok = a.msperm && a.mscnt;
-  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 2u, 0u, 2u);
+  const uint32_t ms = env_u32("OPENR_SPF_BFS_MSBFS", 0u, 0u, 2u);
   if (ms != 0u && ms_ok && (ms_tile_ok(g) || (MsLayout<20>::bytes(g.V) <= kMaxLds && g.V <= MsLayout<20>::kMaxV)) &&
       (ms == 1u || a.n >= g.V))
     return 2;
@@ -1104,13 +1233,14 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
                          int num_cus, hipStream_t s, LaunchInfo* info) {
   // OPENR_SPF_REACH_DIST=2: the next-hop pass writes the distance rows (streaming) instead
   const bool dist2 = env_u32("OPENR_SPF_REACH_DIST", 1u, 1u, 2u) == 2u;
-  const uint32_t flags = nt_stores() | (dist2 ? 2u : 0u);
+  uint32_t flags = nt_stores() | (dist2 ? 2u : 0u);
   const uint32_t mgrid = std::max<uint32_t>(1u, std::min<uint32_t>((g.V + 255u) / 256u, 4u * (uint32_t)num_cus));
   const uint32_t ngrid = std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 255u) / 256u, 4u * (uint32_t)num_cus));
   // a partial batch on the tile-active pass: extended with halo rows (ms_ext_*)
-  const bool ext = pass == 2 && ms_tile_ok(g) && a.n < g.V && a.xsrc && a.xcount && a.xslot && a.xdup && g.crank &&
-                   env_u32("OPENR_SPF_MSBFS_HALO", 1u, 0u, 1u);
+  const bool ext = (pass == 3 || (pass == 2 && ms_tile_ok(g))) && a.n < g.V && a.xsrc && a.xcount && a.xslot &&
+                   a.xdup && g.crank && env_u32("OPENR_SPF_MSBFS_HALO", 1u, 0u, 1u);
   hipError_t err;
+  if (pass == 3 && a.n < g.V && !ext) return hipErrorInvalidValue;  // allsrc_pass checked the scratch
   if (ext) {
     note_launch("ms_ext");
     hipLaunchKernelGGL(ms_ext_clear_kernel, dim3(mgrid), dim3(256), 0, s, a.rowmap, a.xslot, g.V, a.xcount);
@@ -1118,13 +1248,19 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
                        a.xslot, a.xsrc, a.xdup, a.xcount);
     hipLaunchKernelGGL(ms_ext_halo_kernel, dim3(ngrid), dim3(256), 0, s, g, a.sources, a.n, a.rowmap, a.xslot, a.xsrc,
                        a.xcount);
-    hipLaunchKernelGGL(ms_ext_order_kernel, dim3(1), dim3(1024), 0, s, a.xslot, g.V, a.xdup, a.xcount, a.msperm);
+    if (pass == 2)  // batch order of the multi-source pass (the wave-reach pass takes rows as they are)
+      hipLaunchKernelGGL(ms_ext_order_kernel, dim3(1), dim3(1024), 0, s, a.xslot, g.V, a.xdup, a.xcount, a.msperm);
   } else {
     note_launch("reach_map");
     hipLaunchKernelGGL(reach_map_clear_kernel, dim3(mgrid), dim3(256), 0, s, a.rowmap, g.V);
     hipLaunchKernelGGL(reach_map_fill_kernel, dim3(ngrid), dim3(256), 0, s, a.rowmap, a.sources, a.n, g.V);
   }
-  if (ext) {
+  if (pass == 3) {
+    SolveArgs b = a;  // the level pass solves [sources | halo]; the next-hop pass the call's rows
+    if (ext) b.sources = a.xsrc;
+    else b.xcount = nullptr;
+    err = launch_wreach(g, b, half, blk, num_cus, s, info);
+  } else if (ext) {
     SolveArgs b = a;  // the multi-source pass solves [sources | halo]; the next-hop pass the call's rows
     b.sources = a.xsrc;
     if (info) info->kernel = "msbfs_tile_kernel";
@@ -1181,7 +1317,8 @@ hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64
     err = hipGetLastError();
   }
   if (err != hipSuccess) return err;
-  if (a.nh || dist2) {
+  if (pass == 3) flags |= 2u;  // the wave-reach pass writes level rows only
+  if (a.nh || (flags & 2u)) {
     // 8 workgroups of 4 waves per CU, a multiple of the 8 XCDs
     const uint32_t grid2 = 8u * std::max<uint32_t>(1u, std::min<uint32_t>((a.n + 8u * kNhlWaves - 1u) / (8u * kNhlWaves),
                                                                            (uint32_t)num_cus));

@@ -97,7 +97,7 @@ __host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has
 // owns next-hop bytes [3s, 3s + 3); slice 0 also zero-fills the bytes past the last
 // slice.
 template <int FB, int BLOCK, bool SLICED, bool GENERIC>
-__device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
+__device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t k, uint32_t sid, uint32_t slice, uint32_t V,
                                           const uint32_t* st, bool nt) {
   using S = State<FB>;
   const uint32_t tid = threadIdx.x;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t sid, uint
       if ((S::field(st, v) & kCodeMask) == 0u) drow[v] = ~0ull;
   if (!nrow) return;
   if (SLICED) {  // the slice's 29-bit chunks, coalesced; slice_merge packs the bytes
-    uint32_t* trow = a.slice_tmp + ((size_t)sid * a.nsl + slice) * V;
+    uint32_t* trow = a.slice_tmp + ((size_t)(k - a.k0) * a.nsl + slice) * V;  // chunk-local row
     for (uint32_t v = tid; v < V; v += BLOCK) store_row<uint32_t>(&trow[v], S::field(st, v) >> S::kNhs, nt);
     return;
   }
@@ -176,8 +176,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   const uint32_t rmask = ring_cap - 1u;  // RING: ring_cap is a power of two
   const uint32_t nsl = SLICED ? a.nsl : 1u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  // sliced class in chunks: class-local solves [k0, k0 + krows) (a re-run lists global uids)
+  const uint32_t k0 = SLICED ? a.k0 : 0u;
+  const uint32_t in_chunk = !SLICED || !a.krows ? count : count > k0 ? min(a.krows, count - k0) : 0u;
   // a re-run launch with nothing flagged does no work
-  const uint32_t units = from_list ? *ovf_count : count * nsl;
+  const uint32_t units = from_list ? *ovf_count : in_chunk * nsl;
   // nothing flagged: every workgroup leaves at once (no unit is taken, so the scheduling
   // counters stay at rest and no workgroup needs to retire; saves the 256 retire atomics)
   if (from_list && units == 0u) return;
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #endif
 
   for (uint32_t unit = blockIdx.x; unit < units;) {
-    const uint32_t uid = from_list ? a.ovf_list[unit] : unit;  // class-local (solve, slice) index
+    const uint32_t uid = from_list ? a.ovf_list[unit] : k0 * nsl + unit;  // class-local (solve, slice) index
     const uint32_t k = SLICED ? uid / nsl : uid, slice = SLICED ? uid - k * nsl : 0u;
     const uint32_t sid = a.perm ? a.perm[first + k] : k;
     const uint32_t src = a.sources[sid];
@@ -527,7 +530,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t0);
 #endif
-        write_out<FB, BLOCK, SLICED, GENERIC>(a, sid, slice, V, st, nt != 0);
+        write_out<FB, BLOCK, SLICED, GENERIC>(a, k, sid, slice, V, st, nt != 0);
 #ifdef OPENR_SPF_PROFILE
         OPENR_PROF_STAMP(t1);
         OPENR_PROF_ADD(6, t0, t1);
@@ -656,11 +659,14 @@ __global__ __launch_bounds__(256) void slice_merge(SolveArgs a, uint32_t V) {
   __shared__ uint32_t seg[256u * kMaxNb / 4u];
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   const uint32_t nsl = a.nsl, nb = a.nh_bytes, tiles = (V + 255u) / 256u;
+  // this chunk's solves [k0, k0 + in_chunk) of the class
+  const uint32_t in_chunk = !a.krows ? count : count > a.k0 ? min(a.krows, count - a.k0) : 0u;
   uint8_t* segb = reinterpret_cast<uint8_t*>(seg);
-  for (uint64_t blk = blockIdx.x; blk < (uint64_t)count * tiles; blk += gridDim.x) {
-    const uint32_t k = (uint32_t)(blk / tiles), v0 = (uint32_t)(blk - (uint64_t)k * tiles) * 256u;
+  for (uint64_t blk = blockIdx.x; blk < (uint64_t)in_chunk * tiles; blk += gridDim.x) {
+    const uint32_t kc = (uint32_t)(blk / tiles), v0 = (uint32_t)(blk - (uint64_t)kc * tiles) * 256u;
+    const uint32_t k = a.k0 + kc;
     const uint32_t sid = a.perm ? a.perm[first + k] : k;
-    const uint32_t* t = a.slice_tmp + (size_t)sid * nsl * V;
+    const uint32_t* t = a.slice_tmp + (size_t)kc * nsl * V;
     const uint32_t nv = std::min<uint32_t>(256u, V - v0), v = v0 + threadIdx.x;
     uint8_t* dst = a.nh + out_row_of(a, sid) * (size_t)V * nb + (size_t)v0 * nb;
     const bool staged = nb <= kMaxNb;
@@ -720,13 +726,28 @@ hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
     default:
       if (sliced) {
-        if (a.nh && !a.slice_tmp) return hipErrorInvalidValue;
-        hipError_t err = launch_bfs_fb<32, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
-        if (err != hipSuccess || !a.nh) return err;
-        const uint64_t items = (uint64_t)a.n * ((g.V + 255u) / 256u);  // upper bound: (solve, 256-node tile) pairs
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(items, 8192u);
-        hipLaunchKernelGGL(slice_merge, dim3(std::max(grid, 1u)), dim3(256), 0, s, a, g.V);
-        return hipGetLastError();
+        if (!a.nh) {  // no next-hop output: no slice scratch, one launch
+          SolveArgs c = a;
+          c.k0 = c.krows = 0;
+          return launch_bfs_fb<32, true>(g, c, cost, glog, has_ign, ellm, num_cus, s, info);
+        }
+        if (!a.slice_tmp) return hipErrorInvalidValue;
+        // the class in chunks of krows solves (slice_tmp holds one chunk; the launcher sized
+        // krows from its scratch budget); chunks past the class's device-side count exit at once
+        const uint32_t rows = a.krows ? a.krows : std::max(a.n, 1u);
+        for (uint32_t k0 = 0; k0 < a.n; k0 += rows) {
+          SolveArgs c = a;
+          c.k0 = k0;
+          c.krows = rows;
+          hipError_t err = launch_bfs_fb<32, true>(g, c, cost, glog, has_ign, ellm, num_cus, s, info);
+          if (err != hipSuccess) return err;
+          const uint64_t items = (uint64_t)std::min(rows, a.n - k0) * ((g.V + 255u) / 256u);  // (solve, 256-node tile) pairs
+          const uint32_t grid = (uint32_t)std::min<uint64_t>(items, 8192u);
+          hipLaunchKernelGGL(slice_merge, dim3(std::max(grid, 1u)), dim3(256), 0, s, c, g.V);
+          err = hipGetLastError();
+          if (err != hipSuccess) return err;
+        }
+        return hipSuccess;
       }
       return launch_bfs_fb<32, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   }

@@ -1066,11 +1066,7 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     // all-sources batches: a level pass, then next hops from neighbour level rows
     // (spf_allsrc.hip); the rows it lists are re-run by the u16 full-order variant
     if (const int pass = has_ign ? 0 : allsrc_pass(g, a)) {
-      const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
-      const uint32_t qforce = env_u32("OPENR_SPF_REACH_QHALF", 0u, 0u, 65535u);  // tests: force overflows
-      const uint32_t half = qforce ? (std::max<uint32_t>(qforce, g.max_deg + 1u) + 15u) & ~15u
-                                   : (std::max<uint32_t>(64u, need1) + 15u) & ~15u;
-      err = launch_allsrc(pass, g, a, cost, half, blk, num_cus, s, info);
+      err = launch_allsrc(pass, g, a, cost, allsrc_qhalf(g), blk, num_cus, s, info);
       if (err != hipSuccess) return err;
       return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true,
                                                                           blk + 2, blk + 4, num_cus, s, info);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -97,6 +98,11 @@ struct Device {
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
+  // pinned staging of the records and the event of the patch's last launch: a patch does
+  // not wait for its scatter kernel; work on another stream waits for the event instead
+  PatchRec* hrecs = nullptr;
+  size_t hrecs_cap = 0;
+  hipEvent_t patch_ev = nullptr;
   DevBuf<DeltaEdge> delta;
   DevBuf<uint32_t> alist, asrc, acount, alist2, asrc2;  // refresh: listed rows (first / exact stage)
   // exact-order kernel: per-solve slots when a slot does not fit LDS; pop-order rows
@@ -165,6 +171,24 @@ struct openr_spf_ctx {
   // those of the graph before the earlier patch), keeping each edge's oldest state
   bool refreshed = true;
   std::unordered_map<uint32_t, uint32_t> delta_index;  // directed edge -> delta slot
+  // metrics of the usable edges as a multiset (w_min / w_max after a patch without an O(E)
+  // scan) and the number of usable edges whose metric is 0 or above 2^31-1
+  std::map<uint32_t, uint32_t> wcount;
+  uint64_t n_bad_metric = 0;
+  // per-patch marks (stamp == patch_epoch: set during this patch), so a patch costs
+  // O(touched edges) rather than O(E)
+  std::vector<uint32_t> seen_e, dirty_e, dirty_v;
+  uint32_t patch_epoch = 0;
+  void count_metric(uint32_t e, int dir) {  // e's contribution while it is usable
+    if (adj[e] & kEdgeDown) return;
+    const uint64_t m = metric[e];
+    if (m == 0 || m > 0x7FFFFFFFull) {
+      n_bad_metric += dir > 0 ? 1 : (uint64_t)-1;
+      return;
+    }
+    if (dir > 0) ++wcount[(uint32_t)m];
+    else if (auto it = wcount.find((uint32_t)m); it != wcount.end() && --it->second == 0) wcount.erase(it);
+  }
 };
 
 namespace {
@@ -369,6 +393,30 @@ void tile_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col, std::v
     }
   }
   const uint32_t nt = (V + kTileNodes - 1u) / kTileNodes;
+  // within a tile, nodes in id order: on id-ordered meshes (row-major grids) a lane's
+  // neighbours then sit at nearby lanes of the same or the adjacent rows, and a wavefront's
+  // frontier reads spread over the LDS banks instead of colliding
+  for (uint32_t t0 = 0; t0 < V; t0 += kTileNodes)
+    std::sort(tord.begin() + t0, tord.begin() + std::min<uint32_t>(V, t0 + kTileNodes));
+  // Internal tile ids: thread t of the 512-thread kernel owns internal ids t + 512 i (slot i,
+  // tile 8i + wave), and a wave takes its slots in chunks of 4 (kMsChunk). Grown tile s goes
+  // to internal tile T(s) so that consecutive grown tiles — neighbours — share a wave's
+  // chunk: T enumerates (chunk c, wave w, slot r) as 8 (4c + r) + w, skipping ids >= nt; the
+  // last grown tile (the partial one) keeps id nt - 1, so padding ids stay at the end.
+  {
+    std::vector<uint32_t> tmap;
+    for (uint32_t c = 0; tmap.size() + 1u < nt; ++c)
+      for (uint32_t w = 0; w < 8u; ++w)
+        for (uint32_t r = 0; r < 4u; ++r) {
+          const uint32_t T = 8u * (4u * c + r) + w;
+          if (T < nt - 1u) tmap.push_back(T);
+        }
+    tmap.push_back(nt - 1u);
+    std::vector<uint32_t> internal((size_t)nt * kTileNodes, UINT32_MAX);
+    for (uint32_t p = 0; p < V; ++p) internal[(size_t)tmap[p / kTileNodes] * kTileNodes + p % kTileNodes] = tord[p];
+    internal.resize(V);  // ids >= V: the partial last tile's padding
+    tord.swap(internal);
+  }
   std::vector<uint32_t> tinv(V);
   for (uint32_t p = 0; p < V; ++p) tinv[tord[p]] = p;
   tmask.assign((size_t)nt * kTileMaskWords, 0u);
@@ -480,10 +528,18 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     a.nsl = 1;
     mask = 1u << kCls8;
   }
+  a.k0 = a.krows = 0;
   if (fam == kFamCode && ((mask >> kClsSliced) & 1u) && a.nh) {
-    hipError_t err = d.slicetmp.reserve((size_t)a.n * a.nsl * d.g.V);
+    // slice scratch for at most a budget's worth of sliced solves at a time (the class runs
+    // in chunks of krows): 512 MiB, OPENR_SPF_SLICE_ROWS (tests) forces a chunk size
+    const uint64_t per_row = (uint64_t)a.nsl * d.g.V * sizeof(uint32_t);
+    const uint64_t budget_rows = std::max<uint64_t>(1, (512ull << 20) / std::max<uint64_t>(per_row, 1));
+    const uint32_t forced = (uint32_t)std::strtoul(std::getenv("OPENR_SPF_SLICE_ROWS") ? std::getenv("OPENR_SPF_SLICE_ROWS") : "0", nullptr, 10);
+    const uint32_t rows = (uint32_t)std::min<uint64_t>(std::max(a.n, 1u), forced ? forced : budget_rows);
+    hipError_t err = d.slicetmp.reserve((size_t)rows * a.nsl * d.g.V);
     if (err != hipSuccess) return err;
     a.slice_tmp = d.slicetmp.p;
+    a.krows = rows;
   }
   // reach pass scratch (spf_bfs_lvl.hip: dist-level rows of a whole batch, then next hops
   // from neighbour rows); only for batches that can hold every source's neighbours
@@ -494,9 +550,10 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   a.mscnt = nullptr;
   a.xsrc = a.xcount = a.xslot = a.xdup = nullptr;
   if (fam == kFamLvl && !a.tight && !a.ign_ptr && !a.out_row && __builtin_popcount(mask) == 1 &&
-      (a.n >= d.g.V || ms_tile_ok(d.g) || std::getenv("OPENR_SPF_BFS_REACH") || std::getenv("OPENR_SPF_BFS_MSBFS"))) {
-    // a partial batch on the tile-active pass is extended with halo rows (ms_ext_rows)
-    const bool ext = a.n < d.g.V && ms_tile_ok(d.g) && d.g.crank;
+      (a.n >= d.g.V || allsrc_ext_ok(d.g) || std::getenv("OPENR_SPF_BFS_REACH") ||
+       std::getenv("OPENR_SPF_BFS_MSBFS"))) {
+    // a partial batch on the tile-active or wave-reach pass is extended with halo rows (ms_ext_rows)
+    const bool ext = a.n < d.g.V && allsrc_ext_ok(d.g);
     const uint32_t rows = ext ? ms_ext_rows(d.g, a.n) : a.n;
     hipError_t err = d.lvl8.reserve((size_t)rows * reach_row_bytes(d.g.V));
     if (err == hipSuccess) err = d.rowok.reserve(rows);
@@ -964,7 +1021,8 @@ int openr_spf_create(const int* device_ids, int n_devices, openr_spf_ctx** out) 
     hipDeviceProp_t prop;
     if (hipSetDevice(id) != hipSuccess || hipGetDeviceProperties(&prop, id) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&d.ev_begin) != hipSuccess || hipEventCreate(&d.ev_end) != hipSuccess) {
+        hipEventCreate(&d.ev_begin) != hipSuccess || hipEventCreate(&d.ev_end) != hipSuccess ||
+        hipEventCreateWithFlags(&d.patch_ev, hipEventDisableTiming) != hipSuccess) {
       openr_spf_destroy(ctx);
       return fail(OPENR_SPF_ENODEV, "failed to initialise HIP device %d", id);
     }
@@ -1016,6 +1074,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.alist2.release();
     d.asrc2.release();
     d.acount.release();
+    if (d.hrecs) (void)hipHostFree(d.hrecs);
+    if (d.patch_ev) (void)hipEventDestroy(d.patch_ev);
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -1033,6 +1093,10 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   if (gr->row_ptr[0] != 0 || gr->row_ptr[V] != E) return fail(OPENR_SPF_EINVAL, "row_ptr must span [0, E]");
   for (uint32_t u = 0; u < V; ++u)
     if (gr->row_ptr[u + 1] < gr->row_ptr[u]) return fail(OPENR_SPF_EINVAL, "row_ptr not monotone at %u", u);
+  for (Device& d : ctx->devs) {  // a patch's scatter kernel may still read the old graph arrays
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(hipEventSynchronize(d.patch_ev));
+  }
 
   std::vector<uint32_t> adj(E), w(E), win(E), rev(E), lid(E), owner(E);
   std::vector<uint16_t> nbr(E);
@@ -1271,7 +1335,15 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->erec = std::move(erec);
   ctx->ellt = std::move(ellt);
   ctx->delta.clear();
+  ctx->delta_index.clear();
   ctx->delta_valid = false;
+  ctx->wcount.clear();
+  ctx->n_bad_metric = 0;
+  for (uint32_t e = 0; e < E; ++e) ctx->count_metric(e, +1);
+  ctx->seen_e.assign(E, 0);
+  ctx->dirty_e.assign(E, 0);
+  ctx->dirty_v.assign(V, 0);
+  ctx->patch_epoch = 0;
   ctx->has_graph = true;
   return OPENR_SPF_OK;
 }
@@ -1291,12 +1363,20 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
   for (uint32_t i = 0; i < p->n_nodes; ++i)
     if (p->node_ids[i] >= V) return fail(OPENR_SPF_EINVAL, "node id %u out of range (V=%u)", p->node_ids[i], V);
 
+  // per-patch marks: stamps of this patch (epoch wrap: clear the arrays once)
+  if (++ctx->patch_epoch == 0) {
+    std::fill(ctx->seen_e.begin(), ctx->seen_e.end(), 0u);
+    std::fill(ctx->dirty_e.begin(), ctx->dirty_e.end(), 0u);
+    std::fill(ctx->dirty_v.begin(), ctx->dirty_v.end(), 0u);
+    ctx->patch_epoch = 1;
+  }
+  const uint32_t ep = ctx->patch_epoch;
+
   // 1) every directed edge whose (usable, weight, tail overload) may change, old state
   std::vector<uint32_t> cand;
-  std::vector<uint8_t> seen(E, 0);
   auto add = [&](uint32_t e) {
-    if (!seen[e]) {
-      seen[e] = 1;
+    if (ctx->seen_e[e] != ep) {
+      ctx->seen_e[e] = ep;
       cand.push_back(e);
     }
   };
@@ -1312,38 +1392,58 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     return ((ctx->adj[e] & kEdgeDown) ? 0u : 1u) | (ctx->ovl[ctx->owner[e]] ? 2u : 0u);
   };
   std::vector<uint32_t> w0(cand.size()), f0(cand.size());
-  for (size_t k = 0; k < cand.size(); ++k) f0[k] = state(cand[k], &w0[k]);
+  for (size_t k = 0; k < cand.size(); ++k) {
+    f0[k] = state(cand[k], &w0[k]);
+    ctx->count_metric(cand[k], -1);  // re-counted with its new state below
+  }
 
   // 2) apply to the host attributes; collect dirty device elements
-  std::vector<uint8_t> dirty_e(E, 0), dirty_v(V, 0);
+  std::vector<uint32_t> de_list, dv_list;
+  auto dirty_edge = [&](uint32_t e) {
+    if (ctx->dirty_e[e] != ep) {
+      ctx->dirty_e[e] = ep;
+      de_list.push_back(e);
+    }
+  };
+  auto dirty_node = [&](uint32_t u) {
+    if (ctx->dirty_v[u] != ep) {
+      ctx->dirty_v[u] = ep;
+      dv_list.push_back(u);
+    }
+  };
   for (uint32_t i = 0; i < p->n_edges; ++i) {  // Link::setMetricFromNode (LinkState.cpp:195-204)
     const uint32_t e = p->edge_ids[i];
     ctx->metric[e] = p->metric[i];
     ctx->w[e] = (uint32_t)std::min<uint64_t>(p->metric[i], 0xFFFFFFFFull);
     ctx->win[ctx->rev[e]] = ctx->w[e];
-    dirty_e[e] = dirty_e[ctx->rev[e]] = 1;
+    dirty_edge(e);
+    dirty_edge(ctx->rev[e]);
   }
   for (uint32_t i = 0; i < p->n_links; ++i) {  // Link::isUp (LinkState.cpp:233-236), per link
     const uint2 ab = ctx->ledge[p->link_ids[i]];
     for (uint32_t e : {ab.x, ab.y}) {
       ctx->edge_up[e] = p->link_up[i] ? 1 : 0;
       ctx->adj[e] = ctx->col[e] | (p->link_up[i] ? 0u : kEdgeDown);
-      dirty_e[e] = 1;
-      dirty_v[ctx->owner[e]] = 1;  // ellt
+      dirty_edge(e);
+      dirty_node(ctx->owner[e]);  // ellt
     }
   }
   for (uint32_t i = 0; i < p->n_nodes; ++i) {  // LinkState::updateNodeOverloaded / isNodeOverloaded
     const uint32_t x = p->node_ids[i];
     ctx->ovl[x] = p->node_overloaded[i] ? 1 : 0;
-    dirty_v[x] = 1;
-    for (uint32_t e = ctx->row_ptr[x]; e < ctx->row_ptr[x + 1]; ++e) dirty_e[ctx->rev[e]] = 1;  // erec sink flag
+    dirty_node(x);
+    for (uint32_t e = ctx->row_ptr[x]; e < ctx->row_ptr[x + 1]; ++e) dirty_edge(ctx->rev[e]);  // erec sink flag
   }
+  for (uint32_t e : cand) ctx->count_metric(e, +1);
+  // records in element order (as a full scan would emit them)
+  std::sort(de_list.begin(), de_list.end());
+  std::sort(dv_list.begin(), dv_list.end());
 
   // 3) recompute the dirty device elements exactly as set_graph derives them
   std::vector<PatchRec> recs;
+  recs.reserve(5 * de_list.size() + 6 * dv_list.size());
   auto rec = [&](uint32_t arr, uint32_t idx, uint4 val) { recs.push_back(PatchRec{arr, idx, 0u, 0u, val}); };
-  for (uint32_t e = 0; e < E; ++e) {
-    if (!dirty_e[e]) continue;
+  for (uint32_t e : de_list) {
     ctx->erec[e] = make_uint4(ctx->adj[e] | (ctx->ovl[ctx->col[e]] ? kNodeSink : 0u), ctx->win[e], ctx->lid[e],
                               ctx->rev[e]);
     rec(kPatchAdj, e, make_uint4(ctx->adj[e], 0, 0, 0));
@@ -1352,9 +1452,8 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     rec(kPatchWin, e, make_uint4(ctx->win[e], 0, 0, 0));
     rec(kPatchErec, e, ctx->erec[e]);
   }
-  std::vector<uint8_t> dirty_bits((V + 31) / 32 + 1, 0);
-  for (uint32_t u = 0; u < V; ++u) {
-    if (!dirty_v[u]) continue;
+  uint32_t last_word = UINT32_MAX;
+  for (uint32_t u : dv_list) {
     const uint32_t rb = ctx->row_ptr[u], re = ctx->row_ptr[u + 1];
     uint32_t x4[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
     if (!ctx->ovl[u])
@@ -1365,29 +1464,26 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     ctx->row2t[u] = ctx->ovl[u] ? make_uint2(rb | kNodeSink, rb) : make_uint2(rb, re);
     if (ctx->ovl[u]) ctx->ovl_bits[u >> 5] |= 1u << (u & 31u);
     else ctx->ovl_bits[u >> 5] &= ~(1u << (u & 31u));
-    dirty_bits[u >> 5] = 1;
     rec(kPatchEllt, u, ctx->ellt[u]);
     rec(kPatchEllv, u, ellv_of(ctx->ellt[u], V));
     rec(kPatchElld, u, make_uint4(elld_of(ellv_of(ctx->ellt[u], V), u, V), 0, 0, 0));
     rec(kPatchRow2t, u, make_uint4(ctx->row2t[u].x, ctx->row2t[u].y, 0, 0));
     rec(kPatchOvl, u, make_uint4(ctx->ovl[u], 0, 0, 0));
   }
-  for (uint32_t k = 0; k < dirty_bits.size(); ++k)
-    if (dirty_bits[k]) rec(kPatchOvlBits, k, make_uint4(ctx->ovl_bits[k], 0, 0, 0));
-
-  // 4) graph-wide metric facts (kernel choice / ENOTSUP) over the usable edges
-  uint32_t w_min = UINT32_MAX, w_max = 0;
-  bool metric_ok = true;
-  for (uint32_t e = 0; e < E; ++e) {
-    if (ctx->adj[e] & kEdgeDown) continue;
-    const uint64_t m = ctx->metric[e];
-    if (m == 0 || m > 0x7FFFFFFFull) metric_ok = false;
-    else {
-      w_min = std::min<uint32_t>(w_min, (uint32_t)m);
-      w_max = std::max<uint32_t>(w_max, (uint32_t)m);
-    }
+  for (uint32_t u : dv_list) {  // sorted: each touched overload word once, after its bits
+    if ((u >> 5) == last_word) continue;
+    last_word = u >> 5;
+    rec(kPatchOvlBits, last_word, make_uint4(ctx->ovl_bits[last_word], 0, 0, 0));
   }
-  if (w_min == UINT32_MAX) w_min = w_max = 1;
+
+  // 4) graph-wide metric facts (kernel choice / ENOTSUP) over the usable edges, from the
+  //    metric multiset kept current above
+  const bool metric_ok = ctx->n_bad_metric == 0;
+  uint32_t w_min = 1, w_max = 1;  // no usable edge
+  if (!ctx->wcount.empty()) {
+    w_min = ctx->wcount.begin()->first;
+    w_max = ctx->wcount.rbegin()->first;
+  }
 
   // 5) the delta edges of this patch (openr_spf_refresh). Patches with no refresh in
   //    between accumulate: an edge keeps its state from before the first of them, so rows
@@ -1433,14 +1529,25 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     for (size_t k = 0; k < o; ++k) ctx->delta_index.emplace(ctx->delta[k].pad0, (uint32_t)k);
   }
 
-  // 6) upload: one record list + one scatter kernel per replica
+  // 6) upload: one record list + one scatter kernel per replica, on the context's stream
+  //    (host forms run there: ordered); device forms on another stream wait for patch_ev
   for (Device& d : ctx->devs) {
     HIP_TRY(hipSetDevice(d.ordinal));
     if (recs.empty()) continue;
+    HIP_TRY(hipEventSynchronize(d.patch_ev));  // the previous patch's copy has read the staging
+    if (d.hrecs_cap < recs.size()) {
+      if (d.hrecs) HIP_TRY(hipHostFree(d.hrecs));
+      d.hrecs = nullptr;
+      d.hrecs_cap = 0;
+      const size_t cap = std::max<size_t>(recs.size(), 4096);
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.hrecs), cap * sizeof(PatchRec), hipHostMallocDefault));
+      d.hrecs_cap = cap;
+    }
+    std::memcpy(d.hrecs, recs.data(), recs.size() * sizeof(PatchRec));
     HIP_TRY(d.precs.reserve(recs.size()));
-    HIP_TRY(hipMemcpyAsync(d.precs.p, recs.data(), recs.size() * sizeof(PatchRec), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.precs.p, d.hrecs, recs.size() * sizeof(PatchRec), hipMemcpyHostToDevice, d.stream));
     HIP_TRY(launch_patch_apply(d.g, d.precs.p, (uint32_t)recs.size(), d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));  // recs is host memory of this call
+    HIP_TRY(hipEventRecord(d.patch_ev, d.stream));
   }
   ctx->w_min = w_min;
   ctx->w_max = w_max;
@@ -1466,6 +1573,7 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   const uint32_t nd = (uint32_t)ctx->delta.size();
   uint32_t count = 0;
   if (ctx->delta_all && n) {
@@ -1648,6 +1756,7 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   HIP_TRY(reserve_counters(d));
   a.work = d.work.p;
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;
   ctx->stats.batches += 1;
@@ -1713,6 +1822,7 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   uint32_t solved = 0;
   HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_sources, d_changed, s, &solved,
                            (flags & OPENR_SPF_USE_LINK_METRIC) != 0));
@@ -1794,6 +1904,7 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   bool overflow = false;
   HIP_TRY(ksp2_on_device(ctx, d, bp, ip, d_sources, n_sources, d_pair_row, d_pair_dst, n_pairs, tok_cap, d_tok1,
                          d_tok2, s, &overflow));

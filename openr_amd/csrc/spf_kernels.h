@@ -138,9 +138,12 @@ struct SolveArgs {
   const uint32_t* out_row;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
   uint32_t* order;            // nullable [n][V]: pop index per node (exact-order kernel only)
-  // code-family sliced class with next-hop output: [n][nsl][V] 29-bit chunks of the sets
-  // (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
+  // code-family sliced class with next-hop output: [krows][nsl][V] 29-bit chunks of the
+  // sets (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
   uint32_t* slice_tmp;
+  // sliced class with next-hop output, chunked: this launch solves the class-local solves
+  // [k0, k0 + krows) and slice_tmp holds krows of them (row k - k0); krows 0 = the whole class
+  uint32_t k0, krows;
   // reach pass + next hops from neighbour level rows (spf_bfs_lvl.hip, all-sources batches
   // on ELL-only graphs), all nullable (then the pass is not used): u8 level rows
   // [n][reach_row_bytes(V)] (0xFF = unreached), node -> batch row map [V] (UINT32_MAX =
@@ -339,9 +342,16 @@ uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 // the source's neighbours. Rows it cannot finish are appended to a.ovf_list (count in
 // blk[4]) for the caller's u16 full-order re-run. `half` = the reach pass's queue half.
 int allsrc_pass(const DevGraph& g, const SolveArgs& a);
+uint32_t allsrc_qhalf(const DevGraph& g);  // queue half of the per-source passes (1, 3)
 // the tile-active multi-source pass serves g; rows of its extended batch of n sources (halo)
 bool ms_tile_ok(const DevGraph& g);
 uint32_t ms_ext_rows(const DevGraph& g, uint32_t n);
+// a partial all-sources batch on g is extended with halo rows (tile-active or wave-reach pass)
+bool allsrc_ext_ok(const DevGraph& g);
+// wave-reach pass (spf_wreach.hip, pass 3): LDS bytes for queue half qhalf (0: does not apply)
+uint32_t wreach_lds_bytes(const DevGraph& g, uint32_t qhalf);
+hipError_t launch_wreach(const DevGraph& g, const SolveArgs& a, uint32_t qhalf, uint32_t* blk, int num_cus,
+                         hipStream_t s, LaunchInfo* info);
 hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t half, uint32_t* blk,
                          int num_cus, hipStream_t s, LaunchInfo* info);
 uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);

@@ -98,16 +98,21 @@ def test_config2_fabric5000_all_sources(eng, faithful):
 
 def test_config3_grid100_all_sources(eng):
     """100x100 grid, all 10 000 sources in ONE launch (the benchmarked configuration:
-    bench.py solves them in one call, which runs the tile-active multi-source pass
-    msbfs_tile_kernel and the next-hop pass nh_from_levels_kernel), every row against the
-    oracle; plus pathLinks of a source sample."""
+    bench.py solves them in one call, which runs the default all-sources pass
+    CONFIG3_KERNEL), every row against the oracle; plus pathLinks of a source sample."""
     g = T.grid_fast(100)
-    all_sources_vs_oracle(eng, g, 10000, expect_kernel="msbfs_tile_kernel")
+    all_sources_vs_oracle(eng, g, 10000, expect_kernel=CONFIG3_KERNEL)
     pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
 
 
+# the pass a full G100 batch takes by default (spf_allsrc.hip: allsrc_pass)
+CONFIG3_KERNEL = "bfs_ell_kernel"
+
+
 @pytest.mark.parametrize("chunk,env,kernel", [
-    (10000, {"OPENR_SPF_MSBFS_TILE": "0"}, "msbfs_kernel"),
+    (10000, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
+    (10000, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
+    (10000, {"OPENR_SPF_BFS_MSBFS": "1", "OPENR_SPF_MSBFS_TILE": "0"}, "msbfs_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0"}, "bfs_ell_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0", "OPENR_SPF_BFS_WAVE": "1"}, "bfs_wave_kernel"),
@@ -115,8 +120,9 @@ def test_config3_grid100_all_sources(eng):
     (1250, {"OPENR_SPF_BFS_WAVE": "0"}, "bfs_ell_kernel"),
     (1250, {"OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
     (1250, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
-], ids=["full-batch-msbfs-dense", "full-batch-reach", "full-batch-lean", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
-        "shard1250-msbfs"])
+    (1250, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
+], ids=["full-batch-wreach", "full-batch-msbfs-tile", "full-batch-msbfs-dense", "full-batch-reach", "full-batch-lean", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
+        "shard1250-msbfs", "shard1250-wreach"])
 def test_config3_grid100_pass_variants(eng, monkeypatch, chunk, env, kernel):
     """Config 3's other launch shapes, every row against the oracle: the full batch on the
     reach pass and the round-2 lean and wave passes, and the 1 250-source shards of an

@@ -158,6 +158,19 @@ def test_fabric_small_all_sources(eng, faithful):
     check_against_oracle(eng, g, list(range(0, g.num_nodes, 37)), True, check_pathlinks=True)
 
 
+@pytest.mark.parametrize("rows", ["1", "7"])
+def test_sliced_class_in_chunks(eng, monkeypatch, rows):
+    """The code family's sliced class (degree-84 SSWs / FSWs) run in chunks of a few solves
+    with one chunk's slice scratch (OPENR_SPF_SLICE_ROWS forces the chunk size the launcher
+    otherwise derives from its 512 MiB budget): every row as the oracle's, with
+    duplicate sliced sources and a partial last chunk."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "code")
+    monkeypatch.setenv("OPENR_SPF_SLICE_ROWS", rows)
+    g = T.fabric(288 + 3 * 56)
+    srcs = list(range(g.num_nodes)) + list(range(0, 60, 3))
+    check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
+
+
 def test_fabric_5000_sample(eng):
     g = T.fabric(5000)
     assert g.num_nodes == 4992 and g.num_links == 56448

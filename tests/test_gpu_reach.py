@@ -29,15 +29,19 @@ def eng():
     e.close()
 
 
-PASS_KERNEL = {"msbfs": "msbfs_tile_kernel", "msbfs_dense": "msbfs_kernel", "reach": "bfs_reach_kernel"}
+PASS_KERNEL = {"wreach": "bfs_wreach_kernel", "msbfs": "msbfs_tile_kernel", "msbfs_dense": "msbfs_kernel",
+               "reach": "bfs_reach_kernel"}
 
 
-@pytest.fixture(autouse=True, params=["msbfs", "msbfs_dense", "reach"])
+@pytest.fixture(autouse=True, params=["wreach", "msbfs", "msbfs_dense", "reach"])
 def level_pass(request, monkeypatch):
-    """Every test runs on every level pass (forced: also on batches smaller than V):
-    the tile-active multi-source BFS, the dense-pull one and the per-source reach pass."""
+    """Every test runs on every level pass (forced: also on batches smaller than V): the
+    wave-reach pass (one wavefront per source, graph in LDS; partial batches extended with
+    halo rows), the tile-active multi-source BFS, the dense-pull one and the per-source
+    reach pass."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
-    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "0" if request.param == "reach" else "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_WREACH", "1" if request.param == "wreach" else "0")
+    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "0" if request.param in ("reach", "wreach") else "1")
     monkeypatch.setenv("OPENR_SPF_MSBFS_TILE", "0" if request.param == "msbfs_dense" else "1")
     monkeypatch.setenv("OPENR_SPF_BFS_REACH", "1")
     return request.param
@@ -139,21 +143,21 @@ def test_depth_overflow_rerun(eng):
 def test_queue_half_overflow_rerun(eng, monkeypatch, level_pass):
     """A forced 16-entry queue half (reach pass): wide levels overflow it, those solves and
     their neighbours' next-hop rows go to the re-run."""
-    if level_pass != "reach":
-        pytest.skip("the reach pass's queue")
+    if level_pass not in ("reach", "wreach"):
+        pytest.skip("the per-source passes' queues")
     monkeypatch.setenv("OPENR_SPF_REACH_QHALF", "16")
     g = T.grid_fast(24)
     check_batch(eng, g, range(g.num_nodes))
 
 
-def test_partial_batches_missing_neighbours(eng, monkeypatch):
+def test_partial_batches_missing_neighbours(eng, monkeypatch, level_pass):
     """Forced onto batches that do not hold every neighbour (a strong-scaling shard, a
     strided sample, duplicates, sources in random order): sources with a missing
     neighbour row are re-run, the others use the derivation."""
     monkeypatch.setenv("OPENR_SPF_BFS_REACH", "1")
     g = T.grid_fast(30)
     V = g.num_nodes
-    check_batch(eng, g, range(100, 250))
+    check_batch(eng, g, range(100, 250), kernel=PASS_KERNEL[level_pass])
     check_batch(eng, g, range(0, V, 3))
     rng = np.random.default_rng(1)
     perm = rng.permutation(V)
@@ -166,13 +170,13 @@ def test_wider_nh_stride_zero_padded(eng):
     check_batch(eng, g, range(g.num_nodes), nh_bytes=3)
 
 
-def test_grid100_full_batch_is_msbfs(eng, monkeypatch, level_pass):
-    """All 10 000 G100 sources in one call with the multi-source pass in auto mode run
-    it; a sample of rows vs the oracle
-    (test_gpu_configs.py checks every row)."""
+def test_grid100_full_batch(eng, monkeypatch, level_pass):
+    """All 10 000 G100 sources in one call with the pass in auto mode run it; a sample of
+    rows vs the oracle (test_gpu_configs.py checks every row)."""
     if level_pass == "reach":
-        pytest.skip("multi-source passes")
-    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "2")
+        pytest.skip("the reach pass has no auto mode for full batches")
+    monkeypatch.setenv("OPENR_SPF_BFS_WREACH", "2" if level_pass == "wreach" else "0")
+    monkeypatch.setenv("OPENR_SPF_BFS_MSBFS", "0" if level_pass == "wreach" else "2")
     monkeypatch.delenv("OPENR_SPF_BFS_REACH")
     g = T.grid_fast(100)
     eng.set_graph(g)
