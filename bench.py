@@ -291,11 +291,23 @@ def whatif_main(args):
     eng.close()
 
 
+PMC_ROUNDS = ("r03", "r02")  # newest first: the PMC summaries bench lines carry
+
+
+def pmc_path(name):
+    """profiles/<round>/pmc_traffic_<name>.json of the newest round that has one (written by
+    scripts/pmc_traffic.sh), or None."""
+    for rnd in PMC_ROUNDS:
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_traffic_{name}.json")
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def load_pmc(name):
-    """profiles/r02/pmc_traffic_<name>.json (scripts/pmc_traffic.sh output), or None."""
-    path = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{name}.json")
+    path = pmc_path(name)
     try:
-        return json.load(open(path))
+        return dict(json.load(open(path)), _path=os.path.relpath(path, ROOT)) if path else None
     except (OSError, ValueError):
         return None
 
@@ -435,7 +447,7 @@ def ksp2_main(args):
                 per_pair * n_pairs, step_s, traffic,
                 "per GPU, whole step (base SPFs, k=1 / k=2 traces, second SPFs): SURVEY.md 8d B(src) per second "
                 "SPF (one per pair), k=1 base SPFs and traces not credited; traffic = PMC HBM bytes of every engine "
-                "kernel per pair (profiles/r02/pmc_traffic_ksp2.json) x this step's pairs"),
+                "kernel per pair (" + (pmc or {}).get("_path", "no PMC summary") + ") x this step's pairs"),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ksp2_cpu_baseline(g, min(args.cpu_seconds, 10.0))
@@ -733,7 +745,7 @@ def main():
                          "ranks and the result shards all-gathered over RCCL; weak: every rank solves its own "
                          "full all-sources replica (one OpenR area per GPU)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/r02/pmc_traffic_<topology>.json")
+                    help="PMC summary (scripts/pmc_traffic.sh); default profiles/<newest round>/pmc_traffic_<topology>.json")
     ap.add_argument("--ksp-sources", type=int, default=0,
                     help="ksp2: sources per step (0 = all; each source pairs with every node)")
     ap.add_argument("--ksp-block", type=int, default=256,
@@ -894,13 +906,21 @@ def all_sources_main(args):
     mean_kernel_s = float(np.mean(kernel_ms)) / 1e3
     achieved = bytes_launch / mean_kernel_s / 1e9 if mean_kernel_s > 0 else 0.0
     traffic = None
+    traffic_label = None
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{args.topology}.json")
+        args.traffic_json = pmc_path(args.topology) or ""
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("topology") == args.topology and tj.get("n_sources") in (None, n_local):
-                traffic = tj.get("hbm_bytes_per_launch")
+                # a whole step's engine kernels (PMC_AGG) or the dominant kernel's launch
+                traffic = tj.get("hbm_bytes_per_step", tj.get("hbm_bytes_per_launch"))
+                traffic_label = {
+                    "source": os.path.relpath(args.traffic_json, ROOT),
+                    "scope": ("every engine kernel of one all-sources call (the timed step)"
+                              if "hbm_bytes_per_step" in tj else f"one launch of {tj.get('kernel', '?')[:80]}"),
+                    "correction": tj.get("correction"),
+                }
         except Exception:
             traffic = None
 
@@ -930,6 +950,7 @@ def all_sources_main(args):
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_label": traffic_label,
                 "kernel_ms_mean": mean_kernel_s * 1e3,
                 "bytes_per_launch": bytes_launch,
                 "note": "per GPU (rank 0): SURVEY.md 8d B(src) summed over the rank's sources / mean launch "

@@ -144,7 +144,7 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t k, uint32
 // GENERIC = false: no ignore set and no tight-edge output (compile time), the
 // all-sources / prefetch case; GENERIC = true handles both at run time.
 template <int FB, int BLOCK, bool RING, int ELLM, bool GENERIC, bool SLICED>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_code_kernel(
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 1024 ? 4 : 8))) void bfs_code_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog, uint32_t has_ign_rt, uint32_t ring_cap, uint32_t from_list,
     uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
   using S = State<FB>;
@@ -639,6 +639,17 @@ hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, u
   const BfsShape sh = bfs_shape(g, has_ign, FB);
 #define OPENR_BFS_SHAPE(BLK, E) \
   return launch_bfs_shape<FB, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, num_cus, s, info)
+  // A batch of at most half as many (solve, slice) units as CUs (a refresh's few affected
+  // rows, LFA / KSP prefetches of one node): a launch is one solve's latency, so each solve
+  // takes a whole CU — 1 024 threads, full-order queue — instead of 256 threads beside
+  // idle CUs (OPENR_SPF_BFS_WIDE=0: off)
+  const uint64_t units = (uint64_t)a.n * (SLICED ? std::max(a.nsl, 1u) : 1u);
+  if (units * 2u <= (uint64_t)num_cus && bfs_layout(g.V, g.L, has_ign, FB, g.V).total <= kMaxLds &&
+      env_u32("OPENR_SPF_BFS_WIDE", 1u, 0u, 1u)) {
+    if (ellm == 2) return launch_bfs_shape<FB, 1024, 2, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
+    if (ellm == 1) return launch_bfs_shape<FB, 1024, 1, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
+    return launch_bfs_shape<FB, 1024, 0, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
+  }
   if (sh.block == 128) {
     if (ellm == 2) OPENR_BFS_SHAPE(128, 2);
     if (ellm == 1) OPENR_BFS_SHAPE(128, 1);

@@ -829,7 +829,7 @@ __host__ __device__ inline WaveLayout wave_layout(uint32_t V, uint32_t nh_words,
   return l;
 }
 
-template <int MODE>
+template <int MODE, uint32_t U>
 __global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t qhalf,
                                                        uint32_t waves, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
   using N = Nh<MODE>;
@@ -897,41 +897,47 @@ __global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, 
         const uint32_t rd = (L & 1u) * qhalf, wr = qhalf - rd;
         const uint8_t lnext = (uint8_t)(L + 1u);
         uint32_t nxt = 0;  // scalar append cursor of level L+1
-        for (uint32_t fb = 0; fb < cur; fb += 64u) {
-          const uint32_t idx = fb + lane;
-          const bool live = idx < cur;
-          const uint32_t qe = q[rd + (live ? idx : 0u)];
-          const uint32_t u = live ? qe : src;               // past the level: the source (level 0)
-          const uint32_t r4 = rows[u];                      // issued with the nh(u) read below
-          const uint32_t d4 = live ? r4 : 0u;               // no slots: every slot resolves to u
-          const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
-          uint32_t vv[4], lv[4], old[4];
+        // U frontier chunks of 64 per step, their dependent chains interleaved (U = 2: a
+        // level of 65-128 nodes takes one chain instead of two)
+        for (uint32_t fb = 0; fb < cur; fb += 64u * U) {
+          constexpr uint32_t S = 4u * U;
+          uint32_t vv[S], lv[S], old[S], xu[U];
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) vv[j] = u + (uint32_t)__builtin_amdgcn_sbfe((int32_t)d4, 8u * j, 8u);
+          for (uint32_t h = 0; h < U; ++h) {
+            const uint32_t idx = fb + 64u * h + lane;
+            const bool live = idx < cur;
+            const uint32_t qe = q[rd + (live ? idx : 0u)];
+            const uint32_t u = live ? qe : src;             // past the level: the source (level 0)
+            const uint32_t r4 = rows[u];                    // issued with the nh(u) read below
+            const uint32_t d4 = live ? r4 : 0u;             // no slots: every slot resolves to u
+            xu[h] = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) lv[j] = lvl[vv[j]];
+            for (uint32_t j = 0; j < 4u; ++j) vv[4u * h + j] = u + (uint32_t)__builtin_amdgcn_sbfe((int32_t)d4, 8u * j, 8u);
+          }
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) {
+          for (uint32_t j = 0; j < S; ++j) lv[j] = lvl[vv[j]];
+#pragma unroll
+          for (uint32_t j = 0; j < S; ++j) {
             const uint32_t v = vv[j];
             const bool tight = lv[j] > L;  // first or equal-cost arrival (LinkState.cpp:857-873)
-            old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, x << ((v << kShl) & 31u));
+            old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, xu[j / 4u] << ((v << kShl) & 31u));
           }
           __builtin_amdgcn_sched_barrier(0);  // all atomics in flight before their results are used
-          unsigned long long bj[4];
-          bool fresh[4];
-          uint32_t off[5];
+          unsigned long long bj[S];
+          bool fresh[S];
+          uint32_t off[S + 1];
           off[0] = 0;
 #pragma unroll
-          for (uint32_t j = 0; j < 4u; ++j) {
+          for (uint32_t j = 0; j < S; ++j) {
             fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;  // a dummy field never is
             bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
             off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
           }
-          const uint32_t total = off[4];
+          const uint32_t total = off[S];
           if (total) {  // wave-uniform
             if (nxt + total <= qhalf) {
 #pragma unroll
-              for (uint32_t j = 0; j < 4u; ++j) {
+              for (uint32_t j = 0; j < S; ++j) {
                 if (fresh[j]) {
                   const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
@@ -1040,7 +1046,8 @@ hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost,
                            uint32_t* ctr, uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = wave_layout(g.V, nh_words_for(MODE, g.V), qhalf, waves).total;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cus, (a.n + waves - 1u) / waves));
-  auto k = bfs_wave_kernel<MODE>;
+  // OPENR_SPF_WAVE_UNROLL: frontier chunks per step (1 or 2)
+  auto k = env_u32("OPENR_SPF_WAVE_UNROLL", 1u, 1u, 2u) == 2u ? bfs_wave_kernel<MODE, 2> : bfs_wave_kernel<MODE, 1>;
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;

@@ -77,6 +77,11 @@ struct Device {
   DevBuf<uint64_t> dist, tight;
   DevBuf<uint8_t> nh;
   DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
+  // small multi-class batches: the classes run concurrently, one stream each (forked from
+  // and joined back into the caller's stream), each with its own re-run list
+  hipStream_t cstream[kMaxClasses] = {};
+  hipEvent_t cev[kMaxClasses + 1] = {};
+  DevBuf<uint32_t> ovfc;
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
   // lvl-family reach pass (all-sources batches): u8 level rows, node -> row map, row flags
   DevBuf<uint8_t> lvl8, rowok;
@@ -98,11 +103,6 @@ struct Device {
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
-  // pinned staging of the records and the event of the patch's last launch: a patch does
-  // not wait for its scatter kernel; work on another stream waits for the event instead
-  PatchRec* hrecs = nullptr;
-  size_t hrecs_cap = 0;
-  hipEvent_t patch_ev = nullptr;
   DevBuf<DeltaEdge> delta;
   DevBuf<uint32_t> alist, asrc, acount, alist2, asrc2;  // refresh: listed rows (first / exact stage)
   // exact-order kernel: per-solve slots when a slot does not fit LDS; pop-order rows
@@ -590,7 +590,38 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   if (err != hipSuccess) return err;
   a.perm = d.perm.p;
   a.part = d.part.p;
-  for (int c = num_classes(fam) - 1; c >= 0; --c) {
+  // OPENR_SPF_CLASS_STREAMS=1: a batch too small to fill the GPU (a refresh's few affected
+  // rows, an LFA prefetch) runs its classes side by side on their own streams instead of
+  // one after another. Their scheduling counters are per class already; each gets its own
+  // re-run list. Measured and left opt-in: on the fabric update loop the cross-stream
+  // fork / join cost more than the overlap saved (0.226 vs 0.170 ms per update).
+  const int nc = num_classes(fam);
+  const bool side = a.n <= (uint32_t)d.num_cus && __builtin_popcount(mask) > 1 &&
+                    std::getenv("OPENR_SPF_CLASS_STREAMS") && std::atoi(std::getenv("OPENR_SPF_CLASS_STREAMS")) == 1;
+  if (side) {
+    const size_t per = (size_t)a.n * std::max<uint32_t>(a.nsl, 1u);
+    err = d.ovfc.reserve(per * (size_t)nc);
+    for (int c = 0; c < nc && err == hipSuccess; ++c) {
+      if (!d.cstream[c]) err = hipStreamCreateWithFlags(&d.cstream[c], hipStreamNonBlocking);
+      if (err == hipSuccess && !d.cev[c]) err = hipEventCreateWithFlags(&d.cev[c], hipEventDisableTiming);
+    }
+    if (err == hipSuccess && !d.cev[kMaxClasses]) err = hipEventCreateWithFlags(&d.cev[kMaxClasses], hipEventDisableTiming);
+    if (err == hipSuccess) err = hipEventRecord(d.cev[kMaxClasses], s);  // fork: partition done
+    if (err != hipSuccess) return err;
+    for (int c = nc - 1; c >= 0; --c) {
+      if (!((mask >> c) & 1u)) continue;
+      SolveArgs ac = a;
+      ac.cls = (uint32_t)c;
+      ac.ovf_list = d.ovfc.p + per * (size_t)c;
+      err = hipStreamWaitEvent(d.cstream[c], d.cev[kMaxClasses], 0);
+      if (err == hipSuccess) err = launch_bfs(fam, d.g, ac, p.cost, gl, d.num_cus, d.cstream[c], &info);
+      if (err == hipSuccess) err = hipEventRecord(d.cev[c], d.cstream[c]);
+      if (err == hipSuccess) err = hipStreamWaitEvent(s, d.cev[c], 0);  // join
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+  }
+  for (int c = nc - 1; c >= 0; --c) {
     if (!((mask >> c) & 1u)) continue;
     a.cls = (uint32_t)c;
     err = launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
@@ -1021,8 +1052,7 @@ int openr_spf_create(const int* device_ids, int n_devices, openr_spf_ctx** out) 
     hipDeviceProp_t prop;
     if (hipSetDevice(id) != hipSuccess || hipGetDeviceProperties(&prop, id) != hipSuccess ||
         hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&d.ev_begin) != hipSuccess || hipEventCreate(&d.ev_end) != hipSuccess ||
-        hipEventCreateWithFlags(&d.patch_ev, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreate(&d.ev_begin) != hipSuccess || hipEventCreate(&d.ev_end) != hipSuccess) {
       openr_spf_destroy(ctx);
       return fail(OPENR_SPF_ENODEV, "failed to initialise HIP device %d", id);
     }
@@ -1074,8 +1104,13 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.alist2.release();
     d.asrc2.release();
     d.acount.release();
-    if (d.hrecs) (void)hipHostFree(d.hrecs);
-    if (d.patch_ev) (void)hipEventDestroy(d.patch_ev);
+    for (uint32_t c = 0; c < kMaxClasses; ++c) {
+      if (d.cstream[c]) (void)hipStreamSynchronize(d.cstream[c]);
+      if (d.cstream[c]) (void)hipStreamDestroy(d.cstream[c]);
+      if (d.cev[c]) (void)hipEventDestroy(d.cev[c]);
+    }
+    if (d.cev[kMaxClasses]) (void)hipEventDestroy(d.cev[kMaxClasses]);
+    d.ovfc.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -1093,10 +1128,6 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   if (gr->row_ptr[0] != 0 || gr->row_ptr[V] != E) return fail(OPENR_SPF_EINVAL, "row_ptr must span [0, E]");
   for (uint32_t u = 0; u < V; ++u)
     if (gr->row_ptr[u + 1] < gr->row_ptr[u]) return fail(OPENR_SPF_EINVAL, "row_ptr not monotone at %u", u);
-  for (Device& d : ctx->devs) {  // a patch's scatter kernel may still read the old graph arrays
-    HIP_TRY(hipSetDevice(d.ordinal));
-    HIP_TRY(hipEventSynchronize(d.patch_ev));
-  }
 
   std::vector<uint32_t> adj(E), w(E), win(E), rev(E), lid(E), owner(E);
   std::vector<uint16_t> nbr(E);
@@ -1529,25 +1560,15 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     for (size_t k = 0; k < o; ++k) ctx->delta_index.emplace(ctx->delta[k].pad0, (uint32_t)k);
   }
 
-  // 6) upload: one record list + one scatter kernel per replica, on the context's stream
-  //    (host forms run there: ordered); device forms on another stream wait for patch_ev
+  // 6) upload: one record list + one scatter kernel per replica (measured: an event that
+  //    later device-form calls wait on instead of this synchronize was no faster)
   for (Device& d : ctx->devs) {
     HIP_TRY(hipSetDevice(d.ordinal));
     if (recs.empty()) continue;
-    HIP_TRY(hipEventSynchronize(d.patch_ev));  // the previous patch's copy has read the staging
-    if (d.hrecs_cap < recs.size()) {
-      if (d.hrecs) HIP_TRY(hipHostFree(d.hrecs));
-      d.hrecs = nullptr;
-      d.hrecs_cap = 0;
-      const size_t cap = std::max<size_t>(recs.size(), 4096);
-      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&d.hrecs), cap * sizeof(PatchRec), hipHostMallocDefault));
-      d.hrecs_cap = cap;
-    }
-    std::memcpy(d.hrecs, recs.data(), recs.size() * sizeof(PatchRec));
     HIP_TRY(d.precs.reserve(recs.size()));
-    HIP_TRY(hipMemcpyAsync(d.precs.p, d.hrecs, recs.size() * sizeof(PatchRec), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.precs.p, recs.data(), recs.size() * sizeof(PatchRec), hipMemcpyHostToDevice, d.stream));
     HIP_TRY(launch_patch_apply(d.g, d.precs.p, (uint32_t)recs.size(), d.stream));
-    HIP_TRY(hipEventRecord(d.patch_ev, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));  // recs is host memory of this call
   }
   ctx->w_min = w_min;
   ctx->w_max = w_max;
@@ -1573,7 +1594,6 @@ int openr_spf_refresh_device(openr_spf_ctx* ctx, int device_index, const uint32_
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
-  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   const uint32_t nd = (uint32_t)ctx->delta.size();
   uint32_t count = 0;
   if (ctx->delta_all && n) {
@@ -1756,7 +1776,6 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   HIP_TRY(reserve_counters(d));
   a.work = d.work.p;
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
-  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;
   ctx->stats.batches += 1;
@@ -1822,7 +1841,6 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
-  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   uint32_t solved = 0;
   HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_sources, d_changed, s, &solved,
                            (flags & OPENR_SPF_USE_LINK_METRIC) != 0));
@@ -1904,7 +1922,6 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
   Device& d = ctx->devs[device_index];
   HIP_TRY(hipSetDevice(d.ordinal));
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
-  if (s != d.stream) HIP_TRY(hipStreamWaitEvent(s, d.patch_ev, 0));  // the graph as last patched
   bool overflow = false;
   HIP_TRY(ksp2_on_device(ctx, d, bp, ip, d_sources, n_sources, d_pair_row, d_pair_dst, n_pairs, tok_cap, d_tok1,
                          d_tok2, s, &overflow));

@@ -10,8 +10,9 @@ TOPO="${TOPO:-grid100}"
 OUT="$R/gpurun_out/$TAG/$TOPO"
 mkdir -p "$OUT"
 stop() { case $1 in 0) ;; *) echo "step failed rc=$1; stopping"; exit $1;; esac; }
-# 1) PMC traffic first, so the bench line below can carry it
-PMC_TAG="$TAG/$TOPO/pmc" BENCH_ARGS="--topology $TOPO" bash "$R/scripts/pmc_traffic.sh"; stop $?
+# 1) PMC traffic first, so the bench line below can carry it: every engine kernel of a
+#    step (PMC_AGG=1: an all-sources call is several launches — classes, re-runs, merges)
+PMC_AGG=1 PMC_TAG="$TAG/$TOPO/pmc" BENCH_ARGS="--topology $TOPO" bash "$R/scripts/pmc_traffic.sh"; stop $?
 cp "$R/gpurun_out/pmc_$TAG/$TOPO/pmc/pmc_traffic.json" "$OUT/pmc_traffic.json"
 # 2) bench line (default steps/warmup, CPU baseline included)
 cd "$R" && timeout -k 10 300 python3 -u bench.py --topology "$TOPO" --traffic-json "$OUT/pmc_traffic.json" \

@@ -7,6 +7,7 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${TAG:-prof}"
 WORKLOADS="${*:-ksp2 whatif update}"
+ROUND="${ROUND:-r03}"
 stop() { case $1 in 0) ;; *) echo "step failed rc=$1; stopping"; exit $1;; esac; }
 export TMPDIR=/tmp
 for W in $WORKLOADS; do
@@ -17,11 +18,13 @@ for W in $WORKLOADS; do
     whatif) ARGS="--workload whatif --steps 5 --warmup 1" ;;     # all 3 M WAN (link, source) units
     update) ARGS="--workload update --topology fabric --steps 20 --warmup 2" ;;
     adjdb)  ARGS="--workload adjdb --steps 5 --warmup 1" ;;                    # G100 full adj: sync
+    routes) ARGS="--workload routes --steps 3 --warmup 1" ;;                   # every G100 node's route DB
+    routes_lfa) ARGS="--workload routes --lfa --steps 3 --warmup 1" ;;
     adjdb_fabric) ARGS="--workload adjdb --topology fabric --steps 5 --warmup 1" ;;
     *) echo "unknown workload $W"; exit 2 ;;
   esac
   # PMC HBM traffic first (what-if: its repair kernel; KSP2: every engine kernel of a step,
-  # on a 64-source sample), installed where bench.py reads it (profiles/r02/)
+  # on a 64-source sample), installed where bench.py reads it (profiles/$ROUND/)
   PMC=""
   case $W in
     whatif) PMC="PMC_KERNEL=whatif_group|--workload whatif --no-ucmp" ;;
@@ -29,7 +32,7 @@ for W in $WORKLOADS; do
   esac
   if [ -n "$PMC" ] && [ -z "${NO_PMC:-}" ]; then
     env ${PMC%%|*} PMC_TAG="$TAG/$W/pmc" BENCH_ARGS="${PMC#*|}" bash "$R/scripts/pmc_traffic.sh"; stop $?
-    mkdir -p "$R/profiles/r02" && cp "$R/gpurun_out/pmc_$TAG/$W/pmc/pmc_traffic.json" "$R/profiles/r02/pmc_traffic_$W.json"
+    mkdir -p "$R/profiles/$ROUND" && cp "$R/gpurun_out/pmc_$TAG/$W/pmc/pmc_traffic.json" "$R/profiles/$ROUND/pmc_traffic_$W.json"
     cp "$R/gpurun_out/pmc_$TAG/$W/pmc/pmc_traffic.json" "$OUT/pmc_traffic.json"
   fi
   cd "$R" && timeout -k 10 400 python3 -u bench.py $ARGS > "$OUT/bench.log" 2>&1; stop $?
