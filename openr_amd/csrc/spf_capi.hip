@@ -87,6 +87,7 @@ struct Device {
   DevBuf<uint8_t> lvl8, rowok;
   DevBuf<uint32_t> rowmap, msperm, mscnt;
   DevBuf<uint32_t> xsrc, xcount, xslot, xdup;  // extended (halo) batches of the multi-source pass
+  DevBuf<uint16_t> order16;  // 2-bit-code lean pass: per-workgroup BFS order [lean2_max_grid][V]
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -578,6 +579,14 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
       a.xslot = d.xslot.p;
       a.xdup = d.xdup.p;
     }
+  }
+  // 2-bit-code lean pass (spf_bfs_lvl.hip, OPENR_SPF_BFS_LEAN2): its BFS order scratch
+  a.order16 = nullptr;
+  if (fam == kFamLvl && !a.tight && !a.ign_ptr && d.g.V <= 65535u && d.g.max_deg <= 4u &&
+      std::getenv("OPENR_SPF_BFS_LEAN2") && std::atoi(std::getenv("OPENR_SPF_BFS_LEAN2")) == 1) {
+    hipError_t err = d.order16.reserve((size_t)lean2_max_grid(d.num_cus) * d.g.V);
+    if (err != hipSuccess) return err;
+    a.order16 = d.order16.p;
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
@@ -1086,6 +1095,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.xcount.release();
     d.xslot.release();
     d.xdup.release();
+    d.order16.release();
     d.work.release();
     d.perm.release();
     d.part.release();

@@ -163,6 +163,9 @@ struct SolveArgs {
   uint32_t* xcount;
   uint32_t* xslot;
   uint32_t* xdup;
+  // nullable: per-workgroup BFS order scratch [lean2_max_grid][V] of the 2-bit-code lean
+  // pass (bfs_ell2_kernel); the pass is used only when it is set
+  uint16_t* order16;
 };
 // Row stride of SolveArgs::lvl8 (16-byte rows: the next-hop pass reads 16 levels per load)
 __host__ __device__ inline uint32_t reach_row_bytes(uint32_t V) { return (V + 15u) & ~15u; }
@@ -342,7 +345,9 @@ uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 // the source's neighbours. Rows it cannot finish are appended to a.ovf_list (count in
 // blk[4]) for the caller's u16 full-order re-run. `half` = the reach pass's queue half.
 int allsrc_pass(const DevGraph& g, const SolveArgs& a);
-uint32_t allsrc_qhalf(const DevGraph& g);  // queue half of the per-source passes (1, 3)
+uint32_t allsrc_qhalf(const DevGraph& g);
+// workgroups of the 2-bit-code lean pass at most (its order scratch is [this][V] u16)
+inline uint32_t lean2_max_grid(int num_cus) { return 16u * (uint32_t)(num_cus > 0 ? num_cus : 1); }  // queue half of the per-source passes (1, 3)
 // the tile-active multi-source pass serves g; rows of its extended batch of n sources (halo)
 bool ms_tile_ok(const DevGraph& g);
 uint32_t ms_ext_rows(const DevGraph& g, uint32_t n);

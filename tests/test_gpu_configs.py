@@ -111,6 +111,7 @@ CONFIG3_KERNEL = "bfs_ell_kernel"
 
 @pytest.mark.parametrize("chunk,env,kernel", [
     (10000, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
+    (10000, {"OPENR_SPF_BFS_LEAN2": "1"}, "bfs_ell2_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "1", "OPENR_SPF_MSBFS_TILE": "0"}, "msbfs_kernel"),
     (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
@@ -121,7 +122,7 @@ CONFIG3_KERNEL = "bfs_ell_kernel"
     (1250, {"OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
     (1250, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
     (1250, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
-], ids=["full-batch-wreach", "full-batch-msbfs-tile", "full-batch-msbfs-dense", "full-batch-reach", "full-batch-lean", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
+], ids=["full-batch-wreach", "full-batch-lean2", "full-batch-msbfs-tile", "full-batch-msbfs-dense", "full-batch-reach", "full-batch-lean", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
         "shard1250-msbfs", "shard1250-wreach"])
 def test_config3_grid100_pass_variants(eng, monkeypatch, chunk, env, kernel):
     """Config 3's other launch shapes, every row against the oracle: the full batch on the

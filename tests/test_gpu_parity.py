@@ -345,6 +345,45 @@ def test_lean_pass_half_overflow(eng, monkeypatch, capfd, bfs_family):
     assert ("bfs_ell:" in capfd.readouterr().err) == (bfs_family[0] == "lvl")
 
 
+@pytest.mark.parametrize("case", ["grid", "depth", "half", "overload-down", "disconnected"])
+def test_lean2_pass(eng, monkeypatch, case):
+    """The 2-bit-code lean pass (bfs_ell2_kernel: levels as 2-bit codes in LDS, exact
+    levels from a global BFS order scattered back at the write-out), forced on: every
+    row against the oracle, with overloaded nodes and down links, unreached nodes, and
+    both re-run paths (a chain deeper than 253 levels, a forced narrow queue half)."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
+    monkeypatch.setenv("OPENR_SPF_BFS_LEAN2", "1")
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")
+    n = 70
+    names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)]
+    links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
+    links += [(r * n + c, (r + 1) * n + c) for r in range(n - 1) for c in range(n)]
+    ovl = up = None
+    srcs = list(range(0, n * n, 3))
+    if case == "depth":
+        tail = 300
+        names += [f"z{i:03d}" for i in range(tail)]
+        links += [(n * n + i, n * n + i + 1) for i in range(tail - 1)]
+        srcs = [0, n * n - 1, n * n, n * n + tail - 1, n * n + 10, 35 * n + 35] + list(range(0, n * n, 11))
+    if case == "half":
+        monkeypatch.setenv("OPENR_SPF_LEAN_FORCE", "1")
+        monkeypatch.setenv("OPENR_SPF_RING_CAP", "32")
+    if case == "overload-down":
+        rng = np.random.default_rng(5)
+        ovl = (rng.random(n * n) < 0.06).astype(np.uint8)
+        up = (rng.random(len(links)) > 0.06).astype(np.uint8)
+    if case == "disconnected":
+        names += [f"x{i}" for i in range(40)]
+        links += [(n * n + i, n * n + i + 1) for i in range(39)]
+        srcs = srcs + [n * n, n * n + 39]
+    g = T.csr_from_links(names, np.array(links), overloaded=ovl, link_up=up)
+    eng.set_graph(g)
+    dist, _ = check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
+    assert "bfs_ell2_kernel" in eng.last_kernels(), eng.last_kernels()
+    if case == "depth":
+        assert int(dist[2, n * n + 299]) == 299
+
+
 def test_ring_overflow_rerun_list(eng, monkeypatch):
     """A ring too small for the frontier (forced: levels of ~1000 nodes on a random
     expander) flags every solve; the full-order pass re-runs them from the list."""
