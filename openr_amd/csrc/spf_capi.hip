@@ -122,7 +122,7 @@ hipError_t reserve_counters(Device& d) {
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
                    g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld,
-                   g.corder, g.tord, g.tinv, g.tmask, g.crank, g.tlist};
+                   g.corder, g.tord, g.tinv, g.tmask, g.crank, g.tlist, g.erecs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -162,6 +162,7 @@ struct openr_spf_ctx {
   std::vector<uint32_t> adj, w, win, rev, lid, owner, ovl_bits;
   std::vector<uint2> ledge, row2t;
   std::vector<uint4> erec, ellt;
+  std::vector<uint32_t> erec_pos;  // directed edge -> its position in DevGraph::erecs
   // delta edges of the most recent patch (openr_spf_refresh); invalid after set_graph
   std::vector<DeltaEdge> delta;
   bool delta_valid = false;
@@ -1200,6 +1201,21 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   std::vector<uint4> ellt(V), erec(E);
   for (uint32_t e = 0; e < E; ++e)
     erec[e] = make_uint4(adj[e] | (ovl[gr->col[e]] ? kNodeSink : 0u), win[e], lid[e], rev[e]);
+  // rank-sorted copy of every row's in-edge records (KSP tracer, uniform cost)
+  std::vector<uint32_t> erec_pos(E);
+  {
+    std::vector<uint32_t> idx;
+    for (uint32_t u = 0; u < V; ++u) {
+      const uint32_t b = gr->row_ptr[u], e1 = gr->row_ptr[u + 1];
+      idx.resize(e1 - b);
+      for (uint32_t e = b; e < e1; ++e) idx[e - b] = e;
+      std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t rx = gr->name_rank[gr->col[x]], ry = gr->name_rank[gr->col[y]];
+        return rx != ry ? rx < ry : rev[x] < rev[y];
+      });
+      for (uint32_t i = 0; i < idx.size(); ++i) erec_pos[idx[i]] = b + i;
+    }
+  }
   for (uint32_t u = 0; u < V; ++u) {
     uint32_t x[4] = {kEdgeDown, kEdgeDown, kEdgeDown, kEdgeDown};
     if (!ovl[u])
@@ -1295,6 +1311,11 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
       }
     }
     if (err == hipSuccess) err = up(&g.erec, erec.data(), E);
+    if (err == hipSuccess) {
+      std::vector<uint4> erecs(E);
+      for (uint32_t e = 0; e < E; ++e) erecs[erec_pos[e]] = erec[e];
+      err = up(&g.erecs, erecs.data(), E);
+    }
     if (err == hipSuccess) err = up(&g.adj, adj.data(), E);
     if (err == hipSuccess) err = up(&g.w, w.data(), E);
     if (err == hipSuccess) err = up(&g.w64, gr->metric, E);
@@ -1375,6 +1396,7 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
   ctx->row2t = std::move(row2t);
   ctx->erec = std::move(erec);
   ctx->ellt = std::move(ellt);
+  ctx->erec_pos = std::move(erec_pos);
   ctx->delta.clear();
   ctx->delta_index.clear();
   ctx->delta_valid = false;
@@ -1482,7 +1504,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
 
   // 3) recompute the dirty device elements exactly as set_graph derives them
   std::vector<PatchRec> recs;
-  recs.reserve(5 * de_list.size() + 6 * dv_list.size());
+  recs.reserve(6 * de_list.size() + 6 * dv_list.size());
   auto rec = [&](uint32_t arr, uint32_t idx, uint4 val) { recs.push_back(PatchRec{arr, idx, 0u, 0u, val}); };
   for (uint32_t e : de_list) {
     ctx->erec[e] = make_uint4(ctx->adj[e] | (ctx->ovl[ctx->col[e]] ? kNodeSink : 0u), ctx->win[e], ctx->lid[e],
@@ -1492,6 +1514,7 @@ int openr_spf_patch_graph(openr_spf_ctx* ctx, const openr_spf_patch* p) {
     rec(kPatchW64, e, make_uint4((uint32_t)ctx->metric[e], (uint32_t)(ctx->metric[e] >> 32), 0, 0));
     rec(kPatchWin, e, make_uint4(ctx->win[e], 0, 0, 0));
     rec(kPatchErec, e, ctx->erec[e]);
+    rec(kPatchErecS, ctx->erec_pos[e], ctx->erec[e]);
   }
   uint32_t last_word = UINT32_MAX;
   for (uint32_t u : dv_list) {

@@ -30,6 +30,11 @@ struct DevGraph {
                                //     ellv[V] = (V, V, V, V), the row of a lane past the frontier;
                                //     ellv[V + 32k] = four copies of V + 32k (reach pass sentinels)
   uint32_t* elld = nullptr;    // [V] ellv as four signed byte deltas (v - u; 0 = no edge), or null
+  // [E] erec with every row's entries sorted by (name rank of the neighbour, reverse edge):
+  // for uniform cost that is the reference's pathLinks order (DijkstraQ pops equal
+  // distances by name; LinkState.cpp:820-829), so the KSP tracer ranks a frame's
+  // candidates by their position alone
+  uint4* erecs = nullptr;
                                //     when a row has > 4 edges or a column > 127 ids away (wave pass)
   uint32_t* adj = nullptr;     // [E] col | kEdgeDown when !edge_up
   uint32_t* w = nullptr;       // [E] metric u->v (u32; usable edges are in [1, 2^31-1])
@@ -265,6 +270,7 @@ enum PatchArray : uint32_t {
   kPatchAdj = 0, kPatchW, kPatchWin, kPatchErec, kPatchEllt, kPatchRow2t, kPatchOvl, kPatchOvlBits, kPatchEllv,
   kPatchW64,  // val.x = low, val.y = high word
   kPatchElld,
+  kPatchErecS,  // DevGraph::erecs (idx = sorted position)
   kNumPatchArrays
 };
 struct PatchRec {

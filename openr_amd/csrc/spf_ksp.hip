@@ -185,6 +185,27 @@ __device__ __forceinline__ PathCand gather_cand(const KspState& st, uint32_t e, 
   return c;
 }
 
+// Uniform cost (round 3): every tight candidate of v has dist[u] = dist[v] - cost, so the
+// reference's order is (name rank of u, edge) alone, which DevGraph::erecs holds each row
+// in: a candidate's rank is the number of candidates before it in the row (mbcnt of the
+// ballot), with no key exchange and no name-rank load.
+__device__ __forceinline__ PathCand gather_cand_sorted(const KspState& st, uint32_t e, uint32_t end, uint64_t dv) {
+  PathCand c{false, 0, 0, 0, 0};
+  if (e < end) {
+    const uint4 rec = st.g->erecs[e];
+    const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+    if (!(rec.x & kEdgeDown) && !test_bit(st.vis, rec.z) && !test_bit(st.dead, u) &&
+        (u == st.src || !(rec.x & kNodeSink))) {
+      const uint64_t du = dist_of(st, u);
+      c.ok = du != kNoKey && du + rec.y == dv;
+      c.kr = rec.w;
+      c.link = rec.z;
+      c.u = u;
+    }
+  }
+  return c;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t j) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)j);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)j);
@@ -225,15 +246,23 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
   const uint32_t lane = threadIdx.x;
   const uint64_t t0 = st.stats ? clock64() : 0;
   const uint64_t dv = dist_of(st, v);
-  const PathCand c0 = gather_cand(st, r.x + lane, r.y, dv);
-  const PathCand c1 = gather_cand(st, r.x + kWave + lane, r.y, dv);
+  const bool sorted = st.lcost != 0u && st.g->erecs != nullptr;  // wave-uniform
+  const PathCand c0 = sorted ? gather_cand_sorted(st, r.x + lane, r.y, dv) : gather_cand(st, r.x + lane, r.y, dv);
+  const PathCand c1 = sorted ? gather_cand_sorted(st, r.x + kWave + lane, r.y, dv)
+                             : gather_cand(st, r.x + kWave + lane, r.y, dv);
   const uint64_t m0 = __ballot(c0.ok), m1 = __ballot(c1.ok);
   const uint64_t t1 = st.stats ? clock64() : 0;
   const uint32_t cnt = (uint32_t)(__popcll(m0) + __popcll(m1));
   if (beg + cnt > st.arena_cap) return UINT32_MAX;
   uint32_t r0 = 0, r1 = 0;
-  rank_against(m0, c0, c0, c1, r0, r1, st.lcost != 0u);
-  rank_against(m1, c1, c0, c1, r0, r1, st.lcost != 0u);
+  if (sorted) {  // row order is key order: the rank is the position among the candidates
+    r0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+    r1 = (uint32_t)__popcll(m0) +
+         __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+  } else {
+    rank_against(m0, c0, c0, c1, r0, r1, st.lcost != 0u);
+    rank_against(m1, c1, c0, c1, r0, r1, st.lcost != 0u);
+  }
   if (c0.ok) {
     st.ar_e[beg + r0] = (uint32_t)c0.kr;
     st.ar_l[beg + r0] = c0.link;

@@ -36,6 +36,9 @@ __global__ __launch_bounds__(256) void patch_apply(DevGraph g, const PatchRec* r
     case kPatchW: g.w[r.idx] = r.val.x; break;
     case kPatchWin: g.win[r.idx] = r.val.x; break;
     case kPatchErec: g.erec[r.idx] = r.val; break;
+    case kPatchErecS:
+      if (g.erecs) g.erecs[r.idx] = r.val;
+      break;
     case kPatchEllt: g.ellt[r.idx] = r.val; break;
     case kPatchEllv: g.ellv[r.idx] = r.val; break;
     case kPatchElld:
