@@ -147,6 +147,29 @@ __device__ void copy_row16(uint16_t* d16, const uint64_t* drow, uint32_t V) {
   }
 }
 
+// LDS copy of a tagged u16 level row (KSP2 second SPF): entries of another tag are
+// unreached; distance = level x cost, saturated like copy_row16
+__device__ void copy_row16_tagged(uint16_t* d16, const uint16_t* l16, uint32_t V, uint32_t ltag, uint32_t lshift,
+                                  uint64_t lcost) {
+  const uint32_t lane = threadIdx.x, mask = (1u << lshift) - 1u;
+  for (uint32_t i0 = 0; i0 < V; i0 += 8u * kWave) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + j * kWave + lane;
+      x[j] = i < V ? l16[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = i0 + j * kWave + lane;
+      if (i < V) {
+        const uint64_t d = (x[j] >> lshift) == ltag ? (uint64_t)(x[j] & mask) * lcost : 0xFFFFull;
+        d16[i] = d < 0xFFFFull ? (uint16_t)d : (uint16_t)0xFFFFu;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void stat_add(const KspState& st, uint32_t i, uint64_t v) {
   if (st.stats && threadIdx.x == 0) st.stats[i] += v;
 }
@@ -608,6 +631,13 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     if (st.stats) stat_add(st, kStCycInit, clock64() - tp);
     if (!bad && src != dst && ddst != kNoKey) {
       uint32_t src_live = live_src_links(st, dst);
+      // a tagged second-SPF row that will be traced: its LDS copy (the trace's distance
+      // reads then stay in LDS)
+      if (d16 && st.l16 && st.ltag && src_live && ddst < 0xFFFFull) {
+        copy_row16_tagged(d16, st.l16, V, st.ltag, st.lshift, st.lcost);
+        lds_fence();
+        st.use16 = true;
+      }
       while (src_live) {
         const uint64_t tt = st.stats ? clock64() : 0, e0 = st.stats ? st.stats[kStEntries] : 0;
         const int len = trace_one(st, dst);
@@ -673,9 +703,13 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 
 }  // namespace
 
-// OPENR_SPF_KSP_D16=1: keep a u16 copy of the pair's distance row in LDS (fewer
-// wavefronts per CU; measured slower on the fabric, kept as a tuning knob)
-bool ksp_use_d16() { return bfs::env_u32("OPENR_SPF_KSP_D16", 0u, 0u, 1u) != 0; }
+// OPENR_SPF_KSP_D16: keep a u16 copy of the pair's distance row in LDS (fewer wavefronts
+// per CU): 0 never, 1 both traces (measured slower on the fabric in round 2), 2 the k = 2
+// trace only (its tagged second-SPF rows, copied for pairs that trace)
+bool ksp_use_d16(int kind) {
+  const uint32_t k = bfs::env_u32("OPENR_SPF_KSP_D16", 0u, 0u, 2u);
+  return k == 1u || (k == 2u && kind == 2);
+}
 
 // Small tier: a traced path has at most as many hops as the source's BFS depth on
 // uniform-cost graphs; 2x the sampled depth + 8 covers the sample's misses and weighted
@@ -695,21 +729,23 @@ KspCaps ksp_caps(const DevGraph& g, bool full) {
   return c;
 }
 
-uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full) {
+uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full, int kind) {
   const KspCaps c = ksp_caps(g, full);
-  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16()).total;
+  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16(kind)).total;
   return t <= kMaxLds ? t : 0;
 }
 
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
-  return std::max(blocks_for(UINT32_MAX, ksp_tier_lds_bytes(g, false), num_cus, kWave),
-                  blocks_for(UINT32_MAX, ksp_tier_lds_bytes(g, true), num_cus, kWave));
+  uint32_t m = 0;
+  for (int kind = 1; kind <= 2; ++kind)
+    for (bool full : {false, true}) m = std::max(m, blocks_for(UINT32_MAX, ksp_tier_lds_bytes(g, full, kind), num_cus, kWave));
+  return m;
 }
 
 uint32_t ksp_stats_count() { return kKspStats; }
 
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
-  const uint32_t t = ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16()).total;
+  const uint32_t t = ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16(1) || ksp_use_d16(2)).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -724,7 +760,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
   const KspCaps caps = ksp_caps(g, full);
-  const uint32_t lds = ksp_tier_lds_bytes(g, full);
+  const uint32_t lds = ksp_tier_lds_bytes(g, full, kind);
   if (!lds || !qbuf) return hipErrorInvalidValue;
   // a re-run launch covers the listed pairs only; its surplus wavefronts exit at once
   const uint32_t grid = blocks_for(n, lds, num_cus, kWave);  // <= ksp_max_grid: qbuf holds grid * V
@@ -734,7 +770,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
-                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16() ? 1u : 0u,
+                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16(kind) ? 1u : 0u,
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
                      lcost, ltag);
   return hipGetLastError();
