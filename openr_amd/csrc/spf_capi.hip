@@ -606,8 +606,9 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   // re-run list. Measured and left opt-in: on the fabric update loop the cross-stream
   // fork / join cost more than the overlap saved (0.226 vs 0.170 ms per update).
   const int nc = num_classes(fam);
-  const bool side = a.n <= (uint32_t)d.num_cus && __builtin_popcount(mask) > 1 &&
-                    std::getenv("OPENR_SPF_CLASS_STREAMS") && std::atoi(std::getenv("OPENR_SPF_CLASS_STREAMS")) == 1;
+  // (=2: every multi-class batch, so one class's tail overlaps the next class's launch)
+  const int cs_knob = std::getenv("OPENR_SPF_CLASS_STREAMS") ? std::atoi(std::getenv("OPENR_SPF_CLASS_STREAMS")) : 0;
+  const bool side = __builtin_popcount(mask) > 1 && (cs_knob == 2 || (cs_knob == 1 && a.n <= (uint32_t)d.num_cus));
   if (side) {
     const size_t per = (size_t)a.n * std::max<uint32_t>(a.nsl, 1u);
     err = d.ovfc.reserve(per * (size_t)nc);
