@@ -60,18 +60,24 @@ __host__ __device__ inline RoundsLayout rounds_layout(uint32_t V, uint32_t L, bo
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int MODE, typename D, bool GENERIC>
-__global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, uint32_t has_ign_rt, uint32_t* ctr) {
+// BLOCK threads per solve: 64 (one wavefront, LDS ordering alone between rounds) or a
+// multi-wave workgroup for batches that fill under a quarter of the CUs' wave slots (the
+// 1 000-source WAN base SPF of the what-if sweep: ~4 solves per CU). Every round loop
+// strides the frontier / the node range by BLOCK and ends at a workgroup barrier. The
+// append counter of round r is ctl[r % 3]; round r zeroes ctl[(r + 1) % 3], whose last
+// reads (round r - 2's count) all precede round r - 1's barrier.
+template <int MODE, typename D, bool GENERIC, uint32_t BLOCK>
+__global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, uint32_t has_ign_rt, uint32_t* ctr) {
   using N = Nh<MODE>;
   constexpr D INF = (D)~(D)0;
   constexpr int K = 4;
   const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t V = g.V, lane = threadIdx.x;
+  const uint32_t V = g.V, tid = threadIdx.x;
   const uint32_t nh_words = N::words(V);
   const RoundsLayout lay = rounds_layout(V, g.L, has_ign, nh_words, sizeof(D));
   char* base = reinterpret_cast<char*>(smem);
-  uint32_t* ctl = smem;
+  uint32_t* ctl = smem;  // [0..2] rotating append counters, [3] next solve
   D* dist = reinterpret_cast<D*>(base + lay.dist);
   uint32_t* nh = reinterpret_cast<uint32_t*>(base + lay.nh);
   uint16_t* cnt = reinterpret_cast<uint16_t*>(base + lay.cnt);
@@ -81,46 +87,56 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
   const uint32_t vw = (V + 31u) / 32u, ign_words = (g.L + 31u) / 32u;
   const uint32_t tight_words = (g.E + 63u) / 64u;
+  auto sync = [&]() {
+    if constexpr (BLOCK == kWave) lds_fence();
+    else __syncthreads();
+  };
+  uint32_t r = 0;  // round number (append counter rotation)
 
   for (uint32_t sid = blockIdx.x; sid < a.n;) {
     const uint32_t src = a.sources[sid];
     if (src < V) {
-      for (uint32_t v = lane; v < V; v += kWave) dist[v] = INF;
-      for (uint32_t i = lane; i < nh_words; i += kWave) nh[i] = 0;
-      for (uint32_t i = lane; i < vw; i += kWave) inq[i] = 0;
+      for (uint32_t v = tid; v < V; v += BLOCK) dist[v] = INF;
+      for (uint32_t i = tid; i < nh_words; i += BLOCK) nh[i] = 0;
+      for (uint32_t i = tid; i < vw; i += BLOCK) inq[i] = 0;
+      if (tid < 3) ctl[tid] = 0;
       if (has_ign) {
-        for (uint32_t i = lane; i < ign_words; i += kWave) ign[i] = 0;
-        lds_fence();
+        for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
+        sync();
         load_ignore(ign, ign_words, a, sid, g.L);
       }
       uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
-      lds_fence();
-      if (lane == 0) {
+      sync();
+      if (tid == 0) {
         dist[src] = 0;
         fa[0] = (uint16_t)src;
       }
-      lds_fence();
+      sync();
 
       // (1) distance rounds over the frontier of nodes whose distance dropped
       uint16_t *cur = fa, *nxt = fb;
       uint32_t n = 1;
       while (n) {
-        if (lane == 0) ctl[0] = 0;
-        lds_fence();
-        for (uint32_t i = lane; i < n; i += kWave) {
+        uint32_t* const ac = &ctl[r % 3u];
+        if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+        for (uint32_t i = tid; i < n; i += BLOCK) {
           const uint32_t u = cur[i];
           atomicAnd(&inq[u >> 5], ~(1u << (u & 31u)));  // may re-enter the next frontier
-          if (u != src && g.ovl[u]) continue;           // reached, never expanded
+          // the clear is issued before dist[u] is read (LDS operations of a wave complete in
+          // order): an improvement another wave makes after the read finds the bit clear and
+          // re-lists u
+          asm volatile("" ::: "memory");
+          if (u != src && g.ovl[u]) continue;  // reached, never expanded
           const D du = dist[u];
-          const uint2 r = g.row2[u];
-          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+          const uint2 rr = g.row2[u];
+          for (uint32_t e0 = rr.x; e0 < rr.y; e0 += K) {
             uint32_t av[K], wo[K], lv[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j;
-              av[j] = e < r.y ? g.adj[e] : kEdgeDown;
-              wo[j] = e < r.y ? g.w[e] : 0u;
-              lv[j] = (has_ign && e < r.y) ? g.lid[e] : 0u;
+              av[j] = e < rr.y ? g.adj[e] : kEdgeDown;
+              wo[j] = e < rr.y ? g.w[e] : 0u;
+              lv[j] = (has_ign && e < rr.y) ? g.lid[e] : 0u;
             }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -131,14 +147,15 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
                 const D old = atomicMin(&dist[v], cand);
                 if (cand < old) {
                   const uint32_t bit = 1u << (v & 31u);
-                  if (!(atomicOr(&inq[v >> 5], bit) & bit)) nxt[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+                  if (!(atomicOr(&inq[v >> 5], bit) & bit)) nxt[atomicAdd(ac, 1u)] = (uint16_t)v;
                 }
               }
             }
           }
         }
-        lds_fence();
-        n = __builtin_amdgcn_readfirstlane(ctl[0]);
+        sync();
+        n = __builtin_amdgcn_readfirstlane(*ac);
+        ++r;
         uint16_t* t = cur;
         cur = nxt;
         nxt = t;
@@ -146,17 +163,17 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
 
       // (2) tight in-degree of every reached node; the source (and nodes with no tight
       //     in-edge) start the topological rounds
-      if (lane == 0) ctl[0] = 0;
-      lds_fence();
-      for (uint32_t v = lane; v < V; v += kWave) {
+      uint32_t* const ac2 = &ctl[r % 3u];
+      if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+      for (uint32_t v = tid; v < V; v += BLOCK) {
         const D dv = dist[v];
         uint32_t c = 0;
         if (dv != INF && v != src) {
-          const uint2 r = g.row2[v];
-          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+          const uint2 rr = g.row2[v];
+          for (uint32_t e0 = rr.x; e0 < rr.y; e0 += K) {
             uint4 rec[K];  // v->u: {u | down | sink(u), w(u->v), link, rev}
 #pragma unroll
-            for (int j = 0; j < K; ++j) rec[j] = e0 + j < r.y ? g.erec[e0 + j] : make_uint4(kEdgeDown, 0u, 0u, 0u);
+            for (int j = 0; j < K; ++j) rec[j] = e0 + j < rr.y ? g.erec[e0 + j] : make_uint4(kEdgeDown, 0u, 0u, 0u);
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t u = rec[j].x & ~(kEdgeDown | kNodeSink);
@@ -168,30 +185,31 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
           }
         }
         cnt[v] = (uint16_t)c;
-        if (v == src) cur[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+        if (v == src) cur[atomicAdd(ac2, 1u)] = (uint16_t)v;
       }
-      lds_fence();
-      n = __builtin_amdgcn_readfirstlane(ctl[0]);
+      sync();
+      n = __builtin_amdgcn_readfirstlane(*ac2);
+      ++r;
 
       // (3) Kahn rounds: a finished node pushes its set down its tight out-edges; the
       //     decrement that empties a successor's count makes it finished next round
       while (n) {
-        if (lane == 0) ctl[0] = 0;
-        lds_fence();
-        for (uint32_t i = lane; i < n; i += kWave) {
+        uint32_t* const ac = &ctl[r % 3u];
+        if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+        for (uint32_t i = tid; i < n; i += BLOCK) {
           const uint32_t u = cur[i];
           if (u != src && g.ovl[u]) continue;  // a sink has no tight out-edges
           const D du = dist[u];
           const typename N::Val xu = N::load(nh, u);
-          const uint2 r = g.row2[u];
-          for (uint32_t e0 = r.x; e0 < r.y; e0 += K) {
+          const uint2 rr = g.row2[u];
+          for (uint32_t e0 = rr.x; e0 < rr.y; e0 += K) {
             uint32_t av[K], wo[K], lv[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) {
               const uint32_t e = e0 + j;
-              av[j] = e < r.y ? g.adj[e] : kEdgeDown;
-              wo[j] = e < r.y ? g.w[e] : 0u;
-              lv[j] = (has_ign && e < r.y) ? g.lid[e] : 0u;
+              av[j] = e < rr.y ? g.adj[e] : kEdgeDown;
+              wo[j] = e < rr.y ? g.w[e] : 0u;
+              lv[j] = (has_ign && e < rr.y) ? g.lid[e] : 0u;
             }
 #pragma unroll
             for (int j = 0; j < K; ++j) {
@@ -204,50 +222,70 @@ __global__ __launch_bounds__(kWave) void rounds_kernel(DevGraph g, SolveArgs a, 
               if (trow) atomicOr(reinterpret_cast<unsigned long long*>(&trow[e >> 6]), 1ull << (e & 63u));
               const uint32_t sh = 16u * (v & 1u);
               const uint32_t old = atomicSub(reinterpret_cast<uint32_t*>(cnt) + (v >> 1), 1u << sh);
-              if (((old >> sh) & 0xFFFFu) == 1u) nxt[atomicAdd(&ctl[0], 1u)] = (uint16_t)v;
+              if (((old >> sh) & 0xFFFFu) == 1u) nxt[atomicAdd(ac, 1u)] = (uint16_t)v;
             }
           }
         }
-        lds_fence();
-        n = __builtin_amdgcn_readfirstlane(ctl[0]);
+        sync();
+        n = __builtin_amdgcn_readfirstlane(*ac);
+        ++r;
         uint16_t* t = cur;
         cur = nxt;
         nxt = t;
       }
       // (result rows, coalesced; unreached nodes keep UINT64_MAX)
       uint64_t* drow = a.dist + out_row_of(a, sid) * V;
-      for (uint32_t v = lane; v < V; v += kWave) {
+      for (uint32_t v = tid; v < V; v += BLOCK) {
         const D d = dist[v];
         store_row<uint64_t>(&drow[v], d == INF ? ~0ull : (uint64_t)d, true);
       }
       if (a.nh) {
         const uint32_t nb = a.nh_bytes;
         uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
-        for (uint32_t i = lane; i < V * nb; i += kWave) {
+        for (uint32_t i = tid; i < V * nb; i += BLOCK) {
           const uint32_t v = i / nb, j = i - v * nb;
           nrow[i] = (uint8_t)N::byte(nh, v, j);
         }
       }
     }
-    uint32_t nxt_sid = 0;
-    if (lane == 0) nxt_sid = gridDim.x + atomicAdd(&ctr[0], 1u);
-    sid = __builtin_amdgcn_readfirstlane(__shfl(nxt_sid, 0));
+    if constexpr (BLOCK == kWave) {
+      uint32_t nxt_sid = 0;
+      if (tid == 0) nxt_sid = gridDim.x + atomicAdd(&ctr[0], 1u);
+      sid = __builtin_amdgcn_readfirstlane(__shfl(nxt_sid, 0));
+    } else {
+      // every thread is past this solve's write-out before the next one's init
+      if (tid == 0) ctl[3] = gridDim.x + atomicAdd(&ctr[0], 1u);
+      __syncthreads();
+      sid = __builtin_amdgcn_readfirstlane(ctl[3]);
+      __syncthreads();  // ctl[3] read by every wave before a later solve rewrites it
+    }
   }
   retire_workgroup(ctr, nullptr);
 }
 
-template <int MODE, typename D>
-hipError_t launch_rounds_t(const DevGraph& g, const SolveArgs& a, uint32_t lds, uint32_t grid, uint32_t* ctr,
+template <int MODE, typename D, uint32_t BLOCK>
+hipError_t launch_rounds_b(const DevGraph& g, const SolveArgs& a, uint32_t lds, uint32_t grid, uint32_t* ctr,
                            hipStream_t s) {
   const bool has_ign = a.ign_ptr != nullptr;
   const bool generic = has_ign || a.tight != nullptr;
-  auto k = generic ? rounds_kernel<MODE, D, true> : rounds_kernel<MODE, D, false>;
+  auto k = generic ? rounds_kernel<MODE, D, true, BLOCK> : rounds_kernel<MODE, D, false, BLOCK>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
   note_launch("rounds_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, a, (uint32_t)has_ign, ctr);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, (uint32_t)has_ign, ctr);
   return hipGetLastError();
+}
+
+template <int MODE, typename D>
+hipError_t launch_rounds_t(const DevGraph& g, const SolveArgs& a, uint32_t lds, uint32_t block, int num_cus,
+                           uint32_t* ctr, hipStream_t s) {
+  const uint32_t grid = blocks_for(a.n, lds, num_cus, block);
+  switch (block) {
+    case 256u: return launch_rounds_b<MODE, D, 256u>(g, a, lds, grid, ctr, s);
+    case 128u: return launch_rounds_b<MODE, D, 128u>(g, a, lds, grid, ctr, s);
+    default: return launch_rounds_b<MODE, D, kWave>(g, a, lds, grid, ctr, s);
+  }
 }
 
 }  // namespace
@@ -258,22 +296,36 @@ uint32_t rounds_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, 
   return t <= kMaxLds ? t : 0;
 }
 
+// Threads per solve: the widest of 256 / 128 / 64 whose workgroups of the whole batch fit
+// the CUs in one round (LDS and 2 048 threads per CU); a batch that needs more than one
+// round of single-wave solves keeps one wavefront per solve (no barriers).
+// OPENR_SPF_ROUNDS_BLOCK=64|128|256 forces one (tests, A/B).
+uint32_t rounds_block(uint32_t n, uint32_t lds, int num_cus) {
+  const uint32_t knob = env_u32("OPENR_SPF_ROUNDS_BLOCK", 0u, 64u, 256u);
+  if (knob == 64u || knob == 128u || knob == 256u) return knob;
+  const uint64_t per_cu = ((uint64_t)n + (uint64_t)std::max(num_cus, 1) - 1u) / (uint64_t)std::max(num_cus, 1);
+  const uint64_t by_lds = lds ? kMaxLds / lds : 32u;
+  for (uint32_t b : {256u, 128u})
+    if (per_cu <= std::min<uint64_t>(by_lds, 2048u / b)) return b;
+  return kWave;
+}
+
 hipError_t launch_rounds(const DevGraph& g, const SolveArgs& a, bool dist64, int nh_mode, int num_cus, hipStream_t s,
                          LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
   const uint32_t lds = rounds_lds_bytes(g.V, g.L, has_ign, nh_mode, dist64);
   if (!lds || !a.work) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  const uint32_t grid = blocks_for(a.n, lds, num_cus, kWave);
+  const uint32_t block = rounds_block(a.n, lds, num_cus);
   if (info) {
     info->lds_bytes = lds;
-    info->grid = grid;
+    info->grid = blocks_for(a.n, lds, num_cus, block);
     info->kernel = dist64 ? "rounds_kernel<u64>" : "rounds_kernel<u32>";
   }
   uint32_t* ctr = a.work + kFringeCtr;
 #define OPENR_ROUNDS_CASE(M) \
-  case M: return dist64 ? launch_rounds_t<M, unsigned long long>(g, a, lds, grid, ctr, s) \
-                        : launch_rounds_t<M, uint32_t>(g, a, lds, grid, ctr, s);
+  case M: return dist64 ? launch_rounds_t<M, unsigned long long>(g, a, lds, block, num_cus, ctr, s) \
+                        : launch_rounds_t<M, uint32_t>(g, a, lds, block, num_cus, ctr, s);
   switch (nh_mode) {
     OPENR_ROUNDS_CASE(kNhNibble)
     OPENR_ROUNDS_CASE(kNhByte)

@@ -214,6 +214,26 @@ def test_random_graphs(eng, seed, max_metric):
     check_against_oracle(eng, g, srcs, False)
 
 
+@pytest.mark.parametrize("block", ["64", "128", "256"])
+def test_rounds_kernel_block_sizes(eng, monkeypatch, block):
+    """The rounds kernel (spf_rounds.hip) at each workgroup size it picks from: one
+    wavefront per solve (barrier-free rounds) and 2 / 4 wavefronts sharing a solve's
+    frontier with a workgroup barrier per round (small batches). Weighted WAN with
+    parallel links, random graphs with overloads / down links, ignore sets, pathLinks."""
+    monkeypatch.setenv("OPENR_SPF_GENERAL", "rounds")
+    monkeypatch.setenv("OPENR_SPF_ROUNDS_BLOCK", block)
+    g = T.wan(256, 768, 64, seed=3, parallel_fraction=0.05)
+    check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
+    check_against_oracle(eng, g, list(range(0, 256, 9)), True, check_pathlinks=True)
+    rng = np.random.default_rng(int(block))
+    srcs = list(range(0, 256, 4))
+    ign = [sorted(rng.choice(g.num_links, 3, replace=False).tolist()) for _ in srcs]
+    check_against_oracle(eng, g, srcs, True, ignore=ign, check_pathlinks=True)
+    for seed in (1, 2):
+        r = random_graph(500 + seed, 150, 420, 40, p_ovl=0.1, p_down=0.05, p_par=0.1)
+        check_against_oracle(eng, r, list(range(r.num_nodes)), True)
+
+
 def test_uniform_nonunit_cost(eng):
     g = random_graph(11, 120, 300, 1)
     g.metric[:] = 7  # BFS kernel with cost 7
@@ -768,14 +788,18 @@ def test_ksp2_device_capacity_tiers(eng, tier, monkeypatch):
     check_ksp2_against_oracle(eng, g, [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 30)])
 
 
+@pytest.mark.parametrize("lanes", ["2", "1"], ids=["two-lanes", "one-lane"])
 @pytest.mark.parametrize("tag", ["1", "0"], ids=["tagged", "filled"])
-def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
+def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag, lanes):
     """KSP2 second-SPF level rows (code family, uniform cost): tagged — a solve writes only
     the nodes it settles (it stops at the pair's target) as tag << shift | level, and an
     entry with another chunk's tag reads as unreached — or filled (unreached = 0xFFFF).
     Chunks of 7 pairs: on the 300-node graph (9 level bits, tags 1..127) the tags wrap and
-    the rows are zeroed again mid-call; results equal the oracle either way."""
+    the rows are zeroed again mid-call; results equal the oracle either way. Chunks run
+    on one stream (default) or alternate between two stream lanes with their own rows,
+    tags and counters (OPENR_SPF_KSP_LANES=2, opt-in)."""
     monkeypatch.setenv("OPENR_SPF_KSP_TAG", tag)
+    monkeypatch.setenv("OPENR_SPF_KSP_LANES", lanes)
     monkeypatch.setenv("OPENR_SPF_KSP_CHUNK", "7")
     g = random_graph(9, 300, 620, 1, p_ovl=0.05, p_down=0.05, p_par=0.1)
     rng = np.random.default_rng(11)
