@@ -792,7 +792,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
   // re-solve the `count` units listed in wsrc / wlink / wunit (ignore set = the unit's
   // link) and compare each row with its source's base row
-  auto resolve_units = [&](uint32_t count) -> hipError_t {
+  auto resolve_units = [&](uint32_t count, uint32_t base) -> hipError_t {
     hipError_t e2;
     const size_t row = (size_t)V * (8u + nb);
     const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
@@ -801,8 +801,8 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     if ((e2 = d.wiota.reserve((size_t)chunk + 1u)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)chunk * ctx->nsl_max())) != hipSuccess) return e2;
     if ((e2 = launch_iota(d.wiota.p, chunk + 1u, d.num_cus, s)) != hipSuccess) return e2;
-    for (uint32_t off = 0; off < count; off += chunk) {
-      const uint32_t m = std::min(chunk, count - off);
+    for (uint32_t off0 = 0; off0 < count; off0 += chunk) {
+      const uint32_t m = std::min(chunk, count - off0), off = base + off0;
       SolveArgs b{};
       b.sources = d.wsrc.p + off;
       b.n = m;
@@ -832,7 +832,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     // (a unit with more dirty nodes than a wave's slots is re-solved after the launch)
     if (whatif_group_lds_bytes(V, ctx->E, nb, dist64, d.g.max_deg)) {
       const size_t units = (size_t)n_links * n_src;
-      OPENR_TRY(d.wcount.reserve(2));
+      OPENR_TRY(d.wcount.reserve(3));
       OPENR_TRY(d.wsrc.reserve(units));
       OPENR_TRY(d.wlink.reserve(units));
       OPENR_TRY(d.wunit.reserve(units));
@@ -842,13 +842,30 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
                                     d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
                                     d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));
-      uint32_t cnt[2] = {0, 0};  // affected units, units handed over
+      uint32_t cnt[2] = {0, 0};  // affected units, units handed to the list pass
       OPENR_TRY(hipMemcpyAsync(cnt, d.wcount.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
       OPENR_TRY(hipStreamSynchronize(s));
       float ms = 0.f;
       OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
       ctx->stats.last_kernel_ms = ms;
-      if (cnt[1]) OPENR_TRY(resolve_units(cnt[1]));  // units past the slots: re-solved (few, large)
+      // Units past the first pass's slots are large (WAN: 6 533 of 1.01 M affected units
+      // at 96 slots, 151 dirty nodes on average): re-solved (default), or with
+      // OPENR_SPF_WHATIF_LIST=1 repaired again by the list pass with every slot and the
+      // rest re-solved. Measured on the WAN step: 5.18 vs 5.34 ms — a 150-node repair on
+      // one wavefront takes as long as a re-solve on a 256-thread workgroup.
+      const char* lp = std::getenv("OPENR_SPF_WHATIF_LIST");
+      if (cnt[1] && !(lp && std::atoi(lp) == 1)) {
+        OPENR_TRY(resolve_units(cnt[1], 0));
+      } else if (cnt[1]) {
+        OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
+                                      d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
+                                      d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
+                                      d.num_cus, s, d.wunit.p, cnt[1]));
+        uint32_t c2 = 0;
+        OPENR_TRY(hipMemcpyAsync(&c2, d.wcount.p + 2, sizeof(c2), hipMemcpyDeviceToHost, s));
+        OPENR_TRY(hipStreamSynchronize(s));
+        if (c2) OPENR_TRY(resolve_units(c2, cnt[1]));  // past every slot: re-solved (few, large)
+      }
       *solved = cnt[0];
       return hipSuccess;
     }
@@ -872,7 +889,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
                               !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);
   }
-  return resolve_units(count);
+  return resolve_units(count, 0);
 #undef OPENR_TRY
   return hipSuccess;
 }

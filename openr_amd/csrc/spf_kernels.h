@@ -254,12 +254,17 @@ uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
 // Grouped what-if (spf_sweep.hip, the default): one workgroup per (source, chunk of links)
 // stages the source's base rows (dist, next hops, tight mask) in LDS once; its wavefronts
 // filter the links (no tight edge -> 0) and repair the affected ones on private overlays.
-// Writes every changed[i * n_src + j]; *affected = affected units (zeroed by the launcher).
+// Writes every changed[i * n_src + j]; affected[0] = affected units, affected[1] = units
+// that outgrew the first pass's dirty slots (listed in ovf_*[0, affected[1])). With `list`
+// (= ovf_unit of the first pass, n_list = affected[1]) it is the list pass: it repairs the
+// listed units again with every slot and lists the ones that still outgrow them in
+// ovf_*[n_list, n_list + affected[2]) for a re-solve.
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
-                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s);
+                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s,
+                               const uint32_t* list = nullptr, uint32_t n_list = 0);
 // 0 when the grouped repair cannot run on the graph (ids, next-hop width, degree, LDS)
 uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64, uint32_t max_deg);
 

@@ -296,18 +296,18 @@ uint32_t rounds_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, 
   return t <= kMaxLds ? t : 0;
 }
 
-// Threads per solve: the widest of 256 / 128 / 64 whose workgroups of the whole batch fit
-// the CUs in one round (LDS and 2 048 threads per CU); a batch that needs more than one
-// round of single-wave solves keeps one wavefront per solve (no barriers).
-// OPENR_SPF_ROUNDS_BLOCK=64|128|256 forces one (tests, A/B).
+// Threads per solve: 256 for batches of up to four rounds of 256-thread workgroups per CU,
+// one wavefront per solve (no barriers) beyond. Measured on the WAN what-if: the base SPF
+// (1 000 sources) 0.41 -> 0.21 ms, the 6 533 re-solved large units 64 / 128 / 256 threads:
+// step 5.33 / 5.25 / 5.18 ms (a solve's rounds are latency chains: four waves cut each
+// round's serial passes even when the CUs are full). OPENR_SPF_ROUNDS_BLOCK=64|128|256
+// forces one (tests, A/B).
 uint32_t rounds_block(uint32_t n, uint32_t lds, int num_cus) {
   const uint32_t knob = env_u32("OPENR_SPF_ROUNDS_BLOCK", 0u, 64u, 256u);
   if (knob == 64u || knob == 128u || knob == 256u) return knob;
   const uint64_t per_cu = ((uint64_t)n + (uint64_t)std::max(num_cus, 1) - 1u) / (uint64_t)std::max(num_cus, 1);
   const uint64_t by_lds = lds ? kMaxLds / lds : 32u;
-  for (uint32_t b : {256u, 128u})
-    if (per_cu <= std::min<uint64_t>(by_lds, 2048u / b)) return b;
-  return kWave;
+  return per_cu <= 4u * std::min<uint64_t>(by_lds, 2048u / 256u) ? 256u : kWave;
 }
 
 hipError_t launch_rounds(const DevGraph& g, const SolveArgs& a, bool dist64, int nh_mode, int num_cus, hipStream_t s,

@@ -575,6 +575,8 @@ struct GraphView<true> {  // compact LDS copy
 
 constexpr uint32_t kGrpMaxChunk = 2048;  // links per work item
 constexpr uint32_t kGrpMaxCap = 255;     // dirty slots per wave (u8 slot index)
+constexpr uint32_t kGrpCap1 = 96;        // dirty slots per wave of the first pass
+constexpr uint32_t kGrpWaves = 4;        // waves per workgroup of the first pass
 
 struct GrpLayout {
   uint32_t grow, grec, gnbr, govl;                                  // LDS graph (LG only)
@@ -791,6 +793,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   uint32_t nchanged = 0, buckets = 0;
   uint32_t nd = __builtin_amdgcn_readfirstlane(c.ctl[1]), loaded = 0;
   uint32_t ev = 0;
+  uint2 er = make_uint2(0u, 0u);  // the lane's entry's row, loaded with the entry
   D ed = INF;
   bool pend = false, ea = false;  // ea: the lane's entry is in A (its distance may still drop)
   auto load_entries = [&]() {
@@ -799,16 +802,16 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     if (loaded < hi) {
       if (lane >= loaded && lane < hi) {
         ev = c.dlist[lane];
+        er = c.gv.row(ev);  // in flight with the distance read: process() starts at the records
         ed = c.dist_a(ev, ea);
         pend = true;
       }
       loaded = hi;
     }
   };
-  // one dirty node v (wave-uniform) at new distance dv: pull its set over tight in-edges;
-  // if it changed and v keeps its base distance, its tight successors become dirty
-  auto process = [&](uint32_t v, D dv) {
-    const uint2 r = c.gv.row(v);
+  // one dirty node v (wave-uniform, row r) at new distance dv: pull its set over tight
+  // in-edges; if it changed and v keeps its base distance, its tight successors become dirty
+  auto process = [&](uint32_t v, D dv, uint2 r) {
     const uint32_t deg = r.y - r.x;
     uint32_t cur[W], acc[W];
 #pragma unroll
@@ -901,7 +904,9 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     while (m) {
       const int k = __builtin_ctzll(m);
       m &= m - 1ull;
-      process((uint32_t)__builtin_amdgcn_readlane((int)ev, k), mn);
+      process((uint32_t)__builtin_amdgcn_readlane((int)ev, k), mn,
+              make_uint2((uint32_t)__builtin_amdgcn_readlane((int)er.x, k),
+                         (uint32_t)__builtin_amdgcn_readlane((int)er.y, k)));
       if (nd > c.cap) return kGrpOverflow;
     }
     for (uint32_t i0 = 64; i0 < nd0; i0 += 64u) {
@@ -917,7 +922,8 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       while (mo) {
         const int k = __builtin_ctzll(mo);
         mo &= mo - 1ull;
-        process((uint32_t)__builtin_amdgcn_readlane((int)v, k), mn);
+        const uint32_t vk = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+        process(vk, mn, c.gv.row(vk));
         if (nd > c.cap) return kGrpOverflow;
       }
     }
@@ -949,7 +955,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
     uint32_t cap, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
-    uint32_t* ctr, unsigned long long* prof) {
+    uint32_t* ctr, unsigned long long* prof, const uint32_t* list, uint32_t n_list, uint32_t ovf_base) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1010,11 +1016,21 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
   c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
   c.dlist = reinterpret_cast<uint16_t*>(wb + lay.w_dlist);
   const uint32_t chunks = (n_links + chunk - 1u) / chunk;
-  const uint32_t items = n_src * chunks;
+  // list pass: one item per listed unit i * n_src + j (the first pass's overflows)
+  const uint32_t items = list ? n_list : n_src * chunks;
   uint32_t n_aff = 0;
   for (uint32_t item = blockIdx.x; item < items;) {
-    const uint32_t j = item / chunks, ch = item - j * chunks;
-    const uint32_t l0 = ch * chunk, l1 = min(n_links, l0 + chunk);
+    uint32_t j, l0, l1;
+    if (list) {
+      const uint32_t u = list[item];
+      l0 = u / n_src;
+      j = u - l0 * n_src;
+      l1 = l0 + 1u;
+    } else {
+      j = item / chunks;
+      l0 = (item - j * chunks) * chunk;
+      l1 = min(n_links, l0 + chunk);
+    }
     c.src = sources[j];
     // stage source j's base rows (read once per item)
     const uint64_t* drow = base_dist + (size_t)j * V;
@@ -1081,8 +1097,9 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
       if (lane == 0) {
         if (cnt != kGrpOverflow) {
           changed[(size_t)i * n_src + j] = cnt;
-        } else {  // more dirty nodes than slots: re-solved after the launch (openr_spf_whatif)
-          const uint32_t k = atomicAdd(&affected[1], 1u);
+        } else {  // more dirty nodes than slots: repaired again by the list pass with every
+                  // slot, or re-solved after it (openr_spf_whatif)
+          const uint32_t k = ovf_base + atomicAdd(&affected[list ? 2 : 1], 1u);
           ovf_src[k] = c.src;
           ovf_link[k] = c.link;
           ovf_unit[k] = i * n_src + j;
@@ -1094,7 +1111,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
     __syncthreads();
     item = s_item;
   }
-  if (tid == 0 && n_aff) atomicAdd(affected, n_aff);
+  if (tid == 0 && n_aff && !list) atomicAdd(affected, n_aff);  // a listed unit was counted by the first pass
   if (prof && lane == 0) {
     for (int k = 0; k < 8; ++k) atomicAdd(&prof[k], c.pacc[k]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
@@ -1178,9 +1195,15 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
-                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s) {
-  hipError_t err = hipMemsetAsync(affected, 0, 2u * sizeof(uint32_t), s);  // [0] affected, [1] handed over
-  if (err != hipSuccess || !n_links || !n_src) return err;
+                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s,
+                               const uint32_t* list, uint32_t n_list) {
+  hipError_t err = hipSuccess;
+  if (!list) {  // [0] affected, [1] handed to the list pass, [2] handed over by the list pass
+    err = hipMemsetAsync(affected, 0, 3u * sizeof(uint32_t), s);
+    if (err != hipSuccess || !n_links || !n_src) return err;
+  } else if (!n_list) {
+    return hipSuccess;
+  }
   // distances as u16 when every finite one fits (V * w_max < 0xFFFF): half the LDS rows,
   // more workgroups per CU
   const bool d16 = (uint64_t)g.V * (unit_cost ? 1u : w_max) < 0xFFFFull && !bfs::env_u32("OPENR_SPF_WHATIF_D32", 0u, 0u, 1u);
@@ -1188,10 +1211,17 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // the LDS-graph variant (opt-in) with as many waves per workgroup (one workgroup per
   // CU) as fit, else the global-graph variant at OPENR_SPF_WHATIF_WAVES (3) per workgroup
   bool lg = false;
-  uint32_t waves = bfs::env_u32("OPENR_SPF_WHATIF_WAVES", 3u, 1u, kGrpMaxBlock / 64u);  // WAN: 3 / 4 / 8 -> 5.57 / 5.62 / 6.41 ms
-  const uint32_t cap = bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpMaxCap, 1u, kGrpMaxCap);  // tests force small caps
+  // First pass: few dirty slots per wave (LDS per wave ~3.2 KB on the WAN: 8 workgroups of
+  // 4 waves per CU); the units that outgrow them are listed for a re-solve, or (opt-in)
+  // repaired again by the list pass: one wave per workgroup, every slot (kGrpMaxCap), one
+  // unit per item. WAN kernel time (cap / waves): 255 / 3 4.57 ms, 160 / 3 4.07, 128 / 4
+  // 3.66, 96 / 4 3.46, 64 / 4 3.09, 48 / 4 2.90 (fewer slots: more re-solves, see
+  // openr_spf_whatif).
+  uint32_t waves = list ? 1u : bfs::env_u32("OPENR_SPF_WHATIF_WAVES", kGrpWaves, 1u, kGrpMaxBlock / 64u);
+  const uint32_t cap = list ? bfs::env_u32("OPENR_SPF_WHATIF_CAP2", kGrpMaxCap, 1u, kGrpMaxCap)
+                            : bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpCap1, 1u, kGrpMaxCap);  // tests force small caps
   auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch, cap).total; };
-  if (grp_lds_graph_ok(g, w_max, nh_bits)) {
+  if (!list && grp_lds_graph_ok(g, w_max, nh_bits)) {
     for (uint32_t w = kGrpMaxBlock / 64u; w >= 2u; --w) {
       if (layout_bytes(true, w, kGrpMaxChunk) <= kMaxLds) {
         lg = true;
@@ -1212,9 +1242,10 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
   uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
   chunk = std::min(bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30), kGrpMaxChunk);
+  if (list) chunk = 1;  // one unit per item
   const uint32_t lds = layout_bytes(lg, waves, chunk);  // the list sized to the chunk
   const uint64_t slots = slots_for(lds);
-  const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
+  const uint64_t items = list ? (uint64_t)n_list : (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
   // tuning aid: per-phase cycle sums and set sizes, printed after the launch
@@ -1233,7 +1264,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
                        base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed, affected, ovf_src, ovf_link,  \
-                       ovf_unit, ctr, prof);                                                                   \
+                       ovf_unit, ctr, prof, list, n_list, list ? n_list : 0u);                                 \
   } while (0)
   if (d16) {
     if (lg) OPENR_GRP_LAUNCH(uint16_t, true);

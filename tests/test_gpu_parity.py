@@ -553,19 +553,24 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "incr", "solve"])
+@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "group-cap2", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
     (default: graph read from global memory, u16 distances when they fit; or the graph
     staged in LDS too; or u32 / u64 distances), per-unit incremental repair, or full
-    re-solves."""
+    re-solves. group-cap: 3 dirty slots per wave, so most units are re-solved; group-cap2:
+    3 slots, then the opt-in list pass with 5 (OPENR_SPF_WHATIF_LIST=1), so some are
+    repaired twice and the rest re-solved."""
     mode = request.param
     if mode == "group-lds":
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
         monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
-    if mode == "group-cap":  # 3 dirty slots per wave: most units are re-solved
+    if mode in ("group-cap", "group-cap2"):
         monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "3")
+    if mode == "group-cap2":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_LIST", "1")
+        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP2", "5")
     monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     return request.param
 
