@@ -498,7 +498,11 @@ __host__ __device__ inline LeanLayout lean_layout(uint32_t V, uint32_t nh_words,
   return l;
 }
 
-template <int MODE, int BLOCK, bool PROF>
+// DELTA: the transit rows are read as four signed byte deltas (DevGraph::elld, 4 bytes per
+// node instead of the 16-byte ellv row: G100's rows in 40 KB instead of 160 KB, so they stay
+// in the CU's L1); a zero delta (no edge, down link, overloaded row) and a lane past the
+// level resolve to a node whose level is <= L, never tight.
+template <int MODE, int BLOCK, bool PROF, bool DELTA>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_ell_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt,
     unsigned long long* prof) {
@@ -608,8 +612,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
           const uint32_t u = idx < cur ? q : V;  // past the level: the sentinel row
           const bool st = pf && fb == 0u;        // stamps: wave 0's first pass of the level
           if (st) OPENR_LEAN_STAMP(0, u);
-          const uint4 ell = g.ellv[u];  // ellv[V] = sentinel row
-          const uint32_t vv[K] = {ell.x, ell.y, ell.z, ell.w};
+          uint32_t vv[K];
+          if constexpr (DELTA) {
+            const bool live = idx < cur;
+            const uint32_t d4 = g.elld[live ? u : 0u];
+            const uint32_t dd = live ? d4 : 0u;  // past the level: every slot is the sentinel V
+#pragma unroll
+            for (uint32_t j = 0; j < K; ++j) vv[j] = u + (uint32_t)__builtin_amdgcn_sbfe((int32_t)dd, 8u * j, 8u);
+          } else {
+            const uint4 ell = g.ellv[u];  // ellv[V] = sentinel row
+            vv[0] = ell.x;
+            vv[1] = ell.y;
+            vv[2] = ell.z;
+            vv[3] = ell.w;
+          }
           if (st) OPENR_LEAN_STAMP(1, vv[0]);
           const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
           // the level reads issue together, then the atomics
@@ -1058,14 +1074,17 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
   const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
   const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
-  auto k = want_prof ? bfs_ell_kernel<MODE, BLOCK, true> : bfs_ell_kernel<MODE, BLOCK, false>;
+  // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
+  const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
+  auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true> : bfs_ell_kernel<MODE, BLOCK, true, false>)
+                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true> : bfs_ell_kernel<MODE, BLOCK, false, false>);
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
   if (info) {
     info->lds_bytes = lds;
     info->grid = grid;
-    info->kernel = "bfs_ell_kernel<halves,u8>";
+    info->kernel = delta ? "bfs_ell_kernel<halves,u8,delta>" : "bfs_ell_kernel<halves,u8>";
   }
   // tuning aid: per-phase cycle sums of the level loop, printed after the launch
   static unsigned long long* prof_buf = nullptr;
