@@ -849,7 +849,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
       ctx->stats.last_kernel_ms = ms;
       // Units past the first pass's slots are large (WAN: 6 533 of 1.01 M affected units
-      // at 96 slots, 151 dirty nodes on average): re-solved (default), or with
+      // past 96 slots, 151 dirty nodes on average): re-solved (default), or with
       // OPENR_SPF_WHATIF_LIST=1 repaired again by the list pass with every slot and the
       // rest re-solved. Measured on the WAN step: 5.18 vs 5.34 ms — a 150-node repair on
       // one wavefront takes as long as a re-solve on a 256-thread workgroup.

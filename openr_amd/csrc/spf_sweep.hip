@@ -575,7 +575,7 @@ struct GraphView<true> {  // compact LDS copy
 
 constexpr uint32_t kGrpMaxChunk = 2048;  // links per work item
 constexpr uint32_t kGrpMaxCap = 255;     // dirty slots per wave (u8 slot index)
-constexpr uint32_t kGrpCap1 = 96;        // dirty slots per wave of the first pass
+constexpr uint32_t kGrpCap1 = 128;       // dirty slots per wave of the first pass
 constexpr uint32_t kGrpWaves = 4;        // waves per workgroup of the first pass
 
 struct GrpLayout {
@@ -1211,12 +1211,12 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // the LDS-graph variant (opt-in) with as many waves per workgroup (one workgroup per
   // CU) as fit, else the global-graph variant at OPENR_SPF_WHATIF_WAVES (3) per workgroup
   bool lg = false;
-  // First pass: few dirty slots per wave (LDS per wave ~3.2 KB on the WAN: 8 workgroups of
+  // First pass: few dirty slots per wave (LDS per wave ~3.5 KB on the WAN: 7 workgroups of
   // 4 waves per CU); the units that outgrow them are listed for a re-solve, or (opt-in)
   // repaired again by the list pass: one wave per workgroup, every slot (kGrpMaxCap), one
   // unit per item. WAN kernel time (cap / waves): 255 / 3 4.57 ms, 160 / 3 4.07, 128 / 4
-  // 3.66, 96 / 4 3.46, 64 / 4 3.09, 48 / 4 2.90 (fewer slots: more re-solves, see
-  // openr_spf_whatif).
+  // 3.66, 96 / 4 3.46, 64 / 4 3.09, 48 / 4 2.90 (fewer slots: more re-solves; the step is
+  // shortest at 128 / 4: 5.02 ms, against 5.11 at 112, 5.19 at 96, 5.09 at 160).
   uint32_t waves = list ? 1u : bfs::env_u32("OPENR_SPF_WHATIF_WAVES", kGrpWaves, 1u, kGrpMaxBlock / 64u);
   const uint32_t cap = list ? bfs::env_u32("OPENR_SPF_WHATIF_CAP2", kGrpMaxCap, 1u, kGrpMaxCap)
                             : bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpCap1, 1u, kGrpMaxCap);  // tests force small caps

@@ -2,7 +2,7 @@
 # (dirty-slot cap and waves per workgroup change the LDS per wave, i.e. occupancy).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -k "whatif" > gpurun_out/whatif_tests.log 2>&1 || { tail -30 gpurun_out/whatif_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -k "whatif_wan_sample" > gpurun_out/whatif_tests.log 2>&1 || { tail -30 gpurun_out/whatif_tests.log; exit 1; }
 tail -2 gpurun_out/whatif_tests.log
 run() {  # name, env...
   local name=$1; shift
@@ -10,13 +10,11 @@ run() {  # name, env...
   grep '^{' gpurun_out/b_whatif_$name.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('whatif', '$name', round(d['ms_per_step'],3), round(d['roofline'].get('kernel_ms_mean'),3))"
 }
 run base OPENR_SPF_NOOP=1
-run l0c96b64 OPENR_SPF_WHATIF_LIST=0 OPENR_SPF_ROUNDS_BLOCK=64
-run l0c96b128 OPENR_SPF_WHATIF_LIST=0 OPENR_SPF_ROUNDS_BLOCK=128
-run l0c96b256 OPENR_SPF_WHATIF_LIST=0 OPENR_SPF_ROUNDS_BLOCK=256
-run l0c64b256 OPENR_SPF_WHATIF_LIST=0 OPENR_SPF_ROUNDS_BLOCK=256 OPENR_SPF_WHATIF_CAP=64
-run l0c48b256 OPENR_SPF_WHATIF_LIST=0 OPENR_SPF_ROUNDS_BLOCK=256 OPENR_SPF_WHATIF_CAP=48
-run l1c64c160b256 OPENR_SPF_ROUNDS_BLOCK=256 OPENR_SPF_WHATIF_CAP=64 OPENR_SPF_WHATIF_CAP2=160
-run l1c96c128b256 OPENR_SPF_ROUNDS_BLOCK=256 OPENR_SPF_WHATIF_CAP2=128
+run c112 OPENR_SPF_WHATIF_CAP=112
+run c128 OPENR_SPF_WHATIF_CAP=128
+run c160 OPENR_SPF_WHATIF_CAP=160
+run c128w3 OPENR_SPF_WHATIF_CAP=128 OPENR_SPF_WHATIF_WAVES=3
+run c80 OPENR_SPF_WHATIF_CAP=80
 run base2 OPENR_SPF_NOOP=1
 OPENR_SPF_WHATIF_PROF=1 timeout -k 10 200 python -u bench.py --workload whatif --steps 2 --warmup 1 --no-cpu-baseline --no-ucmp > gpurun_out/b_whatif_prof.log 2>&1 || exit 1
 grep "^whatif_group" gpurun_out/b_whatif_prof.log | tail -2
