@@ -895,7 +895,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
 }
 
 // Bytes of second-SPF distance rows a KSP2 batch may hold on a device at once.
-constexpr size_t kKspChunkBytes = size_t(2) << 30;
+constexpr size_t kKspChunkBytes = size_t(8) << 30;  // second-SPF rows + ignore slots per chunk
 
 // getKthPaths(src, dest, 1) and (.., 2) for a batch of pairs on one device: the base SPF
 // of every listed source (the reference's memoized getSpfResult), then per chunk of
@@ -939,8 +939,16 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   const char* tag_env = std::getenv("OPENR_SPF_KSP_TAG");  // 0: untagged rows, unreached fill (A/B)
   const bool tagged = rows16 && tag_max && !(tag_env && std::atoi(tag_env) == 0);
   const size_t row_bytes = (size_t)V * (rows16 ? 2u : 8u);
+  // pairs per chunk from a byte budget for the chunk's rows and ignore slots (8 GiB of the
+  // 288 GB; OPENR_SPF_KSP_CHUNK_MB overrides). Fabric, 512 sources x all destinations, ms
+  // per step by budget: 2 GiB (~150 k pairs) 254.3, 4 GiB 248.3, 8 GiB 246.8, 16 GiB 246.4;
+  // by pairs: 65 536 271.6, 32 768 297.0, 16 384 351.0, 8 192 470.8. Per-chunk launches
+  // and kernel tails dominate, not the rows' cache locality.
+  size_t chunk_budget = kKspChunkBytes;
+  if (const char* e = std::getenv("OPENR_SPF_KSP_CHUNK_MB"); e && std::atoi(e) >= 64 && std::atoi(e) <= 65536)
+    chunk_budget = (size_t)std::atoi(e) << 20;
   uint32_t chunk =
-      (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, kKspChunkBytes / (row_bytes + 4u * ign_cap)));
+      (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, chunk_budget / (row_bytes + 4u * ign_cap)));
   if (const char* e = std::getenv("OPENR_SPF_KSP_CHUNK"))  // pairs per chunk (tests: many chunks, tag wrap)
     if (std::atoi(e) > 0) chunk = std::min<uint32_t>(chunk, (uint32_t)std::atoi(e));
   // OPENR_SPF_KSP_LANES=2: two pipeline lanes (chunks alternate between the caller's
