@@ -10,11 +10,10 @@ run() {  # name, env...
   grep '^{' gpurun_out/b_whatif_$name.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('whatif', '$name', round(d['ms_per_step'],3), round(d['roofline'].get('kernel_ms_mean'),3))"
 }
 run base OPENR_SPF_NOOP=1
-run c112 OPENR_SPF_WHATIF_CAP=112
-run c128 OPENR_SPF_WHATIF_CAP=128
-run c160 OPENR_SPF_WHATIF_CAP=160
-run c128w3 OPENR_SPF_WHATIF_CAP=128 OPENR_SPF_WHATIF_WAVES=3
-run c80 OPENR_SPF_WHATIF_CAP=80
+run w5 OPENR_SPF_WHATIF_WAVES=5
+run w6 OPENR_SPF_WHATIF_WAVES=6
+run c144 OPENR_SPF_WHATIF_CAP=144
+run c128w5c144 OPENR_SPF_WHATIF_CAP=144 OPENR_SPF_WHATIF_WAVES=5
 run base2 OPENR_SPF_NOOP=1
 OPENR_SPF_WHATIF_PROF=1 timeout -k 10 200 python -u bench.py --workload whatif --steps 2 --warmup 1 --no-cpu-baseline --no-ucmp > gpurun_out/b_whatif_prof.log 2>&1 || exit 1
 grep "^whatif_group" gpurun_out/b_whatif_prof.log | tail -2
