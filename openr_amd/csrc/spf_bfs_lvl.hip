@@ -502,8 +502,12 @@ __host__ __device__ inline LeanLayout lean_layout(uint32_t V, uint32_t nh_words,
 // node instead of the 16-byte ellv row: G100's rows in 40 KB instead of 160 KB, so they stay
 // in the CU's L1); a zero delta (no edge, down link, overloaded row) and a lane past the
 // level resolve to a node whose level is <= L, never tight.
-template <int MODE, int BLOCK, bool PROF, bool DELTA>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_ell_kernel(
+// WPE: the waves-per-SIMD target the compiler allocates registers for. LDS caps G100 at
+// 10 workgroups of 2 waves per CU (5 per SIMD); a target of 8 (default) squeezes the pass
+// into 78 SGPRs with 29 spilled to VGPR lanes (v_writelane / v_readlane in the level
+// loop), a target of 5 (OPENR_SPF_LEAN_WPE=5) leaves 106 SGPRs and 6 spills.
+template <int MODE, int BLOCK, bool PROF, bool DELTA, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void bfs_ell_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt,
     unsigned long long* prof) {
   using N = Nh<MODE>;
@@ -1076,8 +1080,11 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
   // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
   const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
-  auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true> : bfs_ell_kernel<MODE, BLOCK, true, false>)
-                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true> : bfs_ell_kernel<MODE, BLOCK, false, false>);
+  // OPENR_SPF_LEAN_WPE=5: the register target with fewer SGPR spills (A/B; 8 by default)
+  const bool wpe8 = env_u32("OPENR_SPF_LEAN_WPE", 8u, 5u, 8u) == 8u;
+  auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true, 8> : bfs_ell_kernel<MODE, BLOCK, true, false, 8>)
+           : wpe8    ? (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 8> : bfs_ell_kernel<MODE, BLOCK, false, false, 8>)
+                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 5> : bfs_ell_kernel<MODE, BLOCK, false, false, 5>);
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;

@@ -950,8 +950,11 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
 
 constexpr uint32_t kGrpMaxBlock = 512;
 
-template <typename D, bool LG, uint32_t W>
-__global__ __launch_bounds__(kGrpMaxBlock) void whatif_group_kernel(
+// WPE: waves per SIMD the compiler must fit registers for (1: no constraint). Unconstrained
+// the default variant takes 119 VGPRs, i.e. 4 waves per SIMD (16 per CU) whatever LDS
+// allows; 5 / 7 force 96 / 72 VGPRs at the price of scratch spills (44 / 140 B per lane).
+template <typename D, bool LG, uint32_t W, int WPE>
+__global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
     uint32_t cap, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
@@ -1256,9 +1259,13 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     prof = prof_buf;
     if (prof) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
   }
+  // OPENR_SPF_WHATIF_WPE=5|7: register target of the <= 32-bit-set variant (A/B)
+  const uint32_t wpe = bfs::env_u32("OPENR_SPF_WHATIF_WPE", 1u, 1u, 8u);
 #define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
   do {                                                                                                         \
-    auto k = nb <= 4u ? whatif_group_kernel<DT, LGV, 1> : whatif_group_kernel<DT, LGV, kGrpNhWords>;                                                                     \
+    auto k = nb <= 4u ? (wpe == 5u ? whatif_group_kernel<DT, LGV, 1, 5>                                        \
+                                   : wpe == 7u ? whatif_group_kernel<DT, LGV, 1, 7> : whatif_group_kernel<DT, LGV, 1, 1>) \
+                      : whatif_group_kernel<DT, LGV, kGrpNhWords, 1>;                                          \
     err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
