@@ -15,7 +15,7 @@ LIBDIR := openr_amd/lib
 CSRC := openr_amd/csrc
 
 ENGINE := $(LIBDIR)/libopenr_spf.so
-ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_bfs.hip $(CSRC)/spf_bfs_lvl.hip $(CSRC)/spf_allsrc.hip $(CSRC)/spf_wreach.hip $(CSRC)/spf_sweep.hip $(CSRC)/spf_fringe.hip $(CSRC)/spf_rounds.hip $(CSRC)/spf_ksp.hip $(CSRC)/spf_update.hip $(CSRC)/spf_exact.hip $(CSRC)/spf_capi.hip
+ENGINE_SRCS := $(CSRC)/spf_kernels.hip $(CSRC)/spf_bfs.hip $(CSRC)/spf_bfs_lvl.hip $(CSRC)/spf_sweep.hip $(CSRC)/spf_fringe.hip $(CSRC)/spf_rounds.hip $(CSRC)/spf_ksp.hip $(CSRC)/spf_update.hip $(CSRC)/spf_exact.hip $(CSRC)/spf_capi.hip
 ENGINE_HDRS := $(CSRC)/spf_kernels.h $(CSRC)/spf_device.h $(CSRC)/spf_bfs_common.h include/openr_spf.h
 ENGINE_OBJS := $(patsubst $(CSRC)/%.hip,$(LIBDIR)/%.o,$(ENGINE_SRCS))
 

@@ -608,8 +608,8 @@ const LinkState::SpfResult& LinkState::materialize(const MemoEntry& e, bool useL
   if (e.row == UINT32_MAX) return e.res;
   MemoEntry& me = const_cast<MemoEntry&>(e);
   std::call_once(*me.once.f, [&]() {
-    const CsrMirror& m = mirror_;
-    const DenseRows& d = dense_[useLinkMetric ? 1 : 0];
+    const CsrMirror& m = e.snap ? e.snap->mirror : mirror_;
+    const DenseRows& d = e.snap ? e.snap->rows[useLinkMetric ? 1 : 0] : dense_[useLinkMetric ? 1 : 0];
     const uint32_t V = (uint32_t)m.names.size(), src = d.src[e.row];
     const uint64_t* dist = d.dist.data() + (size_t)e.row * V;
     const uint8_t* h = d.nh.data() + (size_t)e.row * V * d.nb;
@@ -747,19 +747,26 @@ LinkState::SpfView LinkState::getSpfView(const std::string& nodeName, bool useLi
     v.map_ = &e.res;
     return v;
   }
-  const DenseRows& d = dense_[useLinkMetric ? 1 : 0];
-  v.m_ = &mirror_;
-  const size_t V = mirror_.names.size();
-  v.dist_ = d.dist.data() + (size_t)e.row * V;
-  v.nh_ = d.nh.data() + (size_t)e.row * V * d.nb;
-  v.nb_ = d.nb;
-  v.nbrs_ = &d.nbrs[e.row];
+  v.m_ = e.snap ? &e.snap->mirror : &mirror_;
+  v.rows_ = e.snap ? &e.snap->rows[useLinkMetric ? 1 : 0] : &dense_[useLinkMetric ? 1 : 0];
+  v.row_ = e.row;
+  v.keep_ = e.snap;
   return v;
+}
+
+const uint64_t* LinkState::SpfView::dist() const {
+  const DenseRows& d = *static_cast<const DenseRows*>(rows_);
+  return d.dist.data() + (size_t)row_ * m_->names.size();
+}
+
+const uint8_t* LinkState::SpfView::nh(uint32_t v) const {
+  const DenseRows& d = *static_cast<const DenseRows*>(rows_);
+  return d.nh.data() + ((size_t)row_ * m_->names.size() + v) * d.nb;
 }
 
 int32_t LinkState::SpfView::id(const std::string& node) const {
   auto it = m_->id.find(node);
-  if (it == m_->id.end() || dist_[it->second] == UINT64_MAX) return -1;
+  if (it == m_->id.end() || dist()[it->second] == UINT64_MAX) return -1;
   return (int32_t)it->second;
 }
 
@@ -772,7 +779,7 @@ LinkStateMetric LinkState::SpfView::metric(const std::string& node) const {
   if (map_) return map_->at(node).metric();
   const int32_t v = id(node);
   if (v < 0) throw std::out_of_range("SpfView::metric: " + node + " not reached");
-  return dist_[v];
+  return dist()[v];
 }
 
 std::vector<std::string> LinkState::SpfView::nextHops(const std::string& node) const {
@@ -784,10 +791,30 @@ std::vector<std::string> LinkState::SpfView::nextHops(const std::string& node) c
   }
   const int32_t v = id(node);
   if (v < 0) throw std::out_of_range("SpfView::nextHops: " + node + " not reached");
-  const uint8_t* hv = nh_ + (size_t)v * nb_;
-  for (uint32_t i = 0; i < nbrs_->size(); ++i)
-    if ((hv[i >> 3] >> (i & 7)) & 1u) out.push_back(m_->names[(*nbrs_)[i]]);
+  const DenseRows& d = *static_cast<const DenseRows*>(rows_);
+  const uint8_t* hv = nh((uint32_t)v);
+  const std::vector<uint32_t>& nbrs = d.nbrs[row_];
+  for (uint32_t i = 0; i < nbrs.size(); ++i)
+    if ((hv[i >> 3] >> (i & 7)) & 1u) out.push_back(m_->names[nbrs[i]]);
   return out;
+}
+
+void LinkState::retireDenseRows() {
+  // rows are indexed by the ids of mirror_ (they were solved on it; a pending patch would
+  // have cleared the memo first, so no entry points at a stale row)
+  if (mirrorDirty_) return;
+  std::shared_ptr<RowSnapshot> snap;
+  for (auto& kv : spfResults_) {
+    MemoEntry& e = kv.second;
+    if (e.row == UINT32_MAX || e.snap) continue;
+    if (!snap) {
+      snap = std::make_shared<RowSnapshot>();
+      snap->mirror = std::move(mirror_);
+      snap->rows[0] = std::move(dense_[0]);
+      snap->rows[1] = std::move(dense_[1]);
+    }
+    e.snap = snap;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -362,7 +362,10 @@ class LinkState {
   // Dense view of a memoised SPF (route build fast path, round 3): the same result
   // getSpfResult(node, useLinkMetric) holds — reached nodes, metrics, next hops — read from
   // the memo's dense rows without materialising the SpfResult map. Counts the SPF run like
-  // getSpfResult (first read of the memo entry). Valid until the next topology change.
+  // getSpfResult (first read of the memo entry). The view resolves its row on every access,
+  // so later SPF reads and prefetches (which grow the dense rows) leave it valid; like the
+  // reference's SpfResult reference, it is invalidated by the next adjacency / overload
+  // update of the LinkState (updateAdjacencyDatabase, deleteAdjacencyDatabase, decrementHolds).
   class SpfView {
    public:
     bool reached(const std::string& node) const;
@@ -377,10 +380,11 @@ class LinkState {
     // zero / wrapped metrics): then every call reads it
     const SpfResult* map_ = nullptr;
     const CsrMirror* m_ = nullptr;
-    const uint64_t* dist_ = nullptr;
-    const uint8_t* nh_ = nullptr;
-    uint32_t nb_ = 1;
-    const std::vector<uint32_t>* nbrs_ = nullptr;
+    const void* rows_ = nullptr;  // the DenseRows holding row_ (resolved per access)
+    uint32_t row_ = 0;
+    std::shared_ptr<const void> keep_;  // a retired row snapshot the view reads (see RowSnapshot)
+    const uint64_t* dist() const;
+    const uint8_t* nh(uint32_t v) const;
     int32_t id(const std::string& node) const;
   };
   SpfView getSpfView(const std::string& nodeName, bool useLinkMetric = true) const;
@@ -412,11 +416,15 @@ class LinkState {
       return *this;
     }
   };
+  struct RowSnapshot;
   struct MemoEntry {
     SpfResult res;
     RelaxedFlag counted;
     double ms = 0;
     uint32_t row = UINT32_MAX;  // dense row of the result (materialised into res on first read), or none
+    // the mirror + rows `row` indexes when a rebuild of the mirror retired them (null: the
+    // live mirror_ / dense_)
+    std::shared_ptr<const RowSnapshot> snap;
     LazyOnce once;
   };
   // Dense memo rows per useLinkMetric (round 3): the results the memo holds as the engine
@@ -434,6 +442,16 @@ class LinkState {
     void clear() { *this = DenseRows{}; }
   };
   mutable DenseRows dense_[2];
+  // A structural change that the reference does not count as a topology change (a node's
+  // first adjacency database, a link that is added or removed while not up) keeps the memo
+  // (LinkState.cpp:714-717 clear it only on topologyChanged) but rebuilds the mirror, whose
+  // node ids the dense rows are indexed by. The memo entries that point at rows then move,
+  // with those rows and the mirror they were solved on, into a shared snapshot.
+  struct RowSnapshot {
+    CsrMirror mirror;
+    DenseRows rows[2];
+  };
+  void retireDenseRows();
   mutable UpdateStats ustats_;
   bool denseEligible(bool useLinkMetric) const;
   void refreshDense(bool useLinkMetric, double* ms) const;
@@ -475,8 +493,9 @@ class LinkState {
   std::vector<std::shared_ptr<Link>> getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const;
   std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;
   void markMirrorDirty() {
+    retireDenseRows();  // node ids change with the rebuilt mirror
     mirrorDirty_ = true;
-    dense_[0].clear();  // node ids change with the rebuilt mirror
+    dense_[0].clear();
     dense_[1].clear();
   }
 

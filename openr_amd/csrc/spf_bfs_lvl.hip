@@ -714,299 +714,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
   retire_workgroup(ctr, nullptr);
 }
 
-// ---------------------------------------------------------------------------
-// Lean pass with 2-bit level codes (round 3, `bfs_ell2_kernel`, OPENR_SPF_BFS_LEAN2). The
-// lean pass keeps an exact u8 level per node in LDS (10 KB of its 16.3 KB on G100), yet the
-// level loop only asks one question of it: is v unreached or on level L+1 (tight)? A node
-// u's usable neighbours lie on levels L-1..L+1 once u expands, and a node is never tight
-// again after it has been expanded, so a 2-bit code answers it: 0 = unreached, 1 + (l & 1)
-// = on level l, 3 = final (expanded, the source, the sentinel, an overloaded node after
-// its empty expansion). An arrival from level L is tight iff code(v) is 0 or 1 + ((L + 1) & 1);
-// a frontier node is marked final when its level is expanded. 2.5 KB instead of 10 KB per
-// solve: 16 workgroups per CU instead of 9 on G100.
-//
-// The exact levels (the distance row) come from the BFS order instead: the appending
-// arrival also stores v, coalesced, at its order index in a global per-workgroup array
-// (level l occupies order[bnd[l], bnd[l + 1]), bnd in LDS), and the write-out scatters the
-// order's levels into the LDS region the codes / sets / queue held (after the next-hop row
-// has been written from it), in as many node ranges as that region needs, and streams the
-// distance row out of it. Semantics and fallbacks as bfs_ell_kernel.
-// ---------------------------------------------------------------------------
-struct Lean2Layout {
-  uint32_t bnd, code, nh, ring, dummy, total, region;
-};
-// [0, 32) control, bnd [256] u16, 2-bit codes (node V = sentinel), next-hop words, two
-// queue halves, dummies; region = [code, dummy): the write-out's level chunk
-__host__ __device__ inline Lean2Layout lean2_layout(uint32_t V, uint32_t nh_words, uint32_t ring_cap) {
-  Lean2Layout l;
-  uint32_t off = 32u;
-  l.bnd = off;
-  off += 2u * 256u;
-  l.code = off;
-  off += (4u * ((V + 1u + 15u) / 16u) + 15u) & ~15u;
-  l.nh = off;
-  off += (4u * (nh_words + 1u) + 15u) & ~15u;
-  l.ring = off;
-  off += (2u * ring_cap + 15u) & ~15u;
-  l.dummy = off;
-  l.region = (l.dummy - l.code) & ~15u;
-  off += 4u * 64u;
-  l.total = off;
-  return l;
-}
-
-template <int MODE, int BLOCK>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void bfs_ell2_kernel(
-    DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
-  using N = Nh<MODE>;
-  static_assert(N::kSingle, "single-dword next-hop fields only");
-  constexpr uint32_t kBits = 32u / N::kPer;
-  constexpr uint32_t kLog = kBits == 4 ? 3 : kBits == 8 ? 2 : kBits == 16 ? 1 : 0;
-  constexpr uint32_t kShl = 5u - kLog;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // no static LDS: smem is LDS address 0
-  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nh_words = N::words(V);
-  const Lean2Layout lay = lean2_layout(V, nh_words, ring_cap);
-  lds_u32* const ctl = (lds_u32*)(size_t)0u;  // [0..3] append counters, [7] next unit
-  lds_u16* const bnd = (lds_u16*)(size_t)lay.bnd;
-  lds_u32* const code = (lds_u32*)(size_t)lay.code;
-  lds_u32* const nh = (lds_u32*)(size_t)lay.nh;
-  lds_u16* const ring = (lds_u16*)(size_t)lay.ring;
-  lds_u32* const my_dummy = (lds_u32*)(size_t)(lay.dummy + 4u * lane);
-  lds_u8* const reg8 = (lds_u8*)(size_t)lay.code;  // write-out level chunk
-  lds_u32* const reg32 = (lds_u32*)(size_t)lay.code;
-  const uint32_t code_words = (V + 1u + 15u) / 16u;
-  const uint32_t half = ring_cap / 2u;
-  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
-  uint16_t* const order = a.order16 + (size_t)blockIdx.x * V;  // this workgroup's BFS order
-  *my_dummy = 0xFFFFFFFFu;
-  auto code_of = [&](uint32_t v) { return (code[v >> 4] >> ((v & 15u) * 2u)) & 3u; };
-
-  for (uint32_t unit = blockIdx.x; unit < count;) {
-    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
-    const uint32_t src = a.sources[sid];
-    if (src < V) {  // block-uniform
-      for (uint32_t i = tid; i < code_words; i += BLOCK) code[i] = 0u;
-      for (uint32_t i = tid; i <= nh_words; i += BLOCK) nh[i] = 0u;
-      if (tid < 5) ctl[tid] = 0;
-      __syncthreads();
-      if (tid == 0) {
-        lds_or(&code[src >> 4], 3u << ((src & 15u) * 2u));  // the source: final
-        lds_or(&code[V >> 4], 3u << ((V & 15u) * 2u));      // the ELL sentinel: final
-        bnd[0] = 0;
-        bnd[1] = 1;
-        order[0] = (uint16_t)src;
-      }
-      __syncthreads();
-      // level 0: the source expands even when overloaded; a directly connected node's
-      // next hop is the node itself (LinkState.cpp:867-872). Level 1 goes to half 1.
-      {
-        const uint2 rs = g.row2[src];
-        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
-          const uint32_t e = e0 + tid;
-          bool fresh = false;
-          uint32_t v = 0;
-          if (e < rs.y) {
-            const uint32_t av = g.adj[e];
-            v = av & ~kEdgeDown;
-            if (!(av & kEdgeDown) && v != src) {
-              const uint32_t sh = (v << kShl) & 31u;
-              fresh = ((lds_or(&nh[v >> kLog], (1u << g.nbr[e]) << sh) >> sh) & N::kMask) == 0u;
-            }
-          }
-          const uint32_t slot = wave_append(fresh, reinterpret_cast<uint32_t*>(smem) + 1);
-          if (fresh) {  // slot < deg(src) <= half (host-checked)
-            ring[half + slot] = (uint16_t)v;
-            lds_or(&code[v >> 4], 2u << ((v & 15u) * 2u));  // level 1: code 1 + (1 & 1)
-            order[1u + slot] = (uint16_t)v;
-          }
-        }
-      }
-      __syncthreads();
-
-      uint32_t cur = __builtin_amdgcn_readfirstlane(ctl[1]), L = 1, reached = 1u + cur;
-      if (tid == 0) bnd[2] = (uint16_t)reached;
-      bool overflow = false;  // block-uniform
-      constexpr uint32_t K = 4u, NPP = 64u, NPB = (uint32_t)BLOCK;
-      uint32_t q = ring[half + wave * NPP + lane];
-      while (cur) {
-        if (L + 1u >= 0xFFu) {  // the write-out keeps u8 levels
-          overflow = true;
-          break;
-        }
-        lds_u32* const cnt = &ctl[(L + 1u) & 3u];
-        if (tid == 0) ctl[(L + 2u) & 3u] = 0;
-        const uint32_t rd = (L & 1u) * half, wr = half - rd;
-        const uint32_t cnext = 1u + ((L + 1u) & 1u);  // the code of level L+1
-        for (uint32_t fb = wave * NPP; fb < cur; fb += NPB) {
-          const uint32_t idx = fb + lane;
-          if (fb != wave * NPP) q = ring[rd + idx];
-          const bool live = idx < cur;
-          const uint32_t u = live ? q : V;  // past the level: the sentinel row
-          const uint4 ell = g.ellv[u];
-          const uint32_t vv[K] = {ell.x, ell.y, ell.z, ell.w};
-          const uint32_t x = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);  // final since L-1
-          if (live) lds_or(&code[u >> 4], 3u << ((u & 15u) * 2u));  // u expands now: final
-          uint32_t cv[K], old[K];
-#pragma unroll
-          for (uint32_t j = 0; j < K; ++j) cv[j] = code_of(vv[j]);
-#pragma unroll
-          for (uint32_t j = 0; j < K; ++j) {
-            const uint32_t v = vv[j];
-            const bool tight = cv[j] == 0u || cv[j] == cnext;  // unreached, or on level L+1
-            old[j] = lds_or(tight ? &nh[v >> kLog] : my_dummy, x << ((v << kShl) & 31u));
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          unsigned long long bj[K];
-          bool fresh[K];
-          uint32_t off[K + 1];
-          off[0] = 0;
-#pragma unroll
-          for (uint32_t j = 0; j < K; ++j) {
-            fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;
-            bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
-            off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
-          }
-          const uint32_t total = off[K];
-          if (total) {  // wave-uniform
-            const uint32_t leader = (uint32_t)__builtin_amdgcn_readfirstlane(lane);
-            uint32_t wbase = 0;
-            if (lane == leader) wbase = lds_add(cnt, total);
-            const uint32_t bse = __builtin_amdgcn_readfirstlane(wbase);
-            if (bse + total <= half) {
-#pragma unroll
-              for (uint32_t j = 0; j < K; ++j) {
-                if (fresh[j]) {
-                  const uint32_t slot = bse + off[j] + __builtin_amdgcn_mbcnt_hi(
-                                                           (uint32_t)(bj[j] >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
-                  const uint32_t v = vv[j];
-                  ring[wr + slot] = (uint16_t)v;
-                  // only the appending arrival sets v's code; an earlier reader of this
-                  // level saw 0 (unreached), i.e. tight, as it is
-                  lds_or(&code[v >> 4], cnext << ((v & 15u) * 2u));
-                  order[reached + slot] = (uint16_t)v;
-                }
-              }
-            } else if (lane == leader) {
-              lds_or(cnt, 0x80000000u);
-            }
-          }
-        }
-        lds_barrier();
-        const uint32_t c = __builtin_amdgcn_readfirstlane(*cnt);
-        q = ring[wr + wave * NPP + lane];
-        ++L;
-        if (c >> 31) {
-          overflow = true;
-          break;
-        }
-        cur = c;
-        reached += cur;
-        if (tid == 0) bnd[L + 1u] = (uint16_t)reached;  // read after the next barrier
-        if (reached == V) break;  // every node reached: the newest level cannot expand tightly
-      }
-      if (overflow) {
-        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
-      } else {
-        __syncthreads();  // the order stores and bnd are visible to the workgroup
-        const bool ntb = nt != 0;
-        // next-hop row first: the codes / sets / queue region then takes the levels
-        if (a.nh) {
-          const uint32_t nb = a.nh_bytes;
-          uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
-          const bool aligned4 = ((reinterpret_cast<uintptr_t>(nrow) | V) & 3u) == 0;
-          if (MODE == kNhNibble && nb == 1 && aligned4) {
-            uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
-            for (uint32_t i = tid; i < V / 4u; i += BLOCK) {
-              const uint32_t h = (nh[i >> 1] >> ((i & 1u) * 16u)) & 0xFFFFu;
-              store_row<uint32_t>(&nrow32[i],
-                                  (h & 0xFu) | ((h & 0xF0u) << 4) | ((h & 0xF00u) << 8) | ((h & 0xF000u) << 12), ntb);
-            }
-          } else if (MODE == kNhByte && nb == 1 && aligned4) {
-            uint32_t* nrow32 = reinterpret_cast<uint32_t*>(nrow);
-            for (uint32_t i = tid; i < V / 4u; i += BLOCK) store_row<uint32_t>(&nrow32[i], (uint32_t)nh[i], ntb);
-          } else {
-            for (uint32_t i = tid; i < V * nb; i += BLOCK) {
-              const uint32_t v = i / nb, j = i - v * nb;
-              const uint32_t f = __builtin_amdgcn_ubfe(nh[v >> kLog], v << kShl, kBits);
-              nrow[i] = 8u * j < kBits ? (uint8_t)(f >> (8u * j)) : (uint8_t)0;
-            }
-          }
-        }
-        // distance row: node range [b0, b0 + chunk) at a time through the LDS region
-        uint64_t* drow = a.dist + out_row_of(a, sid) * V;
-        const bool fast = ((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0;
-        const uint32_t chunk = lay.region;  // multiple of 16
-        for (uint32_t b0 = 0; b0 < V; b0 += chunk) {
-          const uint32_t nv = min(chunk, V - b0);
-          __syncthreads();  // the region's previous contents are consumed
-          for (uint32_t i = tid; i < (nv + 3u) / 4u; i += BLOCK) reg32[i] = 0xFFFFFFFFu;  // unreached
-          __syncthreads();
-          uint32_t lev = 0;  // level of order index k: bnd[lev] <= k < bnd[lev + 1]
-          for (uint32_t k = tid; k < reached; k += BLOCK) {
-            while (k >= (uint32_t)bnd[lev + 1u]) ++lev;
-            const uint32_t v = order[k];
-            if (v - b0 < nv) reg8[v - b0] = (uint8_t)lev;
-          }
-          __syncthreads();
-          if (fast) {
-            ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow + b0);
-            for (uint32_t i = tid; i < nv / 4u; i += BLOCK) {
-              const uint32_t w = reg32[i];
-              uint64_t xd[4];
-#pragma unroll
-              for (uint32_t j = 0; j < 4u; ++j) {
-                const uint32_t l = (w >> (8u * j)) & 0xFFu;
-                xd[j] = l != 0xFFu ? (uint64_t)l * cost : ~0ull;
-              }
-              if (ntb) {
-                __builtin_nontemporal_store(xd[0], &d2[2u * i].x);
-                __builtin_nontemporal_store(xd[1], &d2[2u * i].y);
-                __builtin_nontemporal_store(xd[2], &d2[2u * i + 1u].x);
-                __builtin_nontemporal_store(xd[3], &d2[2u * i + 1u].y);
-              } else {
-                d2[2u * i] = make_ulonglong2(xd[0], xd[1]);
-                d2[2u * i + 1u] = make_ulonglong2(xd[2], xd[3]);
-              }
-            }
-          } else {
-            for (uint32_t i = tid; i < nv; i += BLOCK) {
-              const uint32_t l = reg8[i];
-              store_row<uint64_t>(&drow[b0 + i], l != 0xFFu ? (uint64_t)l * cost : ~0ull, ntb);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();  // every lane is done with this unit's LDS and ctl[7]
-    if (tid == 0) ctl[7] = gridDim.x + atomicAdd(&ctr[0], 1u);
-    __syncthreads();
-    unit = ctl[7];
-  }
-  retire_workgroup(ctr, nullptr);
-}
-
-template <int MODE, int BLOCK>
-hipError_t launch_lvl_lean2(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr,
-                            uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
-  const uint32_t lds = lean2_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
-  const uint32_t grid = std::min<uint32_t>(blocks_for(a.n, lds, num_cus, BLOCK), lean2_max_grid(num_cus));
-  auto k = bfs_ell2_kernel<MODE, BLOCK>;
-  hipError_t err =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return err;
-  if (info) {
-    info->lds_bytes = lds;
-    info->grid = grid;
-    info->kernel = "bfs_ell2_kernel<codes2>";
-  }
-  note_launch("bfs_ell2_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, ctr, ovf_count, nt_stores());
-  return hipGetLastError();
-}
-
 // Occupancy first (target workgroups per CU, 8 by default): the full-order u16 variant
 // when it fits the per-workgroup budget, else the u8 ring when a ring wide enough for the
 // estimated two-level frontier fits and the estimated depth stays under the u8 limit;
@@ -1076,15 +783,14 @@ template <int MODE, int BLOCK>
 hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr,
                            uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
-  const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
+  uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
+  // OPENR_SPF_LEAN_WGS (tuning): at most this many workgroups per CU (occupancy sweep)
+  if (const uint32_t cap = env_u32("OPENR_SPF_LEAN_WGS", 0u, 0u, 16u)) grid = std::min<uint32_t>(grid, cap * (uint32_t)num_cus);
   const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
   // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
   const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
-  // OPENR_SPF_LEAN_WPE=5: the register target with fewer SGPR spills (A/B; 8 by default)
-  const bool wpe8 = env_u32("OPENR_SPF_LEAN_WPE", 8u, 5u, 8u) == 8u;
   auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true, 8> : bfs_ell_kernel<MODE, BLOCK, true, false, 8>)
-           : wpe8    ? (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 8> : bfs_ell_kernel<MODE, BLOCK, false, false, 8>)
-                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 5> : bfs_ell_kernel<MODE, BLOCK, false, false, 5>);
+                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 8> : bfs_ell_kernel<MODE, BLOCK, false, false, 8>);
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
@@ -1365,8 +1071,7 @@ hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost,
                            uint32_t* ctr, uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = wave_layout(g.V, nh_words_for(MODE, g.V), qhalf, waves).total;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cus, (a.n + waves - 1u) / waves));
-  // OPENR_SPF_WAVE_UNROLL: frontier chunks per step (1 or 2)
-  auto k = env_u32("OPENR_SPF_WAVE_UNROLL", 1u, 1u, 2u) == 2u ? bfs_wave_kernel<MODE, 2> : bfs_wave_kernel<MODE, 1>;
+  auto k = bfs_wave_kernel<MODE, 1>;
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
@@ -1388,16 +1093,6 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   // Counter block of the class: [0,1] first launch, [2,3] re-run launch, [4] listed units.
   uint32_t* blk = class_counters(a);
   hipError_t err;
-  if constexpr (ELLM == 2 && !SLICED && MODE == kNhNibble) {
-    // all-sources batches: a level pass, then next hops from neighbour level rows
-    // (spf_allsrc.hip); the rows it lists are re-run by the u16 full-order variant
-    if (const int pass = has_ign ? 0 : allsrc_pass(g, a)) {
-      err = launch_allsrc(pass, g, a, cost, allsrc_qhalf(g), blk, num_cus, s, info);
-      if (err != hipSuccess) return err;
-      return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true,
-                                                                          blk + 2, blk + 4, num_cus, s, info);
-    }
-  }
   if constexpr (ELLM == 2 && !SLICED && Nh<MODE>::kSingle) {
     const uint32_t need1 = std::max<uint32_t>(g.max_deg + 1u, g.est_width1 + g.est_width1 / 4u);
     // wave pass (graph in LDS) for small batches when the delta rows fit with >= 4 solve
@@ -1423,9 +1118,7 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     // take the overflow -> u16 re-run path)
     const bool fits = ring_cap / 2u >= need1 || env_u32("OPENR_SPF_LEAN_FORCE", 0u, 0u, 1u) != 0u;
     const bool lean = !has_ign && !a.tight && fits && env_u32("OPENR_SPF_BFS_LEAN", 1u, 0u, 1u);
-    if (lean && a.order16 && g.V <= 65535u && env_u32("OPENR_SPF_BFS_LEAN2", 0u, 0u, 1u))
-      err = launch_lvl_lean2<MODE, BLOCK>(g, a, cost, ring_cap, blk, blk + 4, num_cus, s, info);
-    else if (lean)
+    if (lean)
       err = launch_lvl_lean<MODE, BLOCK>(g, a, cost, ring_cap, blk, blk + 4, num_cus, s, info);
     else
       err = launch_lvl_variant<MODE, BLOCK, uint8_t, true, ELLM, SLICED>(g, a, cost, glog, has_ign, ring_cap, false,
@@ -1437,258 +1130,6 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   if (err != hipSuccess || (g.V <= ring_cap && g.V <= 254u)) return err;  // nothing can overflow
   return launch_lvl_variant<MODE, 256, uint16_t, false, ELLM, SLICED>(g, a, cost, glog, has_ign, g.V, true, blk + 2,
                                                                       blk + 4, num_cus, s, info);
-}
-
-// ---------------------------------------------------------------------------
-// ell16: the ELL-only fast path (every row <= 4 edges: grids) with ONE u16 state per
-// node, [enc:8 | nh:8], enc = 255 - level (0 = unreached; the source is 255, the
-// sentinel node V is 0xFFFF). An arrival over u->v at level L is tight iff v is
-// unreached or already on level L+1, i.e. iff enc(v) <= 254 - L, i.e. iff
-// state(v) < (255 - L) << 8 — one compare against a wave-uniform threshold. The tight
-// arrival's single atomicOr of ((254 - L) << 8 | nh(u)) both sets v's level (idempotent
-// for later equal-cost arrivals) and merges nh(u) into nh(v) (addNextHops,
-// LinkState.cpp:867-872); it returns v's previous state, and the arrival that saw
-// enc == 0 is the first and appends v. No per-edge level store, no separate level array.
-// Semantics are those of bfs_lvl_kernel (closed form of LinkState::runSpf for uniform
-// cost, LinkState.cpp:808-882); a solve deeper than 253 levels, or whose two adjacent
-// levels overflow the ring, is listed for the u16 full-order re-run like the u8 ring.
-// ---------------------------------------------------------------------------
-struct Ell16Layout {
-  uint32_t st, ring, dummy, total;
-};
-__host__ __device__ inline Ell16Layout ell16_layout(uint32_t V, uint32_t ring_cap) {
-  Ell16Layout l;
-  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4]
-  auto take = [&](uint32_t bytes) {
-    uint32_t o = off;
-    off += (bytes + 15u) & ~15u;
-    return o;
-  };
-  l.st = take(4u * ((V + 2u) / 2u));  // u16 per node, node V = sentinel
-  l.ring = take(2u * ring_cap);
-  l.dummy = take(4u * 64u);
-  l.total = off;
-  return l;
-}
-
-__device__ __forceinline__ uint32_t st_get(const uint32_t* st, uint32_t v) {
-  return reinterpret_cast<const uint16_t*>(st)[v];
-}
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void bfs_ell16_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap,
-                                                          uint32_t* ctr, uint32_t* ovf_count, uint32_t nt) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  __shared__ uint32_t s_next;
-  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
-  const Ell16Layout lay = ell16_layout(V, ring_cap);
-  char* base = reinterpret_cast<char*>(smem);
-  uint32_t* ctl = smem;
-  uint32_t* st = reinterpret_cast<uint32_t*>(base + lay.st);
-  uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
-  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
-  uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
-  const uint32_t st_words = (V + 2u) / 2u;
-  const uint32_t rmask = ring_cap - 1u;
-  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
-
-  for (uint32_t unit = blockIdx.x; unit < count;) {
-    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
-    const uint32_t src = a.sources[sid];
-    if (src < V) {  // block-uniform
-      for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
-      if (tid < 8) ctl[tid] = 0;
-      __syncthreads();
-      if (tid == 0) {
-        st16[V] = 0xFFFFu;  // sentinel: level 0, never tight
-        st16[src] = 0xFF00u;
-      }
-      __syncthreads();
-      // level 0: the source expands even when overloaded; a direct neighbour's next hop
-      // is the neighbour itself (LinkState.cpp:867-872)
-      {
-        const uint2 rs = g.row2[src];
-        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
-          const uint32_t e = e0 + tid;
-          bool fresh = false;
-          uint32_t v = 0;
-          if (e < rs.y) {
-            const uint32_t av = g.adj[e];
-            v = av & ~kEdgeDown;
-            if (!(av & kEdgeDown) && v != src) {
-              const uint32_t sh = (v & 1u) * 16u;
-              const uint32_t old = atomicOr(&st[v >> 1], ((254u << 8) | (1u << g.nbr[e])) << sh);
-              fresh = ((old >> sh) & 0xFF00u) == 0u;
-            }
-          }
-          const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
-          if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= ring_cap (host-checked)
-        }
-      }
-      __syncthreads();
-
-      uint32_t head = 1, tail = 1u + ctl[0], L = 1;
-      bool overflow = false;  // block-uniform
-      while (head < tail) {
-        if (L >= 254u) {  // enc(L + 1) = 254 - L must stay >= 1
-          overflow = true;
-          break;
-        }
-        uint32_t* cnt = &ctl[L & 3u];
-        if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
-        const uint32_t thr = (255u - L) << 8;  // tight iff state(v) < thr
-        const uint32_t enc1 = (254u - L) << 8;
-        for (uint32_t fb = head; fb < tail; fb += BLOCK) {
-          if (fb + wave * 64u >= tail) continue;  // this wave has no slice (uniform)
-          const uint32_t idx = fb + tid;
-          uint4 ell = make_uint4(V, V, V, V);  // a lane without a node reads the sentinel row
-          uint32_t val = 0;
-          if (idx < tail) {
-            const uint32_t u = ring[idx & rmask];
-            ell = g.ellv[u];  // down / padding / sink-row slots hold the sentinel V
-            val = enc1 | (st_get(st, u) & 0xFFu);
-          }
-          const uint32_t vv[4] = {ell.x, ell.y, ell.z, ell.w};
-          bool tight[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) tight[j] = (uint32_t)st16[vv[j]] < thr;
-          uint32_t old[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            old[j] = atomicOr(tight[j] ? &st[vv[j] >> 1] : &dummy[lane], tight[j] ? val << ((vv[j] & 1u) * 16u) : 0u);
-          bool fresh[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) fresh[j] = tight[j] && ((old[j] >> ((vv[j] & 1u) * 16u)) & 0xFF00u) == 0u;
-          // wave-aggregated append (as bfs_lvl_kernel)
-          unsigned long long bj[4];
-          uint32_t off[5];
-          off[0] = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
-            off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
-          }
-          const uint32_t total = off[4];
-          if (total) {  // wave-uniform
-            const int leader = __ffsll((long long)__ballot(1)) - 1;
-            uint32_t wbase = 0;
-            if ((int)lane == leader) wbase = atomicAdd(cnt, total);
-            const uint32_t bse = tail + __builtin_amdgcn_readfirstlane(wbase);
-            if (bse + total - head <= ring_cap) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                if (fresh[j]) {
-                  const uint32_t slot = bse + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
-                                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
-                  ring[slot & rmask] = (uint16_t)vv[j];
-                }
-              }
-            } else if ((int)lane == leader) {
-              ctl[4] = 1;  // two adjacent levels exceed the ring
-            }
-          }
-        }
-        lds_barrier();
-        head = tail;
-        tail += *cnt;
-        ++L;
-        if (ctl[4]) {
-          overflow = true;
-          break;
-        }
-        if (tail == V) break;  // every node reached: the newest level cannot expand tightly
-      }
-      if (overflow) {
-        if (tid == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
-      } else {
-        // rows: dist = level * cost (UINT64_MAX unreached), nh = the low nibble/byte
-        uint64_t* drow = a.dist + out_row_of(a, sid) * V;
-        uint8_t* nrow = a.nh ? a.nh + out_row_of(a, sid) * V * a.nh_bytes : nullptr;
-        const uint32_t nb = a.nh_bytes;
-        const bool fast = ((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0 &&
-                          (!nrow || (nb == 1 && (reinterpret_cast<uintptr_t>(nrow) & 3u) == 0));
-        auto dval = [cost](uint32_t s) -> uint64_t { return s ? (uint64_t)(255u - (s >> 8)) * cost : ~0ull; };
-        if (fast) {
-          uint32_t* n4 = reinterpret_cast<uint32_t*>(nrow);
-          for (uint32_t i = tid; i < V / 4u; i += BLOCK) {  // four nodes per lane
-            const uint2 w = reinterpret_cast<const uint2*>(st)[i];
-            const uint32_t s0 = w.x & 0xFFFFu, s1 = w.x >> 16, s2 = w.y & 0xFFFFu, s3 = w.y >> 16;
-            store_row<uint64_t>(&drow[4 * i], dval(s0), nt);
-            store_row<uint64_t>(&drow[4 * i + 1], dval(s1), nt);
-            store_row<uint64_t>(&drow[4 * i + 2], dval(s2), nt);
-            store_row<uint64_t>(&drow[4 * i + 3], dval(s3), nt);
-            if (n4)
-              store_row<uint32_t>(&n4[i], (s0 & 0xFFu) | ((s1 & 0xFFu) << 8) | ((s2 & 0xFFu) << 16) | ((s3 & 0xFFu) << 24),
-                                  nt);
-          }
-        } else {
-          for (uint32_t v = tid; v < V; v += BLOCK) {
-            const uint32_t s = st16[v];
-            store_row<uint64_t>(&drow[v], dval(s), nt);
-            if (nrow) {
-              uint8_t* o = nrow + (size_t)v * nb;
-              o[0] = (uint8_t)(s & 0xFFu);
-              for (uint32_t j = 1; j < nb; ++j) o[j] = 0;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();  // every lane is done with this unit's LDS and s_next
-    if (tid == 0) s_next = gridDim.x + atomicAdd(&ctr[0], 1u);
-    __syncthreads();
-    unit = s_next;
-  }
-  retire_workgroup(ctr, nullptr);
-}
-
-// ell16 eligibility: ELL-only rows, no ignore set / tight output, one next-hop class of
-// <= 8 bits in the low byte, and a ring that fits the occupancy target. Returns the ring
-// capacity (0 = not eligible).
-uint32_t ell16_ring(const DevGraph& g, const SolveArgs& a, bool has_ign, int cls, uint32_t* per_cu) {
-  if (!env_u32("OPENR_SPF_ELL16", 0u, 0u, 1u)) return 0;  // opt-in: 7 vs 10 solves per CU made it slower on G100
-  if (g.max_deg > 4u || has_ign || a.tight || cls != kLvl4 || g.V > 65534u) return 0;
-  const uint32_t fixed = ell16_layout(g.V, 0).total;
-  const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
-  if (env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u) || g.est_depth + 8u >= 254u) return 0;
-  const uint32_t target = env_u32("OPENR_SPF_E16_WGS", 8u, 1u, 16u);
-  for (uint32_t want = target; want >= 1; --want) {
-    const uint32_t budget = kMaxLds / want;
-    if (budget <= fixed) continue;
-    uint32_t cap = 1;
-    while (cap * 2u <= (budget - fixed) / 2u && cap < 8192u) cap *= 2u;
-    if (cap >= need) {
-      const uint32_t forced = env_u32("OPENR_SPF_RING_CAP", 0u, 0u, 65536u);
-      if (forced && (forced & (forced - 1u)) == 0u && forced >= g.max_deg + 2u && forced <= cap) cap = forced;
-      *per_cu = want;
-      return cap;
-    }
-  }
-  return 0;
-}
-
-hipError_t launch_ell16(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t ring_cap, int num_cus,
-                        hipStream_t s, LaunchInfo* info) {
-  constexpr int BLOCK = 128;
-  uint32_t* blk = class_counters(a);
-  const uint32_t lds = ell16_layout(g.V, ring_cap).total;
-  const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
-  auto k = bfs_ell16_kernel<BLOCK>;
-  hipError_t err =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (err != hipSuccess) return err;
-  if (info) {
-    info->lds_bytes = lds;
-    info->grid = grid;
-    info->kernel = "bfs_ell16_kernel";
-  }
-  note_launch("bfs_ell16_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, ring_cap, blk, blk + 4, nt_stores());
-  err = hipGetLastError();
-  if (err != hipSuccess || (g.V <= ring_cap && g.V <= 253u)) return err;  // nothing can overflow
-  // the solves the ring flagged: u16 full-order re-run from the list
-  return launch_lvl_variant<kNhNibble, 256, uint16_t, false, 2, false>(g, a, cost, 0, false, g.V, true, blk + 2,
-                                                                       blk + 4, num_cus, s, nullptr);
 }
 
 template <int MODE, bool SLICED>
@@ -1739,11 +1180,6 @@ hipError_t launch_bfs_lvl(const DevGraph& g, const SolveArgs& a, uint64_t cost, 
   while ((1 << glog) < group_lanes && glog < 6) ++glog;
   // ELL: one lane per frontier node; ELL-only when every row fits the 4 ELL slots
   const int ellm = glog != 0 ? 0 : (g.max_deg <= 4u ? 2 : 1);
-  if (ellm == 2) {
-    uint32_t per_cu = 0;
-    if (const uint32_t cap = ell16_ring(g, a, has_ign, cls, &per_cu))
-      return launch_ell16(g, a, cost, cap, num_cus, s, info);
-  }
   if (sliced) return launch_lvl_ell<kNhW1, true>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
   switch (lvl_class_mode(cls)) {
     case kNhNibble: return launch_lvl_ell<kNhNibble, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);

@@ -83,11 +83,6 @@ struct Device {
   hipEvent_t cev[kMaxClasses + 1] = {};
   DevBuf<uint32_t> ovfc;
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
-  // lvl-family reach pass (all-sources batches): u8 level rows, node -> row map, row flags
-  DevBuf<uint8_t> lvl8, rowok;
-  DevBuf<uint32_t> rowmap, msperm, mscnt;
-  DevBuf<uint32_t> xsrc, xcount, xslot, xdup;  // extended (halo) batches of the multi-source pass
-  DevBuf<uint16_t> order16;  // 2-bit-code lean pass: per-workgroup BFS order [lean2_max_grid][V]
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
@@ -130,8 +125,7 @@ hipError_t reserve_counters(Device& d) {
 
 void free_graph(DevGraph& g) {
   void* ptrs[] = {g.row, g.row2, g.row2t, g.ovl_bits, g.ellt,    g.ellv,  g.adj,  g.w,    g.win, g.rev,
-                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld,
-                   g.corder, g.tord, g.tinv, g.tmask, g.crank, g.tlist, g.erecs};
+                   g.lid, g.nbr,  g.ovl,   g.cls,      g.cls_lvl, g.ledge, g.rank, g.erec, g.w64, g.elld, g.erecs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   g = DevGraph{};
@@ -277,170 +271,6 @@ FrontierEstimate estimate_frontier(uint32_t V, const uint32_t* row_ptr, const ui
   return est;
 }
 
-// Batch order of the multi-source BFS (spf_allsrc.hip) for all-sources calls: a batch of
-// 32 sources costs one dense pass per level of its deepest source, so sources are grouped
-// into compact clusters (BFS from the lowest unassigned node, taking the 32 nearest
-// unassigned nodes: the sources of a batch then reach every node within a few levels of
-// each other) and the clusters are ordered deepest-first (estimated depth: the BFS depth
-// from the cluster's seed plus the cluster's radius), so the dynamically scheduled batches
-// end together. A performance heuristic over the structural graph (every edge, any
-// state): results do not depend on it.
-std::vector<uint32_t> cluster_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col) {
-  constexpr uint32_t kC = 32;
-  std::vector<uint32_t> stamp(V, UINT32_MAX), lvl(V), q;
-  std::vector<uint8_t> taken(V, 0);
-  std::vector<std::pair<uint64_t, uint32_t>> key;  // (depth estimate, cluster) per cluster
-  std::vector<uint32_t> members;
-  std::vector<uint32_t> start;
-  q.reserve(V);
-  uint32_t nclusters = 0;
-  for (uint32_t s = 0; s < V; ++s) {
-    if (taken[s]) continue;
-    const uint32_t c = nclusters++;
-    start.push_back((uint32_t)members.size());
-    uint32_t got = 0, radius = 0;
-    q.clear();
-    q.push_back(s);
-    stamp[s] = c;
-    lvl[s] = 0;
-    for (size_t h = 0; h < q.size() && got < kC; ++h) {
-      const uint32_t u = q[h];
-      if (!taken[u]) {
-        taken[u] = 1;
-        members.push_back(u);
-        radius = lvl[u];
-        ++got;
-      }
-      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
-        const uint32_t v = col[e];
-        if (stamp[v] == c) continue;
-        stamp[v] = c;
-        lvl[v] = lvl[u] + 1u;
-        q.push_back(v);
-      }
-    }
-    key.push_back({(uint64_t)radius, c});
-  }
-  start.push_back((uint32_t)members.size());
-  // depth of a full BFS from each seed (the cluster's first member)
-  std::vector<uint32_t> seen(V, UINT32_MAX);
-  for (uint32_t c = 0; c < nclusters; ++c) {
-    const uint32_t s = members[start[c]];
-    q.clear();
-    q.push_back(s);
-    seen[s] = c;
-    lvl[s] = 0;
-    uint32_t depth = 0;
-    for (size_t h = 0; h < q.size(); ++h) {
-      const uint32_t u = q[h];
-      depth = lvl[u];
-      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
-        const uint32_t v = col[e];
-        if (seen[v] == c) continue;
-        seen[v] = c;
-        lvl[v] = lvl[u] + 1u;
-        q.push_back(v);
-      }
-    }
-    key[c].first += depth;
-  }
-  std::stable_sort(key.begin(), key.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-  std::vector<uint32_t> order;
-  order.reserve(V);
-  for (auto const& kc : key)
-    for (uint32_t i = start[kc.second]; i < start[kc.second + 1]; ++i) order.push_back(members[i]);
-  return order;
-}
-
-// Tile order of the multi-source BFS (spf_allsrc.hip): 64 consecutive internal ids form a
-// tile, the unit whose activity a level tracks, so tiles should be compact (few tiles per
-// BFS level band). Seeds are taken in BFS order from a peripheral node (the farthest from
-// node 0, every component in turn); each unassigned seed grows a tile by BFS over
-// unassigned nodes until the tile holds 64 nodes (a seed whose region runs out leaves the
-// tile to the next seed). A performance heuristic over the structural graph: results do
-// not depend on it. Returns tord (internal -> node); tmask as DevGraph::tmask.
-void tile_order(uint32_t V, const uint32_t* row_ptr, const uint32_t* col, std::vector<uint32_t>& tord,
-                std::vector<uint32_t>& tmask) {
-  auto bfs_order = [&](uint32_t root, std::vector<uint32_t>& seen, uint32_t stamp, std::vector<uint32_t>& out) {
-    size_t h = out.size();
-    out.push_back(root);
-    seen[root] = stamp;
-    for (; h < out.size(); ++h) {
-      const uint32_t u = out[h];
-      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e)
-        if (seen[col[e]] != stamp) {
-          seen[col[e]] = stamp;
-          out.push_back(col[e]);
-        }
-    }
-  };
-  std::vector<uint32_t> seen(V, UINT32_MAX), seeds, tmp;
-  seeds.reserve(V);
-  for (uint32_t s = 0; s < V; ++s) {
-    if (seen[s] != UINT32_MAX) continue;
-    tmp.clear();
-    bfs_order(s, seen, 0u, tmp);  // the component of s; its last node is a peripheral root
-    const uint32_t root = tmp.back();
-    bfs_order(root, seen, 1u, seeds);
-  }
-  std::vector<uint8_t> taken(V, 0);
-  tord.clear();
-  tord.reserve(V);
-  std::vector<uint32_t> q;
-  for (uint32_t s : seeds) {
-    if (taken[s]) continue;
-    q.clear();
-    q.push_back(s);
-    taken[s] = 1;
-    tord.push_back(s);
-    for (size_t h = 0; h < q.size() && tord.size() % kTileNodes; ++h) {
-      const uint32_t u = q[h];
-      for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1] && tord.size() % kTileNodes; ++e)
-        if (!taken[col[e]]) {
-          taken[col[e]] = 1;
-          tord.push_back(col[e]);
-          q.push_back(col[e]);
-        }
-    }
-  }
-  const uint32_t nt = (V + kTileNodes - 1u) / kTileNodes;
-  // within a tile, nodes in id order: on id-ordered meshes (row-major grids) a lane's
-  // neighbours then sit at nearby lanes of the same or the adjacent rows, and a wavefront's
-  // frontier reads spread over the LDS banks instead of colliding
-  for (uint32_t t0 = 0; t0 < V; t0 += kTileNodes)
-    std::sort(tord.begin() + t0, tord.begin() + std::min<uint32_t>(V, t0 + kTileNodes));
-  // Internal tile ids: thread t of the 512-thread kernel owns internal ids t + 512 i (slot i,
-  // tile 8i + wave), and a wave takes its slots in chunks of 4 (kMsChunk). Grown tile s goes
-  // to internal tile T(s) so that consecutive grown tiles — neighbours — share a wave's
-  // chunk: T enumerates (chunk c, wave w, slot r) as 8 (4c + r) + w, skipping ids >= nt; the
-  // last grown tile (the partial one) keeps id nt - 1, so padding ids stay at the end.
-  {
-    std::vector<uint32_t> tmap;
-    for (uint32_t c = 0; tmap.size() + 1u < nt; ++c)
-      for (uint32_t w = 0; w < 8u; ++w)
-        for (uint32_t r = 0; r < 4u; ++r) {
-          const uint32_t T = 8u * (4u * c + r) + w;
-          if (T < nt - 1u) tmap.push_back(T);
-        }
-    tmap.push_back(nt - 1u);
-    std::vector<uint32_t> internal((size_t)nt * kTileNodes, UINT32_MAX);
-    for (uint32_t p = 0; p < V; ++p) internal[(size_t)tmap[p / kTileNodes] * kTileNodes + p % kTileNodes] = tord[p];
-    internal.resize(V);  // ids >= V: the partial last tile's padding
-    tord.swap(internal);
-  }
-  std::vector<uint32_t> tinv(V);
-  for (uint32_t p = 0; p < V; ++p) tinv[tord[p]] = p;
-  tmask.assign((size_t)nt * kTileMaskWords, 0u);
-  for (uint32_t u = 0; u < V; ++u) {
-    const uint32_t t = tinv[u] / kTileNodes;
-    tmask[(size_t)t * kTileMaskWords + t / 32u] |= 1u << (t & 31u);
-    for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) {
-      const uint32_t t2 = tinv[col[e]] / kTileNodes;
-      tmask[(size_t)t * kTileMaskWords + t2 / 32u] |= 1u << (t2 & 31u);
-    }
-  }
-}
-
 // Bytes of exact-order slots (global memory) a device may hold at once.
 constexpr uint64_t kExactScratchBytes = uint64_t(2) << 30;
 
@@ -551,52 +381,6 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     if (err != hipSuccess) return err;
     a.slice_tmp = d.slicetmp.p;
     a.krows = rows;
-  }
-  // reach pass scratch (spf_bfs_lvl.hip: dist-level rows of a whole batch, then next hops
-  // from neighbour rows); only for batches that can hold every source's neighbours
-  a.lvl8 = nullptr;
-  a.rowmap = nullptr;
-  a.rowok = nullptr;
-  a.msperm = nullptr;
-  a.mscnt = nullptr;
-  a.xsrc = a.xcount = a.xslot = a.xdup = nullptr;
-  if (fam == kFamLvl && !a.tight && !a.ign_ptr && !a.out_row && __builtin_popcount(mask) == 1 &&
-      (a.n >= d.g.V || allsrc_ext_ok(d.g) || std::getenv("OPENR_SPF_BFS_REACH") ||
-       std::getenv("OPENR_SPF_BFS_MSBFS"))) {
-    // a partial batch on the tile-active or wave-reach pass is extended with halo rows (ms_ext_rows)
-    const bool ext = a.n < d.g.V && allsrc_ext_ok(d.g);
-    const uint32_t rows = ext ? ms_ext_rows(d.g, a.n) : a.n;
-    hipError_t err = d.lvl8.reserve((size_t)rows * reach_row_bytes(d.g.V));
-    if (err == hipSuccess) err = d.rowok.reserve(rows);
-    if (err == hipSuccess) err = d.rowmap.reserve(d.g.V);
-    if (err == hipSuccess) err = d.msperm.reserve(rows);
-    if (err == hipSuccess) err = d.mscnt.reserve(1);
-    if (ext) {
-      if (err == hipSuccess) err = d.xsrc.reserve(rows);
-      if (err == hipSuccess) err = d.xcount.reserve(2);
-      if (err == hipSuccess) err = d.xslot.reserve(d.g.V);
-      if (err == hipSuccess) err = d.xdup.reserve(std::max<uint32_t>(a.n, 1u));
-    }
-    if (err != hipSuccess) return err;
-    a.lvl8 = d.lvl8.p;
-    a.rowok = d.rowok.p;
-    a.rowmap = d.rowmap.p;
-    a.msperm = d.msperm.p;
-    a.mscnt = d.mscnt.p;
-    if (ext) {
-      a.xsrc = d.xsrc.p;
-      a.xcount = d.xcount.p;
-      a.xslot = d.xslot.p;
-      a.xdup = d.xdup.p;
-    }
-  }
-  // 2-bit-code lean pass (spf_bfs_lvl.hip, OPENR_SPF_BFS_LEAN2): its BFS order scratch
-  a.order16 = nullptr;
-  if (fam == kFamLvl && !a.tight && !a.ign_ptr && d.g.V <= 65535u && d.g.max_deg <= 4u &&
-      std::getenv("OPENR_SPF_BFS_LEAN2") && std::atoi(std::getenv("OPENR_SPF_BFS_LEAN2")) == 1) {
-    hipError_t err = d.order16.reserve((size_t)lean2_max_grid(d.num_cus) * d.g.V);
-    if (err != hipSuccess) return err;
-    a.order16 = d.order16.p;
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
@@ -1173,16 +957,6 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.nh.release();
     d.ovf.release();
     d.slicetmp.release();
-    d.lvl8.release();
-    d.rowok.release();
-    d.rowmap.release();
-    d.msperm.release();
-    d.mscnt.release();
-    d.xsrc.release();
-    d.xcount.release();
-    d.xslot.release();
-    d.xdup.release();
-    d.order16.release();
     d.work.release();
     d.perm.release();
     d.part.release();
@@ -1342,16 +1116,6 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (!cls_mask[f]) cls_mask[f] = 1u;  // no node: class 0
   const FrontierEstimate est = estimate_frontier(V, gr->row_ptr, adj.data(), ovl.data());
   if (w_min == UINT32_MAX) w_min = w_max = 1;  // no usable edge
-  // multi-source BFS batch order (graphs it can serve: every row <= 4 edges, V <= 10 240)
-  std::vector<uint32_t> corder, tord, tmask;
-  {
-    uint32_t md = 0;
-    for (uint32_t u = 0; u < V; ++u) md = std::max(md, gr->row_ptr[u + 1] - gr->row_ptr[u]);
-    if (V && V <= 10240u && md <= 4u) {
-      corder = cluster_order(V, gr->row_ptr, gr->col);
-      tile_order(V, gr->row_ptr, gr->col, tord, tmask);
-    }
-  }
 
   for (Device& d : ctx->devs) {
     HIP_TRY(hipSetDevice(d.ordinal));
@@ -1380,13 +1144,9 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.ovl_bits, ovl_bits.data(), ovl_bits.size());
     if (err == hipSuccess) err = up(&g.ellt, ellt.data(), V);
     if (err == hipSuccess) {
-      // [V] = sentinel row (lean BFS pass); [V + 32k], k < 64: the reach pass's per-lane sentinels
+      // [V] = sentinel row (lean BFS pass)
       std::vector<uint4> ellv(ellv_rows(V), make_uint4(V, V, V, V));
       for (uint32_t u = 0; u < V; ++u) ellv[u] = ellv_of(ellt[u], V);
-      for (uint32_t k = 1; k < kReachSentinels; ++k) {
-        const uint32_t s = V + kReachSentinelStride * k;
-        ellv[s] = make_uint4(s, s, s, s);
-      }
       err = up(&g.ellv, ellv.data(), ellv.size());
       // delta rows (wave pass): every row of <= 4 edges and every column within 127 ids of
       // its row, down edges and overloaded rows included (a patch may bring them back)
@@ -1422,32 +1182,6 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     if (err == hipSuccess) err = up(&g.cls_lvl, cls[kFamLvl].data(), V);
     if (err == hipSuccess) err = up(&g.ledge, ledge.data(), L);
     if (err == hipSuccess) err = up(&g.rank, gr->name_rank, V);
-    if (err == hipSuccess && !corder.empty()) err = up(&g.corder, corder.data(), V);
-    if (err == hipSuccess && !tord.empty()) {
-      std::vector<uint32_t> tinv(V);
-      for (uint32_t p = 0; p < V; ++p) tinv[tord[p]] = p;
-      err = up(&g.tord, tord.data(), V);
-      if (err == hipSuccess) err = up(&g.tinv, tinv.data(), V);
-      if (err == hipSuccess) err = up(&g.tmask, tmask.data(), tmask.size());
-      g.ntiles = (uint32_t)(tmask.size() / kTileMaskWords);
-      std::vector<uint32_t> crank(V);
-      for (uint32_t i = 0; i < V; ++i) crank[corder[i]] = i;
-      if (err == hipSuccess) err = up(&g.crank, crank.data(), V);
-      // neighbour lists (u8 ids; at most 256 tiles by the caller's check)
-      std::vector<uint8_t> tlist((size_t)g.ntiles * kTileList + 4u, 0xFFu);
-      for (uint32_t t = 0; t < g.ntiles && g.ntiles <= 255u; ++t) {
-        uint32_t c = 0;
-        for (uint32_t t2 = 0; t2 < g.ntiles; ++t2) {
-          if (!((tmask[(size_t)t * kTileMaskWords + t2 / 32u] >> (t2 & 31u)) & 1u)) continue;
-          if (c == kTileList) {
-            tlist[(size_t)t * kTileList] = 0xFEu;
-            break;
-          }
-          tlist[(size_t)t * kTileList + c++] = (uint8_t)t2;
-        }
-      }
-      if (err == hipSuccess) err = up(&g.tlist, tlist.data(), tlist.size());
-    }
     d.g = g;
     if (err != hipSuccess) {
       ctx->has_graph = false;

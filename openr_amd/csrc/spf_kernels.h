@@ -28,7 +28,6 @@ struct DevGraph {
   uint4* ellv = nullptr;       // [ellv_rows(V)] ellt with every down / padding slot replaced by the node id V (a
                                //     level sentinel the lvl kernel keeps at 0: never tight, no flag tests);
                                //     ellv[V] = (V, V, V, V), the row of a lane past the frontier;
-                               //     ellv[V + 32k] = four copies of V + 32k (reach pass sentinels)
   uint32_t* elld = nullptr;    // [V] ellv as four signed byte deltas (v - u; 0 = no edge), or null
   // [E] erec with every row's entries sorted by (name rank of the neighbour, reverse edge):
   // for uniform cost that is the reference's pathLinks order (DijkstraQ pops equal
@@ -50,21 +49,7 @@ struct DevGraph {
   uint32_t* rank = nullptr;    // [V] name rank (pathLinks / pop-order tie-break)
   uint4* erec = nullptr;       // [E] packed edge e = u->col: {col | kEdgeDown | kNodeSink if col is
                                //     overloaded, win[e], lid[e], rev[e]} (one 16-byte load per edge)
-  uint32_t* corder = nullptr;  // [V] or null: nodes grouped into compact clusters of 32, the clusters
-                               //     deepest-first (multi-source BFS batches of all-sources calls)
-  // Tile order of the multi-source BFS (null when corder is): internal id p of node
-  // tord[p] (p < V; 64 consecutive internal ids = one tile of compact nodes), tinv = its
-  // inverse, tmask[t][8] = bitmask of the tiles holding a neighbour of a node of tile t
-  // (structural edges, any state; t itself included). ntiles = ceil(V / 64) <= 256.
-  uint32_t* tord = nullptr;
-  uint32_t* tinv = nullptr;
-  uint32_t* tmask = nullptr;
-  uint8_t* tlist = nullptr;    // [ntiles][kTileList] the tiles of tmask[t] (t included) as u8 ids, 0xFF
-                               //     padded; list head 0xFE: more than kTileList (every tile counts)
-  uint32_t ntiles = 0;
-  uint32_t* crank = nullptr;   // [V] or null: position of each node in corder
 };
-constexpr uint32_t kTileNodes = 64, kTileMaskWords = 8, kTileList = 12;
 
 constexpr uint32_t kEdgeDown = 0x80000000u;
 // Sink flag of a transit row: ellt[u].x and row2t[u].x carry it when u is overloaded.
@@ -149,36 +134,8 @@ struct SolveArgs {
   // sliced class with next-hop output, chunked: this launch solves the class-local solves
   // [k0, k0 + krows) and slice_tmp holds krows of them (row k - k0); krows 0 = the whole class
   uint32_t k0, krows;
-  // reach pass + next hops from neighbour level rows (spf_bfs_lvl.hip, all-sources batches
-  // on ELL-only graphs), all nullable (then the pass is not used): u8 level rows
-  // [n][reach_row_bytes(V)] (0xFF = unreached), node -> batch row map [V] (UINT32_MAX =
-  // not in the batch), per-row "level row valid" flags [n]
-  uint8_t* lvl8;
-  uint32_t* rowmap;
-  uint8_t* rowok;
-  // multi-source BFS batch order: position i of the batch sequence is row msperm[i] (null:
-  // row i); mscnt = one scratch word (the permutation test)
-  uint32_t* msperm;
-  uint32_t* mscnt;
-  // batches that do not hold every source's neighbours (tile-active multi-source pass): the
-  // extended batch xsrc = sources followed by the halo (usable, non-overloaded neighbours of
-  // sources the batch lacks; level rows only, for the next-hop pass), *xcount halo rows;
-  // xslot [V] scratch (cluster-order placement), xdup [n] scratch (duplicate rows)
-  uint32_t* xsrc;
-  uint32_t* xcount;
-  uint32_t* xslot;
-  uint32_t* xdup;
-  // nullable: per-workgroup BFS order scratch [lean2_max_grid][V] of the 2-bit-code lean
-  // pass (bfs_ell2_kernel); the pass is used only when it is set
-  uint16_t* order16;
 };
-// Row stride of SolveArgs::lvl8 (16-byte rows: the next-hop pass reads 16 levels per load)
-__host__ __device__ inline uint32_t reach_row_bytes(uint32_t V) { return (V + 15u) & ~15u; }
-// Reach pass sentinels: a lane past the frontier reads the ELL row of node V + 32 * lane,
-// four copies of its own id, whose visited bit lies in a dword of its own (DevGraph::ellv
-// holds these rows; every id >= V is pre-marked visited, so a sentinel slot never appends)
-constexpr uint32_t kReachSentinels = 64, kReachSentinelStride = 32;
-__host__ __device__ constexpr uint32_t ellv_rows(uint32_t V) { return V + kReachSentinelStride * (kReachSentinels - 1u) + 1u; }
+__host__ __device__ constexpr uint32_t ellv_rows(uint32_t V) { return V + 1u; }
 // output row of solve sid (SolveArgs::out_row)
 __host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
   return a.out_row ? (size_t)a.out_row[sid] : (size_t)sid;
@@ -350,26 +307,6 @@ uint32_t bfs_lds_bytes(int family, uint32_t V, uint32_t L, bool has_ignore, int 
 uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 
-// All-sources batches on uniform-cost graphs with rows of <= 4 edges (spf_allsrc.hip):
-// a level pass (2: bit-parallel multi-source BFS, 1: per-source reach pass; 0: neither
-// applies) writes u8 level rows, then every next-hop set is derived from the level rows of
-// the source's neighbours. Rows it cannot finish are appended to a.ovf_list (count in
-// blk[4]) for the caller's u16 full-order re-run. `half` = the reach pass's queue half.
-int allsrc_pass(const DevGraph& g, const SolveArgs& a);
-uint32_t allsrc_qhalf(const DevGraph& g);
-// workgroups of the 2-bit-code lean pass at most (its order scratch is [this][V] u16)
-inline uint32_t lean2_max_grid(int num_cus) { return 16u * (uint32_t)(num_cus > 0 ? num_cus : 1); }  // queue half of the per-source passes (1, 3)
-// the tile-active multi-source pass serves g; rows of its extended batch of n sources (halo)
-bool ms_tile_ok(const DevGraph& g);
-uint32_t ms_ext_rows(const DevGraph& g, uint32_t n);
-// a partial all-sources batch on g is extended with halo rows (tile-active or wave-reach pass)
-bool allsrc_ext_ok(const DevGraph& g);
-// wave-reach pass (spf_wreach.hip, pass 3): LDS bytes for queue half qhalf (0: does not apply)
-uint32_t wreach_lds_bytes(const DevGraph& g, uint32_t qhalf);
-hipError_t launch_wreach(const DevGraph& g, const SolveArgs& a, uint32_t qhalf, uint32_t* blk, int num_cus,
-                         hipStream_t s, LaunchInfo* info);
-hipError_t launch_allsrc(int pass, const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t half, uint32_t* blk,
-                         int num_cus, hipStream_t s, LaunchInfo* info);
 uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
 

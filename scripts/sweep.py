@@ -20,9 +20,10 @@ sys.path.insert(0, ROOT)
 
 KEYS = {"G": "OPENR_SPF_GROUP_LANES", "FULL": "OPENR_SPF_BFS_FULL",
         "WGS": "OPENR_SPF_BFS_WGS", "NT": "OPENR_SPF_NT", "BLK": "OPENR_SPF_BFS_BLOCK",
-        "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL", "E16": "OPENR_SPF_ELL16",
-        "E16W": "OPENR_SPF_E16_WGS", "RING": "OPENR_SPF_RING_CAP", "FL": "OPENR_SPF_FRESH_LVL",
-        "LEAN": "OPENR_SPF_BFS_LEAN", "CLEAN": "OPENR_SPF_CODE_LEAN", "WAVE": "OPENR_SPF_BFS_WAVE", "WMIN": "OPENR_SPF_WAVE_MIN"}
+        "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL",
+        "RING": "OPENR_SPF_RING_CAP", "FL": "OPENR_SPF_FRESH_LVL",
+        "LEAN": "OPENR_SPF_BFS_LEAN", "CLEAN": "OPENR_SPF_CODE_LEAN", "WAVE": "OPENR_SPF_BFS_WAVE", "WMIN": "OPENR_SPF_WAVE_MIN",
+        "LWGS": "OPENR_SPF_LEAN_WGS", "PROF": "OPENR_SPF_BFS_PROF"}
 
 
 def parse(v):

@@ -774,6 +774,33 @@ static bool spfMatchesOracle(const LinkState& ls, const std::vector<uint32_t>& s
   return ok;
 }
 
+// getKthPaths(names[s], names[d], k) for k = 1, 2 equals oracle_kth_paths on the current
+// mirror (link for link, in order) for every (s, d) of srcs x dsts.
+static bool kthMatchesOracle(const LinkState& ls, const std::vector<uint32_t>& srcs, const std::vector<uint32_t>& dsts) {
+  auto const& m = ls.csrMirror();
+  oracle_graph og{(uint32_t)m.names.size(), (uint32_t)m.col.size(), (uint32_t)m.links.size(), m.rowPtr.data(),
+                  m.col.data(), m.metric.data(), m.linkId.data(), m.edgeUp.data(), m.overloaded.data(),
+                  m.nameRank.data()};
+  const uint32_t NE = og.num_dir_edges;
+  std::vector<uint32_t> pptr(NE + 2), pe(NE + 2);
+  bool ok = true;
+  for (uint32_t s : srcs)
+    for (uint32_t d : dsts)
+      for (uint32_t k = 1; k <= 2; ++k) {
+        auto const& paths = ls.getKthPaths(m.names[s], m.names[d], k);
+        const int64_t np = oracle_kth_paths(&og, s, d, k, pptr.data(), NE + 1, pe.data(), NE + 1);
+        bool same = np >= 0 && (size_t)np == paths.size();
+        for (int64_t i = 0; same && i < np; ++i) {
+          same = paths[i].size() == pptr[i + 1] - pptr[i];
+          for (uint32_t j = 0; same && j < paths[i].size(); ++j)
+            same = paths[i][j].get() == m.links[m.linkId[pe[pptr[i] + j]]].get();
+        }
+        if (!same) std::printf("    kth-path mismatch: %s -> %s k=%u\n", m.names[s].c_str(), m.names[d].c_str(), k);
+        ok &= same;
+      }
+  return ok;
+}
+
 // n x n grid adjacency databases (DecisionTest.cpp:4207-4355 names / ifnames), metric w(i, j)
 template <typename W>
 static thrift::AdjacencyDatabase gridDb(int n, int i, int j, W w, bool overloaded = false) {
@@ -827,9 +854,20 @@ TEST_GPU(LinkState_AttributeUpdatesPatchAndRefresh) {
       EXPECT_EQ((uint64_t)(n * n), SpfCounters::get().spfRuns());  // every source read once, counted once
       EXPECT_TRUE(spfMatchesOracle(ls, ids, false));
     }
+    // getKthPaths after the patches: its k = 1 paths trace pathLinks re-derived from the
+    // refreshed rows' distances, its k = 2 paths an ignore-set solve on the patched graph
+    {
+      auto on = ls.updateAdjacencyDatabase(gridDb(n, xi, xj, w, true));
+      EXPECT_TRUE(on.topologyChanged);
+      EXPECT_TRUE(kthMatchesOracle(ls, {0u, (uint32_t)(x - 1), (uint32_t)(n * n - 1)},
+                                   {(uint32_t)(x + 1), (uint32_t)(x + n), (uint32_t)(n * n / 2), 3u}));
+      EXPECT_TRUE(ls.updateAdjacencyDatabase(gridDb(n, xi, xj, w, false)).topologyChanged);
+      EXPECT_TRUE(kthMatchesOracle(ls, {0u, (uint32_t)(x - 1), (uint32_t)(n * n - 1)},
+                                   {(uint32_t)(x + 1), (uint32_t)(x + n), (uint32_t)(n * n / 2), 3u}));
+    }
     EXPECT_EQ(gen, ls.mirrorGeneration());
     EXPECT_EQ(uploads, ls.updateStats().graphUploads);  // patched, never re-uploaded
-    EXPECT_EQ(2u, (unsigned)ls.updateStats().patches);
+    EXPECT_EQ(4u, (unsigned)ls.updateStats().patches);
     // incremental: the refreshes re-solved fewer rows than they kept
     EXPECT_TRUE(ls.updateStats().rowsRefreshed < ls.updateStats().rowsKept);
     // 2) metric change of one adjacency, 3) adjacency overload (link down), then back up
@@ -868,6 +906,80 @@ TEST_GPU(LinkState_AttributeUpdatesPatchAndRefresh) {
     std::printf("    weighted=%d patches=%llu refreshes=%llu rows kept=%llu re-solved=%llu\n", weighted,
                 (unsigned long long)ls.updateStats().patches, (unsigned long long)ls.updateStats().refreshes,
                 (unsigned long long)ls.updateStats().rowsKept, (unsigned long long)ls.updateStats().rowsRefreshed);
+  }
+}
+
+// changes that rebuild the mirror without being topology changes keep
+// the reference's memo (LinkState.cpp:714-717 clears it only on topologyChanged): a new
+// node's first adjacency database that forms no link, and a link that forms while held
+// down (holdUpTtl > 0). The memo entries keep reading the rows of the mirror they were
+// solved on (a retired snapshot), rows solved after the rebuild use the new ids, and every
+// read equals the oracle on the current graph with no SPF re-run.
+TEST_GPU(LinkState_MemoSurvivesNonTopologyRebuild) {
+  const int n = 7;
+  auto w = [](int i, int j, int ii, int jj) { return 1 + (i * 5 + j + ii * 3 + jj) % 4; };
+  LinkState ls(kArea);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) ls.updateAdjacencyDatabase(gridDb(n, i, j, w));
+  std::vector<std::string> all;
+  for (int v = 0; v < n * n; ++v) all.push_back(std::to_string(v));
+  ls.prefetchSpfResults(all);
+  ls.prefetchSpfResults(all, false);
+  auto oldIds = [&]() {
+    std::vector<uint32_t> ids;
+    for (auto const& a : all) ids.push_back(ls.csrMirror().id.at(a));
+    return ids;
+  };
+  EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), true));
+  EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), false));
+  auto viewMatches = [&](bool um) {
+    bool ok = true;
+    for (auto const& s : all) {
+      auto const v = ls.getSpfView(s, um);
+      auto const& r = ls.getSpfResult(s, um);
+      for (auto const& d : ls.csrMirror().names) {
+        auto it = r.find(d);
+        ok &= v.reached(d) == (it != r.end());
+        if (it == r.end()) continue;
+        ok &= v.metric(d) == it->second.metric();
+        auto nh = v.nextHops(d);
+        ok &= std::unordered_set<std::string>(nh.begin(), nh.end()) == it->second.nextHops();
+      }
+    }
+    return ok;
+  };
+  // 1) "zz" (sorts after every grid name) and "!a" (sorts before: every old id shifts by
+  //    one in the rebuilt mirror) advertise adjacencies that are not reciprocated
+  for (const char* nn : {"zz", "!a"}) {
+    auto ch = ls.updateAdjacencyDatabase(createAdjDb(nn, {createAdjacency("0", "y/0", "0/y", 1)}, 900));
+    EXPECT_FALSE(ch.topologyChanged);
+  }
+  SpfCounters::get().reset();
+  EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), true));
+  EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), false));
+  EXPECT_TRUE(viewMatches(true));
+  EXPECT_TRUE(viewMatches(false));
+  EXPECT_EQ(0u, (unsigned)SpfCounters::get().spfRuns());  // memo hits: nothing re-run
+  // rows solved on the rebuilt mirror beside the retired ones
+  EXPECT_TRUE(spfMatchesOracle(ls, {ls.csrMirror().id.at("zz"), ls.csrMirror().id.at("!a")}, true));
+  // 2) a link between 0 and 1 formed while held down: not a topology change either
+  {
+    auto db0 = gridDb(n, 0, 0, w);
+    db0.adjacencies.push_back(createAdjacency("1", "0/h", "1/h", 1));
+    auto db1 = gridDb(n, 0, 1, w);
+    db1.adjacencies.push_back(createAdjacency("0", "1/h", "0/h", 1));
+    EXPECT_FALSE(ls.updateAdjacencyDatabase(db0, 2, 0).topologyChanged);
+    EXPECT_FALSE(ls.updateAdjacencyDatabase(db1, 2, 0).topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), true));
+    EXPECT_TRUE(viewMatches(true));
+    EXPECT_TRUE(spfMatchesOracle(ls, {ls.csrMirror().id.at("zz")}, true));
+    EXPECT_EQ(2u, (unsigned)SpfCounters::get().spfRuns());  // only zz and !a ran
+    // the hold expires: a topology change, the memo is cleared and results follow the link
+    EXPECT_FALSE(ls.decrementHolds().topologyChanged);
+    EXPECT_TRUE(ls.decrementHolds().topologyChanged);
+    EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), true));
+    EXPECT_TRUE(spfMatchesOracle(ls, oldIds(), false));
+    EXPECT_TRUE(viewMatches(true));
   }
 }
 

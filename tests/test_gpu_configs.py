@@ -105,33 +105,21 @@ def test_config3_grid100_all_sources(eng):
     pathlinks_vs_oracle(eng, g, [0, 99, 4950, 5050, 9900, 9999, 1234, 7777])
 
 
-# the pass a full G100 batch takes by default (spf_allsrc.hip: allsrc_pass)
+# the pass a full G100 batch takes by default (spf_bfs_lvl.hip)
 CONFIG3_KERNEL = "bfs_ell_kernel"
 
 
 @pytest.mark.parametrize("chunk,env,kernel", [
-    (10000, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
-    (10000, {"OPENR_SPF_BFS_LEAN2": "1"}, "bfs_ell2_kernel"),
-    (10000, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
-    (10000, {"OPENR_SPF_BFS_MSBFS": "1", "OPENR_SPF_MSBFS_TILE": "0"}, "msbfs_kernel"),
-    (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
-    (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0"}, "bfs_ell_kernel"),
     (10000, {"OPENR_SPF_LEAN_DELTA": "0"}, "bfs_ell_kernel"),
-    (10000, {"OPENR_SPF_BFS_MSBFS": "0", "OPENR_SPF_BFS_REACH": "0", "OPENR_SPF_BFS_WAVE": "1"}, "bfs_wave_kernel"),
+    (10000, {"OPENR_SPF_BFS_WAVE": "1"}, "bfs_wave_kernel"),
     (1250, {}, "bfs_wave_kernel"),
     (1250, {"OPENR_SPF_BFS_WAVE": "0"}, "bfs_ell_kernel"),
-    (1250, {"OPENR_SPF_BFS_REACH": "1"}, "bfs_reach_kernel"),
-    (1250, {"OPENR_SPF_BFS_MSBFS": "1"}, "msbfs_tile_kernel"),
-    (1250, {"OPENR_SPF_BFS_WREACH": "1"}, "bfs_wreach_kernel"),
-], ids=["full-batch-wreach", "full-batch-lean2", "full-batch-msbfs-tile", "full-batch-msbfs-dense", "full-batch-reach", "full-batch-lean", "full-batch-lean-ellv", "full-batch-wave", "shard1250-auto", "shard1250-lean", "shard1250-reach",
-        "shard1250-msbfs", "shard1250-wreach"])
+], ids=["full-batch-lean-ellv", "full-batch-wave", "shard1250-auto", "shard1250-lean"])
 def test_config3_grid100_pass_variants(eng, monkeypatch, chunk, env, kernel):
     """Config 3's other launch shapes, every row against the oracle: the full batch on the
-    reach pass and the round-2 lean (16-byte ellv rows instead of the default delta rows)
-    and wave passes, and the 1 250-source shards of an
-    8-GPU strong-scaling run (per-GPU step: the wave pass by default; the lean pass; the
-    reach and multi-source passes, whose shard-boundary sources lack neighbour rows and
-    take the re-run)."""
+    round-2 lean pass (16-byte ellv rows instead of the default delta rows) and on the wave
+    pass, and the 1 250-source shards of an 8-GPU strong-scaling run (per-GPU step: the
+    wave pass by default; the lean pass)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     all_sources_vs_oracle(eng, T.grid_fast(100), chunk, expect_kernel=kernel)

@@ -365,45 +365,6 @@ def test_lean_pass_half_overflow(eng, monkeypatch, capfd, bfs_family):
     assert ("bfs_ell:" in capfd.readouterr().err) == (bfs_family[0] == "lvl")
 
 
-@pytest.mark.parametrize("case", ["grid", "depth", "half", "overload-down", "disconnected"])
-def test_lean2_pass(eng, monkeypatch, case):
-    """The 2-bit-code lean pass (bfs_ell2_kernel: levels as 2-bit codes in LDS, exact
-    levels from a global BFS order scattered back at the write-out), forced on: every
-    row against the oracle, with overloaded nodes and down links, unreached nodes, and
-    both re-run paths (a chain deeper than 253 levels, a forced narrow queue half)."""
-    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
-    monkeypatch.setenv("OPENR_SPF_BFS_LEAN2", "1")
-    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")
-    n = 70
-    names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)]
-    links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
-    links += [(r * n + c, (r + 1) * n + c) for r in range(n - 1) for c in range(n)]
-    ovl = up = None
-    srcs = list(range(0, n * n, 3))
-    if case == "depth":
-        tail = 300
-        names += [f"z{i:03d}" for i in range(tail)]
-        links += [(n * n + i, n * n + i + 1) for i in range(tail - 1)]
-        srcs = [0, n * n - 1, n * n, n * n + tail - 1, n * n + 10, 35 * n + 35] + list(range(0, n * n, 11))
-    if case == "half":
-        monkeypatch.setenv("OPENR_SPF_LEAN_FORCE", "1")
-        monkeypatch.setenv("OPENR_SPF_RING_CAP", "32")
-    if case == "overload-down":
-        rng = np.random.default_rng(5)
-        ovl = (rng.random(n * n) < 0.06).astype(np.uint8)
-        up = (rng.random(len(links)) > 0.06).astype(np.uint8)
-    if case == "disconnected":
-        names += [f"x{i}" for i in range(40)]
-        links += [(n * n + i, n * n + i + 1) for i in range(39)]
-        srcs = srcs + [n * n, n * n + 39]
-    g = T.csr_from_links(names, np.array(links), overloaded=ovl, link_up=up)
-    eng.set_graph(g)
-    dist, _ = check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
-    assert "bfs_ell2_kernel" in eng.last_kernels(), eng.last_kernels()
-    if case == "depth":
-        assert int(dist[2, n * n + 299]) == 299
-
-
 def test_ring_overflow_rerun_list(eng, monkeypatch):
     """A ring too small for the frontier (forced: levels of ~1000 nodes on a random
     expander) flags every solve; the full-order pass re-runs them from the list."""
@@ -811,21 +772,3 @@ def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag, lanes):
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (1400, 2))])
     g = T.fabric(288 + 56)
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
-
-
-@pytest.mark.parametrize("ring", [None, "256"])
-def test_ell16_kernel_opt_in(eng, monkeypatch, ring):
-    """The opt-in single-u16-state ELL kernel (OPENR_SPF_ELL16=1, spf_bfs_lvl.hip) on grids,
-    a ring forced too small (flagged solves re-run by the full-order pass) and a chain
-    deeper than 253 levels."""
-    monkeypatch.setenv("OPENR_SPF_ELL16", "1")
-    if ring:
-        monkeypatch.setenv("OPENR_SPF_RING_CAP", ring)
-    for n in (10, 33):
-        check_against_oracle(eng, T.grid_fast(n), list(range(n * n)), True, check_pathlinks=False)
-    V = 600
-    g = T.csr_from_links([f"c{i:04d}" for i in range(V)], np.array([(i, i + 1) for i in range(V - 1)]))
-    check_against_oracle(eng, g, [0, 1, 300, 599], True, check_pathlinks=False)
-    g2 = random_graph(7, 400, 700, 1, p_ovl=0.05, p_par=0.0)
-    if int(np.diff(g2.row_ptr).max()) <= 4:
-        check_against_oracle(eng, g2, list(range(g2.num_nodes)), True, check_pathlinks=False)
