@@ -27,13 +27,14 @@ CC ?= gcc
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 CPPTEST := tests/cpp/build/linkstate_test
 DECTEST := tests/cpp/build/decision_test
+DECBENCH := tests/cpp/build/decision_bench
 CPPTEST_SRCS := tests/cpp/linkstate_test.cpp tests/cpp/harness.h oracle/spf_oracle.c oracle/spf_oracle.h
 DECTEST_SRCS := tests/cpp/decision_test.cpp tests/cpp/harness.h openr_amd/csrc/host/HostParallel.h oracle/spf_oracle.c oracle/spf_oracle.h
 
 # "<hash> <files>" of a file list (the same recipe as openr_amd/engine.py:source_hash)
 build_id = $$(cat $(1) | sha256sum | cut -c1-16) $(1)
 
-all: $(ENGINE) $(HOST) oracle $(CPPTEST) $(DECTEST)
+all: $(ENGINE) $(HOST) oracle $(CPPTEST) $(DECTEST) $(DECBENCH)
 
 $(LIBDIR):
 	mkdir -p $@
@@ -66,6 +67,13 @@ $(DECTEST): $(DECTEST_SRCS) $(HOST)
 	$(CC) -O2 -std=c11 -fPIC -c oracle/spf_oracle.c -o tests/cpp/build/spf_oracle_d.o
 	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/decision_test.cpp tests/cpp/build/spf_oracle_d.o \
 	  -DOPENR_TEST_BUILD_ID="\"$(call build_id,$(DECTEST_SRCS))\"" \
+	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
+
+# DecisionBenchmark through the drop-in (bench.py --workload decision); links the oracle as
+# the checker and the faithful-cost CPU baseline
+$(DECBENCH): tests/cpp/decision_bench.cpp $(HOST) oracle
+	mkdir -p tests/cpp/build
+	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/decision_bench.cpp oracle/spf_oracle.o oracle/spf_faithful.o \
 	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 
 oracle:

@@ -27,6 +27,7 @@ sample of the same sources, rank 0 at N=1 only.
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -751,8 +752,10 @@ def main():
     ap.add_argument("--ksp-block", type=int, default=256,
                     help="ksp2: sources per device call within a step (token rows are reused)")
     ap.add_argument("--lfa", action="store_true", help="routes: SpfSolver computeLfaPaths")
+    ap.add_argument("--decision-cases", default="grid:10000:sp,grid:10000:ksp2,grid:1024:ksp2,fabric:5000:sp",
+                    help="decision: topology:size:algo list (BM_DecisionGrid / BM_DecisionFabric parameters)")
     ap.add_argument("--workload", default="all-sources",
-                    choices=["all-sources", "whatif", "ksp2", "update", "adjdb", "routes"],
+                    choices=["all-sources", "whatif", "ksp2", "update", "adjdb", "routes", "decision"],
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
                          "(BASELINE config 4)")
     args = ap.parse_args()
@@ -771,7 +774,61 @@ def main():
         return adjdb_main(args)
     if args.workload == "routes":
         return routes_main(args)
+    if args.workload == "decision":
+        return decision_main(args)
     return all_sources_main(args)
+
+
+def decision_main(args):
+    """DecisionBenchmark through the drop-in (DecisionBenchmark.cpp:12-29,
+    RoutingBenchmarkUtils.cpp:406-479, 517-630): per step, one node's adjacency database is
+    re-advertised with its overload bit toggled and Decision (LFA on) rebuilds its own
+    route DB: LinkState::updateAdjacencyDatabase + SpfSolver::buildRouteDb on the GPU
+    engine. The harness is tests/cpp/decision_bench.cpp (C++, as the reference's
+    benchmark is); it checks the last route DB against oracle SPF rebuilds and prices the
+    reference's cost of the same step on the faithful CPU restatement. One JSON line per
+    (topology, algorithm)."""
+    binary = os.path.join(ROOT, "tests", "cpp", "build", "decision_bench")
+    if not os.path.exists(binary):
+        raise SystemExit("build first: make (tests/cpp/build/decision_bench)")
+    for case in args.decision_cases.split(","):
+        topo, size, algo = case.split(":")
+        # KSP2 on large grids: the reference re-runs one SPF per destination per update
+        steps = args.steps if not (algo == "ksp2" and int(size) >= 10000) else max(2, min(args.steps, 5))
+        cmd = [binary, "--topology", topo, "--size", size, "--algo", algo, "--iters", str(steps),
+               "--warmup", str(max(1, args.warmup)), "--check"]
+        if not args.no_cpu_baseline:
+            cmd += ["--cpu-iters", "1", "--cpu-threads", "16"]
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
+        if p.returncode != 0:
+            sys.stderr.write(p.stdout + p.stderr)
+            raise SystemExit(f"decision_bench failed for {case} (rc {p.returncode})")
+        line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+        cpu = line.get("cpu_baseline")
+        out = {
+            "metric": "DecisionBenchmark: adjacency update (overload toggle) + buildRouteDb(my node), LFA on",
+            "value": 1e3 / line["ms_per_update"],
+            "unit": "updates/s",
+            "n_gpus": 1,
+            "steps": steps,
+            "warmup": max(1, args.warmup),
+            "ms_per_step": line["ms_per_update"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (reference benchmark generators: createGrid / createFabric)",
+            "config": {"workload": f"BM_Decision{'Grid' if topo == 'grid' else 'Fabric'}({size}, "
+                                   f"{line['algo']})", "topology": topo, "size": int(size), "nodes": line["nodes"],
+                       "my_node": line["my_node"], "lfa": True},
+            "decision": line,
+        }
+        if cpu:
+            out["cpu_baseline"] = {"value": 1e3 / cpu["ms_per_update"], "unit": "updates/s", "cores": 1,
+                                   "kind": "port", "sample": cpu["sample"], "ms_per_update": cpu["ms_per_update"],
+                                   "spf_runs_per_update": cpu["spf_runs_per_update"], "ms_per_spf": cpu["ms_per_spf"],
+                                   "ms_route_construction": cpu["ms_route_construction"]}
+        print(json.dumps(out), flush=True)
 
 
 def all_sources_main(args):
