@@ -360,7 +360,7 @@ def ksp2_main(args):
     import torch
     import torch.distributed as dist
 
-    from openr_amd.engine import SpfEngine
+    from openr_amd.engine import SpfEngine, SpfError
     from openr_amd.shard import max_over_ranks, shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -914,23 +914,40 @@ def all_sources_main(args):
         mets = np.unique(np.asarray(g.metric)[np.asarray(g.edge_up) != 0]) if use_metric else np.array([1])
         cost = int(mets[0]) if mets.size == 1 else (1 if mets.size == 0 else 0)
         form = "full"
+        native = False
+        gstep = step
         if args.gather == "compact" and cost > 0:
             fin = d_dist[:n_local][d_dist[:n_local] != -1]
             mx = torch.tensor([float(fin.max().item()) if fin.numel() else 0.0], dtype=torch.float64, device=dev)
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             max_level = int(mx.item()) // cost
             if max_level <= 65534:
-                gb = CompactGather(d_dist[:n_local], d_nh[:n_local], V, world, cost, max_level)
                 form = "levels-u8" if max_level <= 254 else "levels-u16"
+                # fused: the solve writes the level rows itself (OPENR_SPF_EMIT_LEVELS8/16);
+                # the device-side encode of u64 rows only where the engine cannot
+                gb = CompactGather.native(d_nh[:n_local], V, world, cost, max_level, V, dev)
+
+                def gstep():
+                    eng.solve_device(src.data_ptr(), n_local, gb.level_send.data_ptr(), d_nh.data_ptr(), nb, use_metric,
+                                     stream=stream.cuda_stream, level_bytes=gb.level_bytes)
+                try:
+                    gstep()
+                    torch.cuda.synchronize(dev)
+                    native = eng.take_status() == 0
+                except SpfError:
+                    native = False
+                if not native:
+                    gb = CompactGather(d_dist[:n_local], d_nh[:n_local], V, world, cost, max_level)
+                    gstep = step
         if form == "full":
             gb = GatherBuffers(d_dist[:n_local], d_nh[:n_local], V, world)
         for _ in range(max(1, args.warmup)):
-            step()
+            gstep()
             gb.allgather()
         barrier()
         tg = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            gstep()
             gb.allgather()
         barrier()
         gel = max_over_ranks(time.perf_counter() - tg, dev)
@@ -945,14 +962,16 @@ def all_sources_main(args):
                 assert np.array_equal(host[i].astype(np.int64), exp), "gathered result check failed"
         m_rows = max(shard_range(V, r, world)[1] - shard_range(V, r, world)[0] for r in range(world))
         full_bytes = int(m_rows * V * (8 + nb))
-        gather = {"form": form, "ms_per_step": gel / args.steps * 1e3,
+        gather = {"form": form, "fused_level_rows": native, "ms_per_step": gel / args.steps * 1e3,
                   "bytes_per_rank": int(gb.bytes_per_rank) if form != "full" else full_bytes,
                   "bytes_per_rank_full_form": full_bytes,
                   "compute_only_value": None,  # filled below (= value)
                   "gather_inclusive_value": V * args.steps / gel,
                   "collective": ("all_gather_into_tensor (RCCL) of " +
-                                 ("u8/u16 level rows (dist = level x cost on receipt, encoded on the device after "
-                                  "each solve) + next-hop rows" if form != "full" else "dist u64 + next-hop rows") +
+                                 (("u8/u16 level rows written by the solve itself (OPENR_SPF_EMIT_LEVELS8/16; "
+                                   "dist = level x cost on receipt)" if native else
+                                   "u8/u16 level rows (dist = level x cost on receipt, encoded on the device after "
+                                   "each solve)") + " + next-hop rows" if form != "full" else "dist u64 + next-hop rows") +
                                  ", solve included")}
 
     solves_total = (V if strong else V * world) * args.steps

@@ -88,6 +88,13 @@ enum {
   OPENR_SPF_USE_LINK_METRIC = 1u << 0, /* runSpf useLinkMetric; else every hop costs 1 */
   OPENR_SPF_EMIT_TIGHT = 1u << 1,      /* fill tight[] (pathLinks reconstruction)      */
   OPENR_SPF_EMIT_ORDER = 1u << 2,      /* exact-order kernel (openr_spf_solve_order)  */
+  OPENR_SPF_EMIT_LEVELS8 = 1u << 3,    /* solve_device: u8 level rows in d_dist (below) */
+  OPENR_SPF_EMIT_LEVELS16 = 1u << 4,   /* solve_device: u16 level rows in d_dist        */
+};
+
+/* Sticky device-side conditions (openr_spf_take_status) */
+enum {
+  OPENR_SPF_STATUS_LEVEL_OVERFLOW = 1u, /* an EMIT_LEVELS8 row held a finite level > 254 (written 0xFE) */
 };
 
 typedef struct openr_spf_ctx openr_spf_ctx;
@@ -173,11 +180,23 @@ int openr_spf_solve_ignore(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t
    device_ids given to create). All pointers are device memory; d_ignore_ptr may be
    NULL (no ignore sets); d_nh / d_tight may be NULL. `stream` is a hipStream_t
    (NULL = the context's own stream). Asynchronous: returns after enqueueing. */
+/* With OPENR_SPF_EMIT_LEVELS8 / 16 the distance rows are written in level form instead:
+   d_dist points to [n][V] u8 / u16 levels (level = dist / cost; all ones = not in the
+   SpfResult) — the compact rows a strong-scaling rank all-gathers, 1 or 2 bytes per node
+   instead of 8, emitted by the solve itself. Only for graphs on which every usable edge
+   costs the same (or useLinkMetric off) and that run on the level BFS family (uniform-cost
+   rows of <= 4 ELL slots, grids), with no ignore sets and no tight output: otherwise
+   OPENR_SPF_ENOTSUP. A finite level above 254 in a u8 row is written as 0xFE and sets
+   OPENR_SPF_STATUS_LEVEL_OVERFLOW (openr_spf_take_status): use u16 rows for such graphs. */
 int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index,
                            const uint32_t* d_sources, uint32_t n, uint32_t flags,
                            const uint32_t* d_ignore_ptr, const uint32_t* d_ignore_links,
                            uint64_t* d_dist, uint8_t* d_nh, uint32_t nh_bytes,
                            uint64_t* d_tight, void* stream);
+
+/* Waits for device `device_index` to go idle, then returns the OPENR_SPF_STATUS_* bits
+   its device-form calls raised since the last call (and clears them). */
+int openr_spf_take_status(openr_spf_ctx* ctx, int device_index, uint32_t* out_status);
 
 /* Per-link-failure what-if sweep (no reference API: the north-star what-if workload over
    LinkState::runSpf(src, useLinkMetric, {link}), LinkState.cpp:808-882 with the

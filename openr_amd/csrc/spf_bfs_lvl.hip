@@ -74,14 +74,71 @@ int lvl_class_mode(int cls) {
   }
 }
 
-// Writes this solve's dist row (u64) and next-hop row from LDS, coalesced.
+// The distance part of a solve's rows from its levels: u64 distances (level x cost,
+// UINT64_MAX unreached) or, when SolveArgs::lvl_rows is set, the levels themselves (u8 / u16,
+// all ones unreached: the compact form a strong-scaling rank all-gathers),
+// coalesced. Lanes t, t + stride, ... of the writing group.
+template <typename LT>
+__device__ __forceinline__ void store_dist_row(const SolveArgs& a, uint32_t sid, uint32_t V, const LT* lvl,
+                                               uint64_t cost, bool nt, uint32_t t, uint32_t stride) {
+  constexpr uint32_t kUnset = LvlOps<LT>::kUnset;
+  const size_t row = out_row_of(a, sid);
+  if (a.lvl_rows) {
+    if (a.lvl_bytes == 1) {
+      uint8_t* lrow = a.lvl_rows + row * V;
+      if (sizeof(LT) == 1 && ((reinterpret_cast<uintptr_t>(lrow) | V) & 3u) == 0) {
+        const uint32_t* l4 = reinterpret_cast<const uint32_t*>(lvl);  // four u8 levels per dword, as stored
+        uint32_t* o4 = reinterpret_cast<uint32_t*>(lrow);
+        for (uint32_t i = t; i < V / 4u; i += stride) store_row<uint32_t>(&o4[i], l4[i], nt);
+      } else {
+        bool over = false;
+        for (uint32_t v = t; v < V; v += stride) {
+          const uint32_t l = lvl[v];
+          const bool big = l != kUnset && l > 0xFEu;
+          over |= big;
+          lrow[v] = (uint8_t)(l == kUnset ? 0xFFu : big ? 0xFEu : l);
+        }
+        if (over) atomicOr(a.status, kStatusLevelOverflow);
+      }
+    } else {
+      uint16_t* lrow = reinterpret_cast<uint16_t*>(a.lvl_rows) + row * V;
+      for (uint32_t v = t; v < V; v += stride) {
+        const uint32_t l = lvl[v];
+        lrow[v] = (uint16_t)(l == kUnset ? 0xFFFFu : l);
+      }
+    }
+    return;
+  }
+  uint64_t* drow = a.dist + row * V;
+  if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
+    // two nodes per lane: 16-byte stores
+    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
+    for (uint32_t i = t; i < V / 2u; i += stride) {
+      const uint32_t l0 = lvl[2u * i], l1 = lvl[2u * i + 1u];
+      const uint64_t x0 = l0 != kUnset ? (uint64_t)l0 * cost : ~0ull;
+      const uint64_t x1 = l1 != kUnset ? (uint64_t)l1 * cost : ~0ull;
+      if (nt) {
+        __builtin_nontemporal_store(x0, &d2[i].x);
+        __builtin_nontemporal_store(x1, &d2[i].y);
+      } else {
+        d2[i] = make_ulonglong2(x0, x1);
+      }
+    }
+  } else {
+    for (uint32_t v = t; v < V; v += stride) {
+      const uint32_t l = lvl[v];
+      store_row<uint64_t>(&drow[v], l != kUnset ? (uint64_t)l * cost : ~0ull, nt);
+    }
+  }
+}
+
+// Writes this solve's dist row (u64, or level row) and next-hop row from LDS, coalesced.
 // Sliced classes: slice s owns next-hop bytes [4s, 4s + 4); slice 0 also writes the
 // distance row and zero-fills the bytes past the last slice.
 template <int MODE, typename LT, int BLOCK, bool SLICED>
 __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uint32_t slice, uint32_t V,
                                            const LT* lvl, const uint32_t* nh, uint64_t cost, bool nt) {
   using N = Nh<MODE>;
-  using O = LvlOps<LT>;
   const uint32_t tid = threadIdx.x;
   if (SLICED) {
     if (a.nh) {
@@ -99,27 +156,7 @@ __device__ __forceinline__ void write_rows(const SolveArgs& a, uint32_t sid, uin
     }
     if (slice != 0) return;
   }
-  uint64_t* drow = a.dist + out_row_of(a, sid) * V;
-  if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 1u)) == 0) {
-    // two nodes per lane: 16-byte stores
-    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
-    for (uint32_t i = tid; i < V / 2u; i += BLOCK) {
-      const uint32_t l0 = lvl[2u * i], l1 = lvl[2u * i + 1u];
-      const uint64_t x0 = l0 != O::kUnset ? (uint64_t)l0 * cost : ~0ull;
-      const uint64_t x1 = l1 != O::kUnset ? (uint64_t)l1 * cost : ~0ull;
-      if (nt) {
-        __builtin_nontemporal_store(x0, &d2[i].x);
-        __builtin_nontemporal_store(x1, &d2[i].y);
-      } else {
-        d2[i] = make_ulonglong2(x0, x1);
-      }
-    }
-  } else {
-    for (uint32_t v = tid; v < V; v += BLOCK) {
-      const uint32_t l = lvl[v];
-      store_row<uint64_t>(&drow[v], l != O::kUnset ? (uint64_t)l * cost : ~0ull, nt);
-    }
-  }
+  store_dist_row<LT>(a, sid, V, lvl, cost, nt, tid, (uint32_t)BLOCK);
   if (SLICED || !a.nh) return;
   const uint32_t nb = a.nh_bytes;
   uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
@@ -985,9 +1022,9 @@ __global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, 
       if (overflow) {
         if (lane == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
       } else {
-        // rows out: u64 distances from the levels, then the next-hop bytes
-        uint64_t* drow = a.dist + out_row_of(a, sid) * V;
-        if (((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0) {
+        // rows out: u64 distances (or level rows) from the levels, then the next-hop bytes
+        uint64_t* drow = a.dist ? a.dist + out_row_of(a, sid) * V : nullptr;
+        if (!a.lvl_rows && ((reinterpret_cast<uintptr_t>(drow) & 15u) | (V & 3u)) == 0) {
           ulonglong2* d2 = reinterpret_cast<ulonglong2*>(drow);
           for (uint32_t i = lane; i < V / 4u; i += 64u) {
             const uint32_t w = lvl_w[i];
@@ -1008,10 +1045,8 @@ __global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, 
             }
           }
         } else {
-          for (uint32_t v = lane; v < V; v += 64u) {
-            const uint32_t l = lvl[v];
-            store_row<uint64_t>(&drow[v], l != 0xFFu ? (uint64_t)l * cost : ~0ull, nt != 0);
-          }
+          store_dist_row<uint8_t>(a, sid, V, reinterpret_cast<const uint8_t*>(reinterpret_cast<char*>(smem) + slot),
+                                  cost, nt != 0, lane, 64u);
         }
         if (a.nh) {
           const uint32_t nb = a.nh_bytes;

@@ -84,6 +84,7 @@ struct Device {
   DevBuf<uint32_t> ovfc;
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
+  DevBuf<uint32_t> status;  // sticky OPENR_SPF_STATUS_* bits of device-form calls
   DevBuf<uint32_t> perm, part;  // source-class partition of a batch
   // what-if sweep: base SPF rows, the affected-unit work list, chunk result rows
   DevBuf<uint64_t> base_dist, base_tight, wdist;
@@ -958,6 +959,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.ovf.release();
     d.slicetmp.release();
     d.work.release();
+    d.status.release();
     d.perm.release();
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
@@ -1632,6 +1634,22 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   a.nh_bytes = nh_bytes;
   a.tight = d_tight;
   a.nh_bits = ctx->nh_bits;
+  if (flags & (OPENR_SPF_EMIT_LEVELS8 | OPENR_SPF_EMIT_LEVELS16)) {
+    // level rows (the compact strong-scaling exchange): level-family uniform-cost solves
+    if ((flags & OPENR_SPF_EMIT_LEVELS8) && (flags & OPENR_SPF_EMIT_LEVELS16))
+      return fail(OPENR_SPF_EINVAL, "EMIT_LEVELS8 and EMIT_LEVELS16 together");
+    if (plan.exact || !plan.bfs || plan.family != kFamLvl || d_tight || d_ignore_ptr)
+      return fail(OPENR_SPF_ENOTSUP, "level rows need a uniform-cost graph on the level BFS family, no ignore sets "
+                                     "and no tight output");
+    if (!d.status.p) {
+      HIP_TRY(d.status.reserve(1));
+      HIP_TRY(hipMemset(d.status.p, 0, sizeof(uint32_t)));
+    }
+    a.lvl_rows = reinterpret_cast<uint8_t*>(d_dist);
+    a.lvl_bytes = (flags & OPENR_SPF_EMIT_LEVELS8) ? 1u : 2u;
+    a.status = d.status.p;
+    a.dist = nullptr;
+  }
   HIP_TRY(d.ovf.reserve((size_t)n * ctx->nsl_max()));
   a.ovf_list = d.ovf.p;
   HIP_TRY(reserve_counters(d));
@@ -1640,6 +1658,20 @@ int openr_spf_solve_device(openr_spf_ctx* ctx, int device_index, const uint32_t*
   HIP_TRY(launch(ctx, d, plan, a, s));
   ctx->stats.spf_runs += n;
   ctx->stats.batches += 1;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_take_status(openr_spf_ctx* ctx, int device_index, uint32_t* out_status) {
+  if (!ctx || !out_status) return fail(OPENR_SPF_EINVAL, "null argument");
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  Device& d = ctx->devs[device_index];
+  *out_status = 0;
+  if (!d.status.p) return OPENR_SPF_OK;
+  HIP_TRY(hipSetDevice(d.ordinal));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out_status, d.status.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(d.status.p, 0, sizeof(uint32_t)));
   return OPENR_SPF_OK;
 }
 

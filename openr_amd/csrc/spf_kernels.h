@@ -128,6 +128,13 @@ struct SolveArgs {
   const uint32_t* out_row;
   unsigned long long* prof;   // profiling builds only: per-phase cycle sums (nullable)
   uint32_t* order;            // nullable [n][V]: pop index per node (exact-order kernel only)
+  // nullable, level family (OPENR_SPF_EMIT_LEVELS8 / 16): level rows [n][V] of lvl_bytes
+  // (1 or 2) per node here instead of the u64 distance rows (dist = level x cost; all
+  // ones = unreached); a finite level a u8 row cannot hold is written 0xFE and sets
+  // kStatusLevelOverflow in *status
+  uint8_t* lvl_rows;
+  uint32_t lvl_bytes;
+  uint32_t* status;
   // code-family sliced class with next-hop output: [krows][nsl][V] 29-bit chunks of the
   // sets (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
   uint32_t* slice_tmp;
@@ -143,6 +150,7 @@ __host__ __device__ inline size_t out_row_of(const SolveArgs& a, uint32_t sid) {
 constexpr uint32_t kMaxClasses = 8;
 constexpr uint32_t kCtrPerClass = 8;  // [0,1] fast launch, [2,3] re-run launch, [4] flagged solves
 constexpr uint32_t kWorkSlots = kCtrPerClass * kMaxClasses;
+constexpr uint32_t kStatusLevelOverflow = 1u;  // = OPENR_SPF_STATUS_LEVEL_OVERFLOW
 constexpr uint32_t kFringeCtr = kCtrPerClass * (kMaxClasses - 1);  // BFS classes use < 7 blocks
 constexpr uint32_t kIncrCtr = kFringeCtr + 2;                        // incremental what-if
 constexpr uint32_t kExactCtr = kIncrCtr + 2;                         // exact-order kernel

@@ -20,6 +20,9 @@ LIB_PATH = os.path.join(_HERE, "lib", "libopenr_spf.so")
 USE_LINK_METRIC = 1
 EMIT_TIGHT = 2
 EMIT_ORDER = 4
+EMIT_LEVELS8 = 8
+EMIT_LEVELS16 = 16
+STATUS_LEVEL_OVERFLOW = 1
 
 OK, EIO, ENOMEM, ENODEV, EINVAL, E2BIG, ENOTSUP = 0, -5, -12, -19, -22, -7, -95
 
@@ -47,6 +50,7 @@ EXPORTS = (
     "openr_spf_refresh",
     "openr_spf_refresh_device",
     "openr_spf_get_stats",
+    "openr_spf_take_status",
 )
 
 
@@ -137,6 +141,7 @@ def load_library():
     l.openr_spf_refresh.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, P(u32)]
     l.openr_spf_refresh_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, u32, vp, vp, P(u32)]
     l.openr_spf_get_stats.argtypes = [vp, P(SpfStats)]
+    l.openr_spf_take_status.argtypes = [vp, ctypes.c_int, P(u32)]
     for name in EXPORTS:
         if name not in ("openr_spf_last_error", "openr_spf_last_kernels", "openr_spf_limits", "openr_spf_destroy",
                         "openr_spf_build_id"):
@@ -248,14 +253,25 @@ class SpfEngine:
 
     def solve_device(self, d_sources: int, n: int, d_dist: int, d_nh: int = 0, nh_bytes: int = 0,
                      use_link_metric: bool = True, stream: int = 0, device_index: int = 0,
-                     d_ignore_ptr: int = 0, d_ignore_links: int = 0, d_tight: int = 0) -> None:
-        """Device-pointer form (ints are raw device addresses, e.g. torch data_ptr())."""
+                     d_ignore_ptr: int = 0, d_ignore_links: int = 0, d_tight: int = 0, level_bytes: int = 0) -> None:
+        """Device-pointer form (ints are raw device addresses, e.g. torch data_ptr()).
+        level_bytes = 1 / 2: d_dist receives u8 / u16 level rows instead of u64 distances
+        (OPENR_SPF_EMIT_LEVELS8 / 16: uniform-cost graphs on the level BFS family)."""
         flags = (USE_LINK_METRIC if use_link_metric else 0) | (EMIT_TIGHT if d_tight else 0)
+        if level_bytes:
+            flags |= {1: EMIT_LEVELS8, 2: EMIT_LEVELS16}[level_bytes]
         vp = ctypes.c_void_p
         _check(self._lib.openr_spf_solve_device(self._ctx, device_index, vp(d_sources), n, flags,
                                                 vp(d_ignore_ptr or None), vp(d_ignore_links or None), vp(d_dist),
                                                 vp(d_nh or None), nh_bytes or self.nh_bytes, vp(d_tight or None),
                                                 vp(stream or None)))
+
+    def take_status(self, device_index: int = 0) -> int:
+        """OPENR_SPF_STATUS_* bits raised by device-form calls since the last take (waits
+        for the device)."""
+        st = ctypes.c_uint32()
+        _check(self._lib.openr_spf_take_status(self._ctx, device_index, ctypes.byref(st)))
+        return int(st.value)
 
     def whatif(self, links: Sequence[int], sources: Sequence[int], use_link_metric: bool = True
                ) -> Tuple[np.ndarray, int]:

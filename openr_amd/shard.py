@@ -131,11 +131,52 @@ class CompactGather:
                 nb *= int(x)
         self.bytes_per_rank = self.m * V * (self.lv_send.element_size() + nb)
 
+    @classmethod
+    def native(cls, nh_shard, n_units: int, world: int, cost: int, max_level: int, V: int, device):
+        """The fused form: the solve writes this rank's level rows itself
+        (openr_spf_solve_device with OPENR_SPF_EMIT_LEVELS8 / 16 into ``level_send``), so
+        the exchange reads no u64 rows and there is no encode pass. ``level_bytes`` is the
+        flag the solve needs; ``level_send`` [m, V] (m = the largest shard) is its output
+        buffer (rows past this rank's shard stay zero)."""
+        import torch
+
+        obj = cls.__new__(cls)
+        if cost < 1:
+            raise ValueError("cost must be >= 1")
+        if max_level > 65534:
+            raise ValueError("levels do not fit u16: use GatherBuffers")
+        obj.cost = int(cost)
+        obj.dtype = torch.uint8 if max_level <= 254 else torch.int16
+        obj.sentinel = 0xFF if obj.dtype == torch.uint8 else -1
+        obj.level_bytes = 1 if obj.dtype == torch.uint8 else 2
+        obj.dist_shard = None
+        obj.sizes = shard_sizes(n_units, world)
+        obj.m = max(obj.sizes) if obj.sizes else 0
+        obj.world = world
+        obj.lv_send = torch.zeros((obj.m, V), dtype=obj.dtype, device=device)
+        obj.level_send = obj.lv_send
+        obj.lv_full = torch.empty((world * obj.m, V), dtype=obj.dtype, device=device)
+        obj.nh = None
+        nb = 0
+        if nh_shard is not None:
+            tail = tuple(nh_shard.shape[1:])
+            send = nh_shard if nh_shard.shape[0] == obj.m and nh_shard.is_contiguous() else torch.zeros(
+                (obj.m,) + tail, dtype=nh_shard.dtype, device=device)
+            obj.nh = (nh_shard, send, torch.empty((world * obj.m,) + tail, dtype=nh_shard.dtype, device=device))
+            nb = nh_shard.element_size()
+            for x in nh_shard.shape[2:]:
+                nb *= int(x)
+        obj.bytes_per_rank = obj.m * V * (obj.lv_send.element_size() + nb)
+        return obj
+
     def encode(self) -> None:
-        """This rank's u64 rows -> level rows (on the rows' device)."""
+        """This rank's u64 rows -> level rows (on the rows' device); nothing to do in the
+        native form (the solve wrote them)."""
         import torch
 
         d = self.dist_shard
+        if d is None:
+            return
         n = d.shape[0]
         if n == 0:
             return
