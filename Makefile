@@ -76,6 +76,14 @@ $(DECBENCH): tests/cpp/decision_bench.cpp $(HOST) oracle
 	$(CXX) $(CXXFLAGS) -o $@ tests/cpp/decision_bench.cpp oracle/spf_oracle.o oracle/spf_faithful.o \
 	  -L$(LIBDIR) -lopenr_decision -lopenr_spf -pthread -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 
+# Host-side profile of the route build (test infrastructure): the host sources, the
+# DecisionBenchmark harness and the CPU oracle standing in for the GPU engine
+# (tests/cpp/cpu_engine_stub.cpp), compiled with -pg. Not part of `all`; never shipped.
+host_profile: oracle
+	mkdir -p tests/cpp/build
+	$(CXX) -O2 -g -pg -std=c++17 -o tests/cpp/build/host_profile tests/cpp/decision_bench.cpp tests/cpp/cpu_engine_stub.cpp \
+	  $(filter %.cpp,$(HOST_SRCS)) oracle/spf_oracle.o oracle/spf_faithful.o -pthread
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -83,4 +91,4 @@ clean:
 	rm -rf $(LIBDIR) tests/cpp/build
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean host_profile

@@ -93,13 +93,26 @@ std::pair<thrift::PrefixForwardingType, thrift::PrefixForwardingAlgorithm> getPr
 
 // --- PrefixState ------------------------------------------------------------
 
+namespace {
+std::atomic<uint64_t> g_prefixStateUids{0};
+}
+PrefixState::PrefixState() : uid_(++g_prefixStateUids) {}
+PrefixState::PrefixState(const PrefixState& o) : prefixes_(o.prefixes_), uid_(++g_prefixStateUids) {}
+PrefixState& PrefixState::operator=(const PrefixState& o) {
+  prefixes_ = o.prefixes_;
+  ++version_;
+  return *this;
+}
+
 void PrefixState::updatePrefix(const std::string& node, const std::string& area, const thrift::PrefixEntry& entry) {
   prefixes_[entry.prefix].insert_or_assign({node, area}, entry);
+  ++version_;
 }
 
 void PrefixState::deletePrefix(const std::string& node, const std::string& area, const thrift::IpPrefix& prefix) {
   auto it = prefixes_.find(prefix);
   if (it == prefixes_.end()) return;
+  ++version_;
   it->second.erase({node, area});
   if (it->second.empty()) prefixes_.erase(it);
 }
@@ -187,6 +200,7 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
   for (auto& s : solvers) {
     s.counters_ = DecisionCounters{};
     s.bestRoutesCache_.clear();
+    s.bestLazy_.clear();
   }
   // the sequential loop leaves the cache of the last node some area knows (an unknown
   // node's build returns before touching it)
@@ -202,7 +216,10 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
     for (auto const& [_, ls] : als) frozen.push_back(std::make_unique<LinkState::MemoFreeze>(ls));
     parallelFor(nodes.size(), 1, workers, [&](unsigned w, size_t i) {
       auto db = solvers[w].buildRouteDb(nodes[i], als, prefixState);
-      if (i == last) bestRoutesCache_ = solvers[w].bestRoutesCache_;
+      if (i == last) {
+        bestRoutesCache_ = solvers[w].bestRoutesCache_;
+        bestLazy_ = solvers[w].bestLazy_;
+      }
       sink(i, db);
     });
   }
@@ -228,6 +245,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   if (!nodeExist) return std::nullopt;
   counters_.route_build_runs++;
   prefetch(myNodeName, als);
+  views_.clear();
+  viewsOf_ = myNodeName;
+  fast_ = FastCtx{};
 
   // KSP2 prefixes: every destination's first and second paths from here in one device
   // launch per area (LinkState::prefetchKthPaths stages them; selectBestPathsKsp2's
@@ -246,8 +266,40 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
 
   DecisionRouteDb routeDb;
   bestRoutesCache_.clear();
-  for (auto const& [prefix, _] : prefixState.prefixes())
-    if (auto r = createRouteForPrefix(myNodeName, als, prefixState, prefix)) routeDb.addUnicastRoute(std::move(*r));
+  bestLazy_.clear();
+  // advertiser ids of the single-advertiser prefixes on the fast path's mirror, computed
+  // once per (PrefixState contents, mirror)
+  const std::vector<uint32_t>* dstIds = nullptr;
+  // (set up only when there is a prefix: it reads my SPF, which counts as a run, as the
+  // first createRouteForPrefix would)
+  if (!prefixState.prefixes().empty() && fastSetup(als, myNodeName)) {
+    auto& c = dstIds_;
+    if (c.psUid != prefixState.uid() || c.psVersion != prefixState.version() || c.mirrorGen != fast_.m->generation) {
+      c.ids.clear();
+      c.ids.reserve(prefixState.prefixes().size());
+      for (auto const& [prefix, entries] : prefixState.prefixes()) {
+        uint32_t id = UINT32_MAX;
+        if (entries.size() == 1) {
+          auto it = fast_.m->id.find(entries.begin()->first.first);
+          if (it != fast_.m->id.end()) id = it->second;
+        }
+        c.ids.push_back(id);
+      }
+      c.psUid = prefixState.uid();
+      c.psVersion = prefixState.version();
+      c.mirrorGen = fast_.m->generation;
+    }
+    dstIds = &c.ids;
+  }
+  size_t pi = 0;
+  for (auto const& [prefix, entries] : prefixState.prefixes()) {  // key order
+    std::optional<RibUnicastEntry> r;
+    const uint32_t dstId = dstIds ? (*dstIds)[pi] : UINT32_MAX;
+    ++pi;
+    if (!(fast_.state == 1 && fastRoute(myNodeName, prefix, entries, dstId, &r)))
+      r = createRouteForPrefix(myNodeName, als, prefixState, prefix, entries, true);
+    if (r) routeDb.unicastRoutes.insert_or_assign(routeDb.unicastRoutes.end(), prefix, std::move(*r));
+  }
 
   // MPLS routes for every node label (:593-680)
   std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
@@ -317,22 +369,49 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
                                                                std::unordered_map<std::string, LinkState> const& als,
                                                                PrefixState const& prefixState,
                                                                thrift::IpPrefix const& prefix) {
-  counters_.get_route_for_prefix++;
   auto search = prefixState.prefixes().find(prefix);
-  if (search == prefixState.prefixes().end()) return std::nullopt;
-  bestRoutesCache_.erase(prefix);
+  if (search == prefixState.prefixes().end()) {
+    counters_.get_route_for_prefix++;
+    return std::nullopt;
+  }
+  return createRouteForPrefix(myNodeName, als, prefixState, prefix, search->second, false);
+}
 
-  // entries of reachable nodes only
-  PrefixEntries prefixEntries = search->second;
+std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string& myNodeName,
+                                                               std::unordered_map<std::string, LinkState> const& als,
+                                                               PrefixState const& prefixState, thrift::IpPrefix const& prefix,
+                                                               PrefixEntries const& allEntries, bool inOrder) {
+  counters_.get_route_for_prefix++;
+  // buildRouteDb cleared the cache and visits each prefix once, in key order
+  if (!inOrder) {
+    flushBestRoutes();
+    bestRoutesCache_.erase(prefix);
+  }
+
+  // entries of reachable nodes only (the reference filters a copy; the entries are used
+  // in place when every advertiser is reachable)
+  PrefixEntries filteredEntries;
+  const PrefixEntries* entries = &allEntries;
   for (auto const& [area, ls] : als) {
     // dense read of the memoised SPF (an unknown node's result holds only itself)
-    auto const mySpf = ls.getSpfView(myNodeName);
-    for (auto it = prefixEntries.begin(); it != prefixEntries.end();) {
-      const auto& [node, pArea] = it->first;
-      if (area != pArea || mySpf.reached(node)) ++it;
-      else it = prefixEntries.erase(it);
+    auto const& mySpf = views(ls, myNodeName).mine;
+    for (auto const& [na, e] : *entries) {
+      if (area == na.second && !mySpf.reached(na.first)) {
+        if (entries != &filteredEntries) {
+          filteredEntries = *entries;
+          entries = &filteredEntries;
+        }
+        break;
+      }
     }
+    if (entries == &filteredEntries)
+      for (auto it = filteredEntries.begin(); it != filteredEntries.end();) {
+        const auto& [node, pArea] = it->first;
+        if (area != pArea || mySpf.reached(node)) ++it;
+        else it = filteredEntries.erase(it);
+      }
   }
+  const PrefixEntries& prefixEntries = *entries;
   if (prefixEntries.empty()) {
     counters_.no_route_to_prefix++;
     return std::nullopt;
@@ -366,7 +445,8 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
     counters_.no_route_to_prefix++;
     return std::nullopt;
   }
-  bestRoutesCache_.insert_or_assign(prefix, best);
+  if (inOrder) bestRoutesCache_.insert_or_assign(bestRoutesCache_.end(), prefix, best);
+  else bestRoutesCache_.insert_or_assign(prefix, best);
   if (best.hasNode(myNodeName) && !hasSelfPrependLabel) return std::nullopt;  // self-originated
 
   const auto [forwardingType, forwardingAlgo] = getPrefixForwardingTypeAndAlgorithm(prefixEntries, best.allNodeAreas);
@@ -436,6 +516,9 @@ BestRouteSelectionResult SpfSolver::runBestPathSelectionBgp(thrift::IpPrefix con
 // Decision.cpp:782-802
 BestRouteSelectionResult SpfSolver::maybeFilterDrainedNodes(BestRouteSelectionResult&& result,
                                                             std::unordered_map<std::string, LinkState> const& als) const {
+  bool anyDrained = false;
+  for (auto const& [node, area] : result.allNodeAreas) anyDrained |= als.at(area).isNodeOverloaded(node);
+  if (!anyDrained) return std::move(result);  // nothing to filter: the same result, uncopied
   BestRouteSelectionResult filtered = result;
   for (auto it = filtered.allNodeAreas.begin(); it != filtered.allNodeAreas.end();) {
     const auto& [node, area] = *it;
@@ -470,15 +553,18 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsSpf(std::string const& 
                                                              PrefixState const& prefixState) {
   const bool isV4Prefix = prefix.isV4();
   const bool perDestination = forwardingType == thrift::PrefixForwardingType::SR_MPLS;
-  auto filtered = best.allNodeAreas;
+  std::set<NodeAndArea> filteredCopy;
+  const std::set<NodeAndArea>* filtered = &best.allNodeAreas;
   if (best.hasNode(myNodeName) && perDestination) {
     for (auto const& [na, e] : prefixEntries)
       if (na.first == myNodeName && e.prependLabel) {
-        filtered.erase(na);
+        filteredCopy = best.allNodeAreas;
+        filteredCopy.erase(na);
+        filtered = &filteredCopy;
         break;
       }
   }
-  const auto nhm = getNextHopsWithMetric(myNodeName, filtered, perDestination, als);
+  const auto nhm = getNextHopsWithMetric(myNodeName, *filtered, perDestination, als);
   if (nhm.second.empty()) {
     counters_.no_route_to_prefix++;
     return std::nullopt;
@@ -606,8 +692,8 @@ std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric
   Metric shortestMetric = std::numeric_limits<Metric>::max();
   for (auto const& [area, ls] : als) {
     // dense reads of the memoised SPFs (LinkState::SpfView): same results as getSpfResult,
-    // no SpfResult map materialised per route build
-    auto const fromHere = ls.getSpfView(me);
+    // no SpfResult map materialised per route build; views taken once per build
+    auto const& fromHere = views(ls, me).mine;
     auto const mm = getMinCostNodes(fromHere, dstNodeAreas);
     if (shortestMetric < mm.first) continue;
     if (shortestMetric > mm.first) {
@@ -615,39 +701,217 @@ std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric
       nextHopNodes.clear();
     }
     if (mm.second.empty()) continue;
+    static const std::string kNoDst;
     for (auto const& dst : mm.second) {
-      const std::string dstRef = perDestination ? dst : "";
+      const std::string& dstRef = perDestination ? dst : kNoDst;
       // getMetricFromAToB(me, nh) reads the same (already counted) result: nh != me
-      for (auto const& nh : fromHere.nextHops(dst))
-        nextHopNodes[std::make_pair(nh, dstRef)] = shortestMetric - fromHere.metric(nh);
+      fromHere.forEachNextHop(dst, [&](const std::string& nh, Metric dNh) {
+        nextHopNodes[std::make_pair(nh, dstRef)] = shortestMetric - dNh;
+      });
     }
     if (computeLfaPaths_) {
-      for (auto const& link : ls.linksFromNode(me)) {
-        if (!link->isUp()) continue;
-        const auto& nbr = link->getOtherNodeName(me);
-        auto const fromNbr = ls.getSpfView(nbr);
-        const Metric nbrToHere = fromNbr.metric(me);
+      for (auto const& nb : lfaViews(ls, me).nbrs) {  // up links of me, linksFromNode order
+        const auto& nbr = *nb.name;
+        const Metric nbrToHere = nb.toMe;
         for (auto const& [dst, dstArea] : dstNodeAreas) {
           if (area != dstArea) continue;
-          if (!fromNbr.reached(dst)) continue;
-          const Metric dNbr = fromNbr.metric(dst);
+          if (!nb.view.reached(dst)) continue;
+          const Metric dNbr = nb.view.metric(dst);
           if (dNbr < shortestMetric + nbrToHere) {  // RFC 5286
-            const auto key = std::make_pair(nbr, perDestination ? dst : std::string());
+            auto key = std::make_pair(nbr, perDestination ? dst : kNoDst);
             auto it = nextHopNodes.find(key);
-            if (it == nextHopNodes.end()) nextHopNodes.emplace(key, dNbr);
+            if (it == nextHopNodes.end()) nextHopNodes.emplace(std::move(key), dNbr);
             else if (it->second > dNbr) it->second = dNbr;
           }
         }
       }
     }
   }
-  return {shortestMetric, nextHopNodes};
+  return {shortestMetric, std::move(nextHopNodes)};
+}
+
+bool SpfSolver::fastSetup(std::unordered_map<std::string, LinkState> const& als, const std::string& me) {
+  if (fast_.state) return fast_.state == 1;
+  fast_.state = 2;
+  if (als.size() != 1 || enableBestRouteSelection_) return false;
+  const auto& [area, ls] = *als.begin();
+  const auto& mine = views(ls, me).mine;  // read by createRouteForPrefix for every prefix too
+  const LinkState::CsrMirror* m = mine.mirror();
+  if (!m) return false;
+  auto it = m->id.find(me);
+  if (it == m->id.end()) return false;
+  fast_.ls = &ls;
+  fast_.area = &area;
+  fast_.m = m;
+  fast_.me = it->second;
+  const auto& bits = mine.nhNeighbours();
+  auto bitOf = [&](uint32_t id) -> uint32_t {
+    for (uint32_t i = 0; i < bits.size(); ++i)
+      if (bits[i] == id) return i;
+    return UINT32_MAX;
+  };
+  for (auto const& link : ls.linksFromNode(me)) {
+    const std::string& nbr = link->getOtherNodeName(me);
+    auto nid = m->id.find(nbr);
+    if (nid == m->id.end()) return false;
+    const uint32_t b = bitOf(nid->second);
+    if (b == UINT32_MAX) return false;
+    fast_.links.push_back(FastLink{link.get(), b, link->isUp(), link->getMetricFromNode(me), &nbr});
+  }
+  fast_.val.assign(bits.size(), 0);
+  fast_.has.assign(bits.size(), 0);
+  fast_.state = 1;
+  return true;
+}
+
+bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries,
+                          uint32_t dstId, std::optional<RibUnicastEntry>* out) {
+  if (entries.size() != 1) return false;
+  const auto& [na, e] = *entries.begin();
+  if (na.second != *fast_.area || e.type == thrift::PrefixType::BGP ||
+      e.forwardingAlgorithm != thrift::PrefixForwardingAlgorithm::SP_ECMP || e.forwardingType != thrift::PrefixForwardingType::IP)
+    return false;
+  const LinkState::CsrMirror& m = *fast_.m;
+  const auto& mine = views_.front().mine;  // fastSetup: views_ holds this one area
+  const uint64_t* dm = mine.distRow();
+  (void)m;
+  counters_.get_route_for_prefix++;
+  *out = std::nullopt;
+  if (dstId == UINT32_MAX || dm[dstId] == UINT64_MAX) {  // advertiser not reached: entry filtered out
+    counters_.no_route_to_prefix++;
+    return true;
+  }
+  const uint32_t dst = dstId;
+  if (prefix.isV4() && !enableV4_) {
+    counters_.skipped_unicast_route++;
+    return true;
+  }
+  // selectBestRoutes: the single advertiser (maybeFilterDrainedNodes keeps a lone drained one)
+  bestLazy_.emplace_back(prefix, na);  // the best-route cache entry {success, {na}, na}
+  if (dst == fast_.me) {  // self-originated; with a prepend label no next hop leads to it
+    if (e.prependLabel) counters_.no_route_to_prefix++;
+    return true;
+  }
+  // getNextHopsWithMetric(me, {dst}, false): shortest next hops, then RFC 5286 alternates
+  const Metric d = dm[dst];
+  const uint32_t nb = mine.nhBytes();
+  const uint8_t* hv = mine.nhRow() + (size_t)dst * nb;
+  const auto& bits = mine.nhNeighbours();
+  bool any = false;
+  for (uint32_t i = 0; i < bits.size(); ++i) {
+    fast_.has[i] = (hv[i >> 3] >> (i & 7)) & 1u;
+    if (fast_.has[i]) {
+      fast_.val[i] = d - dm[bits[i]];
+      any = true;
+    }
+  }
+  if (computeLfaPaths_) {
+    auto& av = lfaViews(*fast_.ls, me);
+    if (!fast_.lfaReady) {
+      for (auto const& nv : av.nbrs) {
+        uint32_t b = UINT32_MAX;
+        if (nv.view.mirror() == fast_.m) {
+          const uint32_t id = m.id.at(*nv.name);
+          for (uint32_t i = 0; i < bits.size(); ++i)
+            if (bits[i] == id) b = i;
+        }
+        if (b == UINT32_MAX) {  // a neighbour's row on another mirror / map-backed: general path
+          fast_.state = 2;
+          return false;
+        }
+        fast_.lfaBit.push_back(b);
+      }
+      fast_.lfaReady = true;
+    }
+    for (size_t k = 0; k < av.nbrs.size(); ++k) {
+      const Metric dn = av.nbrs[k].view.distRow()[dst];
+      if (dn == UINT64_MAX || !(dn < d + av.nbrs[k].toMe)) continue;
+      const uint32_t b = fast_.lfaBit[k];
+      if (!fast_.has[b]) {
+        fast_.has[b] = 1;
+        fast_.val[b] = dn;
+        any = true;
+      } else if (fast_.val[b] > dn) {
+        fast_.val[b] = dn;
+      }
+    }
+  }
+  if (!any) {
+    counters_.no_route_to_prefix++;
+    return true;
+  }
+  // getNextHopsThrift(me, {dst}, isV4, false, d, ...): every up link to a next-hop node
+  NextHopSet nextHops;
+  const bool v4 = prefix.isV4();
+  for (auto const& fl : fast_.links) {
+    if (!fast_.has[fl.nbrBit] || !fl.up) continue;
+    const Metric over = fl.metric + fast_.val[fl.nbrBit];
+    if (!computeLfaPaths_ && over != d) continue;
+    nextHops.emplace(createNextHop(v4 ? fl.link->getNhV4FromNode(me) : fl.link->getNhV6FromNode(me),
+                                   fl.link->getIfaceFromNode(me), static_cast<int32_t>(over), std::nullopt,
+                                   fl.link->getArea(), *fl.nbr));
+  }
+  // addBestPaths
+  if (e.minNexthop && *e.minNexthop > (int64_t)nextHops.size()) return true;
+  RibUnicastEntry r;
+  r.prefix = prefix;
+  r.nexthops = std::move(nextHops);
+  r.bestPrefixEntry = e;
+  r.bestArea = na.second;
+  r.doNotInstall = false;  // not BGP
+  *out = std::move(r);
+  return true;
+}
+
+void SpfSolver::flushBestRoutes() const {
+  for (auto& [prefix, na] : bestLazy_) {
+    BestRouteSelectionResult best;
+    best.allNodeAreas.emplace(na);
+    best.bestNodeArea = na;
+    best.success = true;
+    bestRoutesCache_.insert_or_assign(std::move(prefix), std::move(best));
+  }
+  bestLazy_.clear();
+}
+
+std::map<thrift::IpPrefix, BestRouteSelectionResult> const& SpfSolver::getBestRoutesCache() const {
+  flushBestRoutes();
+  return bestRoutesCache_;
+}
+
+SpfSolver::AreaViews& SpfSolver::views(const LinkState& ls, const std::string& me) const {
+  if (viewsOf_ != me) {  // a caller outside buildRouteDb (or another node): start over
+    views_.clear();
+    viewsOf_ = me;
+  }
+  for (auto& av : views_)
+    if (av.ls == &ls) return av;
+  AreaViews av;
+  av.ls = &ls;
+  av.mine = ls.getSpfView(me);
+  views_.push_back(std::move(av));
+  return views_.back();
+}
+
+SpfSolver::AreaViews& SpfSolver::lfaViews(const LinkState& ls, const std::string& me) const {
+  AreaViews& av = views(ls, me);
+  if (!av.nbrsReady) {
+    for (auto const& link : ls.linksFromNode(me)) {
+      if (!link->isUp()) continue;
+      const auto& nbr = link->getOtherNodeName(me);
+      NbrView nv{&nbr, ls.getSpfView(nbr), 0};
+      nv.toMe = nv.view.metric(me);
+      av.nbrs.push_back(std::move(nv));
+    }
+    av.nbrsReady = true;
+  }
+  return av;
 }
 
 // Decision.cpp:1210-1317
 NextHopSet SpfSolver::getNextHopsThrift(const std::string& me, const std::set<NodeAndArea>& dstNodeAreas, bool isV4,
                                         bool perDestination, Metric minMetric,
-                                        std::unordered_map<std::pair<std::string, std::string>, Metric> nextHopNodes,
+                                        std::unordered_map<std::pair<std::string, std::string>, Metric> const& nextHopNodes,
                                         std::optional<int32_t> swapLabel,
                                         std::unordered_map<std::string, LinkState> const& als,
                                         PrefixEntries const& prefixEntries) {

@@ -157,12 +157,20 @@ struct DecisionRouteDb {  // Decision.h:80
 class PrefixState {
  public:
   using Entries = std::map<thrift::IpPrefix, PrefixEntries>;
+  PrefixState();
+  PrefixState(const PrefixState& o);
+  PrefixState& operator=(const PrefixState& o);
   void updatePrefix(const std::string& node, const std::string& area, const thrift::PrefixEntry& entry);
   void deletePrefix(const std::string& node, const std::string& area, const thrift::IpPrefix& prefix);
   Entries const& prefixes() const { return prefixes_; }
+  // (uid, version) names this object's current contents: a process-wide id per object
+  // and a count of its mutations (route builds key per-prefix caches on it)
+  uint64_t uid() const { return uid_; }
+  uint64_t version() const { return version_; }
 
  private:
   Entries prefixes_;
+  uint64_t uid_ = 0, version_ = 0;
 };
 
 struct BestRouteSelectionResult {  // Decision.h
@@ -222,11 +230,17 @@ class SpfSolver {
                      std::unordered_map<std::string, LinkState> const& areaLinkStates, PrefixState const& prefixState,
                      const std::function<void(size_t, std::optional<DecisionRouteDb>&)>& sink);
 
+  // (buildRouteDb walks prefixState.prefixes() in key order and hands each entry set in:
+  // no second lookup, and the best-route cache and route map grow at their ends)
+  std::optional<RibUnicastEntry> createRouteForPrefix(const std::string& myNodeName,
+                                                      std::unordered_map<std::string, LinkState> const& areaLinkStates,
+                                                      PrefixState const& prefixState, thrift::IpPrefix const& prefix,
+                                                      PrefixEntries const& entries, bool inOrder);
   std::optional<RibUnicastEntry> createRouteForPrefix(const std::string& myNodeName,
                                                       std::unordered_map<std::string, LinkState> const& areaLinkStates,
                                                       PrefixState const& prefixState, thrift::IpPrefix const& prefix);
 
-  std::map<thrift::IpPrefix, BestRouteSelectionResult> const& getBestRoutesCache() const { return bestRoutesCache_; }
+  std::map<thrift::IpPrefix, BestRouteSelectionResult> const& getBestRoutesCache() const;
   DecisionCounters const& counters() const { return counters_; }
 
  private:
@@ -261,16 +275,76 @@ class SpfSolver {
       std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
   NextHopSet getNextHopsThrift(const std::string& myNodeName, const std::set<NodeAndArea>& dstNodeAreas, bool isV4,
                                bool perDestination, Metric minMetric,
-                               std::unordered_map<std::pair<std::string, std::string>, Metric> nextHopNodes,
+                               std::unordered_map<std::pair<std::string, std::string>, Metric> const& nextHopNodes,
                                std::optional<int32_t> swapLabel,
                                std::unordered_map<std::string, LinkState> const& areaLinkStates,
                                PrefixEntries const& prefixEntries = {});
   void prefetch(const std::string& myNodeName, std::unordered_map<std::string, LinkState> const& areaLinkStates) const;
 
+  // Per route build: the memoised SPF views a build of `me` reads, taken from the
+  // LinkState once per build instead of once per prefix (the first read of each still
+  // counts its SPF run where the reference's first getSpfResult would). Cleared by
+  // buildRouteDb; filled lazily, so a build reads exactly the SPFs the reference does.
+  struct NbrView {
+    const std::string* name;  // the Link's copy of the neighbour name
+    LinkState::SpfView view;
+    Metric toMe;              // neighbour -> me (getMetricFromAToB)
+  };
+  struct AreaViews {
+    const LinkState* ls = nullptr;
+    LinkState::SpfView mine;
+    bool nbrsReady = false;
+    std::vector<NbrView> nbrs;  // LFA: up links of me, linksFromNode order
+  };
+  mutable std::string viewsOf_;
+  mutable std::vector<AreaViews> views_;
+
+  // SP_ECMP / IP fast path of buildRouteDb (one area, dense memo rows from one mirror): the
+  // route of a prefix with a single advertiser computed on node ids — the same
+  // RibUnicastEntry, counters and best-route cache entry as createRouteForPrefix, without
+  // name lookups per route. fast_.state: 0 not set up, 1 usable, 2 not usable (general path).
+  struct FastLink {
+    const Link* link;
+    uint32_t nbrBit;  // the neighbour's next-hop bit in my row
+    bool up;
+    Metric metric;    // from me
+    const std::string* nbr;
+  };
+  struct FastCtx {
+    int state = 0;
+    const LinkState* ls = nullptr;
+    const std::string* area = nullptr;
+    const LinkState::CsrMirror* m = nullptr;
+    uint32_t me = 0;
+    std::vector<FastLink> links;
+    bool lfaReady = false;
+    std::vector<uint32_t> lfaBit;  // per lfaViews(ls, me).nbrs entry: its neighbour's next-hop bit
+    std::vector<Metric> val;       // per next-hop bit: nextHopNodes value
+    std::vector<uint8_t> has;
+  };
+  FastCtx fast_;
+  bool fastSetup(std::unordered_map<std::string, LinkState> const& areaLinkStates, const std::string& me);
+  // true when the prefix was served (*out = its route or none)
+  bool fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries, uint32_t dstId,
+                 std::optional<RibUnicastEntry>* out);
+  AreaViews& views(const LinkState& ls, const std::string& me) const;
+  AreaViews& lfaViews(const LinkState& ls, const std::string& me) const;
+
   const std::string myNodeName_;
   const bool enableV4_, computeLfaPaths_, enableOrderedFib_, bgpDryRun_, enableBestRouteSelection_;
   std::unordered_map<int32_t, std::vector<thrift::NextHopThrift>> staticMplsRoutes_;
-  std::map<thrift::IpPrefix, BestRouteSelectionResult> bestRoutesCache_;
+  mutable std::map<thrift::IpPrefix, BestRouteSelectionResult> bestRoutesCache_;
+  // best-route cache entries of single-advertiser routes built on the fast path, merged
+  // into bestRoutesCache_ when it is read (flushBestRoutes)
+  mutable std::vector<std::pair<thrift::IpPrefix, NodeAndArea>> bestLazy_;
+  void flushBestRoutes() const;
+  // advertiser node ids of a PrefixState's single-advertiser prefixes, in key order, on
+  // one mirror (UINT32_MAX: several advertisers / unknown node)
+  struct DstIds {
+    uint64_t psUid = 0, psVersion = 0, mirrorGen = 0;
+    std::vector<uint32_t> ids;
+  };
+  DstIds dstIds_;
   DecisionCounters counters_;
 };
 

@@ -764,6 +764,12 @@ const uint8_t* LinkState::SpfView::nh(uint32_t v) const {
   return d.nh.data() + ((size_t)row_ * m_->names.size() + v) * d.nb;
 }
 
+uint32_t LinkState::SpfView::nhBytes() const { return static_cast<const DenseRows*>(rows_)->nb; }
+
+const std::vector<uint32_t>& LinkState::SpfView::nhNeighbours() const {
+  return static_cast<const DenseRows*>(rows_)->nbrs[row_];
+}
+
 int32_t LinkState::SpfView::id(const std::string& node) const {
   auto it = m_->id.find(node);
   if (it == m_->id.end() || dist()[it->second] == UINT64_MAX) return -1;
@@ -871,6 +877,7 @@ const LinkState::CsrMirror& LinkState::csrMirror() const {
   // address) never matches this mirror's generation
   static std::atomic<uint64_t> generations{0};
   mirrorGeneration_ = ++generations;
+  mirror_.generation = mirrorGeneration_;
   return mirror_;
 }
 

@@ -354,6 +354,7 @@ class LinkState {
     std::vector<uint32_t> edgeOwner;
     std::unordered_map<const Link*, uint32_t> linkIndex;  // Link -> link id (ignore sets)
     bool metricsPositive = true;  // every usable metric in [1, 2^31-1]: fast kernels
+    uint64_t generation = 0;      // process-wide id of this mirror build (kept by a retired snapshot)
   };
   const CsrMirror& csrMirror() const;
   // process-wide id of the mirror csrMirror() last built (tests: a rebuild changes it)
@@ -373,6 +374,19 @@ class LinkState {
     LinkStateMetric metric(const std::string& node) const;
     // next hops of a reached node (std::out_of_range otherwise)
     std::vector<std::string> nextHops(const std::string& node) const;
+    // f(next-hop name, distance to that next hop) for each next hop of a reached node
+    // (std::out_of_range otherwise): nextHops + metric(nh) without building names
+    template <class F>
+    void forEachNextHop(const std::string& node, F&& f) const;
+    // Dense internals for id-based readers (the route build's fast path): mirror() is null
+    // when the entry is map-backed; ids index mirror()->names. distRow()[v] = the metric of
+    // v (UINT64_MAX: not reached), nhRow()[v * nhBytes() ..] its next-hop bits, bit i =
+    // node nhNeighbours()[i].
+    const CsrMirror* mirror() const { return map_ ? nullptr : m_; }
+    const uint64_t* distRow() const { return dist(); }
+    const uint8_t* nhRow() const { return nh(0); }
+    uint32_t nhBytes() const;
+    const std::vector<uint32_t>& nhNeighbours() const;
 
    private:
     friend class LinkState;
@@ -513,6 +527,22 @@ class LinkState {
   mutable uint64_t mirrorGeneration_ = 0;
   mutable std::shared_ptr<SpfEngineHandle> engine_;
 };
+
+template <class F>
+void LinkState::SpfView::forEachNextHop(const std::string& node, F&& f) const {
+  if (map_) {
+    for (auto const& nh : map_->at(node).nextHops()) f(nh, map_->at(nh).metric());
+    return;
+  }
+  const int32_t v = id(node);
+  if (v < 0) throw std::out_of_range("SpfView::forEachNextHop: " + node + " not reached");
+  const DenseRows& d = *static_cast<const DenseRows*>(rows_);
+  const uint8_t* hv = nh((uint32_t)v);
+  const uint64_t* ds = dist();
+  const std::vector<uint32_t>& nbrs = d.nbrs[row_];
+  for (uint32_t i = 0; i < nbrs.size(); ++i)
+    if ((hv[i >> 3] >> (i & 7)) & 1u) f(m_->names[nbrs[i]], ds[nbrs[i]]);
+}
 
 }  // namespace openr
 

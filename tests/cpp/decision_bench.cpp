@@ -139,6 +139,8 @@ struct Options {
   uint32_t size = 10000, iters = 20, warmup = 2, cpuIters = 0, cpuThreads = 1;
   uint64_t seed = 1;
   bool check = false;
+  bool allRoutes = false;  // --all-routes: every node's route DB (buildRouteDbs), host-side profiling
+  uint32_t routeIters = 0;  // --route-iters N: N memoised rebuilds of my route DB, then exit (profiling)
 };
 
 struct Bench {
@@ -373,6 +375,8 @@ int main(int argc, char** argv) {
     else if (a == "--cpu-threads") o.cpuThreads = (uint32_t)std::stoul(next());
     else if (a == "--seed") o.seed = std::stoull(next());
     else if (a == "--check") o.check = true;
+    else if (a == "--all-routes") o.allRoutes = true;
+    else if (a == "--route-iters") o.routeIters = (uint32_t)std::stoul(next());
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
@@ -386,6 +390,29 @@ int main(int argc, char** argv) {
     const auto tb = clk::now();
     Bench b(o);
     LinkState& ls = b.als.at(kArea);
+    if (o.allRoutes) {
+      // every node's route DB through the streaming buildRouteDbs (the routes workload of
+      // bench.py / openr_routes_build), tallied and freed on the building worker
+      std::vector<std::string> nodes(ls.csrMirror().names);
+      SpfSolver all(nodes[0], false, false);
+      std::vector<uint64_t> cnt(nodes.size());
+      double best = 1e30;
+      for (uint32_t it = 0; it < std::max<uint32_t>(o.iters, 1); ++it) {
+        const auto t0 = clk::now();
+        all.buildRouteDbs(nodes, b.als, b.ps, [&](size_t i, std::optional<DecisionRouteDb>& db) {
+          uint64_t c = 0;
+          if (db)
+            for (auto const& [p, r] : db->unicastRoutes) c += r.nexthops.size();
+          cnt[i] = c;
+        });
+        best = std::min(best, msSince(t0));
+      }
+      uint64_t nhs = 0;
+      for (auto c : cnt) nhs += c;
+      std::printf("{\"workload\": \"all-routes\", \"nodes\": %zu, \"ms_best\": %.1f, \"nexthops\": %llu}\n",
+                  nodes.size(), best, (unsigned long long)nhs);
+      return 0;
+    }
     SpfSolver solver(b.me, false, true);  // Decision(config, computeLfaPaths = true, ...)
     // initial publication: the first route DB (RoutingBenchmarkUtils.cpp:535-538)
     auto t0 = clk::now();
@@ -393,6 +420,13 @@ int main(int argc, char** argv) {
     const double msInitial = msSince(t0);
     const double msSetup = msSince(tb);
     if (!db) throw std::runtime_error("my node is not in the topology");
+    if (o.routeIters) {  // route construction alone (every SPF memoised), for profilers
+      const auto r0 = clk::now();
+      for (uint32_t r = 0; r < o.routeIters; ++r) db = solver.buildRouteDb(b.me, b.als, b.ps);
+      std::printf("{\"workload\": \"route-iters\", \"ms_per_build\": %.3f, \"routes\": %zu}\n",
+                  msSince(r0) / o.routeIters, db->unicastRoutes.size());
+      return 0;
+    }
     double msUpdate = 0, msBuild = 0;
     uint64_t runs = 0, routes = 0;
     std::vector<double> per;
