@@ -697,7 +697,8 @@ def routes_main(args):
         "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u64", "data": "synthetic (benchmark generators, one prefix per node)",
         "config": dict(cfg, workload=cfg["workload"].replace("all-sources", "route-dbs-all-nodes"), lfa=bool(args.lfa),
-                       host_threads=int(os.environ.get("OPENR_HOST_THREADS", "0")) or None),
+                       # HostParallel.h: OPENR_HOST_THREADS, else min(hardware threads, 16)
+                       host_threads=int(os.environ.get("OPENR_HOST_THREADS", "0")) or min(16, os.cpu_count() or 1)),
         "unicast_routes": int(st.unicast_routes), "mpls_routes": int(st.mpls_routes), "nexthops": int(st.nexthops),
         "checksum": f"{st.checksum:016x}", "ms_spf_and_route_build": st.ms_build,
         "peak_rss_mb": rss, "rss_before_build_mb": rss0,
