@@ -672,11 +672,10 @@ def routes_main(args):
     peak_rss_mb = this process's peak resident set (getrusage)."""
     import resource
 
-    import torch
-
     from openr_amd import adjdb
 
-    torch.cuda.set_device(0)
+    # no torch here: the route build drives the engine through its C-ABI on device 0, and
+    # the framework's own resident set is what peak_rss_mb reports
     g, cfg = build_topology(args.topology)
     batch = adjdb.AdjDbBatch.from_columns(adjdb.columns_for_graph(g))
     rb = adjdb.RouteBuilder(batch, "0")

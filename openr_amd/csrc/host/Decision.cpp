@@ -293,11 +293,10 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   }
   size_t pi = 0;
   for (auto const& [prefix, entries] : prefixState.prefixes()) {  // key order
-    std::optional<RibUnicastEntry> r;
     const uint32_t dstId = dstIds ? (*dstIds)[pi] : UINT32_MAX;
     ++pi;
-    if (!(fast_.state == 1 && fastRoute(myNodeName, prefix, entries, dstId, &r)))
-      r = createRouteForPrefix(myNodeName, als, prefixState, prefix, entries, true);
+    if (fast_.state == 1 && fastRoute(myNodeName, prefix, entries, dstId, routeDb.unicastRoutes)) continue;
+    auto r = createRouteForPrefix(myNodeName, als, prefixState, prefix, entries, true);
     if (r) routeDb.unicastRoutes.insert_or_assign(routeDb.unicastRoutes.end(), prefix, std::move(*r));
   }
 
@@ -324,6 +323,19 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
         labelToNode.erase(topLabel);
         labelToNode.emplace(topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry{topLabel, {nh}}));
         continue;
+      }
+      if (fast_.state == 1) {
+        NextHopSet fnh;
+        const int fr = fastLabelNextHops(myNodeName, adjDb.thisNodeName, topLabel, &fnh);
+        if (fr == 0) {
+          counters_.no_route_to_label++;
+          continue;
+        }
+        if (fr == 1) {
+          labelToNode.erase(topLabel);
+          labelToNode.emplace(topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry{topLabel, std::move(fnh)}));
+          continue;
+        }
       }
       auto metricNhs = getNextHopsWithMetric(myNodeName, {{adjDb.thisNodeName, area}}, false, als);
       if (metricNhs.second.empty()) {
@@ -733,7 +745,7 @@ std::pair<Metric, std::unordered_map<std::pair<std::string, std::string>, Metric
 bool SpfSolver::fastSetup(std::unordered_map<std::string, LinkState> const& als, const std::string& me) {
   if (fast_.state) return fast_.state == 1;
   fast_.state = 2;
-  if (als.size() != 1 || enableBestRouteSelection_) return false;
+  if (!fastEnabled_ || als.size() != 1 || enableBestRouteSelection_) return false;
   const auto& [area, ls] = *als.begin();
   const auto& mine = views(ls, me).mine;  // read by createRouteForPrefix for every prefix too
   const LinkState::CsrMirror* m = mine.mirror();
@@ -756,44 +768,28 @@ bool SpfSolver::fastSetup(std::unordered_map<std::string, LinkState> const& als,
     if (nid == m->id.end()) return false;
     const uint32_t b = bitOf(nid->second);
     if (b == UINT32_MAX) return false;
-    fast_.links.push_back(FastLink{link.get(), b, link->isUp(), link->getMetricFromNode(me), &nbr});
+    FastLink fl{link.get(), b, link->isUp(), link->getMetricFromNode(me), &nbr, nid->second, {}, {}};
+    fl.proto6 = createNextHop(link->getNhV6FromNode(me), link->getIfaceFromNode(me), 0, std::nullopt, link->getArea(), nbr);
+    fl.proto4 = createNextHop(link->getNhV4FromNode(me), link->getIfaceFromNode(me), 0, std::nullopt, link->getArea(), nbr);
+    fast_.links.push_back(std::move(fl));
   }
+  // in NextHopThrift order (address, interface: distinct per link, so the metric never
+  // decides), so a v6 route's set is filled at its end
+  std::sort(fast_.links.begin(), fast_.links.end(),
+            [](const FastLink& a, const FastLink& b) { return a.proto6 < b.proto6; });
   fast_.val.assign(bits.size(), 0);
   fast_.has.assign(bits.size(), 0);
   fast_.state = 1;
   return true;
 }
 
-bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries,
-                          uint32_t dstId, std::optional<RibUnicastEntry>* out) {
-  if (entries.size() != 1) return false;
-  const auto& [na, e] = *entries.begin();
-  if (na.second != *fast_.area || e.type == thrift::PrefixType::BGP ||
-      e.forwardingAlgorithm != thrift::PrefixForwardingAlgorithm::SP_ECMP || e.forwardingType != thrift::PrefixForwardingType::IP)
-    return false;
-  const LinkState::CsrMirror& m = *fast_.m;
-  const auto& mine = views_.front().mine;  // fastSetup: views_ holds this one area
+// getNextHopsWithMetric(me, {dst}, perDestination = false) on ids, into fast_.has / val per
+// next-hop bit (d = my distance to dst, reached): 1 when there is a next-hop node, 0 when
+// there is none, -1 when an LFA neighbour's row is not on my mirror (the general path
+// serves the rest of this build)
+int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
+  const auto& mine = views_.front().mine;
   const uint64_t* dm = mine.distRow();
-  (void)m;
-  counters_.get_route_for_prefix++;
-  *out = std::nullopt;
-  if (dstId == UINT32_MAX || dm[dstId] == UINT64_MAX) {  // advertiser not reached: entry filtered out
-    counters_.no_route_to_prefix++;
-    return true;
-  }
-  const uint32_t dst = dstId;
-  if (prefix.isV4() && !enableV4_) {
-    counters_.skipped_unicast_route++;
-    return true;
-  }
-  // selectBestRoutes: the single advertiser (maybeFilterDrainedNodes keeps a lone drained one)
-  bestLazy_.emplace_back(prefix, na);  // the best-route cache entry {success, {na}, na}
-  if (dst == fast_.me) {  // self-originated; with a prepend label no next hop leads to it
-    if (e.prependLabel) counters_.no_route_to_prefix++;
-    return true;
-  }
-  // getNextHopsWithMetric(me, {dst}, false): shortest next hops, then RFC 5286 alternates
-  const Metric d = dm[dst];
   const uint32_t nb = mine.nhBytes();
   const uint8_t* hv = mine.nhRow() + (size_t)dst * nb;
   const auto& bits = mine.nhNeighbours();
@@ -811,13 +807,13 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
       for (auto const& nv : av.nbrs) {
         uint32_t b = UINT32_MAX;
         if (nv.view.mirror() == fast_.m) {
-          const uint32_t id = m.id.at(*nv.name);
+          const uint32_t id = fast_.m->id.at(*nv.name);
           for (uint32_t i = 0; i < bits.size(); ++i)
             if (bits[i] == id) b = i;
         }
         if (b == UINT32_MAX) {  // a neighbour's row on another mirror / map-backed: general path
           fast_.state = 2;
-          return false;
+          return -1;
         }
         fast_.lfaBit.push_back(b);
       }
@@ -836,7 +832,63 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
       }
     }
   }
-  if (!any) {
+  return any ? 1 : 0;
+}
+
+int SpfSolver::fastLabelNextHops(const std::string& me, const std::string& dstName, int32_t label, NextHopSet* out) {
+  const auto it = fast_.m->id.find(dstName);
+  if (it == fast_.m->id.end()) return -1;
+  const uint32_t dst = it->second;
+  const Metric d = views_.front().mine.distRow()[dst];
+  if (d == UINT64_MAX) return 0;  // getMinCostNodes: dst not reached, no next-hop node
+  const int nn = fastNextHopNodes(me, dst, d);
+  if (nn <= 0) return nn;
+  for (auto const& fl : fast_.links) {  // getNextHopsThrift, in NextHopThrift order
+    if (!fast_.has[fl.nbrBit] || !fl.up) continue;
+    const Metric over = fl.metric + fast_.val[fl.nbrBit];
+    if (!computeLfaPaths_ && over != d) continue;
+    thrift::NextHopThrift nh = fl.proto6;
+    nh.metric = static_cast<int32_t>(over);
+    const bool php = fl.nbrId == dst;  // the next hop is the label's node
+    nh.mplsAction = createMplsAction(php ? thrift::MplsActionCode::PHP : thrift::MplsActionCode::SWAP,
+                                     php ? std::nullopt : std::optional<int32_t>(label));
+    out->emplace_hint(out->end(), std::move(nh));
+  }
+  return 1;
+}
+
+bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries,
+                          uint32_t dstId, std::map<thrift::IpPrefix, RibUnicastEntry>& routes) {
+  if (entries.size() != 1) return false;
+  const auto& [na, e] = *entries.begin();
+  if (na.second != *fast_.area || e.type == thrift::PrefixType::BGP ||
+      e.forwardingAlgorithm != thrift::PrefixForwardingAlgorithm::SP_ECMP || e.forwardingType != thrift::PrefixForwardingType::IP)
+    return false;
+  const LinkState::CsrMirror& m = *fast_.m;
+  const auto& mine = views_.front().mine;  // fastSetup: views_ holds this one area
+  const uint64_t* dm = mine.distRow();
+  (void)m;
+  counters_.get_route_for_prefix++;
+  if (dstId == UINT32_MAX || dm[dstId] == UINT64_MAX) {  // advertiser not reached: entry filtered out
+    counters_.no_route_to_prefix++;
+    return true;
+  }
+  const uint32_t dst = dstId;
+  if (prefix.isV4() && !enableV4_) {
+    counters_.skipped_unicast_route++;
+    return true;
+  }
+  // selectBestRoutes: the single advertiser (maybeFilterDrainedNodes keeps a lone drained one)
+  bestLazy_.emplace_back(prefix, na);  // the best-route cache entry {success, {na}, na}
+  if (dst == fast_.me) {  // self-originated; with a prepend label no next hop leads to it
+    if (e.prependLabel) counters_.no_route_to_prefix++;
+    return true;
+  }
+  // getNextHopsWithMetric(me, {dst}, false): shortest next hops, then RFC 5286 alternates
+  const Metric d = dm[dst];
+  const int nn = fastNextHopNodes(me, dst, d);
+  if (nn < 0) return false;
+  if (nn == 0) {
     counters_.no_route_to_prefix++;
     return true;
   }
@@ -847,19 +899,20 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
     if (!fast_.has[fl.nbrBit] || !fl.up) continue;
     const Metric over = fl.metric + fast_.val[fl.nbrBit];
     if (!computeLfaPaths_ && over != d) continue;
-    nextHops.emplace(createNextHop(v4 ? fl.link->getNhV4FromNode(me) : fl.link->getNhV6FromNode(me),
-                                   fl.link->getIfaceFromNode(me), static_cast<int32_t>(over), std::nullopt,
-                                   fl.link->getArea(), *fl.nbr));
+    thrift::NextHopThrift nh = v4 ? fl.proto4 : fl.proto6;
+    nh.metric = static_cast<int32_t>(over);
+    nextHops.emplace_hint(nextHops.end(), std::move(nh));
   }
   // addBestPaths
   if (e.minNexthop && *e.minNexthop > (int64_t)nextHops.size()) return true;
-  RibUnicastEntry r;
+  auto it = routes.emplace_hint(routes.end(), std::piecewise_construct, std::forward_as_tuple(prefix),
+                                std::forward_as_tuple());
+  RibUnicastEntry& r = it->second;
   r.prefix = prefix;
   r.nexthops = std::move(nextHops);
   r.bestPrefixEntry = e;
   r.bestArea = na.second;
   r.doNotInstall = false;  // not BGP
-  *out = std::move(r);
   return true;
 }
 

@@ -208,6 +208,10 @@ class SpfSolver {
   SpfSolver(const std::string& myNodeName, bool enableV4, bool computeLfaPaths, bool enableOrderedFib = false,
             bool bgpDryRun = false, bool enableBestRouteSelection = false);
 
+  // tests: off = every route through the general createRouteForPrefix / label path (the
+  // id-based fast path must build the same DBs)
+  void setFastPathForTesting(bool on) { fastEnabled_ = on; }
+
   // static MPLS routes (updateStaticRoutes): label -> next-hops
   void updateStaticMplsRoutes(const std::unordered_map<int32_t, std::vector<thrift::NextHopThrift>>& add,
                               const std::vector<int32_t>& del);
@@ -309,6 +313,10 @@ class SpfSolver {
     bool up;
     Metric metric;    // from me
     const std::string* nbr;
+    uint32_t nbrId;   // the neighbour's node id on the mirror
+    // getNextHopsThrift's NextHopThrift over this link (v6 / v4 next-hop address), metric 0:
+    // a route copies it and sets the metric
+    thrift::NextHopThrift proto6, proto4;
   };
   struct FastCtx {
     int state = 0;
@@ -324,9 +332,16 @@ class SpfSolver {
   };
   FastCtx fast_;
   bool fastSetup(std::unordered_map<std::string, LinkState> const& areaLinkStates, const std::string& me);
-  // true when the prefix was served (*out = its route or none)
+  bool fastEnabled_ = true;
+  int fastNextHopNodes(const std::string& me, uint32_t dst, Metric d);
+  // the node-label MPLS route's next hops towards dst (getNextHopsWithMetric +
+  // getNextHopsThrift with swapLabel = label, perDestination = false): 1 = *out built, 0 =
+  // no next-hop node (no route to the label), -1 = not on the fast path (general path)
+  int fastLabelNextHops(const std::string& me, const std::string& dst, int32_t label, NextHopSet* out);
+  // true when the prefix was served: its route, if any, is appended to `routes` (prefixes
+  // arrive in key order, so the route is built in place at the end)
   bool fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries, uint32_t dstId,
-                 std::optional<RibUnicastEntry>* out);
+                 std::map<thrift::IpPrefix, RibUnicastEntry>& routes);
   AreaViews& views(const LinkState& ls, const std::string& me) const;
   AreaViews& lfaViews(const LinkState& ls, const std::string& me) const;
 

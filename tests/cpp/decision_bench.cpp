@@ -38,6 +38,7 @@
 //                  [--check] [--cpu-iters C] [--cpu-threads T (faithful runs timed on T threads;
 //                  priced serial, as Decision runs them)] [--seed S]
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -140,6 +141,7 @@ struct Options {
   uint64_t seed = 1;
   bool check = false;
   bool allRoutes = false;  // --all-routes: every node's route DB (buildRouteDbs), host-side profiling
+  size_t routeNodes = 0;   // --route-nodes N: only the first N nodes' DBs (profiling at full size)
   uint32_t routeIters = 0;  // --route-iters N: N memoised rebuilds of my route DB, then exit (profiling)
 };
 
@@ -376,6 +378,7 @@ int main(int argc, char** argv) {
     else if (a == "--seed") o.seed = std::stoull(next());
     else if (a == "--check") o.check = true;
     else if (a == "--all-routes") o.allRoutes = true;
+    else if (a == "--route-nodes" && i + 1 < argc) o.routeNodes = std::stoul(argv[++i]);
     else if (a == "--route-iters") o.routeIters = (uint32_t)std::stoul(next());
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -394,18 +397,28 @@ int main(int argc, char** argv) {
       // every node's route DB through the streaming buildRouteDbs (the routes workload of
       // bench.py / openr_routes_build), tallied and freed on the building worker
       std::vector<std::string> nodes(ls.csrMirror().names);
+      if (o.routeNodes && o.routeNodes < nodes.size()) nodes.resize(o.routeNodes);
       SpfSolver all(nodes[0], false, false);
       std::vector<uint64_t> cnt(nodes.size());
       double best = 1e30;
       for (uint32_t it = 0; it < std::max<uint32_t>(o.iters, 1); ++it) {
         const auto t0 = clk::now();
+        std::atomic<uint64_t> tallyNs{0}, freeNs{0};
         all.buildRouteDbs(nodes, b.als, b.ps, [&](size_t i, std::optional<DecisionRouteDb>& db) {
+          const auto c0 = clk::now();
           uint64_t c = 0;
           if (db)
             for (auto const& [p, r] : db->unicastRoutes) c += r.nexthops.size();
           cnt[i] = c;
+          const auto c1 = clk::now();
+          db.reset();
+          const auto c2 = clk::now();
+          tallyNs += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(c1 - c0).count();
+          freeNs += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(c2 - c1).count();
         });
         best = std::min(best, msSince(t0));
+        std::fprintf(stderr, "all-routes: tally %.1f ms, free %.1f ms (thread-summed)\n", tallyNs.load() / 1e6,
+                     freeNs.load() / 1e6);
       }
       uint64_t nhs = 0;
       for (auto c : cnt) nhs += c;

@@ -1086,7 +1086,10 @@ std::string flatten(const std::optional<DecisionRouteDb>& db) {
     for (auto const& nh : set)
       s += nh.address.addr + "%" + nh.address.ifName.value_or("") + "@" + nh.neighborNodeName.value_or("") + "#" +
            std::to_string(nh.metric) + "w" + std::to_string(nh.weight) +
-           (nh.mplsAction ? "a" + std::to_string((int)nh.mplsAction->action) : "") + ";";
+           (nh.mplsAction ? "a" + std::to_string((int)nh.mplsAction->action) : "") +
+           (nh.mplsAction && nh.mplsAction->swapLabel ? "s" + std::to_string(*nh.mplsAction->swapLabel) : "") +
+           (nh.mplsAction && nh.mplsAction->pushLabels ? "p" + std::to_string(nh.mplsAction->pushLabels->size()) : "") +
+           (nh.area ? "@" + *nh.area : "") + ";";
   };
   for (auto const& [p, r] : db->unicastRoutes) {
     s += p.toString() + "[" + r.bestArea + "]";
@@ -1140,6 +1143,45 @@ TEST_GPU(BuildRouteDbs_HostThreads_MatchSequential) {
   EXPECT_TRUE(std::get<2>(seq) == std::get<2>(par));
   EXPECT_EQ(std::get<2>(seq)[0], (uint64_t)nodes.size() - 2);
   EXPECT_TRUE(std::get<3>(seq) > 0);  // node-label routes present
+}
+
+// The id-based fast path of buildRouteDb (single-advertiser SP_ECMP prefixes and node-label
+// MPLS routes on dense rows, Decision.h FastCtx) against the general path on the same
+// memoised SPFs: identical unicast / MPLS routes, counters and best-route cache, LFA on and
+// off, v4 on and off, with parallel links, asymmetric metrics, node labels, a v4 prefix, a
+// prefix with two advertisers and one advertised by an unknown node.
+TEST_GPU(RouteBuild_FastPath_MatchesGeneralPath) {
+  Wan w(200, 600, 10, 11, true);
+  w.ps.updatePrefix(w.names[5], kDefaultArea, createPrefixEntry(pfx("10.1.0.0/16")));
+  w.ps.updatePrefix(w.names[7], kDefaultArea, createPrefixEntry(pfx("fd77::/64")));
+  w.ps.updatePrefix(w.names[9], kDefaultArea, createPrefixEntry(pfx("fd77::/64")));
+  w.ps.updatePrefix("ghost", kDefaultArea, createPrefixEntry(pfx("fd88::/64")));
+  std::vector<std::string> nodes;
+  for (uint32_t i = 0; i < 200; i += 9) nodes.push_back(w.names[i]);
+  for (const bool lfa : {false, true})
+    for (const bool v4 : {false, true}) {
+      auto run = [&](bool fast) {
+        SpfSolver solver(nodes[0], v4, lfa);
+        solver.setFastPathForTesting(fast);
+        std::vector<std::string> flat;
+        for (auto const& n : nodes) flat.push_back(flatten(solver.buildRouteDb(n, w.als, w.ps)));
+        std::string cache;
+        for (auto const& [p, b] : solver.getBestRoutesCache()) {
+          cache += p.toString() + (b.success ? "+" : "-") + b.bestNodeArea.first + ":";
+          for (auto const& na : b.allNodeAreas) cache += na.first + ",";
+        }
+        auto const& c = solver.counters();
+        std::vector<uint64_t> cnt{c.route_build_runs,     c.get_route_for_prefix, c.no_route_to_prefix,
+                                  c.skipped_unicast_route, c.skipped_mpls_route,   c.duplicate_node_label,
+                                  c.no_route_to_label,     c.incompatible_forwarding_type};
+        return std::make_tuple(flat, cache, cnt);
+      };
+      const auto general = run(false), fast = run(true);
+      EXPECT_TRUE(std::get<0>(general) == std::get<0>(fast));
+      EXPECT_TRUE(std::get<1>(general) == std::get<1>(fast));
+      EXPECT_TRUE(std::get<2>(general) == std::get<2>(fast));
+      EXPECT_TRUE(std::get<0>(fast)[0].find(":fe80") != std::string::npos);  // label routes present
+    }
 }
 
 // KSP2 route DBs with the batched device prefetch (LinkState::prefetchKthPaths) against
