@@ -300,9 +300,18 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
     if (r) routeDb.unicastRoutes.insert_or_assign(routeDb.unicastRoutes.end(), prefix, std::move(*r));
   }
 
-  // MPLS routes for every node label (:593-680)
-  std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
+  // MPLS routes for every node label (:593-680). The reference's label -> (node, route) map
+  // is kept as label -> slot of `cand` (same visiting order, collisions and counters); the
+  // winners then enter the DB in label order.
+  std::unordered_map<int32_t, uint32_t> labelToNode;
+  std::vector<std::pair<const std::string*, RibMplsEntry>> cand;
+  auto put = [&](int32_t label, const std::string* node, RibMplsEntry&& entry) {
+    auto [it, fresh] = labelToNode.emplace(label, (uint32_t)cand.size());
+    if (fresh) cand.emplace_back(node, std::move(entry));
+    else cand[it->second] = std::make_pair(node, std::move(entry));
+  };
   for (auto const& [area, ls] : als) {
+    labelToNode.reserve(labelToNode.size() + ls.getAdjacencyDatabases().size());
     for (auto const& [_, adjDb] : ls.getAdjacencyDatabases()) {
       const int32_t topLabel = adjDb.nodeLabel;
       if (topLabel == 0) continue;  // non-SR mode
@@ -313,15 +322,14 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
       auto it = labelToNode.find(topLabel);
       if (it != labelToNode.end()) {  // collision: the bigger node name keeps the label
         counters_.duplicate_node_label++;
-        if (it->second.first < adjDb.thisNodeName) continue;
+        if (*cand[it->second].first < adjDb.thisNodeName) continue;
       }
       if (adjDb.thisNodeName == myNodeName) {
         thrift::NextHopThrift nh;
         nh.address.addr = "::";
         nh.area = area;
         nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
-        labelToNode.erase(topLabel);
-        labelToNode.emplace(topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry{topLabel, {nh}}));
+        put(topLabel, &adjDb.thisNodeName, RibMplsEntry{topLabel, {nh}});
         continue;
       }
       if (fast_.state == 1) {
@@ -332,8 +340,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
           continue;
         }
         if (fr == 1) {
-          labelToNode.erase(topLabel);
-          labelToNode.emplace(topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry{topLabel, std::move(fnh)}));
+          put(topLabel, &adjDb.thisNodeName, RibMplsEntry{topLabel, std::move(fnh)});
           continue;
         }
       }
@@ -342,16 +349,16 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
         counters_.no_route_to_label++;
         continue;
       }
-      labelToNode.erase(topLabel);
-      labelToNode.emplace(
-          topLabel,
-          std::make_pair(adjDb.thisNodeName,
-                         RibMplsEntry{topLabel, getNextHopsThrift(myNodeName, {{adjDb.thisNodeName, area}}, false,
-                                                                  false, metricNhs.first, metricNhs.second, topLabel,
-                                                                  als)}));
+      put(topLabel, &adjDb.thisNodeName,
+          RibMplsEntry{topLabel, getNextHopsThrift(myNodeName, {{adjDb.thisNodeName, area}}, false, false,
+                                                   metricNhs.first, metricNhs.second, topLabel, als)});
     }
   }
-  for (auto& [_, nodeToEntry] : labelToNode) routeDb.addMplsRoute(std::move(nodeToEntry.second));
+  std::sort(cand.begin(), cand.end(), [](auto const& x, auto const& y) { return x.second.label < y.second.label; });
+  for (auto& [_, entry] : cand) {
+    const int32_t label = entry.label;
+    routeDb.mplsRoutes.emplace_hint(routeDb.mplsRoutes.end(), label, std::move(entry));
+  }
 
   // MPLS routes for our adjacencies (:686-714)
   for (auto const& [_, ls] : als) {
@@ -789,7 +796,6 @@ bool SpfSolver::fastSetup(std::unordered_map<std::string, LinkState> const& als,
 // serves the rest of this build)
 int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
   const auto& mine = views_.front().mine;
-  const uint64_t* dm = mine.distRow();
   const uint32_t nb = mine.nhBytes();
   const uint8_t* hv = mine.nhRow() + (size_t)dst * nb;
   const auto& bits = mine.nhNeighbours();
@@ -797,7 +803,7 @@ int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
   for (uint32_t i = 0; i < bits.size(); ++i) {
     fast_.has[i] = (hv[i >> 3] >> (i & 7)) & 1u;
     if (fast_.has[i]) {
-      fast_.val[i] = d - dm[bits[i]];
+      fast_.val[i] = d - mine.dist(bits[i]);
       any = true;
     }
   }
@@ -820,7 +826,7 @@ int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
       fast_.lfaReady = true;
     }
     for (size_t k = 0; k < av.nbrs.size(); ++k) {
-      const Metric dn = av.nbrs[k].view.distRow()[dst];
+      const Metric dn = av.nbrs[k].view.dist(dst);
       if (dn == UINT64_MAX || !(dn < d + av.nbrs[k].toMe)) continue;
       const uint32_t b = fast_.lfaBit[k];
       if (!fast_.has[b]) {
@@ -839,7 +845,7 @@ int SpfSolver::fastLabelNextHops(const std::string& me, const std::string& dstNa
   const auto it = fast_.m->id.find(dstName);
   if (it == fast_.m->id.end()) return -1;
   const uint32_t dst = it->second;
-  const Metric d = views_.front().mine.distRow()[dst];
+  const Metric d = views_.front().mine.dist(dst);
   if (d == UINT64_MAX) return 0;  // getMinCostNodes: dst not reached, no next-hop node
   const int nn = fastNextHopNodes(me, dst, d);
   if (nn <= 0) return nn;
@@ -864,12 +870,10 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
   if (na.second != *fast_.area || e.type == thrift::PrefixType::BGP ||
       e.forwardingAlgorithm != thrift::PrefixForwardingAlgorithm::SP_ECMP || e.forwardingType != thrift::PrefixForwardingType::IP)
     return false;
-  const LinkState::CsrMirror& m = *fast_.m;
   const auto& mine = views_.front().mine;  // fastSetup: views_ holds this one area
-  const uint64_t* dm = mine.distRow();
-  (void)m;
   counters_.get_route_for_prefix++;
-  if (dstId == UINT32_MAX || dm[dstId] == UINT64_MAX) {  // advertiser not reached: entry filtered out
+  const Metric d = dstId == UINT32_MAX ? UINT64_MAX : mine.dist(dstId);
+  if (d == UINT64_MAX) {  // advertiser not reached: entry filtered out
     counters_.no_route_to_prefix++;
     return true;
   }
@@ -885,7 +889,6 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
     return true;
   }
   // getNextHopsWithMetric(me, {dst}, false): shortest next hops, then RFC 5286 alternates
-  const Metric d = dm[dst];
   const int nn = fastNextHopNodes(me, dst, d);
   if (nn < 0) return false;
   if (nn == 0) {

@@ -611,7 +611,9 @@ const LinkState::SpfResult& LinkState::materialize(const MemoEntry& e, bool useL
     const CsrMirror& m = e.snap ? e.snap->mirror : mirror_;
     const DenseRows& d = e.snap ? e.snap->rows[useLinkMetric ? 1 : 0] : dense_[useLinkMetric ? 1 : 0];
     const uint32_t V = (uint32_t)m.names.size(), src = d.src[e.row];
-    const uint64_t* dist = d.dist.data() + (size_t)e.row * V;
+    std::vector<uint64_t> distv(V);
+    d.load(e.row, 1, distv.data());
+    const uint64_t* dist = distv.data();
     const uint8_t* h = d.nh.data() + (size_t)e.row * V * d.nb;
     const std::vector<uint32_t>& nbrs = d.nbrs[e.row];
     SpfResult res;
@@ -705,12 +707,19 @@ void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool u
   SpfEngineHandle::check(openr_spf_nh_bytes(engine_->ctx(), &nb), "openr_spf_nh_bytes");
   if (d.src.empty()) d.nb = nb;
   const size_t r0 = d.src.size();
-  d.dist.resize((r0 + n) * (size_t)V);
-  d.nh.resize((r0 + n) * (size_t)V * d.nb);
-  SpfEngineHandle::check(openr_spf_solve(engine_->ctx(), ids.data(), n,
-                                         useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u,
-                                         d.dist.data() + r0 * V, d.nh.data() + r0 * V * d.nb, d.nb, nullptr),
-                         "openr_spf_solve");
+  d.V = V;
+  d.resizeRows(r0 + n);
+  // the engine's u64 rows through a staging buffer of at most ~64 MB
+  const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(n, (64u << 20) / (8u * (size_t)std::max(V, 1u))));
+  std::vector<uint64_t> stage((size_t)chunk * V);
+  for (uint32_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint32_t k = std::min(chunk, n - c0);
+    SpfEngineHandle::check(openr_spf_solve(engine_->ctx(), ids.data() + c0, k,
+                                           useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u, stage.data(),
+                                           d.nh.data() + (r0 + c0) * V * d.nb, d.nb, nullptr),
+                           "openr_spf_solve");
+    d.store(r0 + c0, k, stage.data());
+  }
   d.nbrs.resize(r0 + n);
   std::vector<uint32_t> buf(V ? V : 1);
   for (uint32_t k = 0; k < n; ++k) {
@@ -754,9 +763,40 @@ LinkState::SpfView LinkState::getSpfView(const std::string& nodeName, bool useLi
   return v;
 }
 
-const uint64_t* LinkState::SpfView::dist() const {
-  const DenseRows& d = *static_cast<const DenseRows*>(rows_);
-  return d.dist.data() + (size_t)row_ * m_->names.size();
+void LinkState::DenseRows::resizeRows(size_t rows) {
+  if (wide) dist64.resize(rows * V);
+  else dist32.resize(rows * V);
+  nh.resize(rows * V * nb);
+}
+
+void LinkState::DenseRows::store(size_t r0, size_t n, const uint64_t* rows) {
+  const size_t cnt = n * V;
+  if (!wide) {
+    bool fits = true;
+    for (size_t i = 0; i < cnt && fits; ++i) fits = rows[i] == UINT64_MAX || rows[i] < UINT32_MAX;
+    if (!fits) {  // a finite distance past u32: every row widens
+      dist64.resize(dist32.size());
+      for (size_t i = 0; i < dist32.size(); ++i) dist64[i] = dist32[i] == UINT32_MAX ? UINT64_MAX : dist32[i];
+      std::vector<uint32_t>().swap(dist32);
+      wide = true;
+    }
+  }
+  if (wide) {
+    std::copy(rows, rows + cnt, dist64.begin() + r0 * V);
+    return;
+  }
+  uint32_t* o = dist32.data() + r0 * V;
+  for (size_t i = 0; i < cnt; ++i) o[i] = rows[i] == UINT64_MAX ? UINT32_MAX : (uint32_t)rows[i];
+}
+
+void LinkState::DenseRows::load(size_t r0, size_t n, uint64_t* rows) const {
+  const size_t cnt = n * V;
+  if (wide) {
+    std::copy(dist64.begin() + r0 * V, dist64.begin() + r0 * V + cnt, rows);
+    return;
+  }
+  const uint32_t* x = dist32.data() + r0 * V;
+  for (size_t i = 0; i < cnt; ++i) rows[i] = x[i] == UINT32_MAX ? UINT64_MAX : (uint64_t)x[i];
 }
 
 const uint8_t* LinkState::SpfView::nh(uint32_t v) const {
@@ -772,7 +812,7 @@ const std::vector<uint32_t>& LinkState::SpfView::nhNeighbours() const {
 
 int32_t LinkState::SpfView::id(const std::string& node) const {
   auto it = m_->id.find(node);
-  if (it == m_->id.end() || dist()[it->second] == UINT64_MAX) return -1;
+  if (it == m_->id.end() || dist(it->second) == UINT64_MAX) return -1;
   return (int32_t)it->second;
 }
 
@@ -785,7 +825,7 @@ LinkStateMetric LinkState::SpfView::metric(const std::string& node) const {
   if (map_) return map_->at(node).metric();
   const int32_t v = id(node);
   if (v < 0) throw std::out_of_range("SpfView::metric: " + node + " not reached");
-  return dist()[v];
+  return dist((uint32_t)v);
 }
 
 std::vector<std::string> LinkState::SpfView::nextHops(const std::string& node) const {
@@ -1001,10 +1041,22 @@ void LinkState::refreshDense(bool useLinkMetric, double* ms) const {
   if (d.src.empty()) return;
   const auto t0 = std::chrono::steady_clock::now();
   uint32_t resolved = 0;
-  SpfEngineHandle::check(openr_spf_refresh(engine_->ctx(), d.src.data(), (uint32_t)d.src.size(),
-                                           useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u, d.dist.data(),
-                                           d.nh.data(), d.nb, nullptr, &resolved),
-                         "openr_spf_refresh");
+  // the rows pass through the engine as u64 rows, a bounded chunk at a time (rows refresh
+  // independently; the patch delta stays until the next patch)
+  const uint32_t V = d.V, n = (uint32_t)d.src.size();
+  const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(n, (64u << 20) / (8u * (size_t)std::max(V, 1u))));
+  std::vector<uint64_t> stage((size_t)chunk * V);
+  for (uint32_t c0 = 0; c0 < n; c0 += chunk) {
+    const uint32_t k = std::min(chunk, n - c0);
+    d.load(c0, k, stage.data());
+    uint32_t r = 0;
+    SpfEngineHandle::check(openr_spf_refresh(engine_->ctx(), d.src.data() + c0, k,
+                                             useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u, stage.data(),
+                                             d.nh.data() + (size_t)c0 * V * d.nb, d.nb, nullptr, &r),
+                           "openr_spf_refresh");
+    d.store(c0, k, stage.data());
+    resolved += r;
+  }
   ++ustats_.refreshes;
   ustats_.rowsRefreshed += resolved;
   ustats_.rowsKept += d.src.size();

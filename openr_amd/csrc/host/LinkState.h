@@ -379,11 +379,11 @@ class LinkState {
     template <class F>
     void forEachNextHop(const std::string& node, F&& f) const;
     // Dense internals for id-based readers (the route build's fast path): mirror() is null
-    // when the entry is map-backed; ids index mirror()->names. distRow()[v] = the metric of
-    // v (UINT64_MAX: not reached), nhRow()[v * nhBytes() ..] its next-hop bits, bit i =
-    // node nhNeighbours()[i].
+    // when the entry is map-backed; ids index mirror()->names. dist(v) = the metric of v
+    // (UINT64_MAX: not reached), nhRow()[v * nhBytes() ..] its next-hop bits, bit i = node
+    // nhNeighbours()[i].
     const CsrMirror* mirror() const { return map_ ? nullptr : m_; }
-    const uint64_t* distRow() const { return dist(); }
+    inline uint64_t dist(uint32_t v) const;
     const uint8_t* nhRow() const { return nh(0); }
     uint32_t nhBytes() const;
     const std::vector<uint32_t>& nhNeighbours() const;
@@ -397,7 +397,6 @@ class LinkState {
     const void* rows_ = nullptr;  // the DenseRows holding row_ (resolved per access)
     uint32_t row_ = 0;
     std::shared_ptr<const void> keep_;  // a retired row snapshot the view reads (see RowSnapshot)
-    const uint64_t* dist() const;
     const uint8_t* nh(uint32_t v) const;
     int32_t id(const std::string& node) const;
   };
@@ -442,18 +441,35 @@ class LinkState {
     LazyOnce once;
   };
   // Dense memo rows per useLinkMetric (round 3): the results the memo holds as the engine
-  // writes them — u64 distance and next-hop bitset per (source, node) — host-resident. They
+  // writes them — distance and next-hop bitset per (source, node) — host-resident. They
   // outlive attribute-only topology changes (refreshed in place after the engine graph is
   // patched) and are materialised into SpfResult maps only when read.
+  // Distances are kept as u32 (UINT32_MAX = not reached) while every finite one fits, else
+  // as u64 (round 4: G100's 10 000 rows in 500 instead of 900 MB); the engine's u64 rows
+  // pass through a bounded staging buffer.
   struct DenseRows {
     uint32_t nb = 1;
+    uint32_t V = 0;
     std::unordered_map<uint32_t, uint32_t> slot;  // node id -> row
     std::vector<uint32_t> src;                     // row -> node id
-    std::vector<uint64_t> dist;                    // rows x V
+    bool wide = false;                             // distances in dist64 (else dist32)
+    std::vector<uint32_t> dist32;                  // rows x V
+    std::vector<uint64_t> dist64;                  // rows x V
     std::vector<uint8_t> nh;                       // rows x V x nb
     std::vector<std::vector<uint32_t>> nbrs;       // row -> node id of next-hop bit i
     bool stale = false;                            // rows predate a patch: refresh before any read
     void clear() { *this = DenseRows{}; }
+    uint64_t dist(size_t row, uint32_t v) const {
+      const size_t i = row * V + v;
+      if (wide) return dist64[i];
+      const uint32_t x = dist32[i];
+      return x == UINT32_MAX ? UINT64_MAX : (uint64_t)x;
+    }
+    // rows [r0, r0 + n) from engine u64 rows (widens every row first when one does not fit)
+    void store(size_t r0, size_t n, const uint64_t* rows);
+    // rows [r0, r0 + n) as engine u64 rows
+    void load(size_t r0, size_t n, uint64_t* rows) const;
+    void resizeRows(size_t rows);
   };
   mutable DenseRows dense_[2];
   // A structural change that the reference does not count as a topology change (a node's
@@ -538,10 +554,13 @@ void LinkState::SpfView::forEachNextHop(const std::string& node, F&& f) const {
   if (v < 0) throw std::out_of_range("SpfView::forEachNextHop: " + node + " not reached");
   const DenseRows& d = *static_cast<const DenseRows*>(rows_);
   const uint8_t* hv = nh((uint32_t)v);
-  const uint64_t* ds = dist();
   const std::vector<uint32_t>& nbrs = d.nbrs[row_];
   for (uint32_t i = 0; i < nbrs.size(); ++i)
-    if ((hv[i >> 3] >> (i & 7)) & 1u) f(m_->names[nbrs[i]], ds[nbrs[i]]);
+    if ((hv[i >> 3] >> (i & 7)) & 1u) f(m_->names[nbrs[i]], d.dist(row_, nbrs[i]));
+}
+
+inline uint64_t LinkState::SpfView::dist(uint32_t v) const {
+  return static_cast<const DenseRows*>(rows_)->dist(row_, v);
 }
 
 }  // namespace openr

@@ -142,6 +142,7 @@ struct Options {
   bool check = false;
   bool allRoutes = false;  // --all-routes: every node's route DB (buildRouteDbs), host-side profiling
   size_t routeNodes = 0;   // --route-nodes N: only the first N nodes' DBs (profiling at full size)
+  bool nodeLabels = false; // --node-labels: grid node labels (node-label MPLS routes in every DB)
   uint32_t routeIters = 0;  // --route-iters N: N memoised rebuilds of my route DB, then exit (profiling)
 };
 
@@ -165,7 +166,9 @@ struct Bench {
       for (int r = 0; r < n; ++r)
         for (int c = 0; c < n; ++c) {
           const uint32_t id = (uint32_t)(r * n + c);
-          ls.updateAdjacencyDatabase(adjDb(std::to_string(id), gridAdjs(r, c, n), false));
+          auto db = adjDb(std::to_string(id), gridAdjs(r, c, n), false);
+          if (o.nodeLabels) db.nodeLabel = 100001 + id;  // profiling: node-label MPLS routes as openr_routes builds
+          ls.updateAdjacencyDatabase(db);
           thrift::PrefixEntry e;  // createPrefixEntry(nodeToPrefixV6(nodeId + 0)), forwardingAlgorithm
           e.prefix = thrift::IpPrefix{"fc00:" + hex2(id >> 16) + "::" + hex2(id & 0xffff), 128};
           if (ksp2) {
@@ -379,6 +382,7 @@ int main(int argc, char** argv) {
     else if (a == "--check") o.check = true;
     else if (a == "--all-routes") o.allRoutes = true;
     else if (a == "--route-nodes" && i + 1 < argc) o.routeNodes = std::stoul(argv[++i]);
+    else if (a == "--node-labels") o.nodeLabels = true;
     else if (a == "--route-iters") o.routeIters = (uint32_t)std::stoul(next());
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -417,8 +421,15 @@ int main(int argc, char** argv) {
           freeNs += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(c2 - c1).count();
         });
         best = std::min(best, msSince(t0));
-        std::fprintf(stderr, "all-routes: tally %.1f ms, free %.1f ms (thread-summed)\n", tallyNs.load() / 1e6,
-                     freeNs.load() / 1e6);
+        long hwm = 0;
+        if (FILE* f = std::fopen("/proc/self/status", "r")) {
+          char line[256];
+          while (std::fgets(line, sizeof(line), f))
+            if (!std::strncmp(line, "VmHWM:", 6)) hwm = std::atol(line + 6);
+          std::fclose(f);
+        }
+        std::fprintf(stderr, "all-routes: tally %.1f ms, free %.1f ms (thread-summed), peak RSS %.0f MB\n",
+                     tallyNs.load() / 1e6, freeNs.load() / 1e6, hwm / 1024.0);
       }
       uint64_t nhs = 0;
       for (auto c : cnt) nhs += c;

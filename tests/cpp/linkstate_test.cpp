@@ -1011,4 +1011,45 @@ TEST_GPU(LinkState_SpfViewMatchesSpfResult) {
   EXPECT_FALSE(u.reached("0"));
 }
 
+// Dense memo rows hold distances as u32 while every finite one fits and widen to u64 when
+// one does not (round 4): a chain whose far end lies past 2^32 with metrics of 2^31 - 1,
+// read first from a source whose rows fit (u32 rows), then from sources past 2^32 (every
+// row widens), then after a metric change (the refresh path on u64 rows); every result
+// against the oracle.
+TEST_GPU(LinkState_DenseRowsWidenPastU32) {
+  const int n = 8;
+  const int32_t big = 2147483647;
+  auto build = [&](int32_t farMetric) {
+    std::vector<std::pair<int, std::vector<std::pair<int, int>>>> adj;
+    for (int i = 0; i < n; ++i) {
+      std::vector<std::pair<int, int>> a;
+      if (i > 0) a.emplace_back(i - 1, i >= n - 3 ? farMetric : 1);
+      if (i + 1 < n) a.emplace_back(i + 1, i + 1 >= n - 3 ? farMetric : 1);
+      adj.emplace_back(i, a);
+    }
+    return adj;
+  };
+  LinkState ls = getLinkState(build(big));
+  auto const& m = ls.csrMirror();
+  auto id = [&](int i) { return m.id.at(std::to_string(i)); };
+  // node 0 reaches node 7 over 1 + 1 + 1 + 1 + 3 x (2^31 - 1) > 2^32
+  EXPECT_TRUE(spfMatchesOracle(ls, {id(3)}, false));  // hop counts: u32 rows
+  EXPECT_TRUE(spfMatchesOracle(ls, {id(0), id(7)}, true));
+  const auto v = ls.getSpfView("0");
+  EXPECT_EQ(v.metric("7"), (uint64_t)4 + 3ull * (uint64_t)big);
+  EXPECT_TRUE(spfMatchesOracle(ls, {id(1), id(5), id(2)}, true));
+  // a metric change on the far links: attribute patch + refresh of the (now u64) rows
+  for (auto const& [node, adjs] : build(big - 5))
+    if (node >= n - 4) {
+      std::vector<thrift::Adjacency> as;
+      for (auto const& [o, w] : adjs)
+        as.push_back(createAdjacency(std::to_string(o), std::to_string(node) + "/" + std::to_string(o) + "/0",
+                                     std::to_string(o) + "/" + std::to_string(node) + "/0", w,
+                                     (node << 16) + o));
+      ls.updateAdjacencyDatabase(createAdjDb(std::to_string(node), as, node), 0, 0);
+    }
+  EXPECT_TRUE(spfMatchesOracle(ls, {id(0), id(7), id(1), id(5), id(2)}, true));
+  EXPECT_EQ(ls.getSpfView("0").metric("7"), (uint64_t)4 + 3ull * (uint64_t)(big - 5));
+}
+
 int main(int argc, char** argv) { return run_tests(argc, argv); }
