@@ -46,6 +46,18 @@ def main():
 
     g, _ = build_topology("grid100")
     print(f"topology {rss_mb():.0f} MB", flush=True)
+    if os.environ.get("RSS_ENGINE", "1") == "1":  # the engine alone, in this process
+        from openr_amd.engine import SpfEngine
+
+        eng = SpfEngine([0])
+        print(f"engine created {rss_mb():.0f} MB", flush=True)
+        eng.set_graph(g)
+        print(f"graph set {rss_mb():.0f} MB", flush=True)
+        eng.solve(list(range(8)), True)
+        print(f"8 solves {rss_mb():.0f} MB", flush=True)
+        top_maps("engine only")
+        eng.close()
+        print(f"engine closed {rss_mb():.0f} MB", flush=True)
     batch = adjdb.AdjDbBatch.from_columns(adjdb.columns_for_graph(g))
     print(f"adjdb batch {rss_mb():.0f} MB", flush=True)
     rb = adjdb.RouteBuilder(batch, "0")
