@@ -1028,8 +1028,6 @@ void LinkState::applyAttrPatch(const std::vector<std::shared_ptr<Link>>& links, 
 }
 
 bool LinkState::denseEligible(bool useLinkMetric) const {
-  if (const char* e = std::getenv("OPENR_DENSE_MEMO"))  // 0: the materialise-at-solve path (tests)
-    if (std::atoi(e) == 0) return false;
   return !useLinkMetric || csrMirror().metricsPositive;
 }
 

@@ -166,8 +166,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
   // lane's no-op atomic goes to its own all-ones dummy word, so the returned field alone
   // elects the appending arrival
   constexpr bool kLeanT = !GENERIC && ELLM == 0;
-  const bool kLean = kLeanT && (nt & 2u) == 0u;  // (OPENR_SPF_CODE_LEAN=0: the generic loop, A/B)
-  nt &= 1u;
+  const bool kLean = kLeanT;
   if (kLean && tid < 64) dummy[tid] = 0xFFFFFFFFu;
   const uint32_t ign_words = (g.L + 31u) / 32u;
   const uint32_t G = 1u << glog, ngroups = BLOCK >> glog, groups_per_wave = 64u >> glog;
@@ -566,7 +565,7 @@ BfsShape bfs_shape(const DevGraph& g, bool has_ign, uint32_t fb) {
   const uint32_t full = bfs_layout(g.V, g.L, has_ign, fb, g.V).total;
   const uint32_t need = std::max<uint32_t>(std::max<uint32_t>(256u, g.max_deg + 2u), g.est_width2 + g.est_width2 / 4u);
   const bool force_full = env_u32("OPENR_SPF_BFS_FULL", 0u, 0u, 1u) != 0u;
-  for (uint32_t want = env_u32("OPENR_SPF_BFS_WGS", 16u, 1u, 16u); want >= 1; --want) {
+  for (uint32_t want = 16u; want >= 1; --want) {
     const uint32_t budget = kMaxLds / want;
     sh.per_cu = want;
     if (full <= budget) {
@@ -586,8 +585,7 @@ BfsShape bfs_shape(const DevGraph& g, bool has_ign, uint32_t fb) {
   if (forced && (forced & (forced - 1u)) == 0u && forced >= g.max_deg + 2u &&
       fixed + 2u * forced <= kMaxLds / sh.per_cu)
     sh.ring_cap = forced;
-  const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
-  sh.block = blk == 128u || blk == 256u ? blk : (sh.per_cu > 8u ? 128u : 256u);
+  sh.block = sh.per_cu > 8u ? 128u : 256u;
   return sh;
 }
 
@@ -613,8 +611,7 @@ hipError_t launch_bfs_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
   }
   note_launch(RING ? "bfs_code_kernel<ring>" : from_list ? "bfs_code_kernel<full>:rerun" : "bfs_code_kernel<full>");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
-                     (uint32_t)from_list, ctr, ovf_count,
-                     nt_stores() | (env_u32("OPENR_SPF_CODE_LEAN", 1u, 0u, 1u) ? 0u : 2u));
+                     (uint32_t)from_list, ctr, ovf_count, nt_stores());
   return hipGetLastError();
 }
 
@@ -642,10 +639,9 @@ hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, u
   // A batch of at most half as many (solve, slice) units as CUs (a refresh's few affected
   // rows, LFA / KSP prefetches of one node): a launch is one solve's latency, so each solve
   // takes a whole CU — 1 024 threads, full-order queue — instead of 256 threads beside
-  // idle CUs (OPENR_SPF_BFS_WIDE=0: off)
+  // idle CUs
   const uint64_t units = (uint64_t)a.n * (SLICED ? std::max(a.nsl, 1u) : 1u);
-  if (units * 2u <= (uint64_t)num_cus && bfs_layout(g.V, g.L, has_ign, FB, g.V).total <= kMaxLds &&
-      env_u32("OPENR_SPF_BFS_WIDE", 1u, 0u, 1u)) {
+  if (units * 2u <= (uint64_t)num_cus && bfs_layout(g.V, g.L, has_ign, FB, g.V).total <= kMaxLds) {
     if (ellm == 2) return launch_bfs_shape<FB, 1024, 2, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
     if (ellm == 1) return launch_bfs_shape<FB, 1024, 1, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
     return launch_bfs_shape<FB, 1024, 0, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);

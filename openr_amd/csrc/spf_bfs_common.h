@@ -85,7 +85,7 @@ inline uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t h
 
 // Result rows are written once and read by the host / the next consumer, never by the
 // kernel: non-temporal stores keep them from evicting the CSR mirror out of L2.
-inline uint32_t nt_stores() { return env_u32("OPENR_SPF_NT", 1u, 0u, 1u); }
+inline uint32_t nt_stores() { return 1u; }
 
 // Counter block of a source class: [0,1] fast launch, [2,3] re-run launch, [4] solves
 // the fast launch flagged for the re-run (cleared by the re-run's last workgroup).

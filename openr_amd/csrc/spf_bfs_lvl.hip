@@ -809,7 +809,7 @@ hipError_t launch_lvl_variant(const DevGraph& g, const SolveArgs& a, uint64_t co
     info->grid = grid;
     info->kernel = RING ? "bfs_lvl_kernel<ring,u8>" : "bfs_lvl_kernel<full,u16>";
   }
-  const uint32_t flags = nt_stores() | (env_u32("OPENR_SPF_FRESH_LVL", 1u, 0u, 1u) << 1);
+  const uint32_t flags = nt_stores() | (1u << 1);
   note_launch(RING ? "bfs_lvl_kernel<ring,u8>" : from_list ? "bfs_lvl_kernel<full,u16>:rerun" : "bfs_lvl_kernel<full,u16>");
   hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, (uint32_t)has_ign, ring_cap,
                      (uint32_t)from_list, ctr, ovf_count, flags);
@@ -821,8 +821,6 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
                            uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
   uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
-  // OPENR_SPF_LEAN_WGS (tuning): at most this many workgroups per CU (occupancy sweep)
-  if (const uint32_t cap = env_u32("OPENR_SPF_LEAN_WGS", 0u, 0u, 16u)) grid = std::min<uint32_t>(grid, cap * (uint32_t)num_cus);
   const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
   // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
   const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
@@ -1095,7 +1093,7 @@ uint32_t wave_pass_waves(const DevGraph& g, int mode, uint32_t qhalf, uint32_t n
   const WaveLayout one = wave_layout(g.V, nh_words_for(mode, g.V), qhalf, 0);
   if (one.slot0 >= kMaxLds) return 0;
   const uint32_t w = std::min<uint32_t>(8u, (kMaxLds - one.slot0) / one.per_slot);
-  if (w < env_u32("OPENR_SPF_WAVE_MIN", 4u, 1u, 8u)) return 0;
+  if (w < 4u) return 0;  // fewer than 4 solve slots per CU: the lean pass
   const uint64_t cus = (uint64_t)std::max(num_cus, 1);
   if (knob == 2u && (uint64_t)n > 3ull * cus * w) return 0;
   return (uint32_t)std::min<uint64_t>(w, std::max<uint64_t>(1, ((uint64_t)n + cus - 1) / cus));
@@ -1152,7 +1150,7 @@ hipError_t launch_lvl_mode(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     // (OPENR_SPF_LEAN_FORCE=1, tests: also when the halves are too small, so wide levels
     // take the overflow -> u16 re-run path)
     const bool fits = ring_cap / 2u >= need1 || env_u32("OPENR_SPF_LEAN_FORCE", 0u, 0u, 1u) != 0u;
-    const bool lean = !has_ign && !a.tight && fits && env_u32("OPENR_SPF_BFS_LEAN", 1u, 0u, 1u);
+    const bool lean = !has_ign && !a.tight && fits;
     if (lean)
       err = launch_lvl_lean<MODE, BLOCK>(g, a, cost, ring_cap, blk, blk + 4, num_cus, s, info);
     else
@@ -1171,14 +1169,13 @@ template <int MODE, bool SLICED>
 hipError_t launch_lvl_ell(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, bool has_ign, int ellm,
                           int num_cus, hipStream_t s, LaunchInfo* info) {
   const bool vis = SLICED || !Nh<MODE>::kSingle;
-  const LvlShape sh = lvl_shape(g, has_ign, MODE, vis, env_u32("OPENR_SPF_BFS_WGS", kBfsTargetWgs, 1u, 16u));
-  const uint32_t blk = env_u32("OPENR_SPF_BFS_BLOCK", 0u, 0u, 256u);
+  const LvlShape sh = lvl_shape(g, has_ign, MODE, vis, kBfsTargetWgs);
   // 128-thread workgroups when the batch fills the GPU several times over (occupancy hides
   // the level loop's latency: G100 0.863 vs 0.913 ms); 256 threads (four waves per solve,
   // a wide level in one pass) when it fills it at most twice, as a strong-scaling shard
   // does (G100 5 000 sources 0.518 vs 0.556 ms, 2 500: 0.357 vs 0.381 ms)
   const bool small_batch = (uint64_t)a.n <= 2ull * (uint64_t)num_cus * sh.per_cu;
-  const bool b128 = blk == 128u || (blk != 256u && sh.per_cu > 8u && !small_batch);
+  const bool b128 = sh.per_cu > 8u && !small_batch;
 #define OPENR_LVL_MODE(BLK, E) \
   return launch_lvl_mode<MODE, BLK, E, SLICED>(g, a, cost, glog, has_ign, sh.ring_cap, num_cus, s, info)
   if (b128) {

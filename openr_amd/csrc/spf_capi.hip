@@ -79,9 +79,6 @@ struct Device {
   DevBuf<uint32_t> ovf;  // re-run list of the BFS ring variants ([n * slices])
   // small multi-class batches: the classes run concurrently, one stream each (forked from
   // and joined back into the caller's stream), each with its own re-run list
-  hipStream_t cstream[kMaxClasses] = {};
-  hipEvent_t cev[kMaxClasses + 1] = {};
-  DevBuf<uint32_t> ovfc;
   DevBuf<uint32_t> slicetmp;  // code-family sliced class: [n][nsl][V] next-hop chunks
   DevBuf<uint32_t> work;  // dynamic-scheduling counters (kWorkSlots)
   DevBuf<uint32_t> status;  // sticky OPENR_SPF_STATUS_* bits of device-form calls
@@ -320,16 +317,6 @@ int make_plan(const openr_spf_ctx* ctx, uint32_t flags, bool has_ign, Plan* p) {
 }
 
 
-// Tuning overrides (benchmarks only): OPENR_SPF_GROUP_LANES=1|2|4|..|64 lanes per
-// frontier node in the BFS kernel.
-int group_lanes_override(int dflt) {
-  const char* e = std::getenv("OPENR_SPF_GROUP_LANES");
-  if (!e) return dflt;
-  int v = std::atoi(e);
-  return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : dflt;
-}
-
-
 // Uniform-cost solves run per source class (next-hop width): one class -> one launch;
 // several -> a device-side partition of the batch, then one launch per class, the
 // widest first.
@@ -358,7 +345,7 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     if (p.rounds) return launch_rounds(d.g, a, p.dist64, p.nh_mode, d.num_cus, s, &info);
     return launch_fringe(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
   }
-  const int gl = group_lanes_override((int)ctx->group_lanes);
+  const int gl = (int)ctx->group_lanes;
   a.perm = nullptr;
   a.part = nullptr;
   const int fam = p.family;
@@ -394,38 +381,9 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   if (err != hipSuccess) return err;
   a.perm = d.perm.p;
   a.part = d.part.p;
-  // OPENR_SPF_CLASS_STREAMS=1: a batch too small to fill the GPU (a refresh's few affected
-  // rows, an LFA prefetch) runs its classes side by side on their own streams instead of
-  // one after another. Their scheduling counters are per class already; each gets its own
-  // re-run list. Measured and left opt-in: on the fabric update loop the cross-stream
-  // fork / join cost more than the overlap saved (0.226 vs 0.170 ms per update).
+  // classes one after another on the caller's stream (side-by-side class streams were
+  // measured slower: the fork / join cost more than the overlap saved, round 3)
   const int nc = num_classes(fam);
-  // (=2: every multi-class batch, so one class's tail overlaps the next class's launch)
-  const int cs_knob = std::getenv("OPENR_SPF_CLASS_STREAMS") ? std::atoi(std::getenv("OPENR_SPF_CLASS_STREAMS")) : 0;
-  const bool side = __builtin_popcount(mask) > 1 && (cs_knob == 2 || (cs_knob == 1 && a.n <= (uint32_t)d.num_cus));
-  if (side) {
-    const size_t per = (size_t)a.n * std::max<uint32_t>(a.nsl, 1u);
-    err = d.ovfc.reserve(per * (size_t)nc);
-    for (int c = 0; c < nc && err == hipSuccess; ++c) {
-      if (!d.cstream[c]) err = hipStreamCreateWithFlags(&d.cstream[c], hipStreamNonBlocking);
-      if (err == hipSuccess && !d.cev[c]) err = hipEventCreateWithFlags(&d.cev[c], hipEventDisableTiming);
-    }
-    if (err == hipSuccess && !d.cev[kMaxClasses]) err = hipEventCreateWithFlags(&d.cev[kMaxClasses], hipEventDisableTiming);
-    if (err == hipSuccess) err = hipEventRecord(d.cev[kMaxClasses], s);  // fork: partition done
-    if (err != hipSuccess) return err;
-    for (int c = nc - 1; c >= 0; --c) {
-      if (!((mask >> c) & 1u)) continue;
-      SolveArgs ac = a;
-      ac.cls = (uint32_t)c;
-      ac.ovf_list = d.ovfc.p + per * (size_t)c;
-      err = hipStreamWaitEvent(d.cstream[c], d.cev[kMaxClasses], 0);
-      if (err == hipSuccess) err = launch_bfs(fam, d.g, ac, p.cost, gl, d.num_cus, d.cstream[c], &info);
-      if (err == hipSuccess) err = hipEventRecord(d.cev[c], d.cstream[c]);
-      if (err == hipSuccess) err = hipStreamWaitEvent(s, d.cev[c], 0);  // join
-      if (err != hipSuccess) return err;
-    }
-    return hipSuccess;
-  }
   for (int c = nc - 1; c >= 0; --c) {
     if (!((mask >> c) & 1u)) continue;
     a.cls = (uint32_t)c;
@@ -984,13 +942,6 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.alist2.release();
     d.asrc2.release();
     d.acount.release();
-    for (uint32_t c = 0; c < kMaxClasses; ++c) {
-      if (d.cstream[c]) (void)hipStreamSynchronize(d.cstream[c]);
-      if (d.cstream[c]) (void)hipStreamDestroy(d.cstream[c]);
-      if (d.cev[c]) (void)hipEventDestroy(d.cev[c]);
-    }
-    if (d.cev[kMaxClasses]) (void)hipEventDestroy(d.cev[kMaxClasses]);
-    d.ovfc.release();
     if (d.ev_begin) (void)hipEventDestroy(d.ev_begin);
     if (d.ev_end) (void)hipEventDestroy(d.ev_end);
     if (d.stream) (void)hipStreamDestroy(d.stream);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B kernel variants in ONE process on the same device buffers (tuning aid).
 
-  python scripts/sweep.py --topology grid100 --variants "G=1;G=2;G=4;FULL=1,G=4"
+  python scripts/sweep.py --topology grid100 --variants "FAM=lvl;FAM=code;WAVE=1"
 
 Each variant is a ';'-separated list of env overrides read by the engine at
 launch (OPENR_SPF_GROUP_LANES, OPENR_SPF_BFS_FULL). Rounds are interleaved
@@ -18,12 +18,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = {"G": "OPENR_SPF_GROUP_LANES", "FULL": "OPENR_SPF_BFS_FULL",
-        "WGS": "OPENR_SPF_BFS_WGS", "NT": "OPENR_SPF_NT", "BLK": "OPENR_SPF_BFS_BLOCK",
-        "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL",
-        "RING": "OPENR_SPF_RING_CAP", "FL": "OPENR_SPF_FRESH_LVL",
-        "LEAN": "OPENR_SPF_BFS_LEAN", "CLEAN": "OPENR_SPF_CODE_LEAN", "WAVE": "OPENR_SPF_BFS_WAVE", "WMIN": "OPENR_SPF_WAVE_MIN",
-        "LWGS": "OPENR_SPF_LEAN_WGS", "PROF": "OPENR_SPF_BFS_PROF"}
+KEYS = {"FULL": "OPENR_SPF_BFS_FULL", "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL",
+        "RING": "OPENR_SPF_RING_CAP", "WAVE": "OPENR_SPF_BFS_WAVE", "PROF": "OPENR_SPF_BFS_PROF"}
 
 
 def parse(v):
@@ -37,7 +33,7 @@ def parse(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--topology", default="grid100")
-    ap.add_argument("--variants", default="G=1;G=2;G=4")
+    ap.add_argument("--variants", default="FAM=lvl;FAM=code")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-metric", action="store_true")
     args = ap.parse_args()
