@@ -570,7 +570,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) vo
   const uint32_t half = ring_cap / 2u;
   const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
   *my_dummy = 0xFFFFFFFFu;  // only ever ORed afterwards: its fields are never zero
-  // tuning (OPENR_SPF_BFS_PROF): wave 0's cycles per phase of its first pass of every
+  // tuning (OPENR_SPF_PROF): wave 0's cycles per phase of its first pass of every
   // level: [0] barrier -> queue entry, [1] ELL row load, [2] level / set reads, [3] atomics,
   // [4] append, [5] drain + barrier, [6] levels, [7] solves. A stamp follows an asm use of
   // the value the phase waits for, so it is taken once that value has arrived.
@@ -821,7 +821,7 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
                            uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
   const uint32_t lds = lean_layout(g.V, nh_words_for(MODE, g.V), ring_cap).total;
   uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
-  const bool want_prof = env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u) != 0;
+  const bool want_prof = prof_enabled();
   // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
   const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
   auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true, 8> : bfs_ell_kernel<MODE, BLOCK, true, false, 8>)
@@ -1115,7 +1115,7 @@ hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   }
   note_launch("bfs_wave_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(64u * waves), lds, s, g, a, cost, qhalf, waves, ctr, ovf_count, nt_stores());
-  if (env_u32("OPENR_SPF_BFS_PROF", 0u, 0u, 1u))  // tests: which pass ran
+  if (prof_enabled())  // tests: which pass ran
     std::fprintf(stderr, "bfs_wave: grid=%u waves=%u n=%u qhalf=%u lds=%u\n", grid, waves, a.n, qhalf, lds);
   return hipGetLastError();
 }

@@ -94,15 +94,6 @@ struct Device {
   size_t ktag_rows = 0;      // entries of krows16 zeroed for tagging
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
-  // KSP2 second pipeline lane: chunks alternate between the caller's stream (the buffers
-  // above) and kstream (these), so one chunk's kernels fill the other's launch tails
-  hipStream_t kstream = nullptr;
-  hipEvent_t kev[2] = {};
-  DevBuf<uint64_t> krows_b;
-  DevBuf<uint16_t> krows16_b;
-  uint32_t ktag_b = 0;
-  size_t ktag_rows_b = 0;
-  DevBuf<uint32_t> kign_b, kend_b, ksrc_b, kq_b, kretry_b, ovf_b, work_b;
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
@@ -557,6 +548,12 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       b.nh_bits = ctx->nh_bits;
       b.ovf_list = d.ovf.p;
       b.work = d.work.p;
+      // the rounds kernel starts each unit from its source's base rows (only the nodes the
+      // failed link pushes back are re-solved); other kernels solve from scratch
+      b.seed_dist = d.base_dist.p;
+      b.seed_tight = d.base_tight.p;
+      b.seed_unit = d.wunit.p + off;
+      b.seed_nsrc = n_src;
       if ((e2 = launch(ctx, d, ign_plan, b, s)) != hipSuccess) return e2;
       if ((e2 = launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
                                     d_changed, d.num_cus, s)) != hipSuccess)
@@ -591,24 +588,10 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       float ms = 0.f;
       OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
       ctx->stats.last_kernel_ms = ms;
-      // Units past the first pass's slots are large (WAN: 6 533 of 1.01 M affected units
-      // past 96 slots, 151 dirty nodes on average): re-solved (default), or with
-      // OPENR_SPF_WHATIF_LIST=1 repaired again by the list pass with every slot and the
-      // rest re-solved. Measured on the WAN step: 5.18 vs 5.34 ms — a 150-node repair on
-      // one wavefront takes as long as a re-solve on a 256-thread workgroup.
-      const char* lp = std::getenv("OPENR_SPF_WHATIF_LIST");
-      if (cnt[1] && !(lp && std::atoi(lp) == 1)) {
-        OPENR_TRY(resolve_units(cnt[1], 0));
-      } else if (cnt[1]) {
-        OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
-                                      d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
-                                      d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
-                                      d.num_cus, s, d.wunit.p, cnt[1]));
-        uint32_t c2 = 0;
-        OPENR_TRY(hipMemcpyAsync(&c2, d.wcount.p + 2, sizeof(c2), hipMemcpyDeviceToHost, s));
-        OPENR_TRY(hipStreamSynchronize(s));
-        if (c2) OPENR_TRY(resolve_units(c2, cnt[1]));  // past every slot: re-solved (few, large)
-      }
+      // Units past the slots are large (WAN: ~6 500 of 1.02 M affected units, ~150 dirty
+      // nodes on average): re-solved, each starting from its source's base rows (the
+      // rounds kernel's seeded start)
+      if (cnt[1]) OPENR_TRY(resolve_units(cnt[1], 0));
       *solved = cnt[0];
       return hipSuccess;
     }
@@ -682,138 +665,107 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   const char* tag_env = std::getenv("OPENR_SPF_KSP_TAG");  // 0: untagged rows, unreached fill (A/B)
   const bool tagged = rows16 && tag_max && !(tag_env && std::atoi(tag_env) == 0);
   const size_t row_bytes = (size_t)V * (rows16 ? 2u : 8u);
-  // pairs per chunk from a byte budget for the chunk's rows and ignore slots (8 GiB of the
-  // 288 GB; OPENR_SPF_KSP_CHUNK_MB overrides). Fabric, 512 sources x all destinations, ms
-  // per step by budget: 2 GiB (~150 k pairs) 254.3, 4 GiB 248.3, 8 GiB 246.8, 16 GiB 246.4;
-  // by pairs: 65 536 271.6, 32 768 297.0, 16 384 351.0, 8 192 470.8. Per-chunk launches
-  // and kernel tails dominate, not the rows' cache locality.
+  // pairs per chunk from a byte budget for the chunk's rows and ignore slots: 8 GiB of the
+  // 288 GB, capped at half the device memory free at the call, and halved again
+  // when a reservation still fails. Fabric, 512 sources x all destinations, ms per step by
+  // budget: 2 GiB (~150 k pairs) 254.3, 4 GiB 248.3, 8 GiB 246.8, 16 GiB 246.4; by pairs:
+  // 65 536 271.6, 32 768 297.0, 16 384 351.0, 8 192 470.8. Per-chunk launches and kernel
+  // tails dominate, not the rows' cache locality. (Two pipeline lanes alternating chunks
+  // over two streams measured slower, 264.7 vs 254.2 ms: each chunk's kernels already fill
+  // the GPU; removed in round 4.)
   size_t chunk_budget = kKspChunkBytes;
-  if (const char* e = std::getenv("OPENR_SPF_KSP_CHUNK_MB"); e && std::atoi(e) >= 64 && std::atoi(e) <= 65536)
-    chunk_budget = (size_t)std::atoi(e) << 20;
+  {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      chunk_budget = std::min(chunk_budget, std::max<size_t>(free_b / 2u, size_t(64) << 20));
+  }
   uint32_t chunk =
       (uint32_t)std::min<size_t>(n_pairs, std::max<size_t>(1, chunk_budget / (row_bytes + 4u * ign_cap)));
   if (const char* e = std::getenv("OPENR_SPF_KSP_CHUNK"))  // pairs per chunk (tests: many chunks, tag wrap)
     if (std::atoi(e) > 0) chunk = std::min<uint32_t>(chunk, (uint32_t)std::atoi(e));
-  // OPENR_SPF_KSP_LANES=2: two pipeline lanes (chunks alternate between the caller's
-  // stream and a side stream) when the second SPF is the distance-only code-family solve,
-  // whose only scratch is its lane's counters and re-run list (other plans share device
-  // scratch: perm / part, exact slots). Measured and left opt-in: fabric, 512 sources x
-  // all destinations, 264.7 vs 254.2 ms per step with one lane — each chunk's kernels
-  // already fill the GPU, so the second lane adds contention, not tail cover.
-  const char* lanes_env = std::getenv("OPENR_SPF_KSP_LANES");
-  const bool two = rows16 && !ign_plan.exact && n_pairs >= 2 && lanes_env && std::atoi(lanes_env) == 2;
-  if (two) chunk = std::min<uint32_t>(chunk, (n_pairs + 1u) / 2u);
-  struct Lane {
-    DevBuf<uint64_t>* krows;
-    DevBuf<uint16_t>* krows16;
-    uint32_t* tag;
-    size_t* tag_rows;
-    DevBuf<uint32_t> *kign, *kend, *ksrc, *kq, *kretry, *ovf;
-    uint32_t* work;
-    hipStream_t s;
+  auto reserve_chunk = [&](uint32_t c) -> hipError_t {
+    hipError_t e2;
+    if ((e2 = d.kptr.reserve((size_t)c + 1u)) != hipSuccess) return e2;
+    if (rows16) {
+      if ((e2 = d.krows16.reserve((size_t)c * V)) != hipSuccess) return e2;
+    } else if ((e2 = d.krows.reserve((size_t)c * V)) != hipSuccess) {
+      return e2;
+    }
+    if ((e2 = d.kign.reserve((size_t)c * ign_cap)) != hipSuccess) return e2;
+    if ((e2 = d.kend.reserve(c)) != hipSuccess) return e2;
+    if ((e2 = d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V)) != hipSuccess) return e2;
+    if ((e2 = d.ksrc.reserve(c)) != hipSuccess) return e2;
+    if ((e2 = d.ovf.reserve((size_t)c * ctx->nsl_max())) != hipSuccess) return e2;
+    return d.kretry.reserve(8u + 2u * (size_t)c);
   };
-  Lane lanes[2] = {{&d.krows, &d.krows16, &d.ktag, &d.ktag_rows, &d.kign, &d.kend, &d.ksrc, &d.kq, &d.kretry, &d.ovf,
-                    d.work.p, s},
-                   {&d.krows_b, &d.krows16_b, &d.ktag_b, &d.ktag_rows_b, &d.kign_b, &d.kend_b, &d.ksrc_b, &d.kq_b,
-                    &d.kretry_b, &d.ovf_b, nullptr, nullptr}};
-  if (two) {
-    if (!d.work_b.p) {
-      OPENR_TRY(d.work_b.reserve(kWorkSlots));
-      OPENR_TRY(hipMemset(d.work_b.p, 0, kWorkSlots * sizeof(uint32_t)));  // counters live zeroed
-    }
-    if (!d.kstream) OPENR_TRY(hipStreamCreateWithFlags(&d.kstream, hipStreamNonBlocking));
-    for (hipEvent_t& e : d.kev)
-      if (!e) OPENR_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    lanes[1].work = d.work_b.p;
-    lanes[1].s = d.kstream;
+  for (;;) {
+    err = reserve_chunk(chunk);
+    if (err != hipErrorOutOfMemory || chunk == 1) break;
+    (void)hipGetLastError();  // clear the failed allocation
+    chunk = (chunk + 1u) / 2u;
   }
-  OPENR_TRY(d.kptr.reserve((size_t)chunk + 1u));
+  if (err != hipSuccess) return err;
   OPENR_TRY(launch_strided_iota(d.kptr.p, chunk + 1u, ign_cap, d.num_cus, s));
-  for (int p = 0; p < (two ? 2 : 1); ++p) {
-    Lane& B = lanes[p];
-    if (rows16) OPENR_TRY(B.krows16->reserve((size_t)chunk * V));
-    else OPENR_TRY(B.krows->reserve((size_t)chunk * V));
-    if (tagged && *B.tag_rows < (size_t)chunk * V) {  // fresh or grown buffer: no valid tag in it
-      OPENR_TRY(hipMemsetAsync(B.krows16->p, 0, (size_t)chunk * V * sizeof(uint16_t), s));
-      *B.tag_rows = (size_t)chunk * V;
-      *B.tag = 0;
-    }
-    OPENR_TRY(B.kign->reserve((size_t)chunk * ign_cap));
-    OPENR_TRY(B.kend->reserve(chunk));
-    OPENR_TRY(B.kq->reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V));
-    OPENR_TRY(B.ksrc->reserve(chunk));
-    OPENR_TRY(B.ovf->reserve((size_t)chunk * ctx->nsl_max()));
-    OPENR_TRY(B.kretry->reserve(8u + 2u * (size_t)chunk));
+  if (tagged && d.ktag_rows < (size_t)chunk * V) {  // fresh or grown buffer: no valid tag in it
+    OPENR_TRY(hipMemsetAsync(d.krows16.p, 0, (size_t)chunk * V * sizeof(uint16_t), s));
+    d.ktag_rows = (size_t)chunk * V;
+    d.ktag = 0;
   }
-  if (two) {  // fork: the base rows, pointers and zeroed rows are ready for the second lane
-    OPENR_TRY(hipEventRecord(d.kev[0], s));
-    OPENR_TRY(hipStreamWaitEvent(d.kstream, d.kev[0], 0));
-  }
-  // OPENR_SPF_KSP_STATS=1: per-kind trace counters printed to stderr (tuning only)
+  // OPENR_SPF_PROF=1: per-kind trace counters printed to stderr (tuning only)
   const uint32_t nst = ksp_stats_count();
   unsigned long long* kst = nullptr;
-  if (const char* e = std::getenv("OPENR_SPF_KSP_STATS"); e && std::atoi(e) == 1) {
+  if (prof_enabled()) {
     OPENR_TRY(hipMallocAsync(reinterpret_cast<void**>(&kst), 2 * nst * sizeof(unsigned long long), s));
     OPENR_TRY(hipMemsetAsync(kst, 0, 2 * nst * sizeof(unsigned long long), s));
-    if (two) {
-      OPENR_TRY(hipEventRecord(d.kev[0], s));
-      OPENR_TRY(hipStreamWaitEvent(d.kstream, d.kev[0], 0));
-    }
   }
-  uint32_t ci = 0;
-  for (uint32_t first = 0; first < n_pairs; first += chunk, ++ci) {
+  for (uint32_t first = 0; first < n_pairs; first += chunk) {
     const uint32_t m = std::min(chunk, n_pairs - first);
-    Lane& B = lanes[two ? (ci & 1u) : 0u];
-    hipStream_t ls = B.s;
-    uint32_t* rcount = B.kretry->p;  // [0] k = 1, [1] k = 2; [2..5] work counters of the 4 launches
-    uint32_t* wctr = B.kretry->p + 2;
-    uint32_t* rlist1 = B.kretry->p + 8;
+    hipStream_t ls = s;
+    uint32_t* rcount = d.kretry.p;  // [0] k = 1, [1] k = 2; [2..5] work counters of the 4 launches
+    uint32_t* wctr = d.kretry.p + 2;
+    uint32_t* rlist1 = d.kretry.p + 8;
     uint32_t* rlist2 = rlist1 + chunk;
     OPENR_TRY(hipMemsetAsync(rcount, 0, 8u * sizeof(uint32_t), ls));
     // small tier (occupancy), then the full tier over the pairs it could not hold
-    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, B.kign->p, B.kend->p, ign_cap,
-                               d_tok1, tok_cap, d.kstatus.p, B.kq->p, d.num_cus, ls, kst, nullptr, nullptr, rlist1,
+    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, nullptr, nullptr, rlist1,
                                rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u));
-    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, B.kign->p, B.kend->p, ign_cap,
-                               d_tok1, tok_cap, d.kstatus.p, B.kq->p, d.num_cus, ls, kst, rlist1, rcount, nullptr,
+    OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
+                               d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, rlist1, rcount, nullptr,
                                nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u));
-    OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, B.ksrc->p, d.num_cus, ls));
+    OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, ls));
     SolveArgs b{};
-    b.sources = B.ksrc->p;
+    b.sources = d.ksrc.p;
     b.n = m;
     b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, kend[k])
-    b.ign_end = B.kend->p;
-    b.ign_links = B.kign->p;
-    b.dist = rows16 ? nullptr : B.krows->p;
-    b.lvl16 = rows16 ? B.krows16->p : nullptr;
-    uint32_t& tag = *B.tag;  // the tag of the last chunk written into this lane's rows (0: rows all zero)
+    b.ign_end = d.kend.p;
+    b.ign_links = d.kign.p;
+    b.dist = rows16 ? nullptr : d.krows.p;
+    b.lvl16 = rows16 ? d.krows16.p : nullptr;
+    uint32_t& tag = d.ktag;  // the tag of the last chunk written into this lane's rows (0: rows all zero)
     if (tagged) {
       if (tag == tag_max) {  // every tag used since the rows were zeroed: zero them again
-        OPENR_TRY(hipMemsetAsync(B.krows16->p, 0, *B.tag_rows * sizeof(uint16_t), ls));
+        OPENR_TRY(hipMemsetAsync(d.krows16.p, 0, d.ktag_rows * sizeof(uint16_t), ls));
         tag = 0;
       }
       b.lvl_tag = ++tag;
       b.lvl_shift = lshift;
     }
     b.nh_bits = ctx->nh_bits;
-    b.ovf_list = B.ovf->p;
-    b.work = B.work;
+    b.ovf_list = d.ovf.p;
+    b.work = d.work.p;
     b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
     OPENR_TRY(launch(ctx, d, ign_plan, b, ls));
-    const uint64_t* r2 = rows16 ? nullptr : B.krows->p;
-    const uint16_t* r16 = rows16 ? B.krows16->p : nullptr;
-    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, B.kign->p, B.kend->p, ign_cap, d_tok2,
-                               tok_cap, d.kstatus.p, B.kq->p, d.num_cus, ls, kst ? kst + nst : nullptr, nullptr, nullptr,
+    const uint64_t* r2 = rows16 ? nullptr : d.krows.p;
+    const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
+                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, nullptr, nullptr,
                                rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u,
                                tagged ? (b.lvl_tag << 8 | lshift) : 0u));
-    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, B.kign->p, B.kend->p, ign_cap, d_tok2,
-                               tok_cap, d.kstatus.p, B.kq->p, d.num_cus, ls, kst ? kst + nst : nullptr, rlist2,
+    OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
+                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, rlist2,
                                rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u,
                                tagged ? (b.lvl_tag << 8 | lshift) : 0u));
-  }
-  if (two) {  // join: the caller's stream continues after both lanes
-    OPENR_TRY(hipEventRecord(d.kev[1], d.kstream));
-    OPENR_TRY(hipStreamWaitEvent(s, d.kev[1], 0));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);
@@ -926,13 +878,6 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)
       if (p) (void)hipFree(p);
-    for (auto* b : {&d.kign_b, &d.kend_b, &d.ksrc_b, &d.kq_b, &d.kretry_b, &d.ovf_b, &d.work_b}) b->release();
-    d.krows_b.release();
-    d.krows16_b.release();
-    if (d.kstream) (void)hipStreamSynchronize(d.kstream);
-    if (d.kstream) (void)hipStreamDestroy(d.kstream);
-    for (hipEvent_t e : d.kev)
-      if (e) (void)hipEventDestroy(e);
     d.exscratch.release();
     d.order.release();
     d.precs.release();
@@ -1075,7 +1020,6 @@ int openr_spf_set_graph(openr_spf_ctx* ctx, const openr_spf_graph* gr) {
     HIP_TRY(hipStreamSynchronize(d.stream));
     free_graph(d.g);
     d.ktag_rows = 0;  // tagged KSP2 rows of another graph (another level width): zero before reuse
-    d.ktag_rows_b = 0;
     DevGraph g;
     g.V = V;
     g.E = E;

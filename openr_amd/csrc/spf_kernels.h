@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace openr_spf {
 
 // Device copy of the CSR mirror (include/openr_spf.h openr_spf_graph), packed for
@@ -134,6 +136,14 @@ struct SolveArgs {
   // kStatusLevelOverflow in *status
   uint8_t* lvl_rows;
   uint32_t lvl_bytes;
+  // nullable, rounds kernel with an ignore set (what-if re-solves of large units, round 4):
+  // solve sid starts from base row j = seed_unit[sid] % seed_nsrc of seed_dist / seed_tight
+  // (the source's SPF without the ignore set, and its tight-edge mask) instead of from
+  // scratch: only the nodes whose distance the ignored links raise are re-solved
+  const uint64_t* seed_dist;
+  const uint64_t* seed_tight;
+  const uint32_t* seed_unit;
+  uint32_t seed_nsrc;
   uint32_t* status;
   // code-family sliced class with next-hop output: [krows][nsl][V] 29-bit chunks of the
   // sets (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows
@@ -228,8 +238,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
-                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s,
-                               const uint32_t* list = nullptr, uint32_t n_list = 0);
+                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s);
 // 0 when the grouped repair cannot run on the graph (ids, next-hop width, degree, LDS)
 uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64, uint32_t max_deg);
 
@@ -293,7 +302,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint64_t lcost = 0,   // instead of `rows`: dist = level * lcost; non-zero lcost
                                                   // also marks a uniform-cost graph (rank by name / edge)
                             uint32_t ltag = 0);   // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
-uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_KSP_STATS tuning only)
+uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_PROF tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
@@ -317,5 +326,12 @@ uint32_t bfs_lvl_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls);
 
 uint32_t fringe_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int nh_mode, bool dist64);
 constexpr uint32_t kMaxLds = 160 * 1024;
+
+// OPENR_SPF_PROF=1 (tuning only): the kernels' profiling counters (BFS level loops, the
+// what-if repair phases, the KSP2 trace kinds) printed to stderr after each launch
+inline bool prof_enabled() {
+  const char* e = std::getenv("OPENR_SPF_PROF");
+  return e && e[0] == '1';
+}
 
 }  // namespace openr_spf

@@ -40,7 +40,7 @@ constexpr uint32_t kWave = 64;
 constexpr uint32_t kKspProbeAfter = 64;   // DFS frame entries of one trace before the reachability probe
                                          // (OPENR_SPF_KSP_PROBE overrides: tests force 0)
 constexpr uint64_t kNoKey = ~0ull;
-// Optional per-launch counters (OPENR_SPF_KSP_STATS=1; tuning only), indices into KspState::stats
+// Optional per-launch counters (OPENR_SPF_PROF=1; tuning only), indices into KspState::stats
 enum : uint32_t {
   kStPairs, kStTraces, kStPaths, kStEntries, kStCands, kStProbes, kStProbeNeg, kStCyc, kStCycLoad, kStCycProbe,
   kStProbeNodes, kStSteps, kStCycFail, kStEntFail, kStCycInit, kStCycRank, kKspStats
@@ -703,13 +703,9 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
 
 }  // namespace
 
-// OPENR_SPF_KSP_D16: keep a u16 copy of the pair's distance row in LDS (fewer wavefronts
-// per CU): 0 never, 1 both traces (measured slower on the fabric in round 2), 2 the k = 2
-// trace only (its tagged second-SPF rows, copied for pairs that trace)
-bool ksp_use_d16(int kind) {
-  const uint32_t k = bfs::env_u32("OPENR_SPF_KSP_D16", 0u, 0u, 2u);
-  return k == 1u || (k == 2u && kind == 2);
-}
+// A u16 copy of the pair's distance row in LDS was measured slower on the fabric (fewer
+// wavefronts per CU, rounds 2-3) and is not taken; the layout keeps the slot at size 0.
+bool ksp_use_d16(int) { return false; }
 
 // Small tier: a traced path has at most as many hops as the source's BFS depth on
 // uniform-cost graphs; 2x the sampled depth + 8 covers the sample's misses and weighted

@@ -35,7 +35,7 @@ using namespace bfs;
 constexpr uint32_t kWave = 64;
 
 struct RoundsLayout {
-  uint32_t dist, nh, cnt, fa, fb, inq, ign, total;
+  uint32_t dist, nh, cnt, fa, fb, inq, ign, alist, total;
 };
 
 __host__ __device__ inline RoundsLayout rounds_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t nh_words,
@@ -54,11 +54,115 @@ __host__ __device__ inline RoundsLayout rounds_layout(uint32_t V, uint32_t L, bo
   l.fb = take(2u * V);
   l.inq = take(4u * ((V + 31u) / 32u));
   l.ign = has_ign ? take(4u * ((L + 31u) / 32u)) : 0u;
+  l.alist = has_ign ? take(2u * V) : 0u;  // seeded re-solves: the nodes whose distance grows
   l.total = off;
   return l;
 }
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Seeded start of a re-solve with an ignore set (what-if units too large for the repair
+// kernel's slots, round 4): the base SPF's distances, except the set A of nodes whose
+// every base-tight in-edge is lost — over an ignored link, or out of a member of A —
+// which restart at their best entry from outside A. Nodes outside A keep their base
+// distance (a base shortest path avoids the ignored links), so the distance rounds then
+// run over A alone instead of the whole graph. Tight edges come from the base tight mask
+// (seed_tight). Leaves the first frontier (A's members with a finite entry, inq bits set)
+// in cur and returns its size.
+template <typename D, uint32_t BLOCK>
+__device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32_t sid, uint32_t src, D* dist,
+                                   uint16_t* cnt, uint16_t*& cur, uint16_t*& nxt, uint32_t* inq, const uint32_t* ign,
+                                   uint16_t* alist, uint32_t* ctl, uint32_t& r, uint32_t tid, uint32_t tight_words) {
+  constexpr D INF = (D)~(D)0;
+  auto sync = [&]() {
+    if constexpr (BLOCK == kWave) lds_fence();
+    else __syncthreads();
+  };
+  const uint32_t V = g.V;
+  const uint32_t j = a.seed_unit[sid] % a.seed_nsrc;
+  const uint64_t* bd = a.seed_dist + (size_t)j * V;
+  const uint64_t* bt = a.seed_tight + (size_t)j * tight_words;
+  auto tight = [&](uint32_t e) { return ((bt[e >> 6] >> (e & 63u)) & 1ull) != 0; };
+  // (a) base distances; live base-tight in-degree of every node (in-edges over an ignored
+  //     link are lost); A's seeds: nodes that had tight in-edges and lost them all
+  {
+    uint32_t* const ac = &ctl[r % 3u];
+    if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+      const uint64_t b = bd[v];
+      dist[v] = b == UINT64_MAX ? INF : (D)b;
+      uint32_t live = 0, all = 0;
+      if (b != UINT64_MAX && v != src) {
+        const uint2 rr = g.row2[v];
+        for (uint32_t e = rr.x; e < rr.y; ++e) {
+          const uint4 rec = g.erec[e];  // v->u: {u | down | sink(u), w(u->v), link, rev}
+          if (!tight(rec.w)) continue;
+          ++all;
+          live += test_bit(ign, rec.z) ? 0u : 1u;
+        }
+      }
+      cnt[v] = (uint16_t)live;
+      if (all && !live) cur[atomicAdd(ac, 1u)] = (uint16_t)v;
+    }
+    sync();
+  }
+  uint32_t n = __builtin_amdgcn_readfirstlane(ctl[r % 3u]);
+  ++r;
+  // (b) A: rounds down the live base-tight out-edges of A's members (listed in alist)
+  uint32_t na = 0;
+  while (n) {
+    uint32_t* const ac = &ctl[r % 3u];
+    if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+    for (uint32_t i = tid; i < n; i += BLOCK) {
+      const uint32_t u = cur[i];
+      alist[na + i] = (uint16_t)u;
+      dist[u] = INF;  // re-solved below
+      const uint2 rr = g.row2[u];
+      for (uint32_t e = rr.x; e < rr.y; ++e) {
+        if (!tight(e) || test_bit(ign, g.lid[e])) continue;  // an ignored link's loss counted in (a)
+        const uint32_t v = g.adj[e] & ~kEdgeDown;
+        const uint32_t sh = 16u * (v & 1u);
+        const uint32_t old = atomicSub(reinterpret_cast<uint32_t*>(cnt) + (v >> 1), 1u << sh);
+        if (((old >> sh) & 0xFFFFu) == 1u) nxt[atomicAdd(ac, 1u)] = (uint16_t)v;
+      }
+    }
+    na += n;
+    sync();
+    n = __builtin_amdgcn_readfirstlane(*ac);
+    ++r;
+    uint16_t* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  // (c) each member of A enters at its best in-edge from a node outside A (or from a
+  //     member already entered: any finite value is a path length, the rounds improve it)
+  uint32_t* const ac = &ctl[r % 3u];
+  if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+  for (uint32_t i = tid; i < na; i += BLOCK) {
+    const uint32_t v = alist[i];
+    D best = INF;
+    const uint2 rr = g.row2[v];
+    for (uint32_t e = rr.x; e < rr.y; ++e) {
+      const uint4 rec = g.erec[e];
+      if ((rec.x & kEdgeDown) || test_bit(ign, rec.z)) continue;
+      const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+      if (u != src && (rec.x & kNodeSink)) continue;  // an overloaded tail does not expand
+      const D du = dist[u];
+      if (du == INF) continue;
+      const D c = du + (D)rec.y;
+      best = c < best ? c : best;
+    }
+    if (best != INF) {
+      atomicMin(&dist[v], best);
+      atomicOr(&inq[v >> 5], 1u << (v & 31u));
+      cur[atomicAdd(ac, 1u)] = (uint16_t)v;
+    }
+  }
+  sync();
+  n = __builtin_amdgcn_readfirstlane(*ac);
+  ++r;
+  return n;
+}
 
 // BLOCK threads per solve: 64 (one wavefront, LDS ordering alone between rounds) or a
 // multi-wave workgroup for batches that fill under a quarter of the CUs' wave slots (the
@@ -107,15 +211,20 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
       }
       uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
       sync();
-      if (tid == 0) {
-        dist[src] = 0;
-        fa[0] = (uint16_t)src;
-      }
-      sync();
-
-      // (1) distance rounds over the frontier of nodes whose distance dropped
       uint16_t *cur = fa, *nxt = fb;
       uint32_t n = 1;
+      if (GENERIC && a.seed_dist) {
+        n = seed_from_base<D, BLOCK>(g, a, sid, src, dist, cnt, cur, nxt, inq, ign,
+                                     reinterpret_cast<uint16_t*>(base + lay.alist), ctl, r, tid, tight_words);
+      } else {
+        if (tid == 0) {
+          dist[src] = 0;
+          fa[0] = (uint16_t)src;
+        }
+        sync();
+      }
+
+      // (1) distance rounds over the frontier of nodes whose distance dropped
       while (n) {
         uint32_t* const ac = &ctl[r % 3u];
         if (tid == 0) ctl[(r + 1u) % 3u] = 0;

@@ -664,7 +664,7 @@ struct GrpWave {
   uint8_t* didx;           // per unit: 1 + v's dirty slot (adist / anh index), 0 = clean
   uint32_t cap;            // dirty slots
   uint16_t *alist, *dlist;
-  unsigned long long* prof;  // tuning (OPENR_SPF_WHATIF_PROF): per-phase cycles and sizes, or null
+  unsigned long long* prof;  // tuning (OPENR_SPF_PROF): per-phase cycles and sizes, or null
   unsigned long long pacc[8];  // this wave's share of prof, added once when the wave retires
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
@@ -951,14 +951,16 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
 constexpr uint32_t kGrpMaxBlock = 512;
 
 // WPE: waves per SIMD the compiler must fit registers for (1: no constraint). Unconstrained
-// the default variant takes 119 VGPRs, i.e. 4 waves per SIMD (16 per CU) whatever LDS
-// allows; 5 / 7 force 96 / 72 VGPRs at the price of scratch spills (44 / 140 B per lane).
+// the <= 32-bit-set variant takes 119 VGPRs, i.e. 4 waves per SIMD (16 per CU) whatever
+// LDS allows; 7 (its default since round 4) forces 72 VGPRs at the price of 140 B of
+// scratch spills per lane, and the 28 waves per CU the LDS layout allows win (kernel
+// 3.66 -> 2.81 ms on the WAN).
 template <typename D, bool LG, uint32_t W, int WPE>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
     uint32_t cap, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
-    uint32_t* ctr, unsigned long long* prof, const uint32_t* list, uint32_t n_list, uint32_t ovf_base) {
+    uint32_t* ctr, unsigned long long* prof) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1019,21 +1021,10 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
   c.dlist = reinterpret_cast<uint16_t*>(wb + lay.w_dlist);
   const uint32_t chunks = (n_links + chunk - 1u) / chunk;
-  // list pass: one item per listed unit i * n_src + j (the first pass's overflows)
-  const uint32_t items = list ? n_list : n_src * chunks;
+  const uint32_t items = n_src * chunks;
   uint32_t n_aff = 0;
   for (uint32_t item = blockIdx.x; item < items;) {
-    uint32_t j, l0, l1;
-    if (list) {
-      const uint32_t u = list[item];
-      l0 = u / n_src;
-      j = u - l0 * n_src;
-      l1 = l0 + 1u;
-    } else {
-      j = item / chunks;
-      l0 = (item - j * chunks) * chunk;
-      l1 = min(n_links, l0 + chunk);
-    }
+    const uint32_t j = item / chunks, l0 = (item - j * chunks) * chunk, l1 = min(n_links, l0 + chunk);
     c.src = sources[j];
     // stage source j's base rows (read once per item)
     const uint64_t* drow = base_dist + (size_t)j * V;
@@ -1100,9 +1091,8 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
       if (lane == 0) {
         if (cnt != kGrpOverflow) {
           changed[(size_t)i * n_src + j] = cnt;
-        } else {  // more dirty nodes than slots: repaired again by the list pass with every
-                  // slot, or re-solved after it (openr_spf_whatif)
-          const uint32_t k = ovf_base + atomicAdd(&affected[list ? 2 : 1], 1u);
+        } else {  // more dirty nodes than slots: re-solved after the launch (openr_spf_whatif)
+          const uint32_t k = atomicAdd(&affected[1], 1u);
           ovf_src[k] = c.src;
           ovf_link[k] = c.link;
           ovf_unit[k] = i * n_src + j;
@@ -1114,7 +1104,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     __syncthreads();
     item = s_item;
   }
-  if (tid == 0 && n_aff && !list) atomicAdd(affected, n_aff);  // a listed unit was counted by the first pass
+  if (tid == 0 && n_aff) atomicAdd(affected, n_aff);
   if (prof && lane == 0) {
     for (int k = 0; k < 8; ++k) atomicAdd(&prof[k], c.pacc[k]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
@@ -1198,33 +1188,29 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
-                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s,
-                               const uint32_t* list, uint32_t n_list) {
-  hipError_t err = hipSuccess;
-  if (!list) {  // [0] affected, [1] handed to the list pass, [2] handed over by the list pass
-    err = hipMemsetAsync(affected, 0, 3u * sizeof(uint32_t), s);
-    if (err != hipSuccess || !n_links || !n_src) return err;
-  } else if (!n_list) {
-    return hipSuccess;
-  }
+                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s) {
+  // [0] affected units, [1] units listed for a re-solve
+  hipError_t err = hipMemsetAsync(affected, 0, 2u * sizeof(uint32_t), s);
+  if (err != hipSuccess || !n_links || !n_src) return err;
   // distances as u16 when every finite one fits (V * w_max < 0xFFFF): half the LDS rows,
   // more workgroups per CU
   const bool d16 = (uint64_t)g.V * (unit_cost ? 1u : w_max) < 0xFFFFull && !bfs::env_u32("OPENR_SPF_WHATIF_D32", 0u, 0u, 1u);
   const uint32_t db = d16 ? 2u : dist64 ? 8u : 4u;
   // the LDS-graph variant (opt-in) with as many waves per workgroup (one workgroup per
-  // CU) as fit, else the global-graph variant at OPENR_SPF_WHATIF_WAVES (3) per workgroup
+  // CU) as fit, else the global-graph variant at kGrpWaves per workgroup
   bool lg = false;
-  // First pass: few dirty slots per wave (LDS per wave ~3.5 KB on the WAN: 7 workgroups of
-  // 4 waves per CU); the units that outgrow them are listed for a re-solve, or (opt-in)
-  // repaired again by the list pass: one wave per workgroup, every slot (kGrpMaxCap), one
-  // unit per item. WAN kernel time (cap / waves): 255 / 3 4.57 ms, 160 / 3 4.07, 128 / 4
-  // 3.66, 96 / 4 3.46, 64 / 4 3.09, 48 / 4 2.90 (fewer slots: more re-solves; the step is
-  // shortest at 128 / 4: 5.02 ms, against 5.11 at 112, 5.19 at 96, 5.09 at 160).
-  uint32_t waves = list ? 1u : bfs::env_u32("OPENR_SPF_WHATIF_WAVES", kGrpWaves, 1u, kGrpMaxBlock / 64u);
-  const uint32_t cap = list ? bfs::env_u32("OPENR_SPF_WHATIF_CAP2", kGrpMaxCap, 1u, kGrpMaxCap)
-                            : bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpCap1, 1u, kGrpMaxCap);  // tests force small caps
+  // Few dirty slots per wave (LDS per wave ~3.5 KB on the WAN: 7 workgroups of 4 waves per
+  // CU); the units that outgrow them are listed for a re-solve. WAN kernel time (cap /
+  // waves, round 3): 255 / 3 4.57 ms, 160 / 3 4.07, 128 / 4 3.66, 96 / 4 3.46, 64 / 4 3.09,
+  // 48 / 4 2.90 (fewer slots: more re-solves; the step is shortest at 128 / 4: 5.02 ms,
+  // against 5.11 at 112, 5.19 at 96, 5.09 at 160; at 7 waves per SIMD, round 4: 96 4.36,
+  // 112 4.25, 128 4.16, 144 4.17, 160 4.15, 192 4.21 ms). A second pass repairing the
+  // overflowed units with every slot on one wavefront each was slower than the re-solves
+  // (5.34 vs 5.18 ms, round 3; 4.68 vs 4.16 ms, round 4) and was removed.
+  uint32_t waves = kGrpWaves;
+  const uint32_t cap = bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpCap1, 1u, kGrpMaxCap);  // tests force small caps
   auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch, cap).total; };
-  if (!list && grp_lds_graph_ok(g, w_max, nh_bits)) {
+  if (grp_lds_graph_ok(g, w_max, nh_bits)) {
     for (uint32_t w = kGrpMaxBlock / 64u; w >= 2u; --w) {
       if (layout_bytes(true, w, kGrpMaxChunk) <= kMaxLds) {
         lg = true;
@@ -1244,34 +1230,32 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   uint64_t cps = (8u * slots0 + n_src - 1u) / n_src;
   cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
   uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
-  chunk = std::min(bfs::env_u32("OPENR_SPF_WHATIF_CHUNK", chunk, 1u, 1u << 30), kGrpMaxChunk);
-  if (list) chunk = 1;  // one unit per item
+  chunk = std::min(chunk, kGrpMaxChunk);
   const uint32_t lds = layout_bytes(lg, waves, chunk);  // the list sized to the chunk
   const uint64_t slots = slots_for(lds);
-  const uint64_t items = list ? (uint64_t)n_list : (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
+  const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
   // tuning aid: per-phase cycle sums and set sizes, printed after the launch
   static unsigned long long* prof_buf = nullptr;
   unsigned long long* prof = nullptr;
-  if (bfs::env_u32("OPENR_SPF_WHATIF_PROF", 0u, 0u, 1u)) {
+  if (prof_enabled()) {
     if (!prof_buf && hipMalloc(&prof_buf, 16 * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
     prof = prof_buf;
     if (prof) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
   }
-  // OPENR_SPF_WHATIF_WPE=5|7: register target of the <= 32-bit-set variant (A/B)
-  const uint32_t wpe = bfs::env_u32("OPENR_SPF_WHATIF_WPE", 1u, 1u, 8u);
+  // the <= 32-bit-set variant is compiled for 7 waves per SIMD, the occupancy its LDS
+  // layout allows (28 waves per CU): WAN step 5.03 -> 4.17 ms (unconstrained: 119 VGPRs,
+  // 4 waves per SIMD; 5 waves: 4.56 ms), round 4
 #define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
   do {                                                                                                         \
-    auto k = nb <= 4u ? (wpe == 5u ? whatif_group_kernel<DT, LGV, 1, 5>                                        \
-                                   : wpe == 7u ? whatif_group_kernel<DT, LGV, 1, 7> : whatif_group_kernel<DT, LGV, 1, 1>) \
-                      : whatif_group_kernel<DT, LGV, kGrpNhWords, 1>;                                          \
+    auto k = nb <= 4u ? whatif_group_kernel<DT, LGV, 1, 7> : whatif_group_kernel<DT, LGV, kGrpNhWords, 1>;     \
     err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
                        base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed, affected, ovf_src, ovf_link,  \
-                       ovf_unit, ctr, prof, list, n_list, list ? n_list : 0u);                                 \
+                       ovf_unit, ctr, prof);                                                                   \
   } while (0)
   if (d16) {
     if (lg) OPENR_GRP_LAUNCH(uint16_t, true);

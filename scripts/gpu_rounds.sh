@@ -14,7 +14,7 @@ for l in 1 2; do
   OPENR_SPF_KSP_LANES=$l timeout -k 10 300 python -u bench.py --workload ksp2 --topology fabric --ksp-sources 512 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/b_ksp_$l.log 2>&1 || { tail -20 gpurun_out/b_ksp_$l.log; exit 1; }
   grep '^{' gpurun_out/b_ksp_$l.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('ksp lanes', '$l', d['ms_per_step'], d['value'])"
 done
-OPENR_SPF_WHATIF_PROF=1 timeout -k 10 200 python -u bench.py --workload whatif --steps 2 --warmup 1 --no-cpu-baseline --no-ucmp > gpurun_out/b_whatif_prof.log 2>&1 || exit 1
+OPENR_SPF_PROF=1 timeout -k 10 200 python -u bench.py --workload whatif --steps 2 --warmup 1 --no-cpu-baseline --no-ucmp > gpurun_out/b_whatif_prof.log 2>&1 || exit 1
 grep whatif_group gpurun_out/b_whatif_prof.log | tail -1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_whatif -o run --output-format csv -- python3 bench.py --workload whatif --steps 5 --warmup 1 --no-cpu-baseline --no-ucmp > gpurun_out/prof_whatif.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ksp -o run --output-format csv -- python3 bench.py --workload ksp2 --topology fabric --ksp-sources 512 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_ksp.log 2>&1 || exit 1

@@ -10,7 +10,7 @@ timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thre
   > gpurun_out/lean_tests.log 2>&1; rc=$?
 echo "lean tests rc=$rc"; grep -E "FAIL|Error|error|passed|failed" gpurun_out/lean_tests.log | tail -12
 case $rc in 0) ;; *) tail -40 gpurun_out/lean_tests.log; exit $rc;; esac
-OPENR_SPF_BFS_PROF=1 timeout -k 10 200 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-gather > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+OPENR_SPF_PROF=1 timeout -k 10 200 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-gather > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
 grep bfs_ell gpurun_out/prof.log | tail -1
 timeout -k 10 240 python3 -u scripts/sweep.py --topology grid100 --rounds 6 \
   --variants "LWGS=0;LWGS=8;LWGS=7" > gpurun_out/occ.log 2>&1 || { tail -20 gpurun_out/occ.log; exit 1; }

@@ -13,7 +13,7 @@ case $rc in 124|134|137|139) exit $rc;; esac
 timeout -k 10 240 python3 -u scripts/sweep.py --topology grid100 --rounds 6 \
   --variants "LWGS=10;LWGS=9;LWGS=8;LWGS=7;LWGS=6;LWGS=5" > gpurun_out/occ.log 2>&1 || { tail -20 gpurun_out/occ.log; exit 1; }
 cat gpurun_out/occ.log
-OPENR_SPF_BFS_PROF=1 timeout -k 10 200 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+OPENR_SPF_PROF=1 timeout -k 10 200 python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
 grep bfs_ell gpurun_out/prof.log | tail -2
 KFILTER=bfs_ell SQ_TAG=full BENCH_ARGS="--topology grid100" bash scripts/sq_counters.sh || exit 1
 SQ_CMD="scripts/batch_latency.py --topology grid100 --sizes 1250 --reps 3" KFILTER=bfs_wave SQ_TAG=shard bash scripts/sq_counters.sh || exit 1

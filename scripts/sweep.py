@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 KEYS = {"FULL": "OPENR_SPF_BFS_FULL", "FAM": "OPENR_SPF_BFS_FAMILY", "GEN": "OPENR_SPF_GENERAL",
-        "RING": "OPENR_SPF_RING_CAP", "WAVE": "OPENR_SPF_BFS_WAVE", "PROF": "OPENR_SPF_BFS_PROF"}
+        "RING": "OPENR_SPF_RING_CAP", "WAVE": "OPENR_SPF_BFS_WAVE", "PROF": "OPENR_SPF_PROF"}
 
 
 def parse(v):

@@ -125,7 +125,7 @@ def test_config3_grid100_pass_variants(eng, monkeypatch, chunk, env, kernel):
     all_sources_vs_oracle(eng, T.grid_fast(100), chunk, expect_kernel=kernel)
 
 
-@pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "group-cap", "group-cap2", "incr", "solve"])
+@pytest.mark.parametrize("mode", ["group", "group-lds", "group-d32", "group-cap", "group-cap1", "incr", "solve"])
 def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
     """Per-link-failure sweep on the 1k-node WAN (U[1,64] asymmetric metrics): every one
     of the 3 000 links x 16 sources, changed-node counts vs oracle re-solves
@@ -135,10 +135,10 @@ def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
         monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
-    if mode in ("group-cap", "group-cap2"):  # 8 dirty slots in the first pass: larger units are re-solved
+    if mode == "group-cap":  # 8 dirty slots: larger units take the seeded re-solve
         monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "8")
-    if mode == "group-cap2":  # or take the opt-in list pass (every slot) first
-        monkeypatch.setenv("OPENR_SPF_WHATIF_LIST", "1")
+    if mode == "group-cap1":  # 1 slot: nearly every affected unit is re-solved
+        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "1")
     monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     g = T.wan(1000, 3000, 64, seed=1)
     eng.set_graph(g)

@@ -289,11 +289,11 @@ def test_wave_pass(eng, monkeypatch, capfd, case):
     """The wave pass (one wavefront per solve, delta-coded rows staged in LDS; picked for
     small batches of graphs whose rows have <= 4 edges within 127 ids of their node),
     forced on and checked against the oracle, including both re-run paths: a chain
-    deeper than 253 levels and a forced tiny queue half. OPENR_SPF_BFS_PROF makes the pass
+    deeper than 253 levels and a forced tiny queue half. OPENR_SPF_PROF makes the pass
     report itself on stderr (proof that it ran)."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
     monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "1")
-    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    monkeypatch.setenv("OPENR_SPF_PROF", "1")
     n = 40
     names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)]
     links = [(r * n + c, r * n + c + 1) for r in range(n) for c in range(n - 1)]
@@ -323,7 +323,7 @@ def test_wave_pass_not_applicable(eng, monkeypatch, capfd):
     wave pass off even when forced; the lean / generic passes serve the graph."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
     monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "1")
-    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    monkeypatch.setenv("OPENR_SPF_PROF", "1")
     g = T.grid_fast(200)
     check_against_oracle(eng, g, [0, 199, 20100, 39999], True, check_pathlinks=False)
     assert "bfs_wave:" not in capfd.readouterr().err
@@ -334,8 +334,8 @@ def test_lean_pass_depth_overflow(eng, monkeypatch, capfd, bfs_family):
     sampled depth under the u8 limit): a 70 x 70 grid plus a separate 300-node chain whose
     nodes no depth sample starts from. Chain sources run deeper than 253 levels: the lean
     pass flags them at level 254 and the u16 full-order pass re-runs them. (With
-    OPENR_SPF_BFS_PROF the lean pass reports itself on stderr: proof that it ran.)"""
-    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    OPENR_SPF_PROF the lean pass reports itself on stderr: proof that it ran.)"""
+    monkeypatch.setenv("OPENR_SPF_PROF", "1")
     monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")  # small batch: the wave pass would take it
     n, tail = 70, 300
     names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)] + [f"z{i:03d}" for i in range(tail)]
@@ -353,7 +353,7 @@ def test_lean_pass_half_overflow(eng, monkeypatch, capfd, bfs_family):
     """A level wider than a queue half in the lean pass (forced onto a graph whose sampled
     width would otherwise keep it on the generic ring): the solve is flagged and re-run."""
     monkeypatch.setenv("OPENR_SPF_LEAN_FORCE", "1")
-    monkeypatch.setenv("OPENR_SPF_BFS_PROF", "1")
+    monkeypatch.setenv("OPENR_SPF_PROF", "1")
     monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")
     chain, depth = 100, 11
     names = [f"c{i:03d}" for i in range(chain)] + [f"t{i:05d}" for i in range(1, 2 ** (depth + 1) - 1)]
@@ -514,24 +514,21 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "group-cap2", "incr", "solve"])
+@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "group-cap1", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
     (default: graph read from global memory, u16 distances when they fit; or the graph
     staged in LDS too; or u32 / u64 distances), per-unit incremental repair, or full
-    re-solves. group-cap: 3 dirty slots per wave, so most units are re-solved; group-cap2:
-    3 slots, then the opt-in list pass with 5 (OPENR_SPF_WHATIF_LIST=1), so some are
-    repaired twice and the rest re-solved."""
+    re-solves. group-cap: 3 dirty slots per wave, so most units are re-solved; group-cap1:
+    1 slot, so nearly every affected unit takes the seeded re-solve (the rounds kernel
+    starting from the base rows)."""
     mode = request.param
     if mode == "group-lds":
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
         monkeypatch.setenv("OPENR_SPF_WHATIF_D32", "1")
-    if mode in ("group-cap", "group-cap2"):
-        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "3")
-    if mode == "group-cap2":
-        monkeypatch.setenv("OPENR_SPF_WHATIF_LIST", "1")
-        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP2", "5")
+    if mode in ("group-cap", "group-cap1"):
+        monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "3" if mode == "group-cap" else "1")
     monkeypatch.setenv("OPENR_SPF_WHATIF", mode.split("-")[0])
     return request.param
 
@@ -754,18 +751,14 @@ def test_ksp2_device_capacity_tiers(eng, tier, monkeypatch):
     check_ksp2_against_oracle(eng, g, [(h, int(d)) for h in range(3) for d in rng.integers(0, g.num_nodes, 30)])
 
 
-@pytest.mark.parametrize("lanes", ["2", "1"], ids=["two-lanes", "one-lane"])
 @pytest.mark.parametrize("tag", ["1", "0"], ids=["tagged", "filled"])
-def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag, lanes):
+def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
     """KSP2 second-SPF level rows (code family, uniform cost): tagged — a solve writes only
     the nodes it settles (it stops at the pair's target) as tag << shift | level, and an
     entry with another chunk's tag reads as unreached — or filled (unreached = 0xFFFF).
     Chunks of 7 pairs: on the 300-node graph (9 level bits, tags 1..127) the tags wrap and
-    the rows are zeroed again mid-call; results equal the oracle either way. Chunks run
-    on one stream (default) or alternate between two stream lanes with their own rows,
-    tags and counters (OPENR_SPF_KSP_LANES=2, opt-in)."""
+    the rows are zeroed again mid-call; results equal the oracle either way."""
     monkeypatch.setenv("OPENR_SPF_KSP_TAG", tag)
-    monkeypatch.setenv("OPENR_SPF_KSP_LANES", lanes)
     monkeypatch.setenv("OPENR_SPF_KSP_CHUNK", "7")
     g = random_graph(9, 300, 620, 1, p_ovl=0.05, p_down=0.05, p_par=0.1)
     rng = np.random.default_rng(11)
