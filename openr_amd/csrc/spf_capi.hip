@@ -554,8 +554,14 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       b.seed_tight = d.base_tight.p;
       b.seed_unit = d.wunit.p + off;
       b.seed_nsrc = n_src;
+      // ... and compares each solve with the base rows itself (no rows through HBM)
+      const bool fused = ign_plan.rounds && !ign_plan.exact && !ign_plan.bfs;
+      if (fused) {
+        b.seed_nh = d.base_nh.p;
+        b.seed_changed = d_changed;
+      }
       if ((e2 = launch(ctx, d, ign_plan, b, s)) != hipSuccess) return e2;
-      if ((e2 = launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
+      if (!fused && (e2 = launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
                                     d_changed, d.num_cus, s)) != hipSuccess)
         return e2;
     }

@@ -144,6 +144,11 @@ struct SolveArgs {
   const uint64_t* seed_tight;
   const uint32_t* seed_unit;
   uint32_t seed_nsrc;
+  // nullable with seed_dist: instead of writing rows, compare the solve with the base rows
+  // (seed_dist, seed_nh: nh_bytes per node) and store the count of nodes whose distance or
+  // next-hop bytes differ at seed_changed[seed_unit[sid]] (the what-if unit's answer)
+  const uint8_t* seed_nh;
+  uint32_t* seed_changed;
   uint32_t* status;
   // code-family sliced class with next-hop output: [krows][nsl][V] 29-bit chunks of the
   // sets (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows

@@ -80,6 +80,7 @@ __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32
   };
   const uint32_t V = g.V;
   const uint32_t j = a.seed_unit[sid] % a.seed_nsrc;
+  if (a.seed_changed && tid == 0) a.seed_changed[a.seed_unit[sid]] = 0;  // counted at the end
   const uint64_t* bd = a.seed_dist + (size_t)j * V;
   const uint64_t* bt = a.seed_tight + (size_t)j * tight_words;
   auto tight = [&](uint32_t e) { return ((bt[e >> 6] >> (e & 63u)) & 1ull) != 0; };
@@ -342,6 +343,25 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
         cur = nxt;
         nxt = t;
       }
+      if (GENERIC && a.seed_changed) {
+        // what-if unit: the count of nodes whose distance or next-hop bytes differ from the
+        // base rows, instead of the rows (no row round trip through HBM)
+        const uint32_t unit = a.seed_unit[sid], j = unit % a.seed_nsrc, nb = a.nh_bytes;
+        const uint64_t* bd = a.seed_dist + (size_t)j * V;
+        const uint8_t* bh = a.seed_nh + (size_t)j * V * nb;
+        uint32_t c = 0;
+        for (uint32_t v = tid; v < V; v += BLOCK) {
+          const D dv = dist[v];
+          bool diff = (dv == INF ? ~0ull : (uint64_t)dv) != bd[v];
+          for (uint32_t b = 0; b < nb && !diff; ++b) diff = (uint8_t)N::byte(nh, v, b) != bh[(size_t)v * nb + b];
+          c += diff ? 1u : 0u;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if ((tid & 63u) == 0 && c) atomicAdd(&a.seed_changed[unit], c);  // zeroed by the seeded start
+        goto next_solve;
+      }
+      {
       // (result rows, coalesced; unreached nodes keep UINT64_MAX)
       uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       for (uint32_t v = tid; v < V; v += BLOCK) {
@@ -356,7 +376,9 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
           nrow[i] = (uint8_t)N::byte(nh, v, j);
         }
       }
+      }
     }
+  next_solve:
     if constexpr (BLOCK == kWave) {
       uint32_t nxt_sid = 0;
       if (tid == 0) nxt_sid = gridDim.x + atomicAdd(&ctr[0], 1u);
