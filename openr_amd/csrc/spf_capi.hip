@@ -87,6 +87,8 @@ struct Device {
   DevBuf<uint64_t> base_dist, base_tight, wdist;
   DevBuf<uint8_t> base_nh, wnh;
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
+  DevBuf<uint16_t> base_tin;  // what-if base SPF: tight in-degree rows (rounds plan)
+  size_t wiota_n = 0;  // wiota[0, wiota_n) holds 0, 1, 2, ... (kept across calls)
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
   DevBuf<uint64_t> kbase, krows;
   DevBuf<uint16_t> krows16;  // KSP2 second SPFs on the code family: u16 level rows
@@ -488,6 +490,18 @@ int solve_host(openr_spf_ctx* ctx, const uint32_t* sources, uint32_t n, uint32_t
   return OPENR_SPF_OK;
 }
 
+// Identity array 0, 1, ..., n-1 in d.wiota (one-link ignore sets: solve k ignores exactly
+// links[k]); built once and kept while it is long enough.
+hipError_t ensure_iota(Device& d, size_t n, hipStream_t s) {
+  if (n <= d.wiota_n) return hipSuccess;
+  if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  d.wiota_n = 0;
+  hipError_t e = d.wiota.reserve(n);
+  if (e == hipSuccess) e = launch_iota(d.wiota.p, (uint32_t)n, d.num_cus, s);
+  if (e == hipSuccess) d.wiota_n = n;
+  return e;
+}
+
 // Bytes of chunk result rows a what-if sweep may hold on a device at once.
 constexpr size_t kWhatifChunkBytes = size_t(1) << 30;
 
@@ -523,6 +537,12 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   OPENR_TRY(d.ovf.reserve((size_t)n_src * ctx->nsl_max()));
   a.ovf_list = d.ovf.p;
   a.work = d.work.p;
+  // the rounds kernel also leaves each base row's tight in-degrees for the seeded re-solves
+  const bool base_tin = base_plan.rounds && !base_plan.exact && !base_plan.bfs;
+  if (base_tin) {
+    OPENR_TRY(d.base_tin.reserve((size_t)n_src * V));
+    a.tin_out = d.base_tin.p;
+  }
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
   // re-solve the `count` units listed in wsrc / wlink / wunit (ignore set = the unit's
   // link) and compare each row with its source's base row
@@ -532,9 +552,8 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
     const uint32_t chunk = (uint32_t)std::min<size_t>(count, std::max<size_t>(1, kWhatifChunkBytes / row));
     if ((e2 = d.wdist.reserve((size_t)chunk * V)) != hipSuccess) return e2;
     if ((e2 = d.wnh.reserve((size_t)chunk * V * nb)) != hipSuccess) return e2;
-    if ((e2 = d.wiota.reserve((size_t)chunk + 1u)) != hipSuccess) return e2;
+    if ((e2 = ensure_iota(d, (size_t)chunk + 1u, s)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)chunk * ctx->nsl_max())) != hipSuccess) return e2;
-    if ((e2 = launch_iota(d.wiota.p, chunk + 1u, d.num_cus, s)) != hipSuccess) return e2;
     for (uint32_t off0 = 0; off0 < count; off0 += chunk) {
       const uint32_t m = std::min(chunk, count - off0), off = base + off0;
       SolveArgs b{};
@@ -554,6 +573,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       b.seed_tight = d.base_tight.p;
       b.seed_unit = d.wunit.p + off;
       b.seed_nsrc = n_src;
+      b.seed_tin = base_tin ? d.base_tin.p : nullptr;
       // ... and compares each solve with the base rows itself (no rows through HBM)
       const bool fused = ign_plan.rounds && !ign_plan.exact && !ign_plan.bfs;
       if (fused) {
@@ -588,16 +608,74 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
                                     d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
                                     d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));
-      uint32_t cnt[2] = {0, 0};  // affected units, units handed to the list pass
+      // Units past the slots are large (WAN: ~6 500 of 1.02 M affected units, ~150 dirty
+      // nodes on average): re-solved, each starting from its source's base rows (the
+      // rounds kernel's seeded start). On the rounds plan one launch covers them, its
+      // count read on the device (wcount[1]): no host round trip between the kernels.
+      const bool fused = ign_plan.rounds && !ign_plan.exact && !ign_plan.bfs;
+      if (fused) {
+        OPENR_TRY(ensure_iota(d, units + 1u, s));
+        SolveArgs b{};
+        b.sources = d.wsrc.p;
+        b.n = (uint32_t)std::min<size_t>(units, 0xFFFFFFFEu);
+        b.n_dev = d.wcount.p + 1;
+        // two waves per solve: WAN re-solves (6 835 units, 256-thread base SPF) 64 / 128 / 256
+        // threads: span 1.02 / 0.83 / 1.00 ms (more solves resident, rounds still split)
+        b.n_block = 128u;
+        b.ign_ptr = d.wiota.p;  // solve k ignores exactly wlink[k]
+        b.ign_links = d.wlink.p;
+        b.nh_bytes = nb;
+        b.nh_bits = ctx->nh_bits;
+        b.work = d.work.p;
+        b.seed_dist = d.base_dist.p;
+        b.seed_tight = d.base_tight.p;
+        b.seed_unit = d.wunit.p;
+        b.seed_nsrc = n_src;
+        b.seed_tin = base_tin ? d.base_tin.p : nullptr;
+        b.seed_nh = d.base_nh.p;
+        b.seed_changed = d_changed;
+        if (prof_enabled()) {
+          OPENR_TRY(hipMallocAsync(reinterpret_cast<void**>(&b.prof_solve), 10 * units * sizeof(unsigned long long), s));
+          OPENR_TRY(hipMemsetAsync(b.prof_solve, 0, 10 * units * sizeof(unsigned long long), s));
+        }
+        OPENR_TRY(launch(ctx, d, ign_plan, b, s));
+        if (b.prof_solve) {  // tuning aid: the re-solves' phases (100 MHz wall clock) and the tail
+          uint32_t nres = 0;
+          OPENR_TRY(hipMemcpyAsync(&nres, d.wcount.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+          OPENR_TRY(hipStreamSynchronize(s));
+          std::vector<unsigned long long> h(10 * (size_t)nres);
+          OPENR_TRY(hipMemcpy(h.data(), b.prof_solve, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+          OPENR_TRY(hipFreeAsync(b.prof_solve, s));
+          if (nres) {
+            unsigned long long t0 = ~0ull, t1 = 0;
+            double ph[7] = {0}, na = 0, rd = 0, rk = 0, tot = 0;
+            for (uint32_t k = 0; k < nres; ++k) {
+              const unsigned long long* x = &h[10 * (size_t)k];
+              t0 = std::min(t0, x[0]);
+              t1 = std::max(t1, x[7]);
+              for (int q = 0; q < 7; ++q) ph[q] += (double)(x[q + 1] - x[q]) / 100.0;
+              tot += (double)(x[7] - x[0]) / 100.0;
+              na += (double)x[8];
+              rd += (double)(x[9] & 0xFFFFFFFFull);
+              rk += (double)(x[9] >> 32);
+            }
+            std::fprintf(stderr,
+                         "[whatif resolve] n=%u span=%.1fus mean solve %.1fus: seed-a %.1f seed-A %.1f seed-c %.1f "
+                         "dist %.1f indeg %.1f kahn %.1f compare %.1f | |A| %.1f, rounds: A+c+dist %.1f, kahn %.1f, "
+                         "concurrency %.0f\n",
+                         nres, (t1 - t0) / 100.0, tot / nres, ph[0] / nres, ph[1] / nres, ph[2] / nres, ph[3] / nres,
+                         ph[4] / nres, ph[5] / nres, ph[6] / nres, na / nres, rd / nres, rk / nres,
+                         tot / ((t1 - t0) / 100.0));
+          }
+        }
+      }
+      uint32_t cnt[2] = {0, 0};  // affected units, units past the slots
       OPENR_TRY(hipMemcpyAsync(cnt, d.wcount.p, sizeof(cnt), hipMemcpyDeviceToHost, s));
       OPENR_TRY(hipStreamSynchronize(s));
       float ms = 0.f;
       OPENR_TRY(hipEventElapsedTime(&ms, d.ev_begin, d.ev_end));
       ctx->stats.last_kernel_ms = ms;
-      // Units past the slots are large (WAN: ~6 500 of 1.02 M affected units, ~150 dirty
-      // nodes on average): re-solved, each starting from its source's base rows (the
-      // rounds kernel's seeded start)
-      if (cnt[1]) OPENR_TRY(resolve_units(cnt[1], 0));
+      if (!fused && cnt[1]) OPENR_TRY(resolve_units(cnt[1], 0));
       *solved = cnt[0];
       return hipSuccess;
     }
@@ -879,7 +957,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.perm.release();
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
-                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.win_links.p, d.win_src.p, d.wchanged.p,
+                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.base_tin.p, d.win_links.p, d.win_src.p, d.wchanged.p,
                      d.kbase.p,     d.krows.p,      d.krows16.p, d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)

@@ -149,6 +149,17 @@ struct SolveArgs {
   // next-hop bytes differ at seed_changed[seed_unit[sid]] (the what-if unit's answer)
   const uint8_t* seed_nh;
   uint32_t* seed_changed;
+  // rounds kernel: tin_out (nullable, solves without a seed) receives each solve's tight
+  // in-degree row [out_row][V] (u16); seed_tin (nullable, with seed_dist) is such a row set
+  // for the base SPF, so a seeded start reads the counts instead of scanning every in-edge
+  uint16_t* tin_out;
+  const uint16_t* seed_tin;
+  // nullable (rounds kernel, generic): the solve count is min(n, *n_dev), read on the device
+  // (n sizes the grid; n_block = threads per solve, 64 / 128 / 256) -- no host round trip
+  // for a count the previous kernel produced
+  const uint32_t* n_dev;
+  uint32_t n_block;
+  unsigned long long* prof_solve;  // nullable (OPENR_SPF_PROF): rounds kernel per-solve wall-clock start / end
   uint32_t* status;
   // code-family sliced class with next-hop output: [krows][nsl][V] 29-bit chunks of the
   // sets (slice s = bits [29s, 29s + 29)); launch_bfs_code merges them into nh rows

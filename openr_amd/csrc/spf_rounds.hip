@@ -72,7 +72,8 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 template <typename D, uint32_t BLOCK>
 __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32_t sid, uint32_t src, D* dist,
                                    uint16_t* cnt, uint16_t*& cur, uint16_t*& nxt, uint32_t* inq, const uint32_t* ign,
-                                   uint16_t* alist, uint32_t* ctl, uint32_t& r, uint32_t tid, uint32_t tight_words) {
+                                   uint16_t* alist, uint32_t* ctl, uint32_t& r, uint32_t tid, uint32_t tight_words,
+                                   uint32_t& na_out) {
   constexpr D INF = (D)~(D)0;
   auto sync = [&]() {
     if constexpr (BLOCK == kWave) lds_fence();
@@ -86,7 +87,36 @@ __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32
   auto tight = [&](uint32_t e) { return ((bt[e >> 6] >> (e & 63u)) & 1ull) != 0; };
   // (a) base distances; live base-tight in-degree of every node (in-edges over an ignored
   //     link are lost); A's seeds: nodes that had tight in-edges and lost them all
-  {
+  if (a.seed_tin) {
+    // the base SPF's tight in-degree row, less the tight edges of the ignored links (one
+    // lane per listed link; a link listed twice counts once)
+    uint32_t* const ac = &ctl[r % 3u];
+    if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+    const uint16_t* bc = a.seed_tin + (size_t)j * V;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+      const uint64_t b = bd[v];
+      dist[v] = b == UINT64_MAX ? INF : (D)b;
+      cnt[v] = bc[v];
+    }
+    sync();
+    const uint32_t i0 = a.ign_ptr[sid], i1 = a.ign_end ? a.ign_end[sid] : a.ign_ptr[sid + 1];
+    for (uint32_t i = i0 + tid; i < i1; i += BLOCK) {
+      const uint32_t l = a.ign_links[i];
+      bool dup = l >= g.L;
+      for (uint32_t k = i0; k < i && !dup; ++k) dup = a.ign_links[k] == l;
+      if (dup) continue;
+      const uint2 le = g.ledge[l];
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t e = h ? le.y : le.x;
+        if (e == UINT32_MAX || !tight(e)) continue;
+        const uint32_t v = g.adj[e] & ~kEdgeDown;
+        const uint32_t sh = 16u * (v & 1u);
+        const uint32_t old = atomicSub(reinterpret_cast<uint32_t*>(cnt) + (v >> 1), 1u << sh);
+        if (((old >> sh) & 0xFFFFu) == 1u) cur[atomicAdd(ac, 1u)] = (uint16_t)v;
+      }
+    }
+    sync();
+  } else {
     uint32_t* const ac = &ctl[r % 3u];
     if (tid == 0) ctl[(r + 1u) % 3u] = 0;
     for (uint32_t v = tid; v < V; v += BLOCK) {
@@ -107,6 +137,7 @@ __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32
     }
     sync();
   }
+  if (a.prof_solve && tid == 0) a.prof_solve[10 * (size_t)sid + 1] = wall_clock64();
   uint32_t n = __builtin_amdgcn_readfirstlane(ctl[r % 3u]);
   ++r;
   // (b) A: rounds down the live base-tight out-edges of A's members (listed in alist)
@@ -135,6 +166,10 @@ __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32
     cur = nxt;
     nxt = t;
   }
+  if (a.prof_solve && tid == 0) {
+    a.prof_solve[10 * (size_t)sid + 2] = wall_clock64();
+    a.prof_solve[10 * (size_t)sid + 8] = na;
+  }
   // (c) each member of A enters at its best in-edge from a node outside A (or from a
   //     member already entered: any finite value is a path length, the rounds improve it)
   uint32_t* const ac = &ctl[r % 3u];
@@ -162,6 +197,8 @@ __device__ uint32_t seed_from_base(const DevGraph& g, const SolveArgs& a, uint32
   sync();
   n = __builtin_amdgcn_readfirstlane(*ac);
   ++r;
+  if (a.prof_solve && tid == 0) a.prof_solve[10 * (size_t)sid + 3] = wall_clock64();
+  na_out = na;
   return n;
 }
 
@@ -197,9 +234,14 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
     else __syncthreads();
   };
   uint32_t r = 0;  // round number (append counter rotation)
+  uint32_t n_sol = a.n;
+  if (GENERIC && a.n_dev) n_sol = min(n_sol, __builtin_amdgcn_readfirstlane(*a.n_dev));
 
-  for (uint32_t sid = blockIdx.x; sid < a.n;) {
+  for (uint32_t sid = blockIdx.x; sid < n_sol;) {
     const uint32_t src = a.sources[sid];
+    const unsigned long long t_start = (GENERIC && a.prof_solve) ? wall_clock64() : 0ull;
+    const uint32_t r_start = r;
+    uint32_t r_dist = 0, r_kahn = 0;
     if (src < V) {
       for (uint32_t v = tid; v < V; v += BLOCK) dist[v] = INF;
       for (uint32_t i = tid; i < nh_words; i += BLOCK) nh[i] = 0;
@@ -213,10 +255,10 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
       uint64_t* trow = (GENERIC && a.tight) ? a.tight + out_row_of(a, sid) * tight_words : nullptr;
       sync();
       uint16_t *cur = fa, *nxt = fb;
-      uint32_t n = 1;
+      uint32_t n = 1, na = 0;
       if (GENERIC && a.seed_dist) {
         n = seed_from_base<D, BLOCK>(g, a, sid, src, dist, cnt, cur, nxt, inq, ign,
-                                     reinterpret_cast<uint16_t*>(base + lay.alist), ctl, r, tid, tight_words);
+                                     reinterpret_cast<uint16_t*>(base + lay.alist), ctl, r, tid, tight_words, na);
       } else {
         if (tid == 0) {
           dist[src] = 0;
@@ -271,11 +313,14 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
         nxt = t;
       }
 
+      r_dist = r;
+      if (GENERIC && a.prof_solve && tid == 0) a.prof_solve[10 * (size_t)sid + 4] = wall_clock64();
       // (2) tight in-degree of every reached node; the source (and nodes with no tight
-      //     in-edge) start the topological rounds
-      uint32_t* const ac2 = &ctl[r % 3u];
-      if (tid == 0) ctl[(r + 1u) % 3u] = 0;
-      for (uint32_t v = tid; v < V; v += BLOCK) {
+      //     in-edge) start the topological rounds. After a seeded start only A's members
+      //     are counted: a node outside A keeps its distance and gains no tight in-edge
+      //     (every A member's distance grew), so its count is the base count less the
+      //     in-edges the seed took away (the ignored links', A members')
+      auto tight_in = [&](uint32_t v) -> uint32_t {
         const D dv = dist[v];
         uint32_t c = 0;
         if (dv != INF && v != src) {
@@ -294,12 +339,32 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
             }
           }
         }
-        cnt[v] = (uint16_t)c;
-        if (v == src) cur[atomicAdd(ac2, 1u)] = (uint16_t)v;
+        return c;
+      };
+      uint32_t* const ac2 = &ctl[r % 3u];
+      if (tid == 0) ctl[(r + 1u) % 3u] = 0;
+      if (GENERIC && a.seed_dist) {
+        const uint16_t* al = reinterpret_cast<const uint16_t*>(base + lay.alist);
+        for (uint32_t i = tid; i < na; i += BLOCK) {
+          const uint32_t v = al[i];
+          cnt[v] = (uint16_t)tight_in(v);
+        }
+        if (tid == 0) cur[atomicAdd(ac2, 1u)] = (uint16_t)src;
+        sync();
+      } else {
+        for (uint32_t v = tid; v < V; v += BLOCK) {
+          cnt[v] = (uint16_t)tight_in(v);
+          if (v == src) cur[atomicAdd(ac2, 1u)] = (uint16_t)v;
+        }
+        sync();
+        if (GENERIC && a.tin_out) {  // the base SPF of a what-if sweep: counts for seeded starts
+          uint16_t* trow_in = a.tin_out + out_row_of(a, sid) * V;
+          for (uint32_t v = tid; v < V; v += BLOCK) trow_in[v] = cnt[v];
+        }
       }
-      sync();
       n = __builtin_amdgcn_readfirstlane(*ac2);
       ++r;
+      if (GENERIC && a.prof_solve && tid == 0) a.prof_solve[10 * (size_t)sid + 5] = wall_clock64();
 
       // (3) Kahn rounds: a finished node pushes its set down its tight out-edges; the
       //     decrement that empties a successor's count makes it finished next round
@@ -343,6 +408,8 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
         cur = nxt;
         nxt = t;
       }
+      r_kahn = r;
+      if (GENERIC && a.prof_solve && tid == 0) a.prof_solve[10 * (size_t)sid + 6] = wall_clock64();
       if (GENERIC && a.seed_changed) {
         // what-if unit: the count of nodes whose distance or next-hop bytes differ from the
         // base rows, instead of the rows (no row round trip through HBM)
@@ -379,6 +446,11 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
       }
     }
   next_solve:
+    if (GENERIC && a.prof_solve && tid == 0) {
+      a.prof_solve[10 * (size_t)sid] = t_start;
+      a.prof_solve[10 * (size_t)sid + 7] = wall_clock64();
+      a.prof_solve[10 * (size_t)sid + 9] = (unsigned long long)(r_dist - r_start) | ((unsigned long long)(r_kahn - r_dist) << 32);
+    }
     if constexpr (BLOCK == kWave) {
       uint32_t nxt_sid = 0;
       if (tid == 0) nxt_sid = gridDim.x + atomicAdd(&ctr[0], 1u);
@@ -447,7 +519,9 @@ hipError_t launch_rounds(const DevGraph& g, const SolveArgs& a, bool dist64, int
   const uint32_t lds = rounds_lds_bytes(g.V, g.L, has_ign, nh_mode, dist64);
   if (!lds || !a.work) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
-  const uint32_t block = rounds_block(a.n, lds, num_cus);
+  uint32_t block = rounds_block(a.n, lds, num_cus);
+  if (a.n_dev && !std::getenv("OPENR_SPF_ROUNDS_BLOCK") && (a.n_block == 64u || a.n_block == 128u || a.n_block == 256u))
+    block = a.n_block;
   if (info) {
     info->lds_bytes = lds;
     info->grid = blocks_for(a.n, lds, num_cus, block);
