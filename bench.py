@@ -827,7 +827,8 @@ def decision_main(args):
             out["cpu_baseline"] = {"value": 1e3 / cpu["ms_per_update"], "unit": "updates/s", "cores": 1,
                                    "kind": "port", "sample": cpu["sample"], "ms_per_update": cpu["ms_per_update"],
                                    "spf_runs_per_update": cpu["spf_runs_per_update"], "ms_per_spf": cpu["ms_per_spf"],
-                                   "ms_route_construction": cpu["ms_route_construction"]}
+                                   "ms_route_construction": cpu["ms_route_construction"],
+                                   "ms_update_adjdb": cpu.get("ms_update_adjdb")}
         print(json.dumps(out), flush=True)
 
 

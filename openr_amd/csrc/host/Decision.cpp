@@ -244,7 +244,11 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   for (auto const& [_, ls] : als) nodeExist |= ls.hasNode(myNodeName);
   if (!nodeExist) return std::nullopt;
   counters_.route_build_runs++;
-  prefetch(myNodeName, als);
+  // the SPFs this build reads (prefix routes, node-label routes) in one batch; a build with
+  // neither reads none, as the reference's (Decision.cpp:589-680), so nothing is solved
+  bool readsSpf = !prefixState.prefixes().empty();
+  for (auto const& [_, ls] : als) readsSpf |= ls.labeledNodeCount() != 0;
+  if (readsSpf) prefetch(myNodeName, als);
   views_.clear();
   viewsOf_ = myNodeName;
   fast_ = FastCtx{};
@@ -311,7 +315,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
     else cand[it->second] = std::make_pair(node, std::move(entry));
   };
   for (auto const& [area, ls] : als) {
-    labelToNode.reserve(labelToNode.size() + ls.getAdjacencyDatabases().size());
+    if (!ls.labeledNodeCount()) continue;  // every label is 0 (non-SR mode): nothing to visit
+    labelToNode.reserve(labelToNode.size() + ls.labeledNodeCount());
     for (auto const& [_, adjDb] : ls.getAdjacencyDatabases()) {
       const int32_t topLabel = adjDb.nodeLabel;
       if (topLabel == 0) continue;  // non-SR mode

@@ -441,6 +441,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
   thrift::AdjacencyDatabase& stored = adjacencyDatabases_[nodeName];
   thrift::AdjacencyDatabase prior(std::move(stored));
   stored = std::move(db);
+  labeledNodes_ += (stored.nodeLabel != 0 ? 1 : 0) - (prior.nodeLabel != 0 ? 1 : 0);
   const thrift::AdjacencyDatabase& newDb = stored;
   indexAdjacencies(nodeName);
 
@@ -511,6 +512,7 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string&
   auto it = adjacencyDatabases_.find(nodeName);
   if (it != adjacencyDatabases_.end()) {
     removeNode(nodeName);
+    if (it->second.nodeLabel != 0) --labeledNodes_;
     adjacencyDatabases_.erase(it);
     ifIndex_.erase(nodeName);
     clearMemos();

@@ -336,6 +336,9 @@ class LinkState {
   bool hasHolds() const;
   size_t numLinks() const { return allLinks_.size(); }
   size_t numNodes() const { return linkMap_.size(); }
+  // adjacency databases that carry a node label (new: lets a route build skip the
+  // node-label pass, and the SPFs it would read, when there are none)
+  size_t labeledNodeCount() const { return labeledNodes_; }
   std::unordered_map<std::string, thrift::AdjacencyDatabase> const& getAdjacencyDatabases() const {
     return adjacencyDatabases_;
   }
@@ -495,6 +498,7 @@ class LinkState {
   void throwIfFrozen(const char* what, const std::string& key) const;
   mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<LinkState::Path>>
       kthPathResults_;
+  size_t labeledNodes_ = 0;  // adjacency databases with nodeLabel != 0
   struct StagedKsp2 {
     std::vector<Path> k1, k2;
     double ms = 0;  // this pair's share of the launch (decision.spf_ms)

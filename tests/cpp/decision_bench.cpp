@@ -514,15 +514,18 @@ int main(int argc, char** argv) {
         msRoutes += msSince(c0);
       }
       msRoutes /= o.cpuIters;
-      // Decision rebuilds on one thread: the runs are serial
-      const double msIter = runsPerIter * msPerSpf + msRoutes;
-      char buf[512];
+      // Decision rebuilds on one thread: the runs are serial. The adjacency update is the
+      // same host LinkState work on both sides (its mirror patch included), so it is priced
+      // at the measured update time.
+      const double msAdj = msUpdate / K;
+      const double msIter = msAdj + runsPerIter * msPerSpf + msRoutes;
+      char buf[640];
       std::snprintf(buf, sizeof(buf),
-                    "{\"ms_per_update\": %.3f, \"spf_runs_per_update\": %.1f, \"ms_per_spf\": %.3f, "
+                    "{\"ms_per_update\": %.3f, \"ms_update_adjdb\": %.3f, \"spf_runs_per_update\": %.1f, \"ms_per_spf\": %.3f, "
                     "\"ms_route_construction\": %.3f, \"cores\": 1, \"timing_threads\": %u, \"kind\": \"port\", \"sample\": \"%zu faithful "
                     "runSpf (oracle/spf_faithful.cpp) x %u, priced per run; route construction timed on the memoised "
-                    "build\"}",
-                    msIter, runsPerIter, msPerSpf, msRoutes, o.cpuThreads, srcs.size(), o.cpuIters);
+                    "build; adjacency update as measured\"}",
+                    msIter, msAdj, runsPerIter, msPerSpf, msRoutes, o.cpuThreads, srcs.size(), o.cpuIters);
       cpu = buf;
     }
     const auto& m = ls.csrMirror();
