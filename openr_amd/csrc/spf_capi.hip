@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -666,6 +667,31 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
                          nres, (t1 - t0) / 100.0, tot / nres, ph[0] / nres, ph[1] / nres, ph[2] / nres, ph[3] / nres,
                          ph[4] / nres, ph[5] / nres, ph[6] / nres, na / nres, rd / nres, rk / nres,
                          tot / ((t1 - t0) / 100.0));
+            // duration spread, its correlation with |A|, and the solves running over the span
+            std::vector<double> dur(nres), asz(nres);
+            for (uint32_t k = 0; k < nres; ++k) {
+              dur[k] = (double)(h[10 * (size_t)k + 7] - h[10 * (size_t)k]) / 100.0;
+              asz[k] = (double)h[10 * (size_t)k + 8];
+            }
+            std::vector<double> srt = dur;
+            std::sort(srt.begin(), srt.end());
+            const double md = tot / nres, ma = na / nres;
+            double sxy = 0, sxx = 0, syy = 0;
+            for (uint32_t k = 0; k < nres; ++k) {
+              sxy += (dur[k] - md) * (asz[k] - ma);
+              sxx += (dur[k] - md) * (dur[k] - md);
+              syy += (asz[k] - ma) * (asz[k] - ma);
+            }
+            std::fprintf(stderr, "  duration p10 %.1f p50 %.1f p90 %.1f max %.1f us; corr(duration, |A|) %.2f; running at",
+                         srt[nres / 10], srt[nres / 2], srt[nres * 9 / 10], srt.back(),
+                         sxx > 0 && syy > 0 ? sxy / std::sqrt(sxx * syy) : 0.0);
+            for (int q : {10, 25, 50, 75, 90, 95}) {
+              const unsigned long long tq = t0 + (t1 - t0) * q / 100;
+              uint32_t live = 0;
+              for (uint32_t k = 0; k < nres; ++k) live += (h[10 * (size_t)k] <= tq && h[10 * (size_t)k + 7] > tq) ? 1u : 0u;
+              std::fprintf(stderr, " %d%%:%u", q, live);
+            }
+            std::fprintf(stderr, "\n");
           }
         }
       }

@@ -13,5 +13,5 @@ for i in 1 2; do
 done
 if [ "${PROF:-0}" = 1 ]; then
   OPENR_SPF_PROF=1 timeout -k 10 200 python3 -u bench.py --workload whatif --no-cpu-baseline --no-ucmp --steps 3 --warmup 1 > gpurun_out/wprof.log 2>&1 || { tail -5 gpurun_out/wprof.log; exit 1; }
-  grep "whatif resolve" gpurun_out/wprof.log | tail -1
+  grep -A1 "whatif resolve" gpurun_out/wprof.log | tail -2
 fi
