@@ -367,6 +367,27 @@ TEST_CPU(LinkStateTest_MirrorRebuiltOnlyOnTopologyChange) {
   EXPECT_EQ(3u, (unsigned)m2.names.size());
 }
 
+// labeledNodeCount() follows every add, relabel, unlabel and delete (the route build skips
+// its node-label pass, and its SPF prefetch when no prefix needs one, on a count of 0)
+TEST_CPU(LinkStateTest_LabeledNodeCount) {
+  LinkState ls(kArea);
+  EXPECT_EQ(0u, (unsigned)ls.labeledNodeCount());
+  ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 0), 0, 0);
+  EXPECT_EQ(0u, (unsigned)ls.labeledNodeCount());
+  ls.updateAdjacencyDatabase(createAdjDb("b", {createAdjacency("a", "b/a", "a/b", 4)}, 7), 0, 0);
+  EXPECT_EQ(1u, (unsigned)ls.labeledNodeCount());
+  ls.updateAdjacencyDatabase(createAdjDb("b", {createAdjacency("a", "b/a", "a/b", 4)}, 8), 0, 0);  // relabel
+  EXPECT_EQ(1u, (unsigned)ls.labeledNodeCount());
+  ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 5), 0, 0);  // label a
+  EXPECT_EQ(2u, (unsigned)ls.labeledNodeCount());
+  ls.updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 0), 0, 0);  // unlabel a
+  EXPECT_EQ(1u, (unsigned)ls.labeledNodeCount());
+  ls.deleteAdjacencyDatabase("b");
+  EXPECT_EQ(0u, (unsigned)ls.labeledNodeCount());
+  ls.deleteAdjacencyDatabase("b");  // unknown: no change
+  EXPECT_EQ(0u, (unsigned)ls.labeledNodeCount());
+}
+
 // ParallelAdjRingTopologyFixture adjacencies (DecisionTest.cpp:3146-3203)
 static LinkState parallelRing() {
   LinkState ls(kArea);
