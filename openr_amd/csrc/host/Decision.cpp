@@ -249,9 +249,10 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   bool readsSpf = !prefixState.prefixes().empty();
   for (auto const& [_, ls] : als) readsSpf |= ls.labeledNodeCount() != 0;
   if (readsSpf) prefetch(myNodeName, als);
-  views_.clear();
+  // the views / fast-path context live for this build only (released again below): a
+  // LinkState update between two builds moves or frees the rows they point at
+  resetViews();
   viewsOf_ = myNodeName;
-  fast_ = FastCtx{};
 
   // KSP2 prefixes: every destination's first and second paths from here in one device
   // launch per area (LinkState::prefetchKthPaths stages them; selectBestPathsKsp2's
@@ -385,7 +386,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   // static routes (:719-724)
   for (auto const& [topLabel, nhs] : staticMplsRoutes_)
     routeDb.addMplsRoute(RibMplsEntry{topLabel, NextHopSet(nhs.begin(), nhs.end())});
+  resetViews();
   return routeDb;
+}
+
+void SpfSolver::resetViews() const {
+  views_.clear();
+  viewsOf_.clear();
+  fast_ = FastCtx{};
+  ksp2Protos_ = Ksp2Protos{};
 }
 
 // Decision.cpp:401-566
@@ -411,6 +420,16 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefix(const std::string
     flushBestRoutes();
     bestRoutesCache_.erase(prefix);
   }
+  // a call outside buildRouteDb (Decision::rebuildRoutes on an incremental prefix update,
+  // Decision.cpp:1897-1904) takes fresh views of the current memo and drops them on return:
+  // views cached by an earlier build may point at rows a LinkState update has since freed
+  struct ViewScope {
+    const SpfSolver* s;
+    ~ViewScope() {
+      if (s) s->resetViews();
+    }
+  } scope{inOrder ? nullptr : this};
+  if (!inOrder) resetViews();
 
   // entries of reachable nodes only (the reference filters a copy; the entries are used
   // in place when every advertiser is reachable)
@@ -610,6 +629,20 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsKsp2(std::string const&
     counters_.incompatible_forwarding_type++;
     return std::nullopt;
   }
+  // token form (round 5): one area whose LinkState staged every pair this prefix reads
+  // (prefetchKthPaths) builds the next hops on its mirror's ids
+  if (als.size() == 1) {
+    auto const& [area, ls] = *als.begin();
+    std::vector<const std::string*> need;
+    for (auto const& [node, bestArea] : best.allNodeAreas)
+      if (!(node == myNodeName && bestArea == area)) need.push_back(&node);
+    if (!need.empty() && ls.kthPathTokensStaged(myNodeName, need)) {
+      bool any = false;
+      NextHopSet nh = ksp2NextHopsFromTokens(myNodeName, prefix, best, prefixEntries, area, ls, &any);
+      if (!any) return std::nullopt;
+      return addBestPaths(myNodeName, prefix, best, prefixEntries, prefixState, isBgp, std::move(nh));
+    }
+  }
   NextHopSet nextHops;
   std::vector<LinkState::Path> paths;
   for (auto const& [area, ls] : als) {
@@ -657,6 +690,94 @@ std::optional<RibUnicastEntry> SpfSolver::selectBestPathsKsp2(std::string const&
     }
   }
   return addBestPaths(myNodeName, prefix, best, prefixEntries, prefixState, isBgp, std::move(nextHops));
+}
+
+// selectBestPathsKsp2 (Decision.cpp:907-1030) on token rows: a path is [len, e_1 .. e_len]
+// of mirror edge ids from me. pathAInPathB compares link ids (Link equality is identity of
+// the (node, interface) pairs, one Link object per pair in a LinkState); the cost sums the
+// edges' metrics from their tails (getMetricFromNode); the label stack is the node labels
+// of the hops after the first, last hop first, under the advertiser's prepend label.
+NextHopSet SpfSolver::ksp2NextHopsFromTokens(const std::string& me, thrift::IpPrefix const& prefix,
+                                             BestRouteSelectionResult const& best, PrefixEntries const& prefixEntries,
+                                             const std::string& area, const LinkState& ls, bool* any) {
+  const LinkState::CsrMirror& m = ls.csrMirror();
+  std::vector<const uint32_t*> paths;
+  auto addAll = [&](const uint32_t* row) {
+    const uint32_t* p = row + 1;
+    for (uint32_t i = 0; i < row[0]; ++i, p += 1 + p[0]) paths.push_back(p);
+  };
+  for (auto const& [node, bestArea] : best.allNodeAreas) {
+    if (node == me && bestArea == area) continue;
+    addAll(ls.kthPathTokens(me, node, 1));
+  }
+  const size_t firstPathsSize = paths.size();
+  auto inPath = [&](const uint32_t* a, const uint32_t* b) {  // LinkState::pathAInPathB on link ids
+    const uint32_t la = a[0], lb = b[0];
+    if (la > lb) return false;
+    for (uint32_t start = 0; start + la <= lb; ++start) {
+      uint32_t k = 0;
+      while (k < la && m.linkId[a[1 + k]] == m.linkId[b[1 + start + k]]) ++k;
+      if (k == la) return true;
+    }
+    return false;
+  };
+  for (auto const& [node, bestArea] : best.allNodeAreas) {
+    if (area != bestArea) continue;
+    const uint32_t* row = ls.kthPathTokens(me, node, 2);
+    const uint32_t* p = row + 1;
+    for (uint32_t i = 0; i < row[0]; ++i, p += 1 + p[0]) {
+      bool add = true;
+      for (size_t j = 0; j < firstPathsSize && add; ++j) add = !inPath(paths[j], p);
+      if (add) paths.push_back(p);
+    }
+  }
+  *any = !paths.empty();
+  NextHopSet nextHops;
+  if (paths.empty()) return nextHops;
+  auto& pr = ksp2Protos_;
+  const uint32_t meId = m.id.at(me);
+  if (pr.ls != &ls || pr.generation != m.generation || pr.me != meId) {
+    pr = Ksp2Protos{};
+    pr.ls = &ls;
+    pr.generation = m.generation;
+    pr.me = meId;
+    pr.row0 = m.rowPtr[meId];
+    const size_t deg = m.rowPtr[meId + 1] - m.rowPtr[meId];
+    pr.p4.resize(deg);
+    pr.p6.resize(deg);
+    pr.ready.assign(deg, 0);
+  }
+  const auto& labelOf = ls.nodeLabelsById();
+  const bool v4 = prefix.isV4();
+  std::vector<int32_t> labels;
+  for (const uint32_t* p : paths) {
+    const uint32_t len = p[0];
+    const uint32_t* e = p + 1;
+    Metric cost = 0;
+    for (uint32_t j = 0; j < len; ++j) {
+      cost += m.metric[e[j]];
+      if (labelOf[m.col[e[j]]] == LinkState::kNoNodeLabel)  // getAdjacencyDatabases().at(node)
+        throw std::out_of_range("selectBestPathsKsp2: no adjacency database for " + m.names[m.col[e[j]]]);
+    }
+    const std::string& dst = m.names[m.col[e[len - 1]]];
+    auto const& prefixEntry = prefixEntries.at({dst, area});
+    labels.clear();
+    if (prefixEntry.prependLabel) labels.push_back(*prefixEntry.prependLabel);
+    for (uint32_t j = len; j-- > 1;) labels.push_back((int32_t)labelOf[m.col[e[j]]]);  // first hop's label: PHP
+    const uint32_t slot = e[0] - pr.row0;
+    if (!pr.ready[slot]) {
+      auto const& link = m.links[m.linkId[e[0]]];
+      const std::string& nbr = link->getOtherNodeName(me);
+      pr.p6[slot] = createNextHop(link->getNhV6FromNode(me), link->getIfaceFromNode(me), 0, std::nullopt, link->getArea(), nbr);
+      pr.p4[slot] = createNextHop(link->getNhV4FromNode(me), link->getIfaceFromNode(me), 0, std::nullopt, link->getArea(), nbr);
+      pr.ready[slot] = 1;
+    }
+    thrift::NextHopThrift nh = v4 ? pr.p4[slot] : pr.p6[slot];
+    nh.metric = static_cast<int32_t>(cost);
+    if (!labels.empty()) nh.mplsAction = createMplsAction(thrift::MplsActionCode::PUSH, std::nullopt, labels);
+    nextHops.emplace(std::move(nh));
+  }
+  return nextHops;
 }
 
 // Decision.cpp:1032-1092
@@ -895,7 +1016,11 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
   }
   // getNextHopsWithMetric(me, {dst}, false): shortest next hops, then RFC 5286 alternates
   const int nn = fastNextHopNodes(me, dst, d);
-  if (nn < 0) return false;
+  if (nn < 0) {  // the general path serves this prefix: undo what it will count again
+    counters_.get_route_for_prefix--;
+    bestLazy_.pop_back();
+    return false;
+  }
   if (nn == 0) {
     counters_.no_route_to_prefix++;
     return true;

@@ -302,6 +302,7 @@ class SpfSolver {
   };
   mutable std::string viewsOf_;
   mutable std::vector<AreaViews> views_;
+  void resetViews() const;  // drop views_ and fast_ (they point into the LinkState memo)
 
   // SP_ECMP / IP fast path of buildRouteDb (one area, dense memo rows from one mirror): the
   // route of a prefix with a single advertiser computed on node ids — the same
@@ -330,7 +331,7 @@ class SpfSolver {
     std::vector<Metric> val;       // per next-hop bit: nextHopNodes value
     std::vector<uint8_t> has;
   };
-  FastCtx fast_;
+  mutable FastCtx fast_;
   bool fastSetup(std::unordered_map<std::string, LinkState> const& areaLinkStates, const std::string& me);
   bool fastEnabled_ = true;
   int fastNextHopNodes(const std::string& me, uint32_t dst, Metric d);
@@ -342,6 +343,19 @@ class SpfSolver {
   // arrive in key order, so the route is built in place at the end)
   bool fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries, uint32_t dstId,
                  std::map<thrift::IpPrefix, RibUnicastEntry>& routes);
+  // selectBestPathsKsp2 on the staged token rows of one area (LinkState::kthPathTokens):
+  // the same paths, pathAInPathB filter, label stacks, costs and next hops, on ids
+  NextHopSet ksp2NextHopsFromTokens(const std::string& me, thrift::IpPrefix const& prefix,
+                                    BestRouteSelectionResult const& best, PrefixEntries const& prefixEntries,
+                                    const std::string& area, const LinkState& ls, bool* any);
+  struct Ksp2Protos {  // per build: my links' next-hop fields by position in my mirror row
+    const LinkState* ls = nullptr;
+    uint64_t generation = 0;
+    uint32_t me = UINT32_MAX, row0 = 0;
+    std::vector<thrift::NextHopThrift> p4, p6;
+    std::vector<uint8_t> ready;
+  };
+  mutable Ksp2Protos ksp2Protos_;
   AreaViews& views(const LinkState& ls, const std::string& me) const;
   AreaViews& lfaViews(const LinkState& ls, const std::string& me) const;
 

@@ -442,6 +442,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(thrift::AdjacencyD
   thrift::AdjacencyDatabase prior(std::move(stored));
   stored = std::move(db);
   labeledNodes_ += (stored.nodeLabel != 0 ? 1 : 0) - (prior.nodeLabel != 0 ? 1 : 0);
+  ++adjDbVersion_;
   const thrift::AdjacencyDatabase& newDb = stored;
   indexAdjacencies(nodeName);
 
@@ -513,6 +514,7 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string&
   if (it != adjacencyDatabases_.end()) {
     removeNode(nodeName);
     if (it->second.nodeLabel != 0) --labeledNodes_;
+    ++adjDbVersion_;
     adjacencyDatabases_.erase(it);
     ifIndex_.erase(nodeName);
     clearMemos();
@@ -551,6 +553,13 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(const std::string& sr
   auto it = kthPathResults_.find(key);
   if (it != kthPathResults_.end()) return it->second;
   throwIfFrozen("getKthPaths", src + "->" + dest);
+  if (k <= 2) {  // device-traced token rows (prefetchKthPaths): counted like the calls below
+    if (const uint32_t* row = kthPathTokens(src, dest, k)) {
+      std::vector<Path> paths;
+      decodeTokens(row, paths);
+      return kthPathResults_.emplace(key, std::move(paths)).first->second;
+    }
+  }
   if (k <= 2) {  // prefetched: replay the memo and counter effects of the call sequence below
     auto st = kthStaged_.find(std::make_pair(src, dest));
     if (st != kthStaged_.end()) {
@@ -851,18 +860,48 @@ void LinkState::retireDenseRows() {
   // rows are indexed by the ids of mirror_ (they were solved on it; a pending patch would
   // have cleared the memo first, so no entry points at a stale row)
   if (mirrorDirty_) return;
-  std::shared_ptr<RowSnapshot> snap;
+  // live entries per row set; a set most of whose rows are still referenced moves into the
+  // snapshot whole, a sparsely referenced one keeps only those rows (the rest
+  // would stay resident beside the fresh rows until every entry is cleared)
+  std::vector<MemoEntry*> live[2];
   for (auto& kv : spfResults_) {
     MemoEntry& e = kv.second;
     if (e.row == UINT32_MAX || e.snap) continue;
-    if (!snap) {
-      snap = std::make_shared<RowSnapshot>();
-      snap->mirror = std::move(mirror_);
-      snap->rows[0] = std::move(dense_[0]);
-      snap->rows[1] = std::move(dense_[1]);
-    }
-    e.snap = snap;
+    live[kv.first.second ? 1 : 0].push_back(&e);
   }
+  if (live[0].empty() && live[1].empty()) return;
+  auto snap = std::make_shared<RowSnapshot>();
+  snap->mirror = std::move(mirror_);
+  for (int um = 0; um < 2; ++um) {
+    DenseRows& d = dense_[um];
+    if (live[um].empty()) continue;
+    if (2 * live[um].size() >= d.src.size()) {
+      ustats_.rowsRetired += d.src.size();
+      snap->rows[um] = std::move(d);
+    } else {
+      ustats_.rowsRetired += live[um].size();
+      DenseRows& o = snap->rows[um];
+      o.nb = d.nb;
+      o.V = d.V;
+      o.wide = d.wide;
+      o.stale = d.stale;
+      o.resizeRows(live[um].size());
+      const size_t V = d.V, nbv = (size_t)d.V * d.nb;
+      for (uint32_t k = 0; k < live[um].size(); ++k) {
+        MemoEntry& e = *live[um][k];
+        const size_t r = e.row;
+        if (d.wide) std::copy_n(d.dist64.begin() + r * V, V, o.dist64.begin() + k * V);
+        else std::copy_n(d.dist32.begin() + r * V, V, o.dist32.begin() + k * V);
+        std::copy_n(d.nh.begin() + r * nbv, nbv, o.nh.begin() + k * nbv);
+        o.src.push_back(d.src[r]);
+        o.slot.emplace(d.src[r], k);
+        o.nbrs.push_back(d.nbrs[r]);
+        e.row = k;
+      }
+    }
+  }
+  for (auto& l : live)
+    for (MemoEntry* e : l) e->snap = snap;
 }
 
 // ---------------------------------------------------------------------------
@@ -1070,11 +1109,14 @@ void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::
   if (!m.metricsPositive) return;  // the device tracer needs metrics in [1, 2^31-1]
   auto s = m.id.find(src);
   if (s == m.id.end()) return;
+  const uint32_t V = (uint32_t)m.names.size();
+  KspRows* rows = nullptr;
+  if (auto it = kspRows_.find(src); it != kspRows_.end()) rows = &it->second;
   std::vector<uint32_t> dst;
   for (auto const& d : dests) {
     auto it = m.id.find(d);
     if (it == m.id.end() || d == src || kthPathResults_.count(std::make_tuple(src, d, size_t(2))) ||
-        kthStaged_.count(std::make_pair(src, d)))
+        kthStaged_.count(std::make_pair(src, d)) || (rows && rows->off[it->second] != UINT32_MAX))
       continue;
     dst.push_back(it->second);
   }
@@ -1084,30 +1126,138 @@ void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::
   const auto t0 = std::chrono::steady_clock::now();
   ensureEngineGraph();
   const uint32_t n = (uint32_t)dst.size(), cap = 512;  // tokens per pair: [n_paths, (len, edges..)..]
-  std::vector<uint32_t> srcs(n, s->second), tok1((size_t)n * cap), tok2((size_t)n * cap);
+  // the engine writes every row it serves (unserved rows keep the 0xFFFFFFFF marker):
+  // no zero fill of the n x 512 token buffers
+  std::unique_ptr<uint32_t[]> tok1(new uint32_t[(size_t)n * cap]), tok2(new uint32_t[(size_t)n * cap]);
+  const std::vector<uint32_t> srcs(n, s->second);
   for (uint32_t i = 0; i < n; ++i) tok1[(size_t)i * cap] = tok2[(size_t)i * cap] = 0xFFFFFFFFu;
-  const int rc = openr_spf_ksp2(engine_->ctx(), srcs.data(), dst.data(), n, cap, tok1.data(), tok2.data());
+  const int rc = openr_spf_ksp2(engine_->ctx(), srcs.data(), dst.data(), n, cap, tok1.get(), tok2.get());
   if (rc == OPENR_SPF_ENOTSUP) return;
   if (rc != OPENR_SPF_E2BIG) SpfEngineHandle::check(rc, "openr_spf_ksp2");  // E2BIG: overflowed rows stay unmarked
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / n;
-  auto decode = [&](const uint32_t* row, std::vector<Path>& out) {
-    if (row[0] == 0xFFFFFFFFu) return false;
-    size_t at = 1;
-    for (uint32_t p = 0; p < row[0]; ++p) {
-      const uint32_t len = row[at++];
-      Path path;
-      path.reserve(len);
-      for (uint32_t j = 0; j < len; ++j) path.push_back(m.links[m.linkId[row[at++]]]);
-      out.push_back(std::move(path));
-    }
-    return true;
-  };
-  for (uint32_t i = 0; i < n; ++i) {
-    StagedKsp2 st;
-    st.ms = ms;
-    if (!decode(&tok1[(size_t)i * cap], st.k1) || !decode(&tok2[(size_t)i * cap], st.k2)) continue;
-    kthStaged_.emplace(std::make_pair(src, m.names[dst[i]]), std::move(st));
+  // staged as compact token rows on this mirror's edge ids (no Path / shared_ptr<Link>
+  // per hop): k = 1 row then k = 2 row per destination
+  if (!rows) {
+    rows = &kspRows_[src];
+    rows->src = s->second;
+    rows->off.assign(V, UINT32_MAX);
+    rows->memo.assign(V, 0);
   }
+  rows->ms = ms;
+  size_t need = rows->tok.size();
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t* r1 = &tok1[(size_t)i * cap];
+    const uint32_t* r2 = &tok2[(size_t)i * cap];
+    if (r1[0] != 0xFFFFFFFFu && r2[0] != 0xFFFFFFFFu) need += tokenRowLength(r1) + tokenRowLength(r2);
+  }
+  rows->tok.reserve(need);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t* r1 = &tok1[(size_t)i * cap];
+    const uint32_t* r2 = &tok2[(size_t)i * cap];
+    if (r1[0] == 0xFFFFFFFFu || r2[0] == 0xFFFFFFFFu) continue;  // overflowed: getKthPaths' own path
+    rows->off[dst[i]] = (uint32_t)rows->tok.size();
+    rows->tok.insert(rows->tok.end(), r1, r1 + tokenRowLength(r1));
+    rows->tok.insert(rows->tok.end(), r2, r2 + tokenRowLength(r2));
+    // a k = 1 entry the memo already holds is read as a memo hit
+    if (kthPathResults_.count(std::make_tuple(src, m.names[dst[i]], size_t(1)))) rows->memo[dst[i]] |= 1u;
+  }
+}
+
+size_t LinkState::tokenRowLength(const uint32_t* row) {
+  size_t at = 1;
+  for (uint32_t p = 0; p < row[0]; ++p) at += 1 + row[at];
+  return at;
+}
+
+void LinkState::decodeTokens(const uint32_t* row, std::vector<Path>& out) const {
+  size_t at = 1;
+  for (uint32_t p = 0; p < row[0]; ++p) {
+    const uint32_t len = row[at++];
+    Path path;
+    path.reserve(len);
+    for (uint32_t j = 0; j < len; ++j) path.push_back(mirror_.links[mirror_.linkId[row[at++]]]);
+    out.push_back(std::move(path));
+  }
+}
+
+const uint32_t* LinkState::kthPathTokens(const std::string& src, const std::string& dest, size_t k) const {
+  if (k < 1 || k > 2 || kspRows_.empty() || mirrorDirty_) return nullptr;
+  auto it = kspRows_.find(src);
+  if (it == kspRows_.end()) return nullptr;
+  auto d = mirror_.id.find(dest);
+  if (d == mirror_.id.end()) return nullptr;
+  KspRows& r = it->second;
+  const uint32_t o = r.off[d->second];
+  if (o == UINT32_MAX) return nullptr;
+  const uint32_t* row1 = r.tok.data() + o;
+  uint8_t& memo = r.memo[d->second];
+  // getKthPaths(src, dest, 1): the first path computation reads getSpfResult(src, true)
+  // (counted on its first read; the later ones are memo hits)
+  auto k1 = [&]() {
+    if (memo & 1u) return;
+    throwIfFrozen("getKthPaths", src + "->" + dest);
+    if (!r.spfRead) {
+      getSpfResult(src, true);
+      r.spfRead = true;  // the memo entry stays until clearMemos, which drops these rows too
+    }
+    memo |= 1u;
+  };
+  k1();
+  if (k == 1) return row1;
+  const uint32_t* row2 = row1 + tokenRowLength(row1);
+  if (!(memo & 2u)) {  // getKthPaths(src, dest, 2): runSpf(src, true, k = 1 links) when there are any
+    throwIfFrozen("getKthPaths", src + "->" + dest);
+    if (row1[0] > 0) SpfCounters::get().addSpfRun(r.ms);
+    memo |= 2u;
+  }
+  return row2;
+}
+
+bool LinkState::kthPathTokensStaged(const std::string& src, const std::vector<const std::string*>& dests) const {
+  if (kspRows_.empty() || mirrorDirty_) return false;
+  auto it = kspRows_.find(src);
+  if (it == kspRows_.end()) return false;
+  for (const std::string* d : dests) {
+    auto id = mirror_.id.find(*d);
+    if (id == mirror_.id.end() || it->second.off[id->second] == UINT32_MAX) return false;
+  }
+  return true;
+}
+
+void LinkState::convertKspRows() const {
+  if (kspRows_.empty()) return;
+  if (!mirrorDirty_) {
+    for (auto& [src, r] : kspRows_) {
+      for (uint32_t d = 0; d < r.off.size(); ++d) {
+        if (r.off[d] == UINT32_MAX) continue;
+        const uint32_t* row1 = r.tok.data() + r.off[d];
+        const uint32_t* row2 = row1 + tokenRowLength(row1);
+        const std::string& dn = mirror_.names[d];
+        StagedKsp2 st;
+        st.ms = r.ms;
+        decodeTokens(row1, st.k1);
+        decodeTokens(row2, st.k2);
+        if (r.memo[d] & 1u) kthPathResults_.emplace(std::make_tuple(src, dn, size_t(1)), st.k1);
+        if (r.memo[d] & 2u) kthPathResults_.emplace(std::make_tuple(src, dn, size_t(2)), std::move(st.k2));
+        else kthStaged_.emplace(std::make_pair(src, dn), std::move(st));
+      }
+    }
+  }
+  kspRows_.clear();
+}
+
+const std::vector<int64_t>& LinkState::nodeLabelsById() const {
+  const CsrMirror& m = csrMirror();
+  if (nodeLabelsGen_ != mirrorGeneration_ || nodeLabelsAdjVer_ != adjDbVersion_) {
+    nodeLabelsById_.assign(m.names.size(), kNoNodeLabel);
+    for (uint32_t i = 0; i < m.names.size(); ++i) {
+      auto it = adjacencyDatabases_.find(m.names[i]);
+      if (it != adjacencyDatabases_.end()) nodeLabelsById_[i] = it->second.nodeLabel;
+    }
+    nodeLabelsGen_ = mirrorGeneration_;
+    nodeLabelsAdjVer_ = adjDbVersion_;
+  }
+  return nodeLabelsById_;
 }
 
 std::vector<LinkState::SpfResult> LinkState::runSpfBatch(const std::vector<std::string>& srcs, bool useLinkMetric,

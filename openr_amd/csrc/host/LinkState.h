@@ -301,6 +301,19 @@ class LinkState {
   // getKthPaths' own path.
   void prefetchKthPaths(const std::string& src, const std::vector<std::string>& dests) const;
 
+  // Route-build form of getKthPaths (round 5): the k-th paths of (src, dest) as a token row
+  // of the current mirror's edge ids, [n_paths, (len, e_1 .. e_len) ..] with e_1 leaving
+  // src, for a pair prefetchKthPaths staged. It has exactly the memo and counter effects of
+  // getKthPaths(src, dest, k) (k = 1, 2) without building Path vectors of shared_ptr<Link>;
+  // a later getKthPaths of the pair materialises the paths as a memo hit. Null when the
+  // pair is not staged (the caller takes getKthPaths).
+  const uint32_t* kthPathTokens(const std::string& src, const std::string& dest, size_t k) const;
+  // true when kthPathTokens(src, d, 1 and 2) serves every d in `dests` (a pure test)
+  bool kthPathTokensStaged(const std::string& src, const std::vector<const std::string*>& dests) const;
+  // nodeLabel of each mirror node id (its adjacency database's; kNoNodeLabel without one)
+  static constexpr int64_t kNoNodeLabel = INT64_MIN;
+  const std::vector<int64_t>& nodeLabelsById() const;
+
   class LinkStateChange {
    public:
     LinkStateChange() = default;
@@ -414,6 +427,7 @@ class LinkState {
     uint64_t refreshes = 0;     // openr_spf_refresh calls
     uint64_t rowsRefreshed = 0; // rows those refreshes re-solved
     uint64_t rowsKept = 0;      // dense rows carried across a change (not re-solved)
+    uint64_t rowsRetired = 0;   // dense rows a mirror rebuild kept in snapshots for live memo entries
   };
   const UpdateStats& updateStats() const { return ustats_; }
   size_t denseRows(bool useLinkMetric = true) const { return dense_[useLinkMetric ? 1 : 0].src.size(); }
@@ -504,10 +518,30 @@ class LinkState {
     double ms = 0;  // this pair's share of the launch (decision.spf_ms)
   };
   mutable std::unordered_map<std::pair<std::string, std::string>, StagedKsp2> kthStaged_;
+  // Device-traced k = 1 / 2 paths of one source as edge-id token rows of mirror_ (round 5):
+  // what prefetchKthPaths stages, per destination id. `memo` bit k-1: the (src, d, k) entry
+  // exists in the reference's kthPathResults_ (read, counted). A mirror rebuild converts the
+  // rows into kthStaged_ / kthPathResults_ first (their edge ids die with the mirror).
+  struct KspRows {
+    uint32_t src = UINT32_MAX;
+    double ms = 0;                  // per pair share of the launch (decision.spf_ms)
+    std::vector<uint32_t> off;      // per dst id: offset of its k = 1 row in tok (k = 2 row follows), or UINT32_MAX
+    std::vector<uint8_t> memo;
+    std::vector<uint32_t> tok;
+    bool spfRead = false;           // getSpfResult(src) read through this object (k = 1 counting)
+  };
+  mutable std::unordered_map<std::string, KspRows> kspRows_;
+  static size_t tokenRowLength(const uint32_t* row);
+  void decodeTokens(const uint32_t* row, std::vector<Path>& out) const;  // mirror_'s edge ids -> Links
+  void convertKspRows() const;  // kspRows_ -> kthStaged_ / kthPathResults_ (mirror_ still valid)
+  mutable std::vector<int64_t> nodeLabelsById_;
+  mutable uint64_t nodeLabelsGen_ = 0, nodeLabelsAdjVer_ = 0;
+  uint64_t adjDbVersion_ = 0;  // bumped by every adjacency database update / delete
   void clearMemos() const {
     spfResults_.clear();
     kthPathResults_.clear();
     kthStaged_.clear();
+    kspRows_.clear();
   }
   void ensureEngineGraph() const;
 
@@ -527,6 +561,7 @@ class LinkState {
   std::vector<std::shared_ptr<Link>> getOrderedLinkSet(const thrift::AdjacencyDatabase& adjDb) const;
   std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;
   void markMirrorDirty() {
+    convertKspRows();   // edge ids change with the rebuilt mirror
     retireDenseRows();  // node ids change with the rebuilt mirror
     mirrorDirty_ = true;
     dense_[0].clear();

@@ -1184,6 +1184,40 @@ TEST_GPU(RouteBuild_FastPath_MatchesGeneralPath) {
     }
 }
 
+// createRouteForPrefix outside buildRouteDb (Decision::rebuildRoutes on an
+// incremental prefix update, DecisionTest-style) after LinkState updates must read the
+// current SPF memo, not views a previous build cached: a new node with no up link (mirror
+// rebuild) and a metric change (memo cleared, rows patched) between the two calls.
+TEST_GPU(CreateRouteForPrefix_AfterLinkStateUpdate) {
+  Ring r(false, false);
+  auto& ls = r.als.at(kDefaultArea);
+  SpfSolver solver("1", false, false);
+  auto db = solver.buildRouteDb("1", r.als, r.ps);
+  EXPECT_TRUE(db.has_value());
+  EXPECT_EQ(db->unicastRoutes.at(addr4).nexthops, NextHopSet({nhFromAdj(adj12, false, 20), nhFromAdj(adj13, false, 20)}));
+  // a new node whose adjacency nobody reciprocates, then 1 -> 2 gets metric 30
+  EXPECT_FALSE(ls.updateAdjacencyDatabase(createAdjDb("5", {createAdjacency("1", "5/1", "1/5", "fe80::1", "192.168.0.1", 10, 0)}, 5))
+                   .topologyChanged);
+  const auto adj12m = createAdjacency("2", "1/2", "2/1", "fe80::2", "192.168.0.2", 30, 100002);
+  EXPECT_TRUE(ls.updateAdjacencyDatabase(createAdjDb("1", {adj12m, adj13}, 1)).topologyChanged);
+  const uint64_t calls0 = solver.counters().get_route_for_prefix;
+  auto route = solver.createRouteForPrefix("1", r.als, r.ps, addr4);
+  EXPECT_TRUE(route.has_value());
+  if (route) EXPECT_EQ(route->nexthops, NextHopSet({nhFromAdj(adj13, false, 20)}));
+  EXPECT_EQ(calls0 + 1, solver.counters().get_route_for_prefix);
+  auto r2 = solver.createRouteForPrefix("1", r.als, r.ps, addr2);  // 1 -> 2: via 3 and 4 (30) ties the direct link
+  SpfSolver fresh("1", false, false);
+  auto want = fresh.buildRouteDb("1", r.als, r.ps);
+  EXPECT_TRUE(r2.has_value() && want.has_value());
+  if (r2 && want) EXPECT_EQ(r2->nexthops, want->unicastRoutes.at(addr2).nexthops);
+  if (route && want) EXPECT_EQ(route->nexthops, want->unicastRoutes.at(addr4).nexthops);
+  // and a build after the calls still serves the same routes as a fresh solver
+  auto again = solver.buildRouteDb("1", r.als, r.ps);
+  EXPECT_TRUE(again.has_value() && want.has_value() && again->unicastRoutes.size() == want->unicastRoutes.size());
+  if (again && want)
+    for (auto const& [p, e] : want->unicastRoutes) EXPECT_EQ(again->unicastRoutes.at(p).nexthops, e.nexthops);
+}
+
 // KSP2 route DBs with the batched device prefetch (LinkState::prefetchKthPaths) against
 // the call-by-call getKthPaths path: same routes (SR-MPLS push labels, parallel links),
 // same decision.spf_runs, same memoised k-th paths afterwards.

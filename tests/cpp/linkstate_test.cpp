@@ -1004,6 +1004,47 @@ TEST_GPU(LinkState_MemoSurvivesNonTopologyRebuild) {
   }
 }
 
+// a mirror rebuild (a new node) keeps only the dense rows live memo entries
+// still reference. After an attribute change clears the memo, a build reads a few sources
+// again; the rebuild then retires those rows alone, not every row of the set.
+TEST_GPU(LinkState_RetireKeepsOnlyLiveRows) {
+  const int n = 7;
+  auto w = [](int i, int j, int ii, int jj) { return 1 + (i * 3 + j + ii + 2 * jj) % 4; };
+  LinkState ls(kArea);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) ls.updateAdjacencyDatabase(gridDb(n, i, j, w));
+  std::vector<std::string> all;
+  for (int v = 0; v < n * n; ++v) all.push_back(std::to_string(v));
+  ls.prefetchSpfResults(all);
+  EXPECT_EQ((size_t)(n * n), ls.denseRows(true));
+  // overload toggle: the memo is cleared, the rows stay (refreshed on the next read)
+  ls.updateAdjacencyDatabase(gridDb(n, 3, 3, w, true));
+  const std::vector<std::string> reread{"5", "30"};
+  for (auto const& s : reread) ls.getSpfResult(s);
+  const uint64_t retired0 = ls.updateStats().rowsRetired;
+  // "zz" advertises an adjacency nobody reciprocates: a new node, not a topology change
+  EXPECT_FALSE(ls.updateAdjacencyDatabase(createAdjDb("zz", {createAdjacency("0", "y/0", "0/y", 1)}, 900))
+                   .topologyChanged);
+  ls.csrMirror();  // rebuild
+  EXPECT_EQ(retired0 + reread.size(), ls.updateStats().rowsRetired);
+  SpfCounters::get().reset();
+  std::vector<uint32_t> ids;
+  for (auto const& s : reread) ids.push_back(ls.csrMirror().id.at(s));
+  EXPECT_TRUE(spfMatchesOracle(ls, ids, true));  // served from the retired rows
+  for (auto const& s : reread) {
+    auto const v = ls.getSpfView(s);
+    auto const& r = ls.getSpfResult(s);
+    bool ok = true;
+    for (auto const& d : ls.csrMirror().names) {
+      auto it = r.find(d);
+      ok &= v.reached(d) == (it != r.end());
+      if (it != r.end()) ok &= v.metric(d) == it->second.metric();
+    }
+    EXPECT_TRUE(ok);
+  }
+  EXPECT_EQ(0u, (unsigned)SpfCounters::get().spfRuns());  // memo hits
+}
+
 // SpfView (the route build's dense read path) serves what getSpfResult does.
 TEST_GPU(LinkState_SpfViewMatchesSpfResult) {
   const int n = 9;
