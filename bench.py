@@ -752,8 +752,14 @@ def main():
     ap.add_argument("--ksp-block", type=int, default=256,
                     help="ksp2: sources per device call within a step (token rows are reused)")
     ap.add_argument("--lfa", action="store_true", help="routes: SpfSolver computeLfaPaths")
-    ap.add_argument("--decision-cases", default="grid:10000:sp,grid:10000:ksp2,grid:1024:ksp2,fabric:5000:sp",
-                    help="decision: topology:size:algo list (BM_DecisionGrid / BM_DecisionFabric parameters)")
+    ap.add_argument("--decision-cases",
+                    default="grid:10:sp,grid:100:sp,grid:1000:sp,grid:10000:sp,grid:10:ksp2,grid:100:ksp2,grid:1000:ksp2,"
+                            "grid:10000:ksp2,fabric:344:sp,fabric:1000:sp,fabric:5000:sp,fabricp:5000:sp",
+                    help="decision: topology:size:algo list. The reference registers BM_DecisionGrid {10, 100, 1000, "
+                         "10000} x SP_ECMP and {10, 100, 1000} x KSP2_ED_ECMP and BM_DecisionFabric {344, 1000, 5000} "
+                         "(DecisionBenchmark.cpp:12-29; a grid of N is (int)sqrt(N) squared, "
+                         "RoutingBenchmarkUtils.cpp:527); grid:10000:ksp2 is added, and fabricp = the fabric with "
+                         "one prefix per node (the reference's createFabric advertises none)")
     ap.add_argument("--workload", default="all-sources",
                     choices=["all-sources", "whatif", "ksp2", "update", "adjdb", "routes", "decision"],
                     help="whatif: per-link-failure sweep, every (link, source) unit of the WAN topology "
@@ -793,10 +799,11 @@ def decision_main(args):
         raise SystemExit("build first: make (tests/cpp/build/decision_bench)")
     for case in args.decision_cases.split(","):
         topo, size, algo = case.split(":")
-        # KSP2 on large grids: the reference re-runs one SPF per destination per update
-        steps = args.steps if not (algo == "ksp2" and int(size) >= 10000) else max(2, min(args.steps, 5))
+        fabric_prefixes = topo == "fabricp"
+        topo = "fabric" if fabric_prefixes else topo
+        steps = args.steps
         cmd = [binary, "--topology", topo, "--size", size, "--algo", algo, "--iters", str(steps),
-               "--warmup", str(max(1, args.warmup)), "--check"]
+               "--warmup", str(max(1, args.warmup)), "--check"] + (["--fabric-prefixes"] if fabric_prefixes else [])
         if not args.no_cpu_baseline:
             cmd += ["--cpu-iters", "1", "--cpu-threads", "16"]
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=1200)
@@ -819,8 +826,9 @@ def decision_main(args):
             "dtype": "u64",
             "data": "synthetic (reference benchmark generators: createGrid / createFabric)",
             "config": {"workload": f"BM_Decision{'Grid' if topo == 'grid' else 'Fabric'}({size}, "
-                                   f"{line['algo']})", "topology": topo, "size": int(size), "nodes": line["nodes"],
-                       "my_node": line["my_node"], "lfa": True},
+                                   f"{line['algo']})" + (", one prefix per node" if fabric_prefixes else ""),
+                       "topology": topo, "size": int(size), "nodes": line["nodes"],
+                       "my_node": line["my_node"], "lfa": True, "fabric_prefixes": fabric_prefixes},
             "decision": line,
         }
         if cpu:

@@ -144,6 +144,12 @@ struct Options {
   size_t routeNodes = 0;   // --route-nodes N: only the first N nodes' DBs (profiling at full size)
   bool nodeLabels = false; // --node-labels: grid node labels (node-label MPLS routes in every DB)
   uint32_t routeIters = 0;  // --route-iters N: N memoised rebuilds of my route DB, then exit (profiling)
+  // --fabric-prefixes: the intended fabric benchmark: one prefix per node (the reference's
+  // createFabric advertises none, RoutingBenchmarkUtils.cpp:355-400, so its route build
+  // runs no SPF; prefixes fd00:<i>::/128 in node-name order) and every SSW linked to its
+  // plane's FSW in every pod (createFabric's emplace keeps the pod-0 adjacency only, which
+  // leaves pods 1.. unreachable from pod 0)
+  bool fabricPrefixes = false;
 };
 
 struct Bench {
@@ -155,6 +161,7 @@ struct Bench {
   bool ksp2 = false;
   std::mt19937_64 rng;
   std::optional<std::pair<int, int>> selected;  // the node of the previous iteration
+  std::map<std::string, std::string> prefixOwner;  // advertised prefix (string form) -> node name
 
   explicit Bench(const Options& opt) : o(opt), rng(opt.seed) {
     ksp2 = o.algo == "ksp2";
@@ -176,6 +183,7 @@ struct Bench {
             e.forwardingType = thrift::PrefixForwardingType::SR_MPLS;
           }
           ps.updatePrefix(std::to_string(id), kArea, e);
+          prefixOwner[e.prefix.toString()] = std::to_string(id);
         }
     } else {
       const int planes = kFswsPerPod;
@@ -184,7 +192,8 @@ struct Bench {
       for (int p = 0; p < planes; ++p)
         for (int s = 0; s < kSswsPerPlane; ++s) {  // emplace keeps the pod-0 adjacency only
           std::vector<thrift::Adjacency> adjs;
-          fabAdj(fabName(kSsw, p, s), kFsw, 0, p, adjs);
+          // (the intended fabric: an SSW of plane p reaches FSW p of every pod)
+          for (int pod = 0; pod < (o.fabricPrefixes ? pods : 1); ++pod) fabAdj(fabName(kSsw, p, s), kFsw, pod, p, adjs);
           ls.updateAdjacencyDatabase(adjDb(fabName(kSsw, p, s), adjs, false));
         }
       for (int pod = 0; pod < pods; ++pod)
@@ -196,6 +205,21 @@ struct Bench {
         }
       for (int pod = 0; pod < pods; ++pod)
         for (int r = 0; r < kRswsPerPod; ++r) ls.updateAdjacencyDatabase(adjDb(fabName(kRsw, pod, r), rswAdjs(pod, r), false));
+      if (o.fabricPrefixes) {
+        std::vector<std::string> names;
+        for (auto const& [name, _] : ls.getAdjacencyDatabases()) names.push_back(name);
+        std::sort(names.begin(), names.end());
+        for (uint32_t i = 0; i < names.size(); ++i) {
+          thrift::PrefixEntry e;
+          e.prefix = thrift::IpPrefix{"fd00:" + hex2(i >> 16) + "::" + hex2(i & 0xffff), 128};
+          if (ksp2) {
+            e.forwardingAlgorithm = thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP;
+            e.forwardingType = thrift::PrefixForwardingType::SR_MPLS;
+          }
+          ps.updatePrefix(names[i], kArea, e);
+          prefixOwner[e.prefix.toString()] = names[i];
+        }
+      }
     }
   }
 
@@ -312,17 +336,15 @@ std::string checkRoutes(Bench& b, const DecisionRouteDb& db) {
   OracleRows o(m);
   size_t bad = 0, checked = 0;
   if (!b.ksp2) {
-    std::map<std::string, uint32_t> owner;  // prefix -> node
-    for (uint32_t v = 0; v < m.names.size(); ++v)
-      if (b.o.topology == "grid") {
-        const uint32_t id = (uint32_t)std::stoul(m.names[v]);
-        owner["fc00:" + hex2(id >> 16) + "::" + hex2(id & 0xffff) + "/128"] = v;
-      }
+    std::map<std::string, uint32_t> owner;  // prefix -> node id
     size_t reachable = 0;
-    if (b.o.topology == "grid") {
-      const auto& dm = o.of(me).first;
-      for (uint32_t v = 0; v < m.names.size(); ++v) reachable += v != me && dm[v] != UINT64_MAX;
+    const auto& dm = o.of(me).first;
+    for (auto const& [prefix, node] : b.prefixOwner) {
+      const uint32_t v = m.id.at(node);
+      owner[prefix] = v;
+      reachable += v != me && dm[v] != UINT64_MAX;
     }
+    ++checked;  // the route count: every reachable advertiser other than me
     if (db.unicastRoutes.size() != reachable) ++bad;
     for (auto const& [p, route] : db.unicastRoutes) {
       ++checked;
@@ -384,6 +406,7 @@ int main(int argc, char** argv) {
     else if (a == "--route-nodes" && i + 1 < argc) o.routeNodes = std::stoul(argv[++i]);
     else if (a == "--node-labels") o.nodeLabels = true;
     else if (a == "--route-iters") o.routeIters = (uint32_t)std::stoul(next());
+    else if (a == "--fabric-prefixes") o.fabricPrefixes = true;
     else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
       return 2;
@@ -530,12 +553,12 @@ int main(int argc, char** argv) {
     }
     const auto& m = ls.csrMirror();
     std::printf(
-        "{\"workload\": \"decision\", \"topology\": \"%s\", \"size\": %u, \"nodes\": %zu, \"links\": %zu, "
+        "{\"workload\": \"decision\", \"topology\": \"%s\", \"fabric_prefixes\": %s, \"size\": %u, \"nodes\": %zu, \"links\": %zu, "
         "\"algo\": \"%s\", \"my_node\": \"%s\", \"lfa\": true, \"iters\": %u, \"warmup\": %u, "
         "\"ms_per_update\": %.4f, \"ms_update_adjdb\": %.4f, \"ms_build_route_db\": %.4f, \"median_ms\": %.4f, "
         "\"spf_runs_per_update\": %.2f, \"routes\": %llu, \"ms_initial_route_db\": %.2f, \"ms_setup\": %.1f, "
         "\"check\": \"%s\", \"cpu_baseline\": %s}\n",
-        o.topology.c_str(), o.size, m.names.size(), m.links.size(), b.ksp2 ? "KSP2_ED_ECMP" : "SP_ECMP", b.me.c_str(),
+        o.topology.c_str(), o.fabricPrefixes ? "true" : "false", o.size, m.names.size(), m.links.size(), b.ksp2 ? "KSP2_ED_ECMP" : "SP_ECMP", b.me.c_str(),
         o.iters, o.warmup, (msUpdate + msBuild) / K, msUpdate / K, msBuild / K, per.empty() ? 0.0 : per[per.size() / 2],
         (double)runs / K, (unsigned long long)routes, msInitial, msSetup, check.c_str(), cpu.c_str());
     return check.rfind("MISMATCH", 0) == 0 ? 1 : 0;
