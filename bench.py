@@ -74,6 +74,30 @@ def algorithmic_bytes(g, sources: np.ndarray) -> int:
     return int(per.sum())
 
 
+def rows_check(g, d_dist, d_nh, lo: int, n_local: int, use_metric: bool, nrows: int = 8):
+    """The post-run check of the all-sources line: `nrows` evenly spaced rows of the rank's
+    result (u64 distances and every next-hop byte) compared with oracle runSpf rows
+    (oracle/spf_oracle.c, the tests' checker) outside the timed region. Raises on a
+    mismatch."""
+    from oracle.oracle import Oracle
+
+    o = Oracle(g)
+    idx = np.unique(np.linspace(0, n_local - 1, min(nrows, n_local)).astype(np.int64))
+    srcs = (idx + lo).astype(np.uint32)
+    want_d, want_nh = o.all_sources(srcs, use_metric, nthreads=1)
+    got_d = d_dist[idx.tolist()].cpu().numpy().view(np.uint64)
+    got_nh = d_nh[idx.tolist()].cpu().numpy()
+    if got_nh.shape[-1] != want_nh.shape[-1]:
+        raise AssertionError(f"next-hop width {got_nh.shape[-1]} != oracle {want_nh.shape[-1]}")
+    for i, s in enumerate(srcs.tolist()):
+        if not np.array_equal(got_d[i], want_d[i]):
+            raise AssertionError(f"bench result check failed: dist row of source {s}")
+        if not np.array_equal(got_nh[i], want_nh[i]):
+            raise AssertionError(f"bench result check failed: next-hop row of source {s}")
+    return {"rows": len(srcs), "sources": srcs.tolist(), "compared": "u64 dist + next-hop bytes vs oracle runSpf",
+            "result": "ok"}
+
+
 def cpu_baseline(g, seconds: float, use_metric: bool):
     """CPU baselines on the host cores of this box, same all-sources workload, evenly spaced
     source samples sized to ~`seconds` of wall time in all:
@@ -292,7 +316,7 @@ def whatif_main(args):
     eng.close()
 
 
-PMC_ROUNDS = ("r04", "r03", "r02")  # newest first: the PMC summaries bench lines carry
+PMC_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: the PMC summaries bench lines carry
 
 
 def pmc_path(name):
@@ -903,16 +927,12 @@ def all_sources_main(args):
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     elapsed = max_over_ranks(elapsed, dev)  # the slowest rank's clock
 
-    # correctness spot check (grid: Manhattan distances) outside the timed region
+    # correctness check outside the timed region: a handful of full rows of the last step,
+    # distances AND next-hop bytes, against the CPU oracle (tests' checker) on the same graph
     grid_n = {"grid100": 100, "grid10": 10}.get(args.topology)
-    if grid_n and n_local:
-        n = grid_n
-        rows = [0, n_local - 1]
-        host = d_dist[rows].cpu().numpy().view(np.uint64)
-        a = np.arange(V)
-        for r, s in zip(rows, [lo, hi - 1]):
-            exp = np.abs(s % n - a % n) + np.abs(s // n - a // n)
-            assert np.array_equal(host[rows.index(r)].astype(np.int64), exp), "bench result check failed"
+    check = None
+    if n_local:
+        check = rows_check(g, d_dist, d_nh, lo, n_local, use_metric)
 
     gather = None
     if world > 1 and strong and not args.no_gather:
@@ -994,6 +1014,10 @@ def all_sources_main(args):
     traffic_label = None
     if args.traffic_json is None:
         args.traffic_json = pmc_path(args.topology) or ""
+    if args.traffic_json and not os.path.relpath(os.path.abspath(args.traffic_json), ROOT).startswith("profiles" + os.sep):
+        # a bench line cites only tracked evidence: copy the summary into profiles/ first
+        sys.stderr.write(f"bench: ignoring --traffic-json {args.traffic_json} (not under profiles/)\n")
+        args.traffic_json = ""
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -1045,6 +1069,8 @@ def all_sources_main(args):
         if gather is not None:
             gather["compute_only_value"] = value
             out["gather"] = gather
+        if check is not None:
+            out["check"] = check
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(g, args.cpu_seconds, use_metric)
         print(json.dumps(out), flush=True)

@@ -318,9 +318,13 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   for (auto const& [area, ls] : als) {
     if (!ls.labeledNodeCount()) continue;  // every label is 0 (non-SR mode): nothing to visit
     labelToNode.reserve(labelToNode.size() + ls.labeledNodeCount());
-    for (auto const& [_, adjDb] : ls.getAdjacencyDatabases()) {
-      const int32_t topLabel = adjDb.nodeLabel;
-      if (topLabel == 0) continue;  // non-SR mode
+    // the labelled adjacency databases in getAdjacencyDatabases() order, with mirror ids
+    // (the fast path reads my row's mirror: a retired snapshot's ids need the name lookup)
+    const auto& labeled = ls.labeledNodes();
+    const bool sameMirror = fast_.state == 1 && fast_.m == &ls.csrMirror();
+    for (auto const& ln : labeled) {
+      const int32_t topLabel = ln.label;
+      const std::string& nodeName = *ln.name;
       if (!isMplsLabelValid(topLabel)) {
         counters_.skipped_mpls_route++;
         continue;
@@ -328,35 +332,40 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
       auto it = labelToNode.find(topLabel);
       if (it != labelToNode.end()) {  // collision: the bigger node name keeps the label
         counters_.duplicate_node_label++;
-        if (*cand[it->second].first < adjDb.thisNodeName) continue;
+        if (*cand[it->second].first < nodeName) continue;
       }
-      if (adjDb.thisNodeName == myNodeName) {
+      if (nodeName == myNodeName) {
         thrift::NextHopThrift nh;
         nh.address.addr = "::";
         nh.area = area;
         nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
-        put(topLabel, &adjDb.thisNodeName, RibMplsEntry{topLabel, {nh}});
+        put(topLabel, &nodeName, RibMplsEntry{topLabel, {nh}});
         continue;
       }
-      if (fast_.state == 1) {
+      if (fast_.state == 1 && fast_.ls == &ls) {
         NextHopSet fnh;
-        const int fr = fastLabelNextHops(myNodeName, adjDb.thisNodeName, topLabel, &fnh);
+        uint32_t did = ln.id;
+        if (!sameMirror) {
+          auto f = fast_.m->id.find(nodeName);
+          did = f == fast_.m->id.end() ? UINT32_MAX : f->second;
+        }
+        const int fr = fastLabelNextHops(myNodeName, did, topLabel, &fnh);
         if (fr == 0) {
           counters_.no_route_to_label++;
           continue;
         }
         if (fr == 1) {
-          put(topLabel, &adjDb.thisNodeName, RibMplsEntry{topLabel, std::move(fnh)});
+          put(topLabel, &nodeName, RibMplsEntry{topLabel, std::move(fnh)});
           continue;
         }
       }
-      auto metricNhs = getNextHopsWithMetric(myNodeName, {{adjDb.thisNodeName, area}}, false, als);
+      auto metricNhs = getNextHopsWithMetric(myNodeName, {{nodeName, area}}, false, als);
       if (metricNhs.second.empty()) {
         counters_.no_route_to_label++;
         continue;
       }
-      put(topLabel, &adjDb.thisNodeName,
-          RibMplsEntry{topLabel, getNextHopsThrift(myNodeName, {{adjDb.thisNodeName, area}}, false, false,
+      put(topLabel, &nodeName,
+          RibMplsEntry{topLabel, getNextHopsThrift(myNodeName, {{nodeName, area}}, false, false,
                                                    metricNhs.first, metricNhs.second, topLabel, als)});
     }
   }
@@ -967,10 +976,8 @@ int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
   return any ? 1 : 0;
 }
 
-int SpfSolver::fastLabelNextHops(const std::string& me, const std::string& dstName, int32_t label, NextHopSet* out) {
-  const auto it = fast_.m->id.find(dstName);
-  if (it == fast_.m->id.end()) return -1;
-  const uint32_t dst = it->second;
+int SpfSolver::fastLabelNextHops(const std::string& me, uint32_t dst, int32_t label, NextHopSet* out) {
+  if (dst == UINT32_MAX) return -1;
   const Metric d = views_.front().mine.dist(dst);
   if (d == UINT64_MAX) return 0;  // getMinCostNodes: dst not reached, no next-hop node
   const int nn = fastNextHopNodes(me, dst, d);

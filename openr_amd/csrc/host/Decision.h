@@ -338,7 +338,7 @@ class SpfSolver {
   // the node-label MPLS route's next hops towards dst (getNextHopsWithMetric +
   // getNextHopsThrift with swapLabel = label, perDestination = false): 1 = *out built, 0 =
   // no next-hop node (no route to the label), -1 = not on the fast path (general path)
-  int fastLabelNextHops(const std::string& me, const std::string& dst, int32_t label, NextHopSet* out);
+  int fastLabelNextHops(const std::string& me, uint32_t dst, int32_t label, NextHopSet* out);
   // true when the prefix was served: its route, if any, is appended to `routes` (prefixes
   // arrive in key order, so the route is built in place at the end)
   bool fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries, uint32_t dstId,

@@ -1246,8 +1246,26 @@ void LinkState::convertKspRows() const {
   kspRows_.clear();
 }
 
+const std::vector<LinkState::LabeledNode>& LinkState::labeledNodes() const {
+  const CsrMirror& m = csrMirror();
+  std::lock_guard<std::mutex> g(cacheMu_.m);
+  if (labeledListGen_ != mirrorGeneration_ || labeledListAdjVer_ != adjDbVersion_) {
+    labeledList_.clear();
+    labeledList_.reserve(labeledNodes_);
+    for (auto const& [name, db] : adjacencyDatabases_) {
+      if (db.nodeLabel == 0) continue;
+      auto it = m.id.find(name);
+      labeledList_.push_back(LabeledNode{db.nodeLabel, &db.thisNodeName, it == m.id.end() ? UINT32_MAX : it->second});
+    }
+    labeledListGen_ = mirrorGeneration_;
+    labeledListAdjVer_ = adjDbVersion_;
+  }
+  return labeledList_;
+}
+
 const std::vector<int64_t>& LinkState::nodeLabelsById() const {
   const CsrMirror& m = csrMirror();
+  std::lock_guard<std::mutex> g(cacheMu_.m);
   if (nodeLabelsGen_ != mirrorGeneration_ || nodeLabelsAdjVer_ != adjDbVersion_) {
     nodeLabelsById_.assign(m.names.size(), kNoNodeLabel);
     for (uint32_t i = 0; i < m.names.size(); ++i) {

@@ -142,6 +142,14 @@ struct RelaxedFlag {
   }
 };
 
+// A mutex that copies / moves as a fresh one (caches of a copyable object)
+struct CacheMutex {
+  mutable std::mutex m;
+  CacheMutex() = default;
+  CacheMutex(const CacheMutex&) {}
+  CacheMutex& operator=(const CacheMutex&) { return *this; }
+};
+
 template <class T>
 class HoldableValue {
  public:
@@ -352,6 +360,16 @@ class LinkState {
   // adjacency databases that carry a node label (new: lets a route build skip the
   // node-label pass, and the SPFs it would read, when there are none)
   size_t labeledNodeCount() const { return labeledNodes_; }
+  // The adjacency databases with a node label, in getAdjacencyDatabases() iteration order
+  // (the order buildRouteDb visits them, which decides label collisions), with each node's
+  // id on the current mirror: the node-label route pass walks this list instead of hashing
+  // every name per build. Rebuilt after an adjacency database update or a mirror rebuild.
+  struct LabeledNode {
+    int32_t label;
+    const std::string* name;  // the adjacency database's thisNodeName
+    uint32_t id;              // csrMirror().id of the node (UINT32_MAX: not on the mirror)
+  };
+  const std::vector<LabeledNode>& labeledNodes() const;
   std::unordered_map<std::string, thrift::AdjacencyDatabase> const& getAdjacencyDatabases() const {
     return adjacencyDatabases_;
   }
@@ -534,6 +552,11 @@ class LinkState {
   static size_t tokenRowLength(const uint32_t* row);
   void decodeTokens(const uint32_t* row, std::vector<Path>& out) const;  // mirror_'s edge ids -> Links
   void convertKspRows() const;  // kspRows_ -> kthStaged_ / kthPathResults_ (mirror_ still valid)
+  // id-indexed caches read by concurrent route builds (buildRouteDbs workers): the first
+  // reader after a change rebuilds under the lock; no update runs during a build
+  CacheMutex cacheMu_;
+  mutable std::vector<LabeledNode> labeledList_;
+  mutable uint64_t labeledListGen_ = 0, labeledListAdjVer_ = ~0ull;
   mutable std::vector<int64_t> nodeLabelsById_;
   mutable uint64_t nodeLabelsGen_ = 0, nodeLabelsAdjVer_ = 0;
   uint64_t adjDbVersion_ = 0;  // bumped by every adjacency database update / delete
