@@ -665,7 +665,7 @@ struct GrpWave {
   uint32_t cap;            // dirty slots
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_PROF): per-phase cycles and sizes, or null
-  unsigned long long pacc[8];  // this wave's share of prof, added once when the wave retires
+  unsigned long long pacc[1];  // lane 0: this wave's repair count (OPENR_SPF_PROF); the phase sums go to prof directly
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
@@ -936,14 +936,14 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   }
   if (c.prof && lane == 0) {
     pt3 = (long long)__builtin_amdgcn_s_memtime();
-    c.pacc[0] += (unsigned long long)(pt1 - pt0);
-    c.pacc[1] += (unsigned long long)(pt2 - pt1);
-    c.pacc[2] += (unsigned long long)(pt3 - pt2);
-    c.pacc[3] += 1ull;
-    c.pacc[4] += na;
-    c.pacc[5] += nd;
-    c.pacc[6] += buckets;
-    c.pacc[7] += nchanged;
+    atomicAdd(&c.prof[0], (unsigned long long)(pt1 - pt0));
+    atomicAdd(&c.prof[1], (unsigned long long)(pt2 - pt1));
+    atomicAdd(&c.prof[2], (unsigned long long)(pt3 - pt2));
+    c.pacc[0] += 1ull;
+    atomicAdd(&c.prof[4], (unsigned long long)na);
+    atomicAdd(&c.prof[5], (unsigned long long)nd);
+    atomicAdd(&c.prof[6], (unsigned long long)buckets);
+    atomicAdd(&c.prof[7], (unsigned long long)nchanged);
   }
   return nchanged;
 }
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.nb = nb;
   c.unit = unit != 0;
   c.prof = prof;
-  for (int k = 0; k < 8; ++k) c.pacc[k] = 0;
+  c.pacc[0] = 0;
   c.bdist = bdist;
   c.bnh = bnh;
   c.btight = btight;
@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   }
   if (tid == 0 && n_aff) atomicAdd(affected, n_aff);
   if (prof && lane == 0) {
-    for (int k = 0; k < 8; ++k) atomicAdd(&prof[k], c.pacc[k]);
+    atomicAdd(&prof[3], c.pacc[0]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }

@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/r05/whatif"
 mkdir -p "$O" && cd "$R"
 if [ "${TESTS:-1}" = 1 ]; then
-  timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -k "whatif or config4" tests/ > "$O/tests.log" 2>&1; rc=$?
+  timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -k "whatif or config4" tests/ > "$O/tests.log" 2>&1; rc=$?
   echo "whatif tests rc=$rc"; tail -2 "$O/tests.log"
   [ $rc = 0 ] || { grep -E "FAIL|Error|assert" "$O/tests.log" | head -20; exit $rc; }
 fi
