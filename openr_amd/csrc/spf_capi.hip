@@ -88,6 +88,7 @@ struct Device {
   DevBuf<uint64_t> base_dist, base_tight, wdist;
   DevBuf<uint8_t> base_nh, wnh;
   DevBuf<uint32_t> wsrc, wlink, wunit, wcount, wiota, win_links, win_src, wchanged;
+  DevBuf<uint32_t> wchanged_t;  // grouped repair: results source-major, transposed into the caller's rows
   DevBuf<uint16_t> base_tin;  // what-if base SPF: tight in-degree rows (rounds plan)
   size_t wiota_n = 0;  // wiota[0, wiota_n) holds 0, 1, 2, ... (kept across calls)
   // KSP2: base rows, chunk rows, per-chunk ignore slots / sources / pointers, status
@@ -603,11 +604,12 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       OPENR_TRY(d.wsrc.reserve(units));
       OPENR_TRY(d.wlink.reserve(units));
       OPENR_TRY(d.wunit.reserve(units));
+      OPENR_TRY(d.wchanged_t.reserve(units));
       OPENR_TRY(hipEventRecord(d.ev_begin, s));  // the repair kernel's own time -> stats.last_kernel_ms
       OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
                                     d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
-                                    d_changed, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p, d.work.p + kIncrCtr,
-                                    d.num_cus, s));
+                                    d_changed, d.wchanged_t.p, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p,
+                                    d.work.p + kIncrCtr, d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));
       // Units past the slots are large (WAN: ~6 500 of 1.02 M affected units, ~150 dirty
       // nodes on average): re-solved, each starting from its source's base rows (the
@@ -983,7 +985,7 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.perm.release();
     d.part.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
-                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.base_tin.p, d.win_links.p, d.win_src.p, d.wchanged.p,
+                     d.wunit.p,     d.wcount.p,     d.wiota.p, d.base_tin.p, d.win_links.p, d.win_src.p, d.wchanged.p, d.wchanged_t.p,
                      d.kbase.p,     d.krows.p,      d.krows16.p, d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
                      d.kin_src.p,   d.kin_row.p,    d.kin_dst.p, d.ktok1.p,   d.ktok2.p,   d.kq.p, d.kretry.p};
     for (void* p : sweep)

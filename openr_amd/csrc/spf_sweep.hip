@@ -959,7 +959,7 @@ template <typename D, bool LG, uint32_t W, int WPE>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
-    uint32_t cap, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
+    uint32_t cap, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
     uint32_t* ctr, unsigned long long* prof) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -1022,7 +1022,6 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.dlist = reinterpret_cast<uint16_t*>(wb + lay.w_dlist);
   const uint32_t chunks = (n_links + chunk - 1u) / chunk;
   const uint32_t items = n_src * chunks;
-  uint32_t n_aff = 0;
   for (uint32_t item = blockIdx.x; item < items;) {
     const uint32_t j = item / chunks, l0 = (item - j * chunks) * chunk, l1 = min(n_links, l0 + chunk);
     c.src = sources[j];
@@ -1065,7 +1064,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
           hit = tx || ((btight[ee.y >> 6] >> (ee.y & 63u)) & 1ull);
           if (hit) bnode = g.adj[tx ? ee.x : ee.y] & ~kEdgeDown;
         }
-        if (!hit) changed[(size_t)i * n_src + j] = 0;
+        if (!hit) changed_t[(size_t)j * n_links + i] = 0;
       }
       const unsigned long long m = __ballot(hit);
       uint32_t basei = 0;
@@ -1077,7 +1076,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     }
     __syncthreads();
     const uint32_t n_hit = wctl[0];
-    n_aff += tid == 0 ? n_hit : 0u;
+    if (tid == 0 && n_hit) atomicAdd(affected, n_hit);  // per item: no counter live across the repairs
     // waves take the listed units one at a time: the item ends within one repair of balance
     for (;;) {
       uint32_t idx = 0;
@@ -1089,9 +1088,10 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
       c.link = links[i];  // first needed in step (2): the load overlaps step (1)
       const uint32_t cnt = grp_repair(c, lane, V, ent & 0xFFFFu);
       if (lane == 0) {
-        if (cnt != kGrpOverflow) {
-          changed[(size_t)i * n_src + j] = cnt;
-        } else {  // more dirty nodes than slots: re-solved after the launch (openr_spf_whatif)
+        // results source-major (changed_t[j][i]): an item's units share cache lines, where the
+        // link-major API rows put every unit of an item on a line of its own (whatif_transpose)
+        changed_t[(size_t)j * n_links + i] = cnt != kGrpOverflow ? cnt : 0u;
+        if (cnt == kGrpOverflow) {  // more dirty nodes than slots: re-solved after the launch (openr_spf_whatif)
           const uint32_t k = atomicAdd(&affected[1], 1u);
           ovf_src[k] = c.src;
           ovf_link[k] = c.link;
@@ -1104,13 +1104,34 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     __syncthreads();
     item = s_item;
   }
-  if (tid == 0 && n_aff) atomicAdd(affected, n_aff);
   if (prof && lane == 0) {
     atomicAdd(&prof[3], c.pacc[0]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }
   bfs::retire_workgroup(ctr, nullptr);
+}
+
+// changed[i * n_src + j] = changed_t[j * n_links + i] through 64 x 64 LDS tiles (both sides
+// coalesced)
+__global__ __launch_bounds__(256) void whatif_transpose(const uint32_t* changed_t, uint32_t* changed, uint32_t n_links,
+                                                        uint32_t n_src) {
+  __shared__ uint32_t tile[64][65];
+  const uint32_t tl = (n_links + 63u) / 64u, ts = (n_src + 63u) / 64u;
+  for (uint32_t t = blockIdx.x; t < tl * ts; t += gridDim.x) {
+    const uint32_t i0 = (t % tl) * 64u, j0 = (t / tl) * 64u;
+    const uint32_t c = threadIdx.x & 63u, r0 = threadIdx.x >> 6;
+    for (uint32_t r = r0; r < 64u; r += 4u) {  // rows of changed_t: sources j0 + r, links i0 + c
+      const uint32_t j = j0 + r, i = i0 + c;
+      if (j < n_src && i < n_links) tile[r][c] = changed_t[(size_t)j * n_links + i];
+    }
+    __syncthreads();
+    for (uint32_t r = r0; r < 64u; r += 4u) {  // rows of changed: links i0 + r, sources j0 + c
+      const uint32_t i = i0 + r, j = j0 + c;
+      if (i < n_links && j < n_src) changed[(size_t)i * n_src + j] = tile[c][r];
+    }
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(256) void iota_u32(uint32_t* p, uint32_t n) {
@@ -1187,8 +1208,9 @@ uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
-                               uint32_t nh_bits, uint32_t* changed, uint32_t* affected, uint32_t* ovf_src,
-                               uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus, hipStream_t s) {
+                               uint32_t nh_bits, uint32_t* changed, uint32_t* changed_t, uint32_t* affected,
+                               uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus,
+                               hipStream_t s) {
   // [0] affected units, [1] units listed for a re-solve
   hipError_t err = hipMemsetAsync(affected, 0, 2u * sizeof(uint32_t), s);
   if (err != hipSuccess || !n_links || !n_src) return err;
@@ -1254,7 +1276,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
-                       base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed, affected, ovf_src, ovf_link,  \
+                       base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed_t, affected, ovf_src, ovf_link, \
                        ovf_unit, ctr, prof);                                                                   \
   } while (0)
   if (d16) {
@@ -1269,6 +1291,12 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   }
 #undef OPENR_GRP_LAUNCH
   err = hipGetLastError();
+  if (err == hipSuccess) {
+    const uint32_t tiles = ((n_links + 63u) / 64u) * ((n_src + 63u) / 64u);
+    hipLaunchKernelGGL(whatif_transpose, dim3(std::min<uint32_t>(tiles, (uint32_t)num_cus * 8u)), dim3(256), 0, s,
+                       changed_t, changed, n_links, n_src);
+    err = hipGetLastError();
+  }
   if (err == hipSuccess && prof) {
     unsigned long long h[16];
     if (hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess) {
