@@ -66,6 +66,7 @@
 #ifndef OPENR_SPF_H
 #define OPENR_SPF_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -235,6 +236,13 @@ int openr_spf_ksp2_device(openr_spf_ctx* ctx, int device_index, const uint32_t* 
                           uint32_t n_sources, const uint32_t* d_pair_row,
                           const uint32_t* d_pair_dst, uint32_t n_pairs, uint32_t tok_cap,
                           uint32_t* d_tok1, uint32_t* d_tok2, void* stream);
+
+/* Page-locked host memory for the caller-owned host buffers of the batch calls (the
+   openr_spf_ksp2 token rows, solve rows): their device-to-host copies then run at link rate
+   instead of through a pageable staging copy (the DecisionBenchmark G100 KSP2 update copied
+   2 x 20 MB of token rows at ~2.3 GB/s). openr_spf_host_free(NULL) is a no-op. */
+int openr_spf_host_alloc(size_t bytes, void** out);
+void openr_spf_host_free(void* p);
 
 /* In-place attribute patch of the mirror: the link structure —
    rows, columns, link ids — is unchanged; only attributes the reference changes on an

@@ -1126,12 +1126,14 @@ void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::
   const auto t0 = std::chrono::steady_clock::now();
   ensureEngineGraph();
   const uint32_t n = (uint32_t)dst.size(), cap = 512;  // tokens per pair: [n_paths, (len, edges..)..]
-  // the engine writes every row it serves (unserved rows keep the 0xFFFFFFFF marker):
-  // no zero fill of the n x 512 token buffers
-  std::unique_ptr<uint32_t[]> tok1(new uint32_t[(size_t)n * cap]), tok2(new uint32_t[(size_t)n * cap]);
+  // the engine writes every row it serves (unserved rows keep the 0xFFFFFFFF marker): no
+  // zero fill, and the n x 512 token buffers persist across calls (a fresh 40 MB buffer per
+  // G100 build page-faulted on the engine's copy into it)
+  uint32_t* tok1 = kspScratch_.get((size_t)2 * n * cap);
+  uint32_t* tok2 = tok1 + (size_t)n * cap;
   const std::vector<uint32_t> srcs(n, s->second);
   for (uint32_t i = 0; i < n; ++i) tok1[(size_t)i * cap] = tok2[(size_t)i * cap] = 0xFFFFFFFFu;
-  const int rc = openr_spf_ksp2(engine_->ctx(), srcs.data(), dst.data(), n, cap, tok1.get(), tok2.get());
+  const int rc = openr_spf_ksp2(engine_->ctx(), srcs.data(), dst.data(), n, cap, tok1, tok2);
   if (rc == OPENR_SPF_ENOTSUP) return;
   if (rc != OPENR_SPF_E2BIG) SpfEngineHandle::check(rc, "openr_spf_ksp2");  // E2BIG: overflowed rows stay unmarked
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / n;
@@ -1161,6 +1163,21 @@ void LinkState::prefetchKthPaths(const std::string& src, const std::vector<std::
     // a k = 1 entry the memo already holds is read as a memo hit
     if (kthPathResults_.count(std::make_tuple(src, m.names[dst[i]], size_t(1)))) rows->memo[dst[i]] |= 1u;
   }
+}
+
+LinkState::KspScratch::~KspScratch() { openr_spf_host_free(p); }
+
+uint32_t* LinkState::KspScratch::get(size_t n) {
+  if (cap < n) {
+    openr_spf_host_free(p);
+    p = nullptr;
+    cap = 0;
+    void* q = nullptr;
+    SpfEngineHandle::check(openr_spf_host_alloc(n * sizeof(uint32_t), &q), "openr_spf_host_alloc");
+    p = static_cast<uint32_t*>(q);
+    cap = n;
+  }
+  return p;
 }
 
 size_t LinkState::tokenRowLength(const uint32_t* row) {
@@ -1197,7 +1214,9 @@ const uint32_t* LinkState::kthPathTokens(const std::string& src, const std::stri
     if (memo & 1u) return;
     throwIfFrozen("getKthPaths", src + "->" + dest);
     if (!r.spfRead) {
-      getSpfResult(src, true);
+      // the memo read and its counting, without materialising the SpfResult map (the
+      // token rows carry the paths)
+      getSpfView(src, true);
       r.spfRead = true;  // the memo entry stays until clearMemos, which drops these rows too
     }
     memo |= 1u;

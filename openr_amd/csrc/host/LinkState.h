@@ -549,6 +549,24 @@ class LinkState {
     bool spfRead = false;           // getSpfResult(src) read through this object (k = 1 counting)
   };
   mutable std::unordered_map<std::string, KspRows> kspRows_;
+  // prefetchKthPaths' engine token buffers: page-locked (openr_spf_host_alloc), reused
+  // across calls; a copy of the LinkState starts without one
+  struct KspScratch {
+    uint32_t* p = nullptr;
+    size_t cap = 0;
+    KspScratch() = default;
+    KspScratch(const KspScratch&) {}
+    KspScratch& operator=(const KspScratch&) { return *this; }
+    KspScratch(KspScratch&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr, o.cap = 0; }
+    KspScratch& operator=(KspScratch&& o) noexcept {
+      std::swap(p, o.p);
+      std::swap(cap, o.cap);
+      return *this;
+    }
+    ~KspScratch();
+    uint32_t* get(size_t n);
+  };
+  mutable KspScratch kspScratch_;
   static size_t tokenRowLength(const uint32_t* row);
   void decodeTokens(const uint32_t* row, std::vector<Path>& out) const;  // mirror_'s edge ids -> Links
   void convertKspRows() const;  // kspRows_ -> kthStaged_ / kthPathResults_ (mirror_ still valid)

@@ -912,6 +912,21 @@ int openr_spf_abi_version(void) { return OPENR_SPF_ABI_VERSION; }
 
 const char* openr_spf_last_error(void) { return g_last_error.c_str(); }
 
+int openr_spf_host_alloc(size_t bytes, void** out) {
+  if (!out) return fail(OPENR_SPF_EINVAL, "openr_spf_host_alloc: null out");
+  *out = nullptr;
+  const hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return fail(OPENR_SPF_ENOMEM, "openr_spf_host_alloc: %s", hipGetErrorString(e));
+  }
+  return OPENR_SPF_OK;
+}
+
+void openr_spf_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 const char* openr_spf_last_kernels(void) { return g_launch_trace.c_str(); }
 
 void openr_spf_limits(openr_spf_limits_t* out) {

@@ -46,6 +46,8 @@ EXPORTS = (
     "openr_spf_whatif_device",
     "openr_spf_ksp2",
     "openr_spf_ksp2_device",
+    "openr_spf_host_alloc",
+    "openr_spf_host_free",
     "openr_spf_patch_graph",
     "openr_spf_refresh",
     "openr_spf_refresh_device",
@@ -137,6 +139,9 @@ def load_library():
     l.openr_spf_whatif_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, P(ctypes.c_uint64)]
     l.openr_spf_ksp2.argtypes = [vp, vp, vp, u32, u32, vp, vp]
     l.openr_spf_ksp2_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, vp, u32, u32, vp, vp, vp]
+    l.openr_spf_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
+    l.openr_spf_host_free.argtypes = [vp]
+    l.openr_spf_host_free.restype = None
     l.openr_spf_patch_graph.argtypes = [vp, P(SpfPatch)]
     l.openr_spf_refresh.argtypes = [vp, vp, u32, u32, vp, vp, u32, vp, P(u32)]
     l.openr_spf_refresh_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, u32, vp, vp, P(u32)]
@@ -144,7 +149,7 @@ def load_library():
     l.openr_spf_take_status.argtypes = [vp, ctypes.c_int, P(u32)]
     for name in EXPORTS:
         if name not in ("openr_spf_last_error", "openr_spf_last_kernels", "openr_spf_limits", "openr_spf_destroy",
-                        "openr_spf_build_id"):
+                        "openr_spf_build_id", "openr_spf_host_free"):
             getattr(l, name).restype = ctypes.c_int
     _lib = l
     return l

@@ -5,6 +5,7 @@
 // profiling binary, never into libopenr_spf.so / libopenr_decision.so, and nothing in the
 // product loads it: the product has no CPU path (openr_spf_create fails with ENODEV).
 // Only the entry points LinkState calls are served; the rest return ENOTSUP.
+#include <cstdlib>
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -60,6 +61,11 @@ void parallelRows(uint32_t n, F f) {
 
 extern "C" {
 int openr_spf_abi_version(void) { return OPENR_SPF_ABI_VERSION; }
+int openr_spf_host_alloc(size_t bytes, void** out) {
+  *out = std::malloc(bytes ? bytes : 1);
+  return *out ? 0 : OPENR_SPF_ENOMEM;
+}
+void openr_spf_host_free(void* p) { std::free(p); }
 const char* openr_spf_build_id(void) { return "cpu-stub (test infrastructure)"; }
 const char* openr_spf_last_error(void) { return g_err.c_str(); }
 const char* openr_spf_last_kernels(void) { return "cpu_stub"; }
