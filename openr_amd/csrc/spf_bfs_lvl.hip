@@ -1089,188 +1089,6 @@ __global__ __launch_bounds__(512) void bfs_wave_kernel(DevGraph g, SolveArgs a, 
   retire_workgroup(ctr, nullptr);
 }
 
-// Split wave pass (experiment, OPENR_SPF_BFS_WAVE_SPLIT=2): the wave pass with
-// TWO wavefronts per solve slot, so a level of 65-128 nodes is one chain instead of two.
-// The pair shares the slot's levels / next hops / queue halves; wave h expands the
-// frontier chunks h, h+2, ... of each level and appends through a per-half LDS cursor
-// (monotone within a solve: positions are cursor - base, the base being the value read
-// at the previous barrier on that half). Levels are separated by a pair barrier with no
-// s_barrier: each wave drains its LDS ops, bumps the slot's counter and polls one b128
-// word [counter, cursor0, cursor1, overflow] until the partner has bumped it too, so the
-// same read also hands over the next level's width (an overflow is flagged with its
-// level, since the partner may already be one level on when the word is read). The tight test and the first-arrival
-// rule are the wave pass's: a level byte the partner has just set to L+1 is still > L,
-// and the next-hop atomics decide first arrival across both waves.
-template <int MODE>
-__global__ __launch_bounds__(1024) void bfs_wave2_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t qhalf,
-                                                         uint32_t slots, uint32_t* ctr, uint32_t* ovf_count,
-                                                         uint32_t nt) {
-  using N = Nh<MODE>;
-  static_assert(N::kSingle, "single-dword next-hop fields only");
-  constexpr uint32_t kBits = 32u / N::kPer;
-  constexpr uint32_t kLog = kBits == 4 ? 3 : kBits == 8 ? 2 : kBits == 16 ? 1 : 0;
-  constexpr uint32_t kShl = 5u - kLog;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id();
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t s = wave >> 1, h = wave & 1u, pl = lane + 64u * h;  // pl: lane within the pair
-  const uint32_t nh_words = N::words(V);
-  const WaveLayout lay = wave_layout(V, nh_words, qhalf, slots);
-  const uint32_t slot = lay.slot0 + s * lay.per_slot;
-  lds_u32* const rows = (lds_u32*)(size_t)0u;
-  lds_u8* const lvl = (lds_u8*)(size_t)slot;
-  lds_u32* const lvl_w = (lds_u32*)(size_t)slot;
-  lds_u32* const nh = (lds_u32*)(size_t)(slot + lay.nh);
-  lds_u16* const q = (lds_u16*)(size_t)(slot + lay.q);
-  lds_u32* const sync = (lds_u32*)(size_t)(lay.total + 16u * s);
-  lds_u32* const my_dummy = (lds_u32*)(size_t)(lay.dummy + 4u * lane);
-  for (uint32_t i = tid; i < V; i += blockDim.x) rows[i] = g.elld[i];
-  if (wave == 0) *my_dummy = 0xFFFFFFFFu;
-  if (tid < 4u * slots) ((lds_u32*)(size_t)lay.total)[tid] = 0u;
-  __syncthreads();
-  uint32_t gen = 0;  // pair barriers passed (both waves count alike)
-  // pair barrier: returns [counter, cursor0, cursor1, overflow] as of both waves' arrival
-  auto pair_sync = [&]() -> u32x4 {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS ops are done
-    ++gen;
-    if (lane == 0) lds_add(&sync[0], 1u);
-    u32x4 w;
-    do {
-      asm volatile("" ::: "memory");
-      w = *(volatile lds_u128*)sync;
-    } while (__builtin_amdgcn_readfirstlane(w.x) < 2u * gen);
-    w.y = __builtin_amdgcn_readfirstlane(w.y);
-    w.z = __builtin_amdgcn_readfirstlane(w.z);
-    w.w = __builtin_amdgcn_readfirstlane(w.w);
-    return w;
-  };
-  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
-  const uint32_t lvl_words = (V + 3u) / 4u;
-  for (uint32_t unit = blockIdx.x * slots + s; unit < count; unit += gridDim.x * slots) {
-    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
-    const uint32_t src = a.sources[sid];
-    if (src >= V) continue;  // pair-uniform
-    for (uint32_t i = pl; i < lvl_words; i += 128u) lvl_w[i] = 0xFFFFFFFFu;
-    for (uint32_t i = pl; i < nh_words; i += 128u) nh[i] = 0u;
-    if (h == 0 && lane == 0) {
-      sync[1] = 0u;
-      sync[2] = 0u;
-      sync[3] = 0u;
-    }
-    pair_sync();
-    if (h == 0) {  // level 0 (as the wave pass), by the first wave of the pair
-      if (lane == 0) lvl[src] = 0;
-      uint32_t cur = 0;
-      const uint2 rs = g.row2[src];
-      for (uint32_t e0 = rs.x; e0 < rs.y; e0 += 64u) {
-        const uint32_t e = e0 + lane;
-        bool fresh = false;
-        uint32_t v = 0;
-        if (e < rs.y) {
-          const uint32_t av = g.adj[e];
-          v = av & ~kEdgeDown;
-          if (!(av & kEdgeDown) && v != src) {
-            const uint32_t sh = (v << kShl) & 31u;
-            fresh = ((lds_or(&nh[v >> kLog], (1u << g.nbr[e]) << sh) >> sh) & N::kMask) == 0u;
-            lvl[v] = 1;
-          }
-        }
-        const unsigned long long b = __builtin_amdgcn_ballot_w64(fresh);
-        if (fresh)
-          q[qhalf + cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
-              (uint16_t)v;
-        cur += (uint32_t)__popcll(b);
-      }
-      if (lane == 0) sync[2] = cur;
-    }
-    u32x4 w = pair_sync();
-    uint32_t base0 = 0, base1 = w.z, cur = w.z;
-    uint32_t L = 1, reached = 1u + cur;
-    bool overflow = false;
-    while (cur) {
-      if (L + 1u >= 0xFFu) {
-        overflow = true;
-        break;
-      }
-      const uint32_t prd = L & 1u, pwr = 1u - prd;
-      const uint32_t rd = prd * qhalf, wr = pwr * qhalf;
-      const uint32_t base = pwr ? base1 : base0;
-      const uint8_t lnext = (uint8_t)(L + 1u);
-      for (uint32_t fb = 64u * h; fb < cur; fb += 128u) {
-        uint32_t vv[4], lv[4], old[4];
-        const uint32_t idx = fb + lane;
-        const bool live = idx < cur;
-        const uint32_t qe = q[rd + (live ? idx : 0u)];
-        const uint32_t u = live ? qe : src;
-        const uint32_t r4 = rows[u];
-        const uint32_t d4 = live ? r4 : 0u;
-        const uint32_t xu = __builtin_amdgcn_ubfe(nh[u >> kLog], u << kShl, kBits);
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) vv[j] = u + (uint32_t)__builtin_amdgcn_sbfe((int32_t)d4, 8u * j, 8u);
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) lv[j] = lvl[vv[j]];
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-          const uint32_t v = vv[j];
-          old[j] = lds_or(lv[j] > L ? &nh[v >> kLog] : my_dummy, xu << ((v << kShl) & 31u));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        unsigned long long bj[4];
-        bool fresh[4];
-        uint32_t off[5];
-        off[0] = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {
-          fresh[j] = __builtin_amdgcn_ubfe(old[j], vv[j] << kShl, kBits) == 0u;
-          bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
-          off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
-        }
-        const uint32_t total = off[4];
-        if (total) {  // wave-uniform: claim [pos, pos + total) of the write half
-          uint32_t p = 0;
-          if (lane == 0) p = lds_add(&sync[1u + pwr], total);
-          const uint32_t pos = __builtin_amdgcn_readfirstlane(p) - base;
-          if (pos + total <= qhalf) {
-#pragma unroll
-            for (uint32_t j = 0; j < 4u; ++j) {
-              if (fresh[j]) {
-                const uint32_t k =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
-                q[wr + pos + off[j] + k] = (uint16_t)vv[j];
-                lvl[vv[j]] = lnext;
-              }
-            }
-          } else if (lane == 0) {
-            sync[3] = L;  // level L's appends outgrow their half
-          }
-        }
-      }
-      w = pair_sync();
-      const uint32_t end = pwr ? w.z : w.y;
-      if (w.w && w.w <= L) {  // (a partner already past this barrier may flag level L + 1)
-        overflow = true;
-        break;
-      }
-      cur = end - base;
-      if (pwr)
-        base1 = end;
-      else
-        base0 = end;
-      ++L;
-      reached += cur;
-      if (reached == V) break;
-    }
-    if (overflow) {
-      if (h == 0 && lane == 0) a.ovf_list[atomicAdd(ovf_count, 1u)] = unit;
-    } else {
-      wave_rows_out<MODE>(a, sid, V, slot, reinterpret_cast<const uint8_t*>(smem) + slot, nh, cost, nt != 0, pl, 128u);
-    }
-    pair_sync();  // the partner's row reads are done before the slot is re-initialised
-  }
-  __syncthreads();
-  retire_workgroup(ctr, nullptr);
-}
-
 // Wavefronts per workgroup for the wave pass, 0 when it does not apply. One workgroup per
 // CU holds the delta rows plus up to W solve slots (W >= 4 by LDS), spread so every CU
 // gets work. Auto (OPENR_SPF_BFS_WAVE unset / 2): batches of at most three rounds of W
@@ -1294,36 +1112,9 @@ uint32_t wave_pass_waves(const DevGraph& g, int mode, uint32_t qhalf, uint32_t n
 template <int MODE>
 hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t qhalf, uint32_t waves,
                            uint32_t* ctr, uint32_t* ovf_count, int num_cus, hipStream_t s, LaunchInfo* info) {
-  // OPENR_SPF_BFS_WAVE_SPLIT (experiments): 0 = one wavefront per solve,
-  // 1 = the same with two frontier chunks interleaved per step, 2 = two wavefronts per solve
-  const uint32_t split = env_u32("OPENR_SPF_BFS_WAVE_SPLIT", 0u, 0u, 2u);
-  if (split == 2u) {
-    uint32_t slots = waves, lds = 0;
-    for (; slots; --slots) {
-      lds = wave_layout(g.V, nh_words_for(MODE, g.V), qhalf, slots).total + 16u * slots;
-      if (lds <= kMaxLds) break;
-    }
-    if (!slots) return hipErrorInvalidValue;  // (wave_pass_waves admitted >= 4 slots)
-    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cus, (a.n + slots - 1u) / slots));
-    auto k = bfs_wave2_kernel<MODE>;
-    hipError_t err =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (err != hipSuccess) return err;
-    if (info) {
-      info->lds_bytes = lds;
-      info->grid = grid;
-      info->kernel = "bfs_wave2_kernel<lds-graph>";
-    }
-    note_launch("bfs_wave2_kernel");
-    hipLaunchKernelGGL(k, dim3(grid), dim3(128u * slots), lds, s, g, a, cost, qhalf, slots, ctr, ovf_count,
-                       nt_stores());
-    if (prof_enabled())
-      std::fprintf(stderr, "bfs_wave: split grid=%u slots=%u n=%u qhalf=%u lds=%u\n", grid, slots, a.n, qhalf, lds);
-    return hipGetLastError();
-  }
   const uint32_t lds = wave_layout(g.V, nh_words_for(MODE, g.V), qhalf, waves).total;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cus, (a.n + waves - 1u) / waves));
-  auto k = split ? bfs_wave_kernel<MODE, 2> : bfs_wave_kernel<MODE, 1>;
+  auto k = bfs_wave_kernel<MODE, 1>;
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;
@@ -1335,8 +1126,7 @@ hipError_t launch_lvl_wave(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   note_launch("bfs_wave_kernel");
   hipLaunchKernelGGL(k, dim3(grid), dim3(64u * waves), lds, s, g, a, cost, qhalf, waves, ctr, ovf_count, nt_stores());
   if (prof_enabled())  // tests: which pass ran
-    std::fprintf(stderr, "bfs_wave: grid=%u waves=%u n=%u qhalf=%u lds=%u u=%u\n", grid, waves, a.n, qhalf, lds,
-                 split ? 2u : 1u);
+    std::fprintf(stderr, "bfs_wave: grid=%u waves=%u n=%u qhalf=%u lds=%u\n", grid, waves, a.n, qhalf, lds);
   return hipGetLastError();
 }
 

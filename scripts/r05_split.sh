@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 shard experiment: wave-pass parity for the split variants, then
-# the shard-size kernel times of the three variants interleaved.
+# the shard-size kernel times of the three variants interleaved. The split variants were
+# removed after this measurement: run it on commit 919d97c.
 set -o pipefail
 mkdir -p gpurun_out/split
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "wave_pass" -x -v --timeout 120 --timeout-method thread \

@@ -284,18 +284,15 @@ def test_deep_bfs_u8_overflow_rerun(eng, monkeypatch, full):
     check_against_oracle(eng, g, srcs, True, ignore=ignore)
 
 
-@pytest.mark.parametrize("split", ["0", "1", "2"])
 @pytest.mark.parametrize("case", ["grid", "depth", "half", "overload-down"])
-def test_wave_pass(eng, monkeypatch, capfd, case, split):
+def test_wave_pass(eng, monkeypatch, capfd, case):
     """The wave pass (one wavefront per solve, delta-coded rows staged in LDS; picked for
     small batches of graphs whose rows have <= 4 edges within 127 ids of their node),
     forced on and checked against the oracle, including both re-run paths: a chain
     deeper than 253 levels and a forced tiny queue half. OPENR_SPF_PROF makes the pass
-    report itself on stderr (proof that it ran). `split` covers the experiment variants
-    (DESIGN.md §7): 1 = two frontier chunks per step, 2 = two wavefronts per solve."""
+    report itself on stderr (proof that it ran)."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "lvl")
     monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "1")
-    monkeypatch.setenv("OPENR_SPF_BFS_WAVE_SPLIT", split)
     monkeypatch.setenv("OPENR_SPF_PROF", "1")
     n = 40
     names = [f"g{r:02d}-{c:02d}" for r in range(n) for c in range(n)]
@@ -318,9 +315,7 @@ def test_wave_pass(eng, monkeypatch, capfd, case, split):
     dist, _ = check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
     if case == "depth":
         assert int(dist[2, n * n + 299]) == 299
-    err = capfd.readouterr().err
-    assert "bfs_wave:" in err
-    assert ("bfs_wave: split" in err) == (split == "2")
+    assert "bfs_wave:" in capfd.readouterr().err
 
 
 def test_wave_pass_not_applicable(eng, monkeypatch, capfd):
