@@ -31,9 +31,11 @@
 // barrier per level.
 //
 // Field widths by source class (distinct degree d of the source = next-hop set width):
-//   8 bits (d <= 5), 16 bits (d <= 13), 32 bits (d <= 29), and 32-bit fields holding
-//   29-bit slices of the set for d > 29 (one workgroup pass per (solve, slice); the slices'
-//   chunks are merged into the next-hop bytes afterwards, slice_merge).
+//   8 bits (d <= 5), 16 bits (d <= 13), 32 bits (d <= 29); d > 29: the wide pass (one
+//   unit per solve, a multi-word bit stream per node, bfs_wide_kernel) or, with an ignore
+//   set / tight-edge output, 32-bit fields holding 29-bit slices of the set (one workgroup
+//   pass per (solve, slice); the slices' chunks merged into the next-hop bytes afterwards,
+//   slice_merge).
 //
 // No MFMA: min-plus relaxation is not a matrix contraction (DESIGN.md "Roofline").
 #include <algorithm>
@@ -77,7 +79,7 @@ struct BfsLayout {
 // array (capacity V, never wraps) in the fallback path.
 __host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t fb, uint32_t ring_cap) {
   BfsLayout l;
-  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4]
+  uint32_t off = 64;  // control: append counters [0..3], overflow flag [4], target [5], pull sums [8..11]
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
@@ -131,6 +133,54 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t k, uint32
     const uint32_t x = S::field(st, v) >> S::kNhs;
     nrow[i] = j < 4u ? (uint8_t)(x >> (8u * j)) : (uint8_t)0;
   }
+}
+
+// Direction choice for level L -> L+1 (lean edge loop; Beamer et al.'s direction-optimizing
+// BFS): push expands the frontier's out-edges, pull scans every unreached node's edges for
+// in-neighbours on level L. With every link present in both directions and up / down per
+// link (set_graph enforces both), v's tight in-edges u -> v are exactly the usable edges
+// v -> u of v's own row whose head u is on level L and not a sink. Called only when the
+// unreached nodes are few next to the frontier (a candidate level); this pass settles
+// level L as push would (distances, sink marks — so level-L sinks never read as level L)
+// and sums the frontier's transit-row lengths (m_f) and the unreached nodes' row lengths
+// (m_u). Pull when m_u < m_f. `npc` counts the candidate levels: the two sum slots
+// alternate, each zeroed one candidate before its use (>= 1 barrier after its last read).
+template <int FB, int BLOCK, bool RING>
+__device__ __forceinline__ bool choose_pull(const DevGraph& g, uint32_t* st, uint32_t* ctl, const uint16_t* ring,
+                                            uint32_t rmask, uint32_t head, uint32_t tail, uint64_t* drow, uint64_t dL,
+                                            uint32_t& npc) {
+  using S = State<FB>;
+  const uint32_t tid = threadIdx.x, V = g.V;
+  uint32_t* sums = &ctl[8u + 2u * (npc & 1u)];
+  if (tid == 0) {
+    ctl[8u + 2u * ((npc + 1u) & 1u)] = 0;
+    ctl[9u + 2u * ((npc + 1u) & 1u)] = 0;
+  }
+  ++npc;
+  uint32_t mf = 0, mu = 0;
+  for (uint32_t i = head + tid; i < tail; i += BLOCK) {
+    const uint32_t u = ring[RING ? (i & rmask) : i];
+    const uint2 r = g.row2t[u];
+    if (drow) drow[u] = dL;
+    if (r.x & kNodeSink) atomicOr(&st[S::word(u)], kCodeSettledSink << S::shift(u));
+    else mf += r.y - r.x;
+  }
+  for (uint32_t v = tid; v < V; v += BLOCK)
+    if ((S::field(st, v) & kCodeMask) == 0u) {
+      const uint2 r = g.row2[v];
+      mu += r.y - r.x;
+    }
+#pragma unroll
+  for (uint32_t o = 32; o; o >>= 1) {
+    mf += __shfl_xor(mf, o);
+    mu += __shfl_xor(mu, o);
+  }
+  if (__lane_id() == 0) {
+    atomicAdd(&sums[0], mf);
+    atomicAdd(&sums[1], mu);
+  }
+  lds_barrier();
+  return sums[1] < sums[0];
 }
 
 // ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
@@ -209,7 +259,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
       for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
       if (has_ign)
         for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
-      if (tid < 8) ctl[tid] = 0;
+      if (tid < 16) ctl[tid] = 0;
       __syncthreads();
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
@@ -255,6 +305,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
 
       uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2);
       bool overflow = false;  // block-uniform
+      uint32_t npc = 0;       // candidate levels for the pull direction (choose_pull)
       while (head < tail) {
         uint32_t* cnt = &ctl[L & 3u];
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
@@ -311,6 +362,62 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
             }
           }
         }
+        bool pull = false;  // block-uniform
+        if (kLeanT && !a.target && a.pull && V - tail <= a.pull * (tail - head))
+          pull = choose_pull<FB, BLOCK, RING>(g, st, ctl, ring, rmask, head, tail, own_dist ? drow : nullptr, dL, npc);
+        if (kLeanT && pull) {
+          // pull: each unreached node (G lanes, K edges per lane in flight) ORs nh(u) of its
+          // level-L in-neighbours u (bit 0 marks a hit when nh is empty: distances only);
+          // the node's owner group is its only writer this level
+          const uint32_t cL = level_code(L);
+          for (uint32_t vb = 0; vb < V; vb += ngroups) {
+            if (vb + wave * groups_per_wave >= V) continue;  // uniform
+            const uint32_t v = vb + group;
+            uint32_t beg = 0, end = 0;
+            if (v < V && (S::field(st, v) & kCodeMask) == 0u) {
+              const uint2 r = g.row2[v];
+              beg = r.x;
+              end = r.y;
+            }
+            uint32_t x = 0;
+            for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
+              uint32_t vv[K], f[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                const uint32_t e = e0 + j * G;
+                const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;
+                vv[j] = (raw & kEdgeDown) ? V : raw;  // the sentinel: settled, never level L
+              }
+#pragma unroll
+              for (int j = 0; j < K; ++j) f[j] = S::field(st, vv[j]);
+#pragma unroll
+              for (int j = 0; j < K; ++j)
+                if ((f[j] & kCodeMask) == cL) x |= (f[j] & S::kNhMask) | 1u;
+            }
+#pragma unroll
+            for (uint32_t o = 1; o < 64u; o <<= 1)
+              if (o < G) x |= __shfl_xor(x, o);
+            const bool fresh = lane_g == 0 && x != 0u;
+            if (fresh) atomicOr(&st[S::word(v)], ((x & S::kNhMask) | cnext) << S::shift(v));
+            const unsigned long long b = __builtin_amdgcn_ballot_w64(fresh);
+            if (b) {  // wave-uniform; the first active lane claims the slots (readfirstlane)
+              const int leader = __ffsll((long long)__ballot(1)) - 1;
+              uint32_t wbase = 0;
+              if ((int)lane == leader) wbase = atomicAdd(cnt, (uint32_t)__popcll(b));
+              const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
+              if (!RING || base + (uint32_t)__popcll(b) - head <= ring_cap) {
+                if (fresh)
+                  ring[RING ? ((base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))) &
+                               rmask)
+                            : base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = (uint16_t)v;
+              } else if ((int)lane == leader) {
+                ctl[4] = 1;  // two adjacent levels exceed the ring
+              }
+            }
+          }
+        } else
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
           if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
           OPENR_PROF_STAMP(t0);
@@ -705,6 +812,308 @@ __global__ __launch_bounds__(256) void slice_merge(SolveArgs a, uint32_t V) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wide pass: the sliced class (next-hop sets wider than 29 bits) in ONE unit per solve.
+// The sliced pass runs a source's BFS once per 29-bit slice (a degree-84 fabric switch:
+// three full traversals) and merges the slices' scratch rows afterwards (slice_merge).
+// Here the node state is a multi-word bit stream per node: word 0 = [29 next-hop bits |
+// 3-bit level code] exactly as the 32-bit class, words 1..nw-1 = the next 32 bits each
+// (next-hop bit b sits at stream position b + 3). The tight test, the first-arrival
+// election and the append read word 0 only, so the BFS order is computed once; a tight
+// edge then ORs nh(u)'s upper words into v's (plain ds_or, no return, only where u's word
+// is non-zero — on a fabric most sets span one or two words). The row is written straight
+// from LDS: byte j of v's set is stream bits [8j + 3, 8j + 11), assembled a dword of the
+// output row per lane — no slice scratch, no merge launch. Lean edge loop only (no ignore
+// set, no tight-edge output; CSR rows, G lanes per frontier node as the lean pass); full
+// BFS order (never wraps).
+// ---------------------------------------------------------------------------
+struct WideLayout {
+  uint32_t st, ext, ring, dummy, total;
+};
+__host__ __device__ inline WideLayout wide_layout(uint32_t V, uint32_t nw) {
+  WideLayout l;
+  uint32_t off = 64;  // control: append counters [0..3], pull sums [8..11]
+  auto take = [&](uint32_t bytes) {
+    uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.st = take(4u * (V + 1u));  // + node V: the settled sentinel
+  l.ext = take(4u * V * (nw - 1u));
+  l.ring = take(2u * V);
+  l.dummy = take(4u * 64u);
+  l.total = off;
+  return l;
+}
+
+template <int BLOCK, uint32_t NW>
+__global__ __launch_bounds__(BLOCK) void bfs_wide_kernel(DevGraph g, SolveArgs a, uint64_t cost, uint32_t glog,
+                                                         uint32_t nw, uint32_t* ctr, uint32_t nt) {
+  using S = State<32>;
+  constexpr int K = (int)kBfsEdgesPerLane;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ uint32_t s_next;
+  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const WideLayout lay = wide_layout(V, nw);
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  uint32_t* st = reinterpret_cast<uint32_t*>(base + lay.st);
+  uint32_t* ext = reinterpret_cast<uint32_t*>(base + lay.ext);  // [nw - 1][V]
+  uint16_t* ring = reinterpret_cast<uint16_t*>(base + lay.ring);
+  uint32_t* dummy = reinterpret_cast<uint32_t*>(base + lay.dummy);
+  if (tid < 64) dummy[tid] = 0xFFFFFFFFu;
+  const uint32_t G = 1u << glog, ngroups = BLOCK >> glog, groups_per_wave = 64u >> glog;
+  const uint32_t group = tid >> glog, lane_g = tid & (G - 1u);
+  const uint32_t ne = nw - 1u;  // upper words (nw <= NW, the compiled bound)
+  const uint32_t count = a.perm ? a.part[a.cls] : a.n, first = a.perm ? a.part[kMaxClasses + a.cls] : 0u;
+  for (uint32_t unit = blockIdx.x; unit < count;) {
+    const uint32_t sid = a.perm ? a.perm[first + unit] : unit;
+    const uint32_t src = a.sources[sid];
+    if (src < V) {  // block-uniform
+      uint64_t* drow = a.dist + out_row_of(a, sid) * V;
+      for (uint32_t i = tid; i < V + 1u; i += BLOCK) st[i] = 0;
+      for (uint32_t i = tid; i < ne * V; i += BLOCK) ext[i] = 0;
+      if (tid < 16) ctl[tid] = 0;
+      __syncthreads();
+      if (tid == 0) {
+        st[V] = kCodeSettledSink;  // the sentinel
+        st[src] = level_code(0);
+        drow[src] = 0;
+      }
+      __syncthreads();
+      // level 0: the source's own row (even when overloaded); a directly connected node's
+      // next hop is the node itself (LinkState.cpp:867-872)
+      {
+        const uint2 rs = g.row2[src];
+        for (uint32_t e0 = rs.x; e0 < rs.y; e0 += BLOCK) {
+          const uint32_t e = e0 + tid;
+          bool fresh = false;
+          uint32_t v = 0;
+          if (e < rs.y) {
+            const uint32_t av = g.adj[e];
+            v = av & ~kEdgeDown;
+            if (!(av & kEdgeDown) && v != src) {
+              const uint32_t pos = g.nbr[e] + S::kNhs, w = pos >> 5;
+              fresh = (atomicOr(&st[v], (w == 0u ? 1u << pos : 0u) | level_code(1)) & kCodeMask) == 0u;
+              if (w != 0u) atomicOr(&ext[(w - 1u) * V + v], 1u << (pos & 31u));
+            }
+          }
+          const uint32_t slot = 1u + wave_append(fresh, &ctl[0]);
+          if (fresh) ring[slot] = (uint16_t)v;  // slot < 1 + deg(src) <= V
+        }
+      }
+      __syncthreads();
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2), npc = 0;
+      while (head < tail) {
+        uint32_t* cnt = &ctl[L & 3u];
+        if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
+        const uint64_t dL = (uint64_t)L * cost;
+        bool pull = false;  // block-uniform (choose_pull)
+        if (a.pull && V - tail <= a.pull * (tail - head)) pull = choose_pull<32, BLOCK, false>(g, st, ctl, ring, 0u, head, tail, drow, dL, npc);
+        if (pull) {
+          // pull (as the 32-bit lean pass), all words: the owner group of an unreached node
+          // is its only writer this level, so its words are plain stores
+          const uint32_t cL = level_code(L);
+          for (uint32_t vb = 0; vb < V; vb += ngroups) {
+            if (vb + wave * groups_per_wave >= V) continue;  // uniform
+            const uint32_t v = vb + group;
+            uint32_t beg = 0, end = 0;
+            if (v < V && (st[v] & kCodeMask) == 0u) {
+              const uint2 r = g.row2[v];
+              beg = r.x;
+              end = r.y;
+            }
+            uint32_t x = 0, xs[NW - 1u];
+#pragma unroll
+            for (uint32_t q = 0; q < NW - 1u; ++q) xs[q] = 0;
+            for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
+              uint32_t vv[K], f[K];
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                const uint32_t e = e0 + j * G;
+                const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;
+                vv[j] = (raw & kEdgeDown) ? V : raw;
+              }
+#pragma unroll
+              for (int j = 0; j < K; ++j) f[j] = st[vv[j]];
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                if ((f[j] & kCodeMask) == cL) {
+                  x |= (f[j] & S::kNhMask) | 1u;
+#pragma unroll
+                  for (uint32_t q = 0; q < NW - 1u; ++q)
+                    if (q < ne) xs[q] |= ext[q * V + vv[j]];
+                }
+              }
+            }
+#pragma unroll
+            for (uint32_t o = 1; o < 64u; o <<= 1) {
+              if (o < G) {
+                x |= __shfl_xor(x, o);
+#pragma unroll
+                for (uint32_t q = 0; q < NW - 1u; ++q) xs[q] |= __shfl_xor(xs[q], o);
+              }
+            }
+            const bool fresh = lane_g == 0 && x != 0u;
+            if (fresh) {
+              st[v] = (x & S::kNhMask) | cnext;
+#pragma unroll
+              for (uint32_t q = 0; q < NW - 1u; ++q)
+                if (q < ne) ext[q * V + v] = xs[q];
+            }
+            const uint32_t slot = wave_append(fresh, cnt);
+            if (fresh) ring[tail + slot] = (uint16_t)v;
+          }
+        } else
+        for (uint32_t fb = head; fb < tail; fb += ngroups) {
+          if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no frontier node (uniform)
+          const uint32_t idx = fb + group;
+          const bool live = idx < tail;
+          uint32_t u = V, beg = 0, end = 0;
+          if (live) {
+            u = ring[idx];
+            const uint2 r = g.row2t[u];  // empty (beg flagged kNodeSink) for overloaded nodes
+            beg = r.x;
+            end = r.y;
+            if (lane_g == 0) {
+              drow[u] = dL;  // u settled on level L
+              if (beg & kNodeSink) atomicOr(&st[u], kCodeSettledSink);
+            }
+          }
+          // nh(u) (final: u was reached a level ago): word 0 + the code of level L+1, and
+          // the upper words (the sentinel's, for a lane past the level, are never used)
+          const uint32_t xu = (st[u] & S::kNhMask) | cnext;
+          uint32_t xe[NW - 1u];
+#pragma unroll
+          for (uint32_t s = 0; s < NW - 1u; ++s) xe[s] = (s < ne && live) ? ext[s * V + u] : 0u;
+          for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
+            uint32_t vv[K], cw[K], old[K];
+            bool tight[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t e = e0 + j * G;
+              const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;
+              vv[j] = (raw & kEdgeDown) ? V : raw;  // padding / down edge: the sentinel
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) cw[j] = st[vv[j]];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              const uint32_t c = cw[j] & kCodeMask;
+              tight[j] = c == 0u || c == cnext;  // first or equal-cost arrival (LinkState.cpp:857-873)
+              old[j] = atomicOr(tight[j] ? &st[vv[j]] : &dummy[lane], xu);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+#pragma unroll
+              for (uint32_t s = 0; s < NW - 1u; ++s)
+                if (tight[j] && xe[s]) atomicOr(&ext[s * V + vv[j]], xe[s]);
+            bool fresh[K];
+            unsigned long long bj[K];
+            uint32_t off[K + 1];
+            off[0] = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+              fresh[j] = (old[j] & kCodeMask) == 0u;  // a dummy word never is
+              bj[j] = __builtin_amdgcn_ballot_w64(fresh[j]);
+              off[j + 1] = off[j] + (uint32_t)__popcll(bj[j]);
+            }
+            const uint32_t total = off[K];
+            if (total) {  // wave-uniform
+              const int leader = __ffsll((long long)__ballot(1)) - 1;
+              uint32_t wbase = 0;
+              if ((int)lane == leader) wbase = atomicAdd(cnt, total);
+              const uint32_t slot0 = tail + __builtin_amdgcn_readfirstlane(wbase);
+#pragma unroll
+              for (int j = 0; j < K; ++j) {
+                if (fresh[j]) {
+                  const uint32_t slot = slot0 + off[j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bj[j] >> 32),
+                                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bj[j], 0u));
+                  ring[slot] = (uint16_t)vv[j];
+                }
+              }
+            }
+          }
+        }
+        lds_barrier();
+        head = tail;
+        tail += *cnt;
+        ++L;
+        cnext = cnext == 3u ? 1u : cnext + 1u;
+        if (tail == V) {
+          // every node is reached: no edge out of level [head, tail) can be tight
+          for (uint32_t i = head + tid; i < tail; i += BLOCK) drow[ring[i]] = (uint64_t)L * cost;
+          break;
+        }
+      }
+      // rows out: UINT64_MAX for unreached nodes, then the next-hop bytes, a dword of the
+      // row per lane (byte q of the dword: node (4i + q) / nb, byte (4i + q) % nb)
+      for (uint32_t v = tid; v < V; v += BLOCK)
+        if ((st[v] & kCodeMask) == 0u) drow[v] = ~0ull;
+      const uint32_t nb = a.nh_bytes;
+      uint8_t* nrow = a.nh + out_row_of(a, sid) * V * nb;
+      // 32 bits of v's stream from bit p (p >= 3: never the code)
+      auto bits32 = [&](uint32_t v, uint32_t p) -> uint32_t {
+        const uint32_t w = p >> 5, sh = p & 31u;
+        const uint32_t lo = w == 0u ? st[v] : w < nw ? ext[(w - 1u) * V + v] : 0u;
+        const uint32_t hi = w + 1u < nw ? ext[w * V + v] : 0u;
+        return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
+      };
+      const uint32_t row_bytes = V * nb;
+      if (((reinterpret_cast<uintptr_t>(nrow) | row_bytes) & 3u) == 0) {
+        uint32_t* n32 = reinterpret_cast<uint32_t*>(nrow);
+        for (uint32_t i = tid; i < row_bytes / 4u; i += BLOCK) {
+          const uint32_t p = 4u * i, v = p / nb, j = p - v * nb, n0 = min(4u, nb - j);
+          uint32_t x = bits32(v, 8u * j + S::kNhs);
+          if (n0 < 4u) x = (x & ((1u << (8u * n0)) - 1u)) | (bits32(v + 1u, S::kNhs) << (8u * n0));
+          store_row<uint32_t>(&n32[i], x, nt != 0);
+        }
+      } else {
+        for (uint32_t i = tid; i < row_bytes; i += BLOCK) {
+          const uint32_t v = i / nb, j = i - v * nb;
+          nrow[i] = (uint8_t)bits32(v, 8u * j + S::kNhs);
+        }
+      }
+    }
+    __syncthreads();  // every lane is done with this unit's LDS and s_next
+    if (tid == 0) s_next = gridDim.x + atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    unit = s_next;
+  }
+  retire_workgroup(ctr, nullptr);
+}
+
+// Upper words of the wide pass for a class of nsl 29-bit slices (bits <= 29 * nsl).
+uint32_t wide_words(uint32_t nsl) { return 1u + (29u * (nsl - 1u) + 31u) / 32u; }
+
+template <int BLOCK, uint32_t NW>
+hipError_t launch_wide_nw(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, uint32_t nw,
+                          int num_cus, hipStream_t s, LaunchInfo* info) {
+  const uint32_t lds = wide_layout(g.V, nw).total;
+  const uint32_t grid = blocks_for(a.n, lds, num_cus, BLOCK);
+  auto k = bfs_wide_kernel<BLOCK, NW>;
+  hipError_t err =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (err != hipSuccess) return err;
+  if (info) {
+    info->lds_bytes = lds;
+    info->grid = grid;
+    info->kernel = "bfs_wide_kernel";
+  }
+  note_launch("bfs_wide_kernel");
+  hipLaunchKernelGGL(k, dim3(grid), dim3(BLOCK), lds, s, g, a, cost, glog, nw, class_counters(a), nt_stores());
+  return hipGetLastError();
+}
+
+template <int BLOCK>
+hipError_t launch_wide(const DevGraph& g, const SolveArgs& a, uint64_t cost, uint32_t glog, uint32_t nw, int num_cus,
+                       hipStream_t s, LaunchInfo* info) {
+  if (nw <= 2u) return launch_wide_nw<BLOCK, 2>(g, a, cost, glog, nw, num_cus, s, info);
+  if (nw <= 3u) return launch_wide_nw<BLOCK, 3>(g, a, cost, glog, nw, num_cus, s, info);
+  if (nw <= 4u) return launch_wide_nw<BLOCK, 4>(g, a, cost, glog, nw, num_cus, s, info);
+  return launch_wide_nw<BLOCK, 8>(g, a, cost, glog, nw, num_cus, s, info);
+}
+
 uint32_t field_bits(int cls) { return cls == kCls8 ? 8u : cls == kCls16 ? 16u : 32u; }
 }  // namespace
 
@@ -715,11 +1124,25 @@ uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls) {
   return t <= kMaxLds ? t : 0;
 }
 
+static hipError_t launch_bfs_code_args(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
+                                       int num_cus, hipStream_t s, LaunchInfo* info);
+
 hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
                            hipStream_t s, LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
   const int cls = (int)a.cls;
   if (!bfs_code_lds_bytes(g.V, g.L, has_ign, cls)) return hipErrorInvalidValue;
+  // pull candidates: the unreached nodes at most 8x the frontier (OPENR_SPF_PULL: another
+  // factor; 0 = push only, tests / A/B)
+  SolveArgs ap = a;
+  ap.pull = env_u32("OPENR_SPF_PULL", 8u, 0u, 1024u);
+  return launch_bfs_code_args(g, ap, cost, group_lanes, num_cus, s, info);
+}
+
+static hipError_t launch_bfs_code_args(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
+                                       int num_cus, hipStream_t s, LaunchInfo* info) {
+  const bool has_ign = a.ign_ptr != nullptr;
+  const int cls = (int)a.cls;
   const bool sliced = cls == kClsSliced;
   if (sliced && (a.nsl < 1u || a.nsl > 11u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;
@@ -733,6 +1156,17 @@ hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost,
     case 16: return launch_bfs_fb<16, false>(g, a, cost, glog, has_ign, ellm, num_cus, s, info);
     default:
       if (sliced) {
+        // the wide pass (one unit per solve) where it applies: next-hop output, lean edge
+        // loop (no ignore set / tight-edge output), sets of <= 8 words, the full-order state
+        // in LDS. 512-thread workgroups (fabric 5 000: 0.632 ms per all-sources launch vs
+        // 0.706 with 256 and 0.651 with 1 024; sliced pass 0.790). OPENR_SPF_WIDE (tests,
+        // A/B): 0 = the sliced pass, 2 = 256-thread workgroups.
+        const uint32_t nw = wide_words(a.nsl);
+        const uint32_t wide = env_u32("OPENR_SPF_WIDE", 1u, 0u, 2u);
+        if (a.nh && !has_ign && !a.tight && nw <= 8u && wide_layout(g.V, nw).total <= kMaxLds && wide != 0u) {
+          if (wide == 2u) return launch_wide<256>(g, a, cost, glog, nw, num_cus, s, info);
+          return launch_wide<512>(g, a, cost, glog, nw, num_cus, s, info);
+        }
         if (!a.nh) {  // no next-hop output: no slice scratch, one launch
           SolveArgs c = a;
           c.k0 = c.krows = 0;

@@ -165,16 +165,23 @@ def test_sliced_class_in_chunks(eng, monkeypatch, rows):
     otherwise derives from its 512 MiB budget): every row as the oracle's, with
     duplicate sliced sources and a partial last chunk."""
     monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "code")
+    monkeypatch.setenv("OPENR_SPF_WIDE", "0")  # the sliced pass (the wide pass has no scratch)
     monkeypatch.setenv("OPENR_SPF_SLICE_ROWS", rows)
     g = T.fabric(288 + 3 * 56)
     srcs = list(range(g.num_nodes)) + list(range(0, 60, 3))
     check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
 
 
-def test_fabric_5000_sample(eng):
+@pytest.mark.parametrize("wide", ["1", "2", "0"])
+def test_fabric_5000_sample(eng, monkeypatch, bfs_family, wide):
+    """Degree-84 sources: the wide pass (512 / 256 threads) and the sliced pass (code
+    family; the lvl family has its own 32-bit slices)."""
+    monkeypatch.setenv("OPENR_SPF_WIDE", wide)
     g = T.fabric(5000)
     assert g.num_nodes == 4992 and g.num_links == 56448
     check_against_oracle(eng, g, [0, 287, 288, 289, 1000, 4991, 2500], True, check_pathlinks=True)
+    eng.solve([0, 300, 1000], True)  # two degree-84 sources (an SSW, an FSW) and an RSW
+    assert ("bfs_wide_kernel" in eng.last_kernels()) == (wide != "0" and bfs_family[0] == "code")
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -376,6 +383,7 @@ def test_ring_overflow_rerun_list(eng, monkeypatch):
     check_against_oracle(eng, g, srcs, True, check_pathlinks=False)
     d2, n2, _ = eng.solve(srcs, True)
     assert np.array_equal(d1, d2) and np.array_equal(n1, n2)
+    monkeypatch.setenv("OPENR_SPF_WIDE", "0")  # the sliced pass: its (solve, slice) units ring
     hub = hub_graph(4)  # sliced classes: every (solve, slice) unit is listed on its own
     check_against_oracle(eng, hub, list(range(hub.num_nodes)), True, check_pathlinks=False)
 
@@ -450,8 +458,13 @@ def hub_graph(seed, V=300, L=700, hub_deg=(40, 75, 130)):
     return T.csr_from_links(names, links, m, m, ovl)
 
 
+@pytest.mark.parametrize("wide", ["1", "0"])
 @pytest.mark.parametrize("seed", [0, 1])
-def test_source_classes_and_sliced_next_hops(eng, seed):
+def test_source_classes_and_sliced_next_hops(eng, monkeypatch, seed, wide):
+    """Every source class in one batch; sets wider than 29 bits through the wide pass (2-5
+    words per node) or the sliced pass (OPENR_SPF_WIDE=0); with an ignore set always the
+    sliced pass."""
+    monkeypatch.setenv("OPENR_SPF_WIDE", wide)
     g = hub_graph(seed)
     assert g.max_distinct_degree() > 128  # 5 slices of 32 next-hop bits for the largest hub
     srcs = list(range(g.num_nodes))
@@ -463,10 +476,12 @@ def test_source_classes_and_sliced_next_hops(eng, seed):
     check_against_oracle(eng, g, sub, True, ignore=ignore)
 
 
-def test_sliced_next_hops_wide_stride(eng, bfs_family):
-    """Sliced next-hop sets (29-bit code-family chunks merged into bytes, or 32-bit lvl
-    slices) into a caller stride wider than the set: the set's bytes as the oracle's, every
-    byte past them zero."""
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_sliced_next_hops_wide_stride(eng, bfs_family, monkeypatch, wide):
+    """Sliced next-hop sets (code family: the wide pass's word streams or 29-bit chunks
+    merged into bytes; lvl family: 32-bit slices) into a caller stride wider than the set:
+    the set's bytes as the oracle's, every byte past them zero."""
+    monkeypatch.setenv("OPENR_SPF_WIDE", wide)
     g = hub_graph(4)
     eng.set_graph(g)
     o = Oracle(g)
@@ -641,6 +656,38 @@ def fabric_with_faults(seed, n_ovl=12, n_down=60):
     nodes = rng.choice(g.num_nodes, n_ovl, replace=False)
     links = rng.choice(g.num_links, n_down, replace=False)
     return g.patched([], [], links, [0] * len(links), nodes, [1] * len(nodes)), nodes
+
+
+@pytest.mark.parametrize("pull", ["0", "1", "8", "1024"])
+def test_code_family_pull_levels(eng, monkeypatch, pull):
+    """Direction-optimising levels of the code family's lean passes (spf_bfs.hip
+    choose_pull): a level whose unreached nodes number at most OPENR_SPF_PULL x the
+    frontier may be solved by pull (unreached nodes OR the next hops of their level-L
+    in-neighbours) when their edges are fewer than the frontier's. Factor 0 = push only,
+    1024 = every level a candidate. Fabrics with sinks and down links (pull reads v's own
+    row: link state per link), a hub graph (wide-pass words and the sliced pass), a random
+    graph with parallel links, a small forced ring, and distances-only solves."""
+    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "code")
+    monkeypatch.setenv("OPENR_SPF_PULL", pull)
+    g, _ = fabric_with_faults(7)
+    check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
+    hub = hub_graph(5)
+    check_against_oracle(eng, hub, list(range(hub.num_nodes)), True, check_pathlinks=False)
+    monkeypatch.setenv("OPENR_SPF_WIDE", "0")
+    check_against_oracle(eng, hub, list(range(0, hub.num_nodes, 3)), True, check_pathlinks=False)
+    monkeypatch.delenv("OPENR_SPF_WIDE")
+    rg = random_graph(11, 2000, 9000, 1, p_ovl=0.05, p_down=0.05, p_par=0.1)
+    check_against_oracle(eng, rg, list(range(0, rg.num_nodes, 5)), True, check_pathlinks=False)
+    monkeypatch.setenv("OPENR_SPF_RING_CAP", "256")
+    check_against_oracle(eng, rg, list(range(0, rg.num_nodes, 13)), True, check_pathlinks=False)
+    monkeypatch.delenv("OPENR_SPF_RING_CAP")
+    eng.set_graph(g)
+    o = Oracle(g)
+    srcs = list(range(0, g.num_nodes, 7))
+    d_only, nh, _ = eng.solve(srcs, True, want_nh=False)
+    assert nh is None
+    for i, s_ in enumerate(srcs):
+        np.testing.assert_array_equal(d_only[i], o.run_spf(int(s_), True, None).dist)
 
 
 @pytest.mark.parametrize("seed", [0, 1])
