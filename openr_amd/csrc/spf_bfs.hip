@@ -79,7 +79,7 @@ struct BfsLayout {
 // array (capacity V, never wraps) in the fallback path.
 __host__ __device__ inline BfsLayout bfs_layout(uint32_t V, uint32_t L, bool has_ign, uint32_t fb, uint32_t ring_cap) {
   BfsLayout l;
-  uint32_t off = 64;  // control: append counters [0..3], overflow flag [4], target [5], pull sums [8..11]
+  uint32_t off = 32;  // control: append counters [0..3], overflow flag [4], target [5]
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
@@ -133,54 +133,6 @@ __device__ __forceinline__ void write_out(const SolveArgs& a, uint32_t k, uint32
     const uint32_t x = S::field(st, v) >> S::kNhs;
     nrow[i] = j < 4u ? (uint8_t)(x >> (8u * j)) : (uint8_t)0;
   }
-}
-
-// Direction choice for level L -> L+1 (lean edge loop; Beamer et al.'s direction-optimizing
-// BFS): push expands the frontier's out-edges, pull scans every unreached node's edges for
-// in-neighbours on level L. With every link present in both directions and up / down per
-// link (set_graph enforces both), v's tight in-edges u -> v are exactly the usable edges
-// v -> u of v's own row whose head u is on level L and not a sink. Called only when the
-// unreached nodes are few next to the frontier (a candidate level); this pass settles
-// level L as push would (distances, sink marks — so level-L sinks never read as level L)
-// and sums the frontier's transit-row lengths (m_f) and the unreached nodes' row lengths
-// (m_u). Pull when m_u < m_f. `npc` counts the candidate levels: the two sum slots
-// alternate, each zeroed one candidate before its use (>= 1 barrier after its last read).
-template <int FB, int BLOCK, bool RING>
-__device__ __forceinline__ bool choose_pull(const DevGraph& g, uint32_t* st, uint32_t* ctl, const uint16_t* ring,
-                                            uint32_t rmask, uint32_t head, uint32_t tail, uint64_t* drow, uint64_t dL,
-                                            uint32_t& npc) {
-  using S = State<FB>;
-  const uint32_t tid = threadIdx.x, V = g.V;
-  uint32_t* sums = &ctl[8u + 2u * (npc & 1u)];
-  if (tid == 0) {
-    ctl[8u + 2u * ((npc + 1u) & 1u)] = 0;
-    ctl[9u + 2u * ((npc + 1u) & 1u)] = 0;
-  }
-  ++npc;
-  uint32_t mf = 0, mu = 0;
-  for (uint32_t i = head + tid; i < tail; i += BLOCK) {
-    const uint32_t u = ring[RING ? (i & rmask) : i];
-    const uint2 r = g.row2t[u];
-    if (drow) drow[u] = dL;
-    if (r.x & kNodeSink) atomicOr(&st[S::word(u)], kCodeSettledSink << S::shift(u));
-    else mf += r.y - r.x;
-  }
-  for (uint32_t v = tid; v < V; v += BLOCK)
-    if ((S::field(st, v) & kCodeMask) == 0u) {
-      const uint2 r = g.row2[v];
-      mu += r.y - r.x;
-    }
-#pragma unroll
-  for (uint32_t o = 32; o; o >>= 1) {
-    mf += __shfl_xor(mf, o);
-    mu += __shfl_xor(mu, o);
-  }
-  if (__lane_id() == 0) {
-    atomicAdd(&sums[0], mf);
-    atomicAdd(&sums[1], mu);
-  }
-  lds_barrier();
-  return sums[1] < sums[0];
 }
 
 // ELLM: 0 = CSR rows only; 1 = the first 4 edges of a row from one 16-byte ELL load,
@@ -259,7 +211,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
       for (uint32_t i = tid; i < st_words; i += BLOCK) st[i] = 0;
       if (has_ign)
         for (uint32_t i = tid; i < ign_words; i += BLOCK) ign[i] = 0;
-      if (tid < 16) ctl[tid] = 0;
+      if (tid < 8) ctl[tid] = 0;
       __syncthreads();
       if (has_ign) load_ignore(ign, ign_words, a, sid, g.L);
       if (tid == 0) {
@@ -305,7 +257,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
 
       uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2);
       bool overflow = false;  // block-uniform
-      uint32_t npc = 0;       // candidate levels for the pull direction (choose_pull)
       while (head < tail) {
         uint32_t* cnt = &ctl[L & 3u];
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
@@ -362,62 +313,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
             }
           }
         }
-        bool pull = false;  // block-uniform
-        if (kLeanT && !a.target && a.pull && V - tail <= a.pull * (tail - head))
-          pull = choose_pull<FB, BLOCK, RING>(g, st, ctl, ring, rmask, head, tail, own_dist ? drow : nullptr, dL, npc);
-        if (kLeanT && pull) {
-          // pull: each unreached node (G lanes, K edges per lane in flight) ORs nh(u) of its
-          // level-L in-neighbours u (bit 0 marks a hit when nh is empty: distances only);
-          // the node's owner group is its only writer this level
-          const uint32_t cL = level_code(L);
-          for (uint32_t vb = 0; vb < V; vb += ngroups) {
-            if (vb + wave * groups_per_wave >= V) continue;  // uniform
-            const uint32_t v = vb + group;
-            uint32_t beg = 0, end = 0;
-            if (v < V && (S::field(st, v) & kCodeMask) == 0u) {
-              const uint2 r = g.row2[v];
-              beg = r.x;
-              end = r.y;
-            }
-            uint32_t x = 0;
-            for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
-              uint32_t vv[K], f[K];
-#pragma unroll
-              for (int j = 0; j < K; ++j) {
-                const uint32_t e = e0 + j * G;
-                const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;
-                vv[j] = (raw & kEdgeDown) ? V : raw;  // the sentinel: settled, never level L
-              }
-#pragma unroll
-              for (int j = 0; j < K; ++j) f[j] = S::field(st, vv[j]);
-#pragma unroll
-              for (int j = 0; j < K; ++j)
-                if ((f[j] & kCodeMask) == cL) x |= (f[j] & S::kNhMask) | 1u;
-            }
-#pragma unroll
-            for (uint32_t o = 1; o < 64u; o <<= 1)
-              if (o < G) x |= __shfl_xor(x, o);
-            const bool fresh = lane_g == 0 && x != 0u;
-            if (fresh) atomicOr(&st[S::word(v)], ((x & S::kNhMask) | cnext) << S::shift(v));
-            const unsigned long long b = __builtin_amdgcn_ballot_w64(fresh);
-            if (b) {  // wave-uniform; the first active lane claims the slots (readfirstlane)
-              const int leader = __ffsll((long long)__ballot(1)) - 1;
-              uint32_t wbase = 0;
-              if ((int)lane == leader) wbase = atomicAdd(cnt, (uint32_t)__popcll(b));
-              const uint32_t base = tail + __builtin_amdgcn_readfirstlane(wbase);
-              if (!RING || base + (uint32_t)__popcll(b) - head <= ring_cap) {
-                if (fresh)
-                  ring[RING ? ((base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))) &
-                               rmask)
-                            : base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] = (uint16_t)v;
-              } else if ((int)lane == leader) {
-                ctl[4] = 1;  // two adjacent levels exceed the ring
-              }
-            }
-          }
-        } else
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
           if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no slice (uniform)
           OPENR_PROF_STAMP(t0);
@@ -832,7 +727,7 @@ struct WideLayout {
 };
 __host__ __device__ inline WideLayout wide_layout(uint32_t V, uint32_t nw) {
   WideLayout l;
-  uint32_t off = 64;  // control: append counters [0..3], pull sums [8..11]
+  uint32_t off = 32;  // control: append counters [0..3]
   auto take = [&](uint32_t bytes) {
     uint32_t o = off;
     off += (bytes + 15u) & ~15u;
@@ -873,7 +768,7 @@ __global__ __launch_bounds__(BLOCK) void bfs_wide_kernel(DevGraph g, SolveArgs a
       uint64_t* drow = a.dist + out_row_of(a, sid) * V;
       for (uint32_t i = tid; i < V + 1u; i += BLOCK) st[i] = 0;
       for (uint32_t i = tid; i < ne * V; i += BLOCK) ext[i] = 0;
-      if (tid < 16) ctl[tid] = 0;
+      if (tid < 8) ctl[tid] = 0;
       __syncthreads();
       if (tid == 0) {
         st[V] = kCodeSettledSink;  // the sentinel
@@ -903,68 +798,11 @@ __global__ __launch_bounds__(BLOCK) void bfs_wide_kernel(DevGraph g, SolveArgs a
         }
       }
       __syncthreads();
-      uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2), npc = 0;
+      uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2);
       while (head < tail) {
         uint32_t* cnt = &ctl[L & 3u];
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
         const uint64_t dL = (uint64_t)L * cost;
-        bool pull = false;  // block-uniform (choose_pull)
-        if (a.pull && V - tail <= a.pull * (tail - head)) pull = choose_pull<32, BLOCK, false>(g, st, ctl, ring, 0u, head, tail, drow, dL, npc);
-        if (pull) {
-          // pull (as the 32-bit lean pass), all words: the owner group of an unreached node
-          // is its only writer this level, so its words are plain stores
-          const uint32_t cL = level_code(L);
-          for (uint32_t vb = 0; vb < V; vb += ngroups) {
-            if (vb + wave * groups_per_wave >= V) continue;  // uniform
-            const uint32_t v = vb + group;
-            uint32_t beg = 0, end = 0;
-            if (v < V && (st[v] & kCodeMask) == 0u) {
-              const uint2 r = g.row2[v];
-              beg = r.x;
-              end = r.y;
-            }
-            uint32_t x = 0, xs[NW - 1u];
-#pragma unroll
-            for (uint32_t q = 0; q < NW - 1u; ++q) xs[q] = 0;
-            for (uint32_t e0 = beg + lane_g; __any(e0 < end); e0 += G * K) {
-              uint32_t vv[K], f[K];
-#pragma unroll
-              for (int j = 0; j < K; ++j) {
-                const uint32_t e = e0 + j * G;
-                const uint32_t raw = e < end ? g.adj[e] : kEdgeDown;
-                vv[j] = (raw & kEdgeDown) ? V : raw;
-              }
-#pragma unroll
-              for (int j = 0; j < K; ++j) f[j] = st[vv[j]];
-#pragma unroll
-              for (int j = 0; j < K; ++j) {
-                if ((f[j] & kCodeMask) == cL) {
-                  x |= (f[j] & S::kNhMask) | 1u;
-#pragma unroll
-                  for (uint32_t q = 0; q < NW - 1u; ++q)
-                    if (q < ne) xs[q] |= ext[q * V + vv[j]];
-                }
-              }
-            }
-#pragma unroll
-            for (uint32_t o = 1; o < 64u; o <<= 1) {
-              if (o < G) {
-                x |= __shfl_xor(x, o);
-#pragma unroll
-                for (uint32_t q = 0; q < NW - 1u; ++q) xs[q] |= __shfl_xor(xs[q], o);
-              }
-            }
-            const bool fresh = lane_g == 0 && x != 0u;
-            if (fresh) {
-              st[v] = (x & S::kNhMask) | cnext;
-#pragma unroll
-              for (uint32_t q = 0; q < NW - 1u; ++q)
-                if (q < ne) ext[q * V + v] = xs[q];
-            }
-            const uint32_t slot = wave_append(fresh, cnt);
-            if (fresh) ring[tail + slot] = (uint16_t)v;
-          }
-        } else
         for (uint32_t fb = head; fb < tail; fb += ngroups) {
           if (fb + wave * groups_per_wave >= tail) continue;  // this wave has no frontier node (uniform)
           const uint32_t idx = fb + group;
@@ -1124,25 +962,11 @@ uint32_t bfs_code_lds_bytes(uint32_t V, uint32_t L, bool has_ignore, int cls) {
   return t <= kMaxLds ? t : 0;
 }
 
-static hipError_t launch_bfs_code_args(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
-                                       int num_cus, hipStream_t s, LaunchInfo* info);
-
 hipError_t launch_bfs_code(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes, int num_cus,
                            hipStream_t s, LaunchInfo* info) {
   const bool has_ign = a.ign_ptr != nullptr;
   const int cls = (int)a.cls;
   if (!bfs_code_lds_bytes(g.V, g.L, has_ign, cls)) return hipErrorInvalidValue;
-  // pull candidates: the unreached nodes at most 8x the frontier (OPENR_SPF_PULL: another
-  // factor; 0 = push only, tests / A/B)
-  SolveArgs ap = a;
-  ap.pull = env_u32("OPENR_SPF_PULL", 8u, 0u, 1024u);
-  return launch_bfs_code_args(g, ap, cost, group_lanes, num_cus, s, info);
-}
-
-static hipError_t launch_bfs_code_args(const DevGraph& g, const SolveArgs& a, uint64_t cost, int group_lanes,
-                                       int num_cus, hipStream_t s, LaunchInfo* info) {
-  const bool has_ign = a.ign_ptr != nullptr;
-  const int cls = (int)a.cls;
   const bool sliced = cls == kClsSliced;
   if (sliced && (a.nsl < 1u || a.nsl > 11u)) return hipErrorInvalidValue;
   if (a.n == 0) return hipSuccess;

@@ -111,9 +111,6 @@ struct SolveArgs {
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
   uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class)
-  // code family, lean passes: a level is a pull candidate when the unreached nodes number
-  // at most pull x the frontier (spf_bfs.hip choose_pull); 0 = push only (set by launch_bfs_code)
-  uint32_t pull;
   // nullable, honoured by dist_only code-family solves: solve sid may stop once the level
   // of target[sid] is known; nodes at the target's distance or farther, other than the
   // target, then read UINT64_MAX (a KSP trace to the target only reads nodes nearer)

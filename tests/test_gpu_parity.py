@@ -658,38 +658,6 @@ def fabric_with_faults(seed, n_ovl=12, n_down=60):
     return g.patched([], [], links, [0] * len(links), nodes, [1] * len(nodes)), nodes
 
 
-@pytest.mark.parametrize("pull", ["0", "1", "8", "1024"])
-def test_code_family_pull_levels(eng, monkeypatch, pull):
-    """Direction-optimising levels of the code family's lean passes (spf_bfs.hip
-    choose_pull): a level whose unreached nodes number at most OPENR_SPF_PULL x the
-    frontier may be solved by pull (unreached nodes OR the next hops of their level-L
-    in-neighbours) when their edges are fewer than the frontier's. Factor 0 = push only,
-    1024 = every level a candidate. Fabrics with sinks and down links (pull reads v's own
-    row: link state per link), a hub graph (wide-pass words and the sliced pass), a random
-    graph with parallel links, a small forced ring, and distances-only solves."""
-    monkeypatch.setenv("OPENR_SPF_BFS_FAMILY", "code")
-    monkeypatch.setenv("OPENR_SPF_PULL", pull)
-    g, _ = fabric_with_faults(7)
-    check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
-    hub = hub_graph(5)
-    check_against_oracle(eng, hub, list(range(hub.num_nodes)), True, check_pathlinks=False)
-    monkeypatch.setenv("OPENR_SPF_WIDE", "0")
-    check_against_oracle(eng, hub, list(range(0, hub.num_nodes, 3)), True, check_pathlinks=False)
-    monkeypatch.delenv("OPENR_SPF_WIDE")
-    rg = random_graph(11, 2000, 9000, 1, p_ovl=0.05, p_down=0.05, p_par=0.1)
-    check_against_oracle(eng, rg, list(range(0, rg.num_nodes, 5)), True, check_pathlinks=False)
-    monkeypatch.setenv("OPENR_SPF_RING_CAP", "256")
-    check_against_oracle(eng, rg, list(range(0, rg.num_nodes, 13)), True, check_pathlinks=False)
-    monkeypatch.delenv("OPENR_SPF_RING_CAP")
-    eng.set_graph(g)
-    o = Oracle(g)
-    srcs = list(range(0, g.num_nodes, 7))
-    d_only, nh, _ = eng.solve(srcs, True, want_nh=False)
-    assert nh is None
-    for i, s_ in enumerate(srcs):
-        np.testing.assert_array_equal(d_only[i], o.run_spf(int(s_), True, None).dist)
-
-
 @pytest.mark.parametrize("seed", [0, 1])
 def test_fabric_faults_all_sources_and_ksp2(eng, seed):
     """Last-level skip (every node reached) and the KSP2 second SPF's target pull tests
