@@ -648,6 +648,15 @@ hipError_t launch_bfs_fb(const DevGraph& g, const SolveArgs& a, uint64_t cost, u
     if (ellm == 1) return launch_bfs_shape<FB, 1024, 1, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
     return launch_bfs_shape<FB, 1024, 0, SLICED>(g, a, cost, glog, has_ign, 0u, num_cus, s, info);
   }
+  // High-degree graphs (G > 1 lanes per frontier node, CSR rows) with at most 8 solves per
+  // CU by LDS, full solves (no ignore set, no target): 512-thread workgroups, four per CU —
+  // fewer solves in flight, each with twice the lanes (fabric 16-bit class: all-sources
+  // launch 0.628 -> 0.601 ms). The KSP2 second SPFs (ignore set + target) keep 256 threads
+  // (fabric all pairs 2 453 vs 2 504 ms with 512). OPENR_SPF_BFS_BLOCK=256 (tests, A/B): the
+  // 256-thread shape everywhere.
+  if (ellm == 0 && sh.block == 256 && !has_ign && !a.target &&
+      env_u32("OPENR_SPF_BFS_BLOCK", 512u, 256u, 512u) == 512u)
+    OPENR_BFS_SHAPE(512, 0);
   if (sh.block == 128) {
     if (ellm == 2) OPENR_BFS_SHAPE(128, 2);
     if (ellm == 1) OPENR_BFS_SHAPE(128, 1);

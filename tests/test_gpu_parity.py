@@ -151,8 +151,12 @@ def test_grid100_all_sources_properties(eng):
 
 
 # --- fabrics / WAN -------------------------------------------------------------
+@pytest.mark.parametrize("block", ["512", "256"])
 @pytest.mark.parametrize("faithful", [False, True])
-def test_fabric_small_all_sources(eng, faithful):
+def test_fabric_small_all_sources(eng, monkeypatch, faithful, block):
+    """All sources of a 3-pod fabric; the code family's high-degree classes on 512-thread
+    workgroups (default) and on the 256-thread shape (OPENR_SPF_BFS_BLOCK=256)."""
+    monkeypatch.setenv("OPENR_SPF_BFS_BLOCK", block)
     g = T.fabric(288 + 3 * 56, faithful=faithful)  # 3 pods, max degree 84
     check_against_oracle(eng, g, list(range(g.num_nodes)), True, check_pathlinks=False)
     check_against_oracle(eng, g, list(range(0, g.num_nodes, 37)), True, check_pathlinks=True)
