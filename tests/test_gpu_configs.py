@@ -151,6 +151,39 @@ def test_config4_wan_whatif_all_links(eng, mode, monkeypatch):
     assert changed.sum() > 0 and solved >= len(sources)
 
 
+def test_config4_wan_whatif_full_workload(eng):
+    """The whole benchmarked what-if workload — every one of the 3 000 links x every one
+    of the 1 000 sources, 3 M units — in the default mode (grouped repair + seeded
+    re-solves), each unit's changed-node count against the oracle's re-solve
+    runSpf(src, true, {link}) (the oracle runs on the host's worker threads)."""
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    links = np.arange(g.num_links, dtype=np.uint32)
+    sources = np.arange(g.num_nodes, dtype=np.uint32)
+    changed, solved = eng.whatif(links, sources, True)
+    want = Oracle(g).whatif(links, sources, True)
+    bad = np.argwhere(changed != want)
+    assert bad.size == 0, f"{len(bad)} (link, source) units differ: {bad[:8].tolist()}"
+    assert changed.shape == (3000, 1000) and changed.sum() > 0
+
+
+def test_config5_fabric_ksp2_more_sources(eng):
+    """KSP2 on the fabric for 40 more sources spread over the id range (SSWs, FSWs and
+    RSWs of many pods) x every destination: 199 680 pairs (0.8 % of the benchmarked 24.9 M),
+    both path lists edge for edge against the oracle."""
+    g = T.fabric(5000)
+    eng.set_graph(g)
+    V = g.num_nodes
+    srcs = np.linspace(1, V - 2, 40).astype(np.uint32)
+    src = np.repeat(srcs, V)
+    dst = np.tile(np.arange(V, dtype=np.uint32), len(srcs))
+    t1, t2 = eng.ksp2_tokens(src, dst, 1024)
+    o1, o2 = Oracle(g).ksp2_tokens(src, dst, 1024)
+    for i in range(len(src)):
+        for k, (a, b) in enumerate(((t1, o1), (t2, o2))):
+            assert decode_paths(a[i]) == decode_paths(b[i]), (int(src[i]), int(dst[i]), k + 1)
+
+
 def test_config5_fabric_ksp2_all_destinations(eng):
     """KSP2 on the fabric: getKthPaths(src, dst, 1) and (.., 2) for EVERY destination of an
     SSW, an FSW and an RSW source (3 x 4 992 pairs), traced on the device, edge for edge
