@@ -304,7 +304,8 @@ def whatif_main(args):
                 "B(src) credited per what-if unit (link x source), units resolved by its fused tight-edge filter "
                 f"included (affected units only: {bytes_solved / kern_s / 1e9:.1f} GB/s credited). The repair reads "
                 "base rows staged once per (source, link chunk) in LDS instead of solving, so credited frac > 1; "
-                "its bound is LDS latency, not HBM (DESIGN.md 5.3)"), kernel_ms_mean=kern_s * 1e3),
+                "its bound is LDS latency, not HBM (DESIGN.md 5.3)", pmc=pmc,
+                scope="one launch of whatif_group_kernel"), kernel_ms_mean=kern_s * 1e3),
         }
         if ucmp is not None:
             out["ucmp_routes"] = ucmp
@@ -337,9 +338,10 @@ def load_pmc(name):
         return None
 
 
-def roofline_with_physical(credited_bytes, seconds, traffic, note):
+def roofline_with_physical(credited_bytes, seconds, traffic, note, pmc=None, scope=None):
     """HBM roofline of a launch / step: `credited_bytes` are SURVEY.md 8d's algorithmic bytes,
-    `traffic` the PMC-measured HBM bytes of the same launch (or None). Where the credited
+    `traffic` the PMC-measured HBM bytes of the same launch (or None), taken from the tracked
+    summary `pmc` (load_pmc: its path goes into traffic_label.source). Where the credited
     fraction exceeds 1 (the kernel does not move the bytes the formula credits), the
     reported achieved / frac are the physical ones, the credited ones kept."""
     credited = credited_bytes / seconds / 1e9 if seconds > 0 else 0.0
@@ -349,6 +351,8 @@ def roofline_with_physical(credited_bytes, seconds, traffic, note):
          "credited_gbs": credited, "credited_frac": credited / HBM_PEAK_GBS,
          "physical_gbs": phys, "physical_frac": phys / HBM_PEAK_GBS if phys is not None else None,
          "seconds_per_launch": seconds, "note": note}
+    if traffic is not None and pmc:
+        r["traffic_label"] = {"source": pmc.get("_path"), "scope": scope, "correction": pmc.get("correction")}
     if credited / HBM_PEAK_GBS > 1.0 and phys is not None:
         r["achieved"], r["frac"] = phys, phys / HBM_PEAK_GBS
         r["note"] = note + "; credited frac > 1, so achieved / frac are the PMC-measured (physical) bytes"
@@ -472,7 +476,9 @@ def ksp2_main(args):
                 per_pair * n_pairs, step_s, traffic,
                 "per GPU, whole step (base SPFs, k=1 / k=2 traces, second SPFs): SURVEY.md 8d B(src) per second "
                 "SPF (one per pair), k=1 base SPFs and traces not credited; traffic = PMC HBM bytes of every engine "
-                "kernel per pair (" + (pmc or {}).get("_path", "no PMC summary") + ") x this step's pairs"),
+                "kernel per pair (" + (pmc or {}).get("_path", "no PMC summary") + ") x this step's pairs",
+                pmc=pmc, scope="every engine kernel of a KSP2 step on the summary's sources, per pair, x this "
+                              "step's pairs"),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ksp2_cpu_baseline(g, min(args.cpu_seconds, 10.0))
