@@ -2,6 +2,8 @@
 # Round 5 experiment: the code family's lean edge loop with 8 edges per lane (k8), the next
 # step's edge loads issued before this step's LDS work (pf4), and both (pf8), against the
 # default (4 edges, no prefetch). Fabric all-sources launch time + fabric parity per variant.
+# The variant libraries (_variants/<name>/, untracked) were compile-time builds of
+# spf_bfs.hip whose experiment macros were removed after this measurement.
 set -o pipefail
 O=gpurun_out/lean_var; mkdir -p $O
 cp openr_amd/lib/libopenr_spf.so $O/default.so
