@@ -98,6 +98,7 @@ struct Device {
   size_t ktag_rows = 0;      // entries of krows16 zeroed for tagging
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
+  DevBuf<uint32_t> kkeep, kpart;  // KSP pairs that need a second SPF; its count as a class partition
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
@@ -341,6 +342,10 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
     return launch_fringe(d.g, a, p.delta, p.dist64, p.nh_mode, d.num_cus, s, &info);
   }
   const int gl = (int)ctx->group_lanes;
+  // a caller's list of the batch (KSP2 second SPFs: the pairs ksp_select_pairs kept) is
+  // honoured by the single-class distance-only launch; every other launch partitions
+  const uint32_t* list = a.perm;
+  const uint32_t* list_part = a.part;
   a.perm = nullptr;
   a.part = nullptr;
   const int fam = p.family;
@@ -367,6 +372,10 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   }
   if (__builtin_popcount(mask) == 1) {
     a.cls = (uint32_t)__builtin_ctz(mask);
+    if (a.dist_only && list) {  // part[cls] = listed count, part[kMaxClasses + cls] = 0
+      a.perm = list;
+      a.part = list_part;
+    }
     return launch_bfs(fam, d.g, a, p.cost, gl, d.num_cus, s, &info);
   }
   hipError_t err = d.perm.reserve(std::max<uint32_t>(a.n, 1u));
@@ -777,6 +786,11 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   const char* tag_env = std::getenv("OPENR_SPF_KSP_TAG");  // 0: untagged rows, unreached fill (A/B)
   const bool tagged = rows16 && tag_max && !(tag_env && std::atoi(tag_env) == 0);
   const size_t row_bytes = (size_t)V * (rows16 ? 2u : 8u);
+  // pairs whose k = 2 answer is empty by construction skip the second SPF and the k = 2
+  // trace (ksp_select_pairs); the code family's single-class distance-only launch takes
+  // the kept list. OPENR_SPF_KSP_SKIP=0: every pair solved and traced (A/B, tests).
+  const char* skip_env = std::getenv("OPENR_SPF_KSP_SKIP");
+  const bool skip = rows16 && !(skip_env && std::atoi(skip_env) == 0);
   // pairs per chunk from a byte budget for the chunk's rows and ignore slots: 8 GiB of the
   // 288 GB, capped at half the device memory free at the call, and halved again
   // when a reservation still fails. Fabric, 512 sources x all destinations, ms per step by
@@ -808,6 +822,8 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     if ((e2 = d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V)) != hipSuccess) return e2;
     if ((e2 = d.ksrc.reserve(c)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)c * ctx->nsl_max())) != hipSuccess) return e2;
+    if (skip && (e2 = d.kkeep.reserve(c)) != hipSuccess) return e2;
+    if (skip && (e2 = d.kpart.reserve(2u * kMaxClasses)) != hipSuccess) return e2;
     return d.kretry.reserve(8u + 2u * (size_t)c);
   };
   for (;;) {
@@ -845,10 +861,22 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, rlist1, rcount, nullptr,
                                nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u));
-    OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, ls));
+    const uint32_t* keep = nullptr;  // chunk-local pairs left for the second SPF (skip)
+    const uint32_t* keep_count = nullptr;
+    if (skip) {
+      OPENR_TRY(hipMemsetAsync(d.kpart.p, 0, 2u * kMaxClasses * sizeof(uint32_t), ls));
+      OPENR_TRY(launch_ksp_select_pairs(d.g, d_sources, d_prow, d_pdst, first, m, d_tok1, d_tok2, tok_cap, d.ksrc.p,
+                                        d.kkeep.p, d.kpart.p + kCls8, d.num_cus, ls));
+      keep = d.kkeep.p;
+      keep_count = d.kpart.p + kCls8;
+    } else {
+      OPENR_TRY(launch_gather_sources(d_sources, d_prow, first, m, d.ksrc.p, d.num_cus, ls));
+    }
     SolveArgs b{};
     b.sources = d.ksrc.p;
     b.n = m;
+    b.perm = keep;  // launch(): the distance-only class runs over keep[0 .. *keep_count)
+    b.part = skip ? d.kpart.p : nullptr;
     b.ign_ptr = d.kptr.p;  // pair k ignores kign[k * ign_cap, kend[k])
     b.ign_end = d.kend.p;
     b.ign_links = d.kign.p;
@@ -871,7 +899,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     const uint64_t* r2 = rows16 ? nullptr : d.krows.p;
     const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
-                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, nullptr, nullptr,
+                               tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, keep, keep_count,
                                rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u,
                                tagged ? (b.lvl_tag << 8 | lshift) : 0u));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,

@@ -324,6 +324,14 @@ uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_ma
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);
+// After the k = 1 trace of a chunk: pairs whose k = 2 answer is empty by construction get
+// n_paths = 0 in tok2; the others are listed (chunk-local k, list[0 .. *count), count
+// zeroed by the caller) for the second SPF and the k = 2 trace. Also writes out_src[k] =
+// the pair's source for every k (launch_gather_sources).
+hipError_t launch_ksp_select_pairs(const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
+                                   const uint32_t* pdst, uint32_t first, uint32_t n, const uint32_t* tok1,
+                                   uint32_t* tok2, uint32_t tok_cap, uint32_t* out_src, uint32_t* list,
+                                   uint32_t* count, int num_cus, hipStream_t s);
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg);
 
 // Exact-order kernel (spf_exact.hip): LinkState::runSpf's heap process replayed per solve

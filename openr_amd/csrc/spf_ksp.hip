@@ -701,6 +701,46 @@ __global__ __launch_bounds__(256) void gather_sources(const uint32_t* sources, c
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) out[i] = sources[prow[first + i]];
 }
 
+// getKthPaths(src, dest, 2) (LinkState.cpp:762-791) is empty without a second SPF when
+//  * k = 1 found no path (dest unreached, or src == dest): the ignore set is empty, so
+//    k = 2 re-traces the same base result and finds nothing either;
+//  * the k = 1 paths use every link of src, or every link of dest: they are edge-disjoint
+//    and simple (positive metrics), so each uses a distinct first and a distinct last
+//    link, and n_paths == |row| means the whole row is ignored. runSpf(src, true, ignore)
+//    then settles src alone, or never dest, and res.count(dest) == 0. (A row holding a
+//    self-loop is longer than the links a path can use: such pairs are kept.)
+// On the fabric every RSW -> RSW pair (65 % of all pairs) is of the second kind.
+// Those pairs get n_paths = 0 here; the rest are appended to `list` for the second SPF
+// and the k = 2 trace. A k = 1 row marked bad (0xFFFFFFFF) is kept.
+__global__ __launch_bounds__(256) void ksp_select_pairs(DevGraph g, const uint32_t* sources, const uint32_t* prow,
+                                                        const uint32_t* pdst, uint32_t first, uint32_t n,
+                                                        const uint32_t* tok1, uint32_t* tok2, uint32_t tok_cap,
+                                                        uint32_t* out_src, uint32_t* list, uint32_t* count) {
+  const uint32_t lane = __lane_id();
+  for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {  // block-uniform: whole waves ballot
+    const uint32_t k = i0 + threadIdx.x;
+    bool keep = false;
+    if (k < n) {
+      const uint32_t pair = first + k;
+      const uint32_t src = sources[prow[pair]], dst = pdst[pair];
+      out_src[k] = src;
+      const uint32_t np = tok1[(size_t)pair * tok_cap];
+      bool empty = np == 0u;
+      if (np != 0u && np != 0xFFFFFFFFu && src < g.V && dst < g.V) {
+        const uint2 rs = g.row2[src], rd = g.row2[dst];
+        empty = np == rs.y - rs.x || np == rd.y - rd.x;
+      }
+      if (empty) tok2[(size_t)pair * tok_cap] = 0u;
+      keep = !empty;
+    }
+    const uint64_t b = __ballot(keep);
+    uint32_t at = 0;
+    if (lane == 0 && b) at = atomicAdd(count, (uint32_t)__popcll(b));
+    at = __shfl(at, 0);
+    if (keep) list[at + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = k;
+  }
+}
+
 }  // namespace
 
 // A u16 copy of the pair's distance row in LDS was measured slower on the fabric (fewer
@@ -784,6 +824,17 @@ hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, 
   if (!n) return hipSuccess;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255u) / 256u, (uint32_t)num_cus * 8u));
   hipLaunchKernelGGL(gather_sources, dim3(grid), dim3(256), 0, s, sources, prow, first, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_ksp_select_pairs(const DevGraph& g, const uint32_t* sources, const uint32_t* prow,
+                                   const uint32_t* pdst, uint32_t first, uint32_t n, const uint32_t* tok1,
+                                   uint32_t* tok2, uint32_t tok_cap, uint32_t* out_src, uint32_t* list,
+                                   uint32_t* count, int num_cus, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255u) / 256u, (uint32_t)num_cus * 8u));
+  hipLaunchKernelGGL(ksp_select_pairs, dim3(grid), dim3(256), 0, s, g, sources, prow, pdst, first, n, tok1, tok2,
+                     tok_cap, out_src, list, count);
   return hipGetLastError();
 }
 

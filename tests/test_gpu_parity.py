@@ -784,3 +784,24 @@ def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (1400, 2))])
     g = T.fabric(288 + 56)
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
+
+
+@pytest.mark.parametrize("skip", ["1", "0"], ids=["skip", "solve-all"])
+def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip):
+    """Pairs whose k = 2 answer is empty by construction (no k = 1 path, or k = 1 paths
+    that use every link of the source or of the destination) skip the second SPF and the
+    k = 2 trace (ksp_select_pairs). Two-pod fabric: every RSW -> RSW pair is such a pair
+    (8 edge-disjoint paths over the 8 uplinks); leaves and self-loop-free hubs of a
+    random graph with parallel links, down links and sinks; both forms vs the oracle."""
+    monkeypatch.setenv("OPENR_SPF_KSP_SKIP", skip)
+    g = T.fabric(288 + 2 * 56)
+    V = g.num_nodes
+    rsw = [u for u in range(V) if g.names[u].startswith("3-")]
+    pairs = [(s, d) for s in rsw[::9] for d in range(V)]
+    got = check_ksp2_against_oracle(eng, g, pairs)
+    assert sum(1 for (s, d), (k1, k2) in zip(pairs, got) if d in rsw and s != d and len(k1) == 8 and not k2) > 0
+    gf, ovl = fabric_with_faults(3)
+    rng = np.random.default_rng(17)
+    check_ksp2_against_oracle(eng, gf, [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (400, 2))])
+    gr = random_graph(77, 90, 140, 1, p_ovl=0.08, p_down=0.08, p_par=0.2)
+    check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 3) for d in range(gr.num_nodes)])
