@@ -474,18 +474,30 @@ __device__ uint32_t live_src_links(const KspState& st, uint32_t dst) {
 // would re-enter it, skip or fail every candidate again and return nullopt, so the paths
 // found are the same. Returns the path length (edges in fr_edge[1..len], dest side
 // first), 0 for src == dest, -1 for no path, -2 when the DFS outgrows its frames/arena.
-__device__ int trace_one(const KspState& st, uint32_t dst) {
+//
+// `resume`: the previous trace of this pair found a path, and its dest frame (frame 0,
+// arena [0, fr_cnt[0])) is still in place. The reference's next call restarts at dest and
+// walks dest's pathLinks from the first: every one before fr_idx[0] was inserted into the
+// visited set by the previous calls (or has a dead tail), so it skips them all and goes on
+// at fr_idx[0]. The frame resumes there instead of gathering dest's row again; links
+// visited and tails killed since the gather are caught by the checks at each pop.
+__device__ int trace_one(const KspState& st, uint32_t dst, bool resume) {
   if (st.src == dst) return 0;
   const uint32_t lane = threadIdx.x;
-  const uint32_t c0 = load_path_links(st, dst, 0);
-  if (c0 == UINT32_MAX) return -2;
-  if (lane == 0) {
-    st.fr_node[0] = dst;
-    st.fr_beg[0] = 0;
-    st.fr_cnt[0] = c0;
-    st.fr_idx[0] = 0;
+  uint32_t c0;
+  if (resume) {
+    c0 = st.fr_cnt[0];
+  } else {
+    c0 = load_path_links(st, dst, 0);
+    if (c0 == UINT32_MAX) return -2;
+    if (lane == 0) {
+      st.fr_node[0] = dst;
+      st.fr_beg[0] = 0;
+      st.fr_cnt[0] = c0;
+      st.fr_idx[0] = 0;
+    }
+    lds_fence();
   }
-  lds_fence();
   uint32_t sp = 1, top = c0, entries = 0;
   bool probed = false;
   while (sp > 0) {
@@ -558,7 +570,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t ltag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, use_d16 != 0);
+  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, (use_d16 & 1u) != 0);
+  const bool resume_ok = (use_d16 & 2u) != 0;  // trace_one may resume dest's frame
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
   st.g = &g;
@@ -638,9 +651,10 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
         lds_fence();
         st.use16 = true;
       }
+      bool resume = false;  // trace_one: dest's frame kept from the last path found
       while (src_live) {
         const uint64_t tt = st.stats ? clock64() : 0, e0 = st.stats ? st.stats[kStEntries] : 0;
-        const int len = trace_one(st, dst);
+        const int len = trace_one(st, dst, resume);
         if (st.stats) {
           stat_add(st, kStTraces, 1);
           if (len <= 0) {
@@ -668,6 +682,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
         nign += (uint32_t)len;
         ++npaths;
         --src_live;
+        resume = resume_ok;
       }
     }
     if (lane == 0) {
@@ -806,7 +821,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
-                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30), ksp_use_d16(kind) ? 1u : 0u,
+                     bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30),
+                     (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1),
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
                      lcost, ltag);
   return hipGetLastError();

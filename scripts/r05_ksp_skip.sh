@@ -10,8 +10,8 @@ cd "$R" && timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-
   tests/test_gpu_parity.py -k "ksp2" tests/test_gpu_configs.py::test_config5_fabric_ksp2_all_destinations \
   tests/test_gpu_configs.py::test_config5_fabric_ksp2_more_sources > "$OUT/tests.txt" 2>&1; stop $?
 tail -2 "$OUT/tests.txt"
-for S in 1 0; do
-  OPENR_SPF_KSP_SKIP=$S timeout -k 10 300 python3 -u bench.py --workload ksp2 --steps 2 --warmup 1 --no-cpu-baseline \
-    > "$OUT/bench_skip$S.log" 2>&1; stop $?
-  echo "skip=$S $(grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_skip$S.log")"
+for S in ${SKIPS:-1 0}; do
+  OPENR_SPF_KSP_SKIP=$S OPENR_SPF_KSP_RESUME=${RESUME:-1} timeout -k 10 300 python3 -u bench.py --workload ksp2 --steps 2 --warmup 1 --no-cpu-baseline \
+    > "$OUT/bench_skip${S}_resume${RESUME:-1}.log" 2>&1; stop $?
+  echo "skip=$S $(grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_skip${S}_resume${RESUME:-1}.log")"
 done
