@@ -257,6 +257,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
 
       uint32_t head = 1, tail = 1u + ctl[0], L = 1, cnext = level_code(2);
       bool overflow = false;  // block-uniform
+      // pull test (2): the target's usable in-neighbours w, one per lane (w = V: none), and
+      // their rows, loaded at the first test of the solve and kept for the later levels
+      uint32_t pw_w = V, pw_beg = 0, pw_end = 0;
+      bool pw_ready = false;  // block-uniform
       while (head < tail) {
         uint32_t* cnt = &ctl[L & 3u];
         if (tid == 0) ctl[(L + 1u) & 3u] = 0;  // last read three barriers ago
@@ -275,6 +279,72 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
             if ((S::field(st, t) & kCodeMask) == 0u) {
               const uint2 rt = g.row2[t];
               const uint32_t cL = level_code(L);
+              if (rt.y - rt.x <= (uint32_t)BLOCK && !(a.dist_only & 2u)) {  // bit 1: per-wave form (A/B)
+                // t's row spread over the block (entry wave + lane * waves): test (1) is one
+                // ballot, and the unreached w's rows are scanned four at a time with every
+                // load in flight at once, instead of one w per wave with three dependent
+                // loads each (t's record, w's row bounds, w's row) at every level
+                if (!pw_ready) {
+                  pw_ready = true;
+                  const uint32_t i = rt.x + wave + (BLOCK / 64u) * lane;
+                  if (i < rt.y) {
+                    const uint4 rw = g.erec[i];  // t->w: {w | flags, ., link, .}
+                    if (!((rw.x & (kEdgeDown | kNodeSink)) || (has_ign && test_bit(ign, rw.z)))) {
+                      pw_w = rw.x & ~(kEdgeDown | kNodeSink);
+                      const uint2 rr = g.row2[pw_w];
+                      pw_beg = rr.x;
+                      pw_end = rr.y;
+                    }
+                  }
+                }
+                const uint32_t cw = pw_w < V ? (S::field(st, pw_w) & kCodeMask) : 0xFFu;
+                hit1 = __any(cw == cL);
+                uint64_t m = __ballot(cw == 0u);
+                const uint32_t* er = reinterpret_cast<const uint32_t*>(g.erec);
+                while (m) {
+                  uint32_t bw[4], bb[4], be[4];
+#pragma unroll
+                  for (int b = 0; b < 4; ++b) {
+                    const uint32_t j = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+                    const bool has = m != 0u;
+                    m &= m - 1u;
+                    bw[b] = has ? (uint32_t)__builtin_amdgcn_readlane((int)pw_w, (int)j) : V;
+                    bb[b] = has ? (uint32_t)__builtin_amdgcn_readlane((int)pw_beg, (int)j) : 0u;
+                    be[b] = has ? (uint32_t)__builtin_amdgcn_readlane((int)pw_end, (int)j) : 0u;
+                  }
+                  uint32_t rx[8], rz[8];
+#pragma unroll
+                  for (int c = 0; c < 8; ++c) {  // w->x records: w b = c / 2, chunk c % 2
+                    const uint32_t e = bb[c >> 1] + (uint32_t)(c & 1) * 64u + lane;
+                    const bool in = e < be[c >> 1];
+                    rx[c] = in ? er[4u * e] : kEdgeDown;
+                    rz[c] = in ? er[4u * e + 2u] : 0u;
+                  }
+#pragma unroll
+                  for (int b = 0; b < 4; ++b) {
+                    if (bw[b] >= V) continue;  // wave-uniform
+                    bool q = false;
+#pragma unroll
+                    for (int c = 2 * b; c < 2 * b + 2; ++c) {
+                      const uint32_t x = rx[c] & ~(kEdgeDown | kNodeSink);
+                      q |= !(rx[c] & (kEdgeDown | kNodeSink)) && !(has_ign && test_bit(ign, rz[c])) &&
+                           (S::field(st, x) & kCodeMask) == cL;
+                    }
+                    for (uint32_t e = bb[b] + 128u + lane; e < be[b]; e += 64u) {  // rows past 128 edges
+                      const uint32_t xr = er[4u * e];
+                      q |= !(xr & (kEdgeDown | kNodeSink)) && !(has_ign && test_bit(ign, er[4u * e + 2u])) &&
+                           (S::field(st, xr & ~(kEdgeDown | kNodeSink)) & kCodeMask) == cL;
+                    }
+                    if (__any(q)) {  // w lies on level L+1 (its code was 0, so no level-L test reads it)
+                      hit2 = true;
+                      if (lane == 0) {
+                        atomicOr(&st[S::word(bw[b])], cnext << S::shift(bw[b]));
+                        put(bw[b], L + 1u);
+                      }
+                    }
+                  }
+                }
+              } else
               for (uint32_t i = rt.x + wave; i < rt.y; i += BLOCK / 64u) {
                 const uint4 rw = g.erec[i];  // t->w: {w | flags, ., link, .} (same for all lanes)
                 if ((rw.x & (kEdgeDown | kNodeSink)) || (has_ign && test_bit(ign, rw.z))) continue;

@@ -354,6 +354,9 @@ hipError_t launch(const openr_spf_ctx* ctx, Device& d, const Plan& p, SolveArgs 
   a.dist_only = 0;
   if (fam == kFamCode && !a.nh && !a.tight) {  // distances only (KSP2 SPFs): 8-bit fields, no slices
     a.dist_only = 1;
+    // OPENR_SPF_KSP_PULL=0: the target's pull test (2) one neighbour per wave (A/B, tests)
+    if (const char* e = std::getenv("OPENR_SPF_KSP_PULL"))
+      if (std::atoi(e) == 0) a.dist_only |= 2u;
     a.nsl = 1;
     mask = 1u << kCls8;
   }

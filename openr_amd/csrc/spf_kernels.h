@@ -110,7 +110,8 @@ struct SolveArgs {
   const uint32_t* part;       // [2 * kMaxClasses]: counts, then offsets
   uint32_t cls;
   uint32_t nsl;               // next-hop slices per solve (sliced class), else 1
-  uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class)
+  uint32_t dist_only;         // code family: no next-hop output, so no next-hop bits (one class);
+                              // bit 1: the KSP2 target's pull test (2) in its per-wave form (A/B)
   // nullable, honoured by dist_only code-family solves: solve sid may stop once the level
   // of target[sid] is known; nodes at the target's distance or farther, other than the
   // target, then read UINT64_MAX (a KSP trace to the target only reads nodes nearer)
