@@ -484,9 +484,10 @@ __device__ uint32_t live_src_links(const KspState& st, uint32_t dst) {
 __device__ int trace_one(const KspState& st, uint32_t dst, bool resume) {
   if (st.src == dst) return 0;
   const uint32_t lane = threadIdx.x;
-  uint32_t c0;
+  uint32_t c0, i0 = 0;
   if (resume) {
-    c0 = st.fr_cnt[0];
+    c0 = __builtin_amdgcn_readfirstlane(st.fr_cnt[0]);
+    i0 = __builtin_amdgcn_readfirstlane(st.fr_idx[0]);
   } else {
     c0 = load_path_links(st, dst, 0);
     if (c0 == UINT32_MAX) return -2;
@@ -494,37 +495,43 @@ __device__ int trace_one(const KspState& st, uint32_t dst, bool resume) {
       st.fr_node[0] = dst;
       st.fr_beg[0] = 0;
       st.fr_cnt[0] = c0;
-      st.fr_idx[0] = 0;
     }
     lds_fence();
   }
-  uint32_t sp = 1, top = c0, entries = 0;
+  // the top frame's (next index, count, arena begin) live in registers (wave-uniform);
+  // fr_idx of a frame is written when a child is pushed over it and read back on the pop
+  uint32_t sp = 1, top = c0, entries = 0, fi = i0, fc = c0, fb = 0;
   bool probed = false;
   while (sp > 0) {
     const uint32_t f = sp - 1;
     stat_add(st, kStSteps, 1);
-    const uint32_t idx = st.fr_idx[f], cnt = st.fr_cnt[f], beg = st.fr_beg[f];
-    if (idx >= cnt) {  // exhausted: std::nullopt back to the caller frame
+    if (fi >= fc) {  // exhausted: std::nullopt back to the caller frame
       const uint32_t v = st.fr_node[f];
       if (lane == 0) st.dead[v >> 5] |= 1u << (v & 31u);
-      lds_fence();
-      top -= cnt;
+      top -= fc;
       --sp;
+      if (sp) {
+        fi = __builtin_amdgcn_readfirstlane(st.fr_idx[sp - 1]);
+        fc = __builtin_amdgcn_readfirstlane(st.fr_cnt[sp - 1]);
+        fb = __builtin_amdgcn_readfirstlane(st.fr_beg[sp - 1]);
+      }
+      lds_fence();
       continue;
     }
-    const uint32_t link = st.ar_l[beg + idx], u = st.ar_u[beg + idx];
+    const uint32_t idx = fi++;
+    const uint32_t link = st.ar_l[fb + idx], u = st.ar_u[fb + idx];
     const bool fresh = !test_bit(st.vis, link);
     const bool live = !test_bit(st.dead, u);
-    if (lane == 0) {
-      st.fr_idx[f] = idx + 1u;
-      if (fresh && live) st.vis[link >> 5] |= 1u << (link & 31u);
-    }
+    if (lane == 0 && fresh && live) st.vis[link >> 5] |= 1u << (link & 31u);
     lds_fence();
     if (!fresh || !live) continue;  // insert() failed, or a subtree known to fail
     if (sp >= st.max_depth) return -2;
-    const uint32_t re = st.ar_e[beg + idx];
+    const uint32_t re = st.ar_e[fb + idx];
     if (u == st.src) {
-      if (lane == 0) st.fr_edge[sp] = re;
+      if (lane == 0) {
+        st.fr_edge[sp] = re;
+        st.fr_idx[f] = fi;  // frame 0's position for a resumed next trace
+      }
       lds_fence();
       return (int)sp;
     }
@@ -535,13 +542,16 @@ __device__ int trace_one(const KspState& st, uint32_t dst, bool resume) {
     const uint32_t c = load_path_links(st, u, top);
     if (c == UINT32_MAX) return -2;
     if (lane == 0) {
+      st.fr_idx[f] = fi;
       st.fr_edge[sp] = re;
       st.fr_node[sp] = u;
       st.fr_beg[sp] = top;
       st.fr_cnt[sp] = c;
-      st.fr_idx[sp] = 0;
     }
     lds_fence();
+    fi = 0;
+    fc = c;
+    fb = top;
     top += c;
     ++sp;
   }
