@@ -88,7 +88,16 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   return l;
 }
 
+// The tracer's workgroup is one wavefront, and a wavefront's LDS instructions execute in
+// issue order, so a read issued after another lane's write sees it: between LDS accesses
+// of the tracer only the compiler's order must hold (the hardware wait, s_waitcnt
+// lgkmcnt(0), stalled every DFS step for nothing). Results in registers get their waits
+// from the compiler as usual. OPENR_SPF_KSP_WAIT builds keep the wait (A/B).
+#ifdef OPENR_SPF_KSP_WAIT
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#else
+__device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
+#endif
 
 struct KspState {
   const DevGraph* g;
