@@ -55,8 +55,10 @@ constexpr uint32_t kD16Budget = 64u * 1024u;  // LDS per wavefront up to which t
 // deg = largest row (candidate scratch of one frame); frames / arena = DFS capacity
 // (KspCaps: a small tier sized from the graph's depth for occupancy, and the full tier
 // that re-runs the pairs the small one could not hold).
+// pack: node ids and link ids below 2^16, an arena entry's tail and link share a word
+// (ar_l = link | u << 16, no ar_u): 4 B less per entry, more wavefronts per CU.
 __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg, uint32_t frames, uint32_t arena,
-                                                bool want_d16) {
+                                                bool want_d16, bool pack) {
   KspLayout l;
   uint32_t off = 16;  // control: [0] candidate count
   auto take = [&](uint32_t bytes) {
@@ -73,7 +75,7 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.fr_idx = take(4u * frames);
   l.ar_e = take(4u * arena);
   l.ar_l = take(4u * arena);
-  l.ar_u = take(4u * arena);
+  l.ar_u = pack ? 0u : take(4u * arena);
   // candidate scratch of load_path_links_long only: rows of <= 128 in-edges rank in registers
   const uint32_t sdeg = deg > 2u * kWave ? deg : 0u;
   l.skd = take(8u * sdeg);
@@ -108,6 +110,7 @@ struct KspState {
   uint32_t* dead;  // nodes whose DFS subtree failed: they can never reach src again
   uint32_t *fr_node, *fr_edge, *fr_beg, *fr_cnt, *fr_idx;  // DFS frames
   uint32_t *ar_e, *ar_l, *ar_u;                            // per-frame sorted pathLinks
+  bool pack;  // ar_l holds link | u << 16 (ksp_layout)
   uint64_t *skd, *skr;
   uint32_t *sl, *su;  // candidate scratch: link, tail
   uint32_t* seen;  // reachability probe: visited nodes (V bits)
@@ -297,13 +300,21 @@ __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg
   }
   if (c0.ok) {
     st.ar_e[beg + r0] = (uint32_t)c0.kr;
-    st.ar_l[beg + r0] = c0.link;
-    st.ar_u[beg + r0] = c0.u;
+    if (st.pack) {
+      st.ar_l[beg + r0] = c0.link | (c0.u << 16);
+    } else {
+      st.ar_l[beg + r0] = c0.link;
+      st.ar_u[beg + r0] = c0.u;
+    }
   }
   if (c1.ok) {
     st.ar_e[beg + r1] = (uint32_t)c1.kr;
-    st.ar_l[beg + r1] = c1.link;
-    st.ar_u[beg + r1] = c1.u;
+    if (st.pack) {
+      st.ar_l[beg + r1] = c1.link | (c1.u << 16);
+    } else {
+      st.ar_l[beg + r1] = c1.link;
+      st.ar_u[beg + r1] = c1.u;
+    }
   }
   lds_fence();
   if (st.stats) {
@@ -362,8 +373,12 @@ __device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_
       rank += (od < kd || (od == kd && orr < kr)) ? 1u : 0u;
     }
     st.ar_e[beg + rank] = (uint32_t)kr;  // re
-    st.ar_l[beg + rank] = st.sl[i];
-    st.ar_u[beg + rank] = st.su[i];
+    if (st.pack) {
+      st.ar_l[beg + rank] = st.sl[i] | (st.su[i] << 16);
+    } else {
+      st.ar_l[beg + rank] = st.sl[i];
+      st.ar_u[beg + rank] = st.su[i];
+    }
   }
   lds_fence();
   if (st.stats) {
@@ -528,7 +543,8 @@ __device__ int trace_one(const KspState& st, uint32_t dst, bool resume) {
       continue;
     }
     const uint32_t idx = fi++;
-    const uint32_t link = st.ar_l[fb + idx], u = st.ar_u[fb + idx];
+    const uint32_t al = st.ar_l[fb + idx];
+    const uint32_t link = st.pack ? al & 0xFFFFu : al, u = st.pack ? al >> 16 : st.ar_u[fb + idx];
     const bool fresh = !test_bit(st.vis, link);
     const bool live = !test_bit(st.dead, u);
     if (lane == 0 && fresh && live) st.vis[link >> 5] |= 1u << (link & 31u);
@@ -589,7 +605,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t ltag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, (use_d16 & 1u) != 0);
+  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, (use_d16 & 1u) != 0, (use_d16 & 8u) != 0);
   const bool resume_ok = (use_d16 & 2u) != 0;  // trace_one may resume dest's frame
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
@@ -604,7 +620,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
   st.fr_idx = reinterpret_cast<uint32_t*>(base + lay.fr_idx);
   st.ar_e = reinterpret_cast<uint32_t*>(base + lay.ar_e);
   st.ar_l = reinterpret_cast<uint32_t*>(base + lay.ar_l);
-  st.ar_u = reinterpret_cast<uint32_t*>(base + lay.ar_u);
+  st.ar_u = lay.ar_u ? reinterpret_cast<uint32_t*>(base + lay.ar_u) : nullptr;
+  st.pack = (use_d16 & 8u) != 0;
   st.skd = reinterpret_cast<uint64_t*>(base + lay.skd);
   st.skr = reinterpret_cast<uint64_t*>(base + lay.skr);
   st.sl = reinterpret_cast<uint32_t*>(base + lay.sl);
@@ -781,6 +798,12 @@ __global__ __launch_bounds__(256) void ksp_select_pairs(DevGraph g, const uint32
 // wavefronts per CU, rounds 2-3) and is not taken; the layout keeps the slot at size 0.
 bool ksp_use_d16(int) { return false; }
 
+// Packed arena entries (ksp_layout) when node and link ids fit 16 bits. Fabric small
+// tier: 11.9 -> 10.9 KB per wavefront. OPENR_SPF_KSP_PACK=0: unpacked (A/B, tests).
+bool ksp_pack(uint32_t V, uint32_t L) {
+  return V <= 65536u && L <= 65536u && bfs::env_u32("OPENR_SPF_KSP_PACK", 1u, 0u, 1u) != 0u;
+}
+
 // Small tier: a traced path has at most as many hops as the source's BFS depth on
 // uniform-cost graphs; 2x the sampled depth + 8 covers the sample's misses and weighted
 // graphs' longer hop counts, and the arena holds that many frames of typical width.
@@ -801,7 +824,7 @@ KspCaps ksp_caps(const DevGraph& g, bool full) {
 
 uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full, int kind) {
   const KspCaps c = ksp_caps(g, full);
-  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16(kind)).total;
+  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16(kind), ksp_pack(g.V, g.L)).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -815,7 +838,8 @@ uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
 uint32_t ksp_stats_count() { return kKspStats; }
 
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
-  const uint32_t t = ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16(1) || ksp_use_d16(2)).total;
+  const uint32_t t =
+      ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16(1) || ksp_use_d16(2), ksp_pack(V, L)).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -841,7 +865,8 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   hipLaunchKernelGGL(k, dim3(grid), dim3(kWave), lds, s, g, sources, prow, pdst, first, n, rows, ign_io, ign_end,
                      ign_cap, tok, tok_cap, status, qbuf,
                      bfs::env_u32("OPENR_SPF_KSP_PROBE", kKspProbeAfter, 0u, 1u << 30),
-                     (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1),
+                     (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1) |
+                         (ksp_pack(g.V, g.L) ? 8u : 0u),
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
                      lcost, ltag);
   return hipGetLastError();

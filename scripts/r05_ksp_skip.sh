@@ -11,7 +11,7 @@ cd "$R" && timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-
   tests/test_gpu_configs.py::test_config5_fabric_ksp2_more_sources > "$OUT/tests.txt" 2>&1; stop $?
 tail -2 "$OUT/tests.txt"
 for S in ${SKIPS:-1 0}; do
-  OPENR_SPF_KSP_SKIP=$S OPENR_SPF_KSP_RESUME=${RESUME:-1} OPENR_SPF_KSP_PULL=${PULL:-1} timeout -k 10 300 python3 -u bench.py --workload ksp2 --steps 2 --warmup 1 --no-cpu-baseline \
-    > "$OUT/bench_skip${S}_resume${RESUME:-1}_pull${PULL:-1}.log" 2>&1; stop $?
-  echo "skip=$S $(grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_skip${S}_resume${RESUME:-1}_pull${PULL:-1}.log")"
+  OPENR_SPF_KSP_SKIP=$S OPENR_SPF_KSP_RESUME=${RESUME:-1} OPENR_SPF_KSP_PULL=${PULL:-1} OPENR_SPF_KSP_PACK=${PACK:-1} timeout -k 10 300 python3 -u bench.py --workload ksp2 --steps 2 --warmup 1 --no-cpu-baseline \
+    > "$OUT/bench_skip${S}_resume${RESUME:-1}_pull${PULL:-1}_pack${PACK:-1}.log" 2>&1; stop $?
+  echo "skip=$S $(grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_skip${S}_resume${RESUME:-1}_pull${PULL:-1}_pack${PACK:-1}.log")"
 done

@@ -786,20 +786,23 @@ def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
 
 
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["arena-packed", "arena-wide"])
 @pytest.mark.parametrize("pull", ["1", "0"], ids=["pull-batched", "pull-per-wave"])
 @pytest.mark.parametrize("resume", ["1", "0"], ids=["resume", "regather"])
 @pytest.mark.parametrize("skip", ["1", "0"], ids=["skip", "solve-all"])
-def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip, resume, pull):
+def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip, resume, pull, pack):
     """Pairs whose k = 2 answer is empty by construction (no k = 1 path, or k = 1 paths
     that use every link of the source or of the destination) skip the second SPF and the
     k = 2 trace (ksp_select_pairs). Two-pod fabric: every RSW -> RSW pair is such a pair
     (8 edge-disjoint paths over the 8 uplinks); leaves and self-loop-free hubs of a
     random graph with parallel links, down links and sinks; both forms vs the oracle.
     Also with and without the tracer resuming dest's frame between a pair's paths, and
-    with the second SPF's pull test (2) batched over the block or one neighbour per wave."""
+    with the second SPF's pull test (2) batched over the block or one neighbour per wave,
+    and with the tracer's arena entries packed (tail | link in one word) or not."""
     monkeypatch.setenv("OPENR_SPF_KSP_SKIP", skip)
     monkeypatch.setenv("OPENR_SPF_KSP_RESUME", resume)  # trace_one resumes dest's frame
     monkeypatch.setenv("OPENR_SPF_KSP_PULL", pull)  # the second SPF's target pull test (2) form
+    monkeypatch.setenv("OPENR_SPF_KSP_PACK", pack)  # tracer arena: tail and link in one word
     g = T.fabric(288 + 2 * 56)
     V = g.num_nodes
     rsw = [u for u in range(V) if g.names[u].startswith("3-")]
