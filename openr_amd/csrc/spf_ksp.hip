@@ -58,7 +58,7 @@ constexpr uint32_t kD16Budget = 64u * 1024u;  // LDS per wavefront up to which t
 // pack: node ids and link ids below 2^16, an arena entry's tail and link share a word
 // (ar_l = link | u << 16, no ar_u): 4 B less per entry, more wavefronts per CU.
 __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t deg, uint32_t frames, uint32_t arena,
-                                                bool want_d16, bool pack) {
+                                                bool want_d16, bool pack, bool stats_on = false) {
   KspLayout l;
   uint32_t off = 16;  // control: [0] candidate count
   auto take = [&](uint32_t bytes) {
@@ -83,7 +83,7 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.sl = take(4u * sdeg);
   l.su = take(4u * sdeg);
   l.seen = take(4u * ((V + 31u) / 32u));
-  l.stats = take(8u * kKspStats);
+  l.stats = stats_on ? take(8u * kKspStats) : 0u;  // OPENR_SPF_PROF launches only
   l.d16 = 0;
   if (want_d16 && off + 2u * V + 16u <= kD16Budget) l.d16 = take(2u * V);
   l.total = off;
@@ -605,7 +605,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t ltag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
-  const KspLayout lay = ksp_layout(V, g.L, g.max_deg, frames, arena, (use_d16 & 1u) != 0, (use_d16 & 8u) != 0);
+  const KspLayout lay =
+      ksp_layout(V, g.L, g.max_deg, frames, arena, (use_d16 & 1u) != 0, (use_d16 & 8u) != 0, gstats != nullptr);
   const bool resume_ok = (use_d16 & 2u) != 0;  // trace_one may resume dest's frame
   char* base = reinterpret_cast<char*>(smem);
   KspState st;
@@ -822,9 +823,10 @@ KspCaps ksp_caps(const DevGraph& g, bool full) {
   return c;
 }
 
-uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full, int kind) {
+uint32_t ksp_tier_lds_bytes(const DevGraph& g, bool full, int kind, bool stats_on = false) {
   const KspCaps c = ksp_caps(g, full);
-  const uint32_t t = ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16(kind), ksp_pack(g.V, g.L)).total;
+  const uint32_t t =
+      ksp_layout(g.V, g.L, g.max_deg, c.frames, c.arena, ksp_use_d16(kind), ksp_pack(g.V, g.L), stats_on).total;
   return t <= kMaxLds ? t : 0;
 }
 
@@ -854,7 +856,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
   const KspCaps caps = ksp_caps(g, full);
-  const uint32_t lds = ksp_tier_lds_bytes(g, full, kind);
+  const uint32_t lds = ksp_tier_lds_bytes(g, full, kind, stats != nullptr);
   if (!lds || !qbuf) return hipErrorInvalidValue;
   // a re-run launch covers the listed pairs only; its surplus wavefronts exit at once
   const uint32_t grid = blocks_for(n, lds, num_cus, kWave);  // <= ksp_max_grid: qbuf holds grid * V
