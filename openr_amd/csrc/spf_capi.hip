@@ -822,7 +822,7 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     }
     if ((e2 = d.kign.reserve((size_t)c * ign_cap)) != hipSuccess) return e2;
     if ((e2 = d.kend.reserve(c)) != hipSuccess) return e2;
-    if ((e2 = d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * V)) != hipSuccess) return e2;
+    if ((e2 = d.kq.reserve((size_t)ksp_max_grid(d.g, d.num_cus) * (V + (V + 31u) / 32u))) != hipSuccess) return e2;
     if ((e2 = d.ksrc.reserve(c)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)c * ctx->nsl_max())) != hipSuccess) return e2;
     if (skip && (e2 = d.kkeep.reserve(c)) != hipSuccess) return e2;

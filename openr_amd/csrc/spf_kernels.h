@@ -321,7 +321,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                                                   // also marks a uniform-cost graph (rank by name / edge)
                             uint32_t ltag = 0);   // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_PROF tuning only)
-uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * V u32
+uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * (V + ceil(V / 32)) u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);
 hipError_t launch_gather_sources(const uint32_t* sources, const uint32_t* prow, uint32_t first, uint32_t n,
                                  uint32_t* out, int num_cus, hipStream_t s);

@@ -82,7 +82,7 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
   l.skr = take(8u * sdeg);
   l.sl = take(4u * sdeg);
   l.su = take(4u * sdeg);
-  l.seen = take(4u * ((V + 31u) / 32u));
+  l.seen = 0;  // the probe's visited bits live in global scratch after the queue (st.seen)
   l.stats = stats_on ? take(8u * kKspStats) : 0u;  // OPENR_SPF_PROF launches only
   l.d16 = 0;
   if (want_d16 && off + 2u * V + 16u <= kD16Budget) l.d16 = take(2u * V);
@@ -406,15 +406,13 @@ __device__ bool reachable(const KspState& st, uint32_t sp, uint32_t next) {
   const uint32_t lane = threadIdx.x, vw = (g.V + 31u) / 32u;
   const uint64_t t0 = st.stats ? clock64() : 0;
   for (uint32_t i = lane; i < vw; i += kWave) st.seen[i] = 0;
-  lds_fence();
+  __threadfence_block();  // the bits are global scratch (the probe is rare; LDS buys waves)
   if (lane == 0) {
     uint32_t t = 0;
     for (uint32_t i = 0; i <= sp; ++i) {
       const uint32_t x = i < sp ? st.fr_node[i] : next;
-      if (!(st.seen[x >> 5] & (1u << (x & 31u)))) {
-        st.seen[x >> 5] |= 1u << (x & 31u);
-        st.q[t++] = x;
-      }
+      const uint32_t bit = 1u << (x & 31u);
+      if (!(atomicOr(&st.seen[x >> 5], bit) & bit)) st.q[t++] = x;
     }
     st.ctl[1] = t;
   }
@@ -627,8 +625,9 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
   st.skr = reinterpret_cast<uint64_t*>(base + lay.skr);
   st.sl = reinterpret_cast<uint32_t*>(base + lay.sl);
   st.su = reinterpret_cast<uint32_t*>(base + lay.su);
-  st.seen = reinterpret_cast<uint32_t*>(base + lay.seen);
-  st.q = qbuf + (size_t)blockIdx.x * V;
+  // per-wavefront global scratch: the probe's queue (V) and its visited bits (vw words)
+  st.q = qbuf + (size_t)blockIdx.x * (V + (V + 31u) / 32u);
+  st.seen = st.q + V;
   st.probe_after = probe_after;
   st.max_depth = frames;
   st.arena_cap = arena;
