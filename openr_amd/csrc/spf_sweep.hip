@@ -665,7 +665,6 @@ struct GrpWave {
   uint32_t cap;            // dirty slots
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_PROF): per-phase cycles and sizes, or null
-  unsigned long long pacc[1];  // lane 0: this wave's repair count (OPENR_SPF_PROF); the phase sums go to prof directly
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
@@ -796,19 +795,6 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
   uint2 er = make_uint2(0u, 0u);  // the lane's entry's row, loaded with the entry
   D ed = INF;
   bool pend = false, ea = false;  // ea: the lane's entry is in A (its distance may still drop)
-  auto load_entries = [&]() {
-    if (pend && ea) ed = c.adist[lane];  // entry i sits in lane i and in slot i
-    const uint32_t hi = min(nd, 64u);
-    if (loaded < hi) {
-      if (lane >= loaded && lane < hi) {
-        ev = c.dlist[lane];
-        er = c.gv.row(ev);  // in flight with the distance read: process() starts at the records
-        ed = c.dist_a(ev, ea);
-        pend = true;
-      }
-      loaded = hi;
-    }
-  };
   // one dirty node v (wave-uniform, row r) at new distance dv: pull its set over tight
   // in-edges; if it changed and v keeps its base distance, its tight successors become dirty
   auto process = [&](uint32_t v, D dv, uint2 r) {
@@ -851,10 +837,12 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       acc[k] = wave_or_prefix(acc[k], min(deg, 64u));
       diff |= acc[k] != __builtin_amdgcn_readfirstlane(cur[k]);
     }
-    if (diff && lane == 0) {
-      uint8_t* o = c.anh + (size_t)(c.didx[v] - 1u) * nb;
-      for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
-      c.nhm[v >> 5] |= 1u << (v & 31u);
+    if (diff) {
+      if (lane == 0) {
+        uint8_t* o = c.anh + (size_t)(c.didx[v] - 1u) * nb;
+        for (uint32_t b = 0; b < nb; ++b) o[b] = (uint8_t)(acc[b >> 2] >> (8u * (b & 3u)));
+        c.nhm[v >> 5] |= 1u << (v & 31u);
+      }
     }
     if (in_a || diff) ++nchanged;
     if (!diff || in_a || dv == INF || !c.expands(v)) return;
@@ -879,24 +867,37 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       nd += (uint32_t)__popcll(m);
     }
   };
-  load_entries();
-  bool first = true;
+  // Every exit of the bucket loop is wave-uniform and seen as such by the compiler: nd,
+  // loaded and the exit flags are scalars (ballots, readfirstlane), and the lanes' entry
+  // loads (the only divergent branch of the loop body outside process()) join at the top
+  // of the body, not at the latch ("the hang").
+  bool first = true, ovf = false;
   D last = 0;
   for (;;) {
+    // the lanes' entries: A members re-read their (relaxed) distance, new entries load
+    if (pend && ea) ed = c.adist[lane];  // entry i sits in lane i and in slot i
+    const uint32_t hi = min(nd, 64u);
+    if (lane >= loaded && lane < hi) {
+      ev = c.dlist[lane];
+      er = c.gv.row(ev);  // in flight with the distance read: process() starts at the records
+      ed = c.dist_a(ev, ea);
+      pend = true;
+    }
+    loaded = hi;
     // bucket minimum over pending entries (lanes, then the LDS overflow beyond 64)
     D mn = pend ? ed : INF;
-    bool anyp = __ballot(pend) != 0;
+    unsigned long long anyb = __ballot(pend);
     for (uint32_t i0 = 64; i0 < nd; i0 += 64u) {
       const uint32_t i = i0 + lane;
+      bool p = false;
       if (i < nd) {
         const D d = c.dist(c.dlist[i]);
-        const bool p = first || d > last;
+        p = first || d > last;
         mn = (p && d < mn) ? d : mn;
-        anyp |= __ballot(p) != 0;
       }
-      anyp = __ballot(anyp) != 0;
+      anyb |= __ballot(p);
     }
-    if (!anyp) break;
+    if (!anyb) break;
     mn = wave_min_t(mn);
     ++buckets;
     unsigned long long m = __ballot(pend && ed == mn);
@@ -907,9 +908,13 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
       process((uint32_t)__builtin_amdgcn_readlane((int)ev, k), mn,
               make_uint2((uint32_t)__builtin_amdgcn_readlane((int)er.x, k),
                          (uint32_t)__builtin_amdgcn_readlane((int)er.y, k)));
-      if (nd > c.cap) return kGrpOverflow;
+      nd = __builtin_amdgcn_readfirstlane(nd);
+      if (nd > c.cap) {
+        ovf = true;
+        break;
+      }
     }
-    for (uint32_t i0 = 64; i0 < nd0; i0 += 64u) {
+    for (uint32_t i0 = 64; !ovf && i0 < nd0; i0 += 64u) {
       const uint32_t i = i0 + lane;
       uint32_t v = 0;
       bool hit = false;
@@ -924,27 +929,33 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
         mo &= mo - 1ull;
         const uint32_t vk = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
         process(vk, mn, c.gv.row(vk));
-        if (nd > c.cap) return kGrpOverflow;
+        nd = __builtin_amdgcn_readfirstlane(nd);
+        if (nd > c.cap) {
+          ovf = true;
+          break;
+        }
       }
     }
+    if (ovf) break;
     if (pend && ed == mn) pend = false;
     first = false;
     last = mn;
     if (mn == INF) break;  // unreachable nodes expand nothing: this was the last bucket
     lds_fence();
-    load_entries();
   }
+  if (ovf) return kGrpOverflow;
   if (c.prof && lane == 0) {
     pt3 = (long long)__builtin_amdgcn_s_memtime();
     atomicAdd(&c.prof[0], (unsigned long long)(pt1 - pt0));
     atomicAdd(&c.prof[1], (unsigned long long)(pt2 - pt1));
     atomicAdd(&c.prof[2], (unsigned long long)(pt3 - pt2));
-    c.pacc[0] += 1ull;
+    atomicAdd(&c.prof[3], 1ull);
     atomicAdd(&c.prof[4], (unsigned long long)na);
     atomicAdd(&c.prof[5], (unsigned long long)nd);
     atomicAdd(&c.prof[6], (unsigned long long)buckets);
     atomicAdd(&c.prof[7], (unsigned long long)nchanged);
   }
+  __builtin_amdgcn_wave_barrier();  // the lane-0 branch joins here, not at the caller's latch
   return nchanged;
 }
 
@@ -965,7 +976,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_item;
-  const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+  const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform to the compiler: per-wave LDS pointers stay scalar
   const uint32_t block = blockDim.x, waves = block >> 6;
   const uint32_t tw = (E + 63u) / 64u, vw = (V + 31u) / 32u;
   const GrpLayout lay = grp_layout(V, E, nb, sizeof(D), LG, waves, chunk, cap);
@@ -1004,7 +1015,6 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.nb = nb;
   c.unit = unit != 0;
   c.prof = prof;
-  c.pacc[0] = 0;
   c.bdist = bdist;
   c.bnh = bnh;
   c.btight = btight;
@@ -1098,6 +1108,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
           ovf_unit[k] = i * n_src + j;
         }
       }
+      __builtin_amdgcn_wave_barrier();  // the lane-0 branch joins here: the latch is taken by the whole wave
     }
     __syncthreads();  // every wave is done with this item's shared rows and s_item
     if (tid == 0) s_item = gridDim.x + atomicAdd(&ctr[0], 1u);
@@ -1105,7 +1116,6 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     item = s_item;
   }
   if (prof && lane == 0) {
-    atomicAdd(&prof[3], c.pacc[0]);
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }
