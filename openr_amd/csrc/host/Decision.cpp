@@ -732,7 +732,15 @@ NextHopSet SpfSolver::ksp2NextHopsFromTokens(const std::string& me, thrift::IpPr
   };
   for (auto const& [node, bestArea] : best.allNodeAreas) {
     if (area != bestArea) continue;
+    if (node == me) {
+      // an anycast prefix this node also advertises: getKthPaths(me, me, 2) is empty in the
+      // reference (traceOnePath(me, me) is the empty path, LinkState.cpp:404-406). prefetchKthPaths
+      // stages no (me, me) row, so take the general path for its memo and counter effects.
+      (void)ls.getKthPaths(me, me, 2);
+      continue;
+    }
     const uint32_t* row = ls.kthPathTokens(me, node, 2);
+    if (!row) throw std::logic_error("ksp2NextHopsFromTokens: (" + me + ", " + node + ") not staged");
     const uint32_t* p = row + 1;
     for (uint32_t i = 0; i < row[0]; ++i, p += 1 + p[0]) {
       bool add = true;

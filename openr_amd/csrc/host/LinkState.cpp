@@ -1268,18 +1268,18 @@ void LinkState::convertKspRows() const {
 const std::vector<LinkState::LabeledNode>& LinkState::labeledNodes() const {
   const CsrMirror& m = csrMirror();
   std::lock_guard<std::mutex> g(cacheMu_.m);
-  if (labeledListGen_ != mirrorGeneration_ || labeledListAdjVer_ != adjDbVersion_) {
-    labeledList_.clear();
-    labeledList_.reserve(labeledNodes_);
+  if (labeledList_.gen != mirrorGeneration_ || labeledList_.adjVer != adjDbVersion_) {
+    labeledList_.list.clear();
+    labeledList_.list.reserve(labeledNodes_);
     for (auto const& [name, db] : adjacencyDatabases_) {
       if (db.nodeLabel == 0) continue;
       auto it = m.id.find(name);
-      labeledList_.push_back(LabeledNode{db.nodeLabel, &db.thisNodeName, it == m.id.end() ? UINT32_MAX : it->second});
+      labeledList_.list.push_back(LabeledNode{db.nodeLabel, &db.thisNodeName, it == m.id.end() ? UINT32_MAX : it->second});
     }
-    labeledListGen_ = mirrorGeneration_;
-    labeledListAdjVer_ = adjDbVersion_;
+    labeledList_.gen = mirrorGeneration_;
+    labeledList_.adjVer = adjDbVersion_;
   }
-  return labeledList_;
+  return labeledList_.list;
 }
 
 const std::vector<int64_t>& LinkState::nodeLabelsById() const {

@@ -573,8 +573,24 @@ class LinkState {
   // id-indexed caches read by concurrent route builds (buildRouteDbs workers): the first
   // reader after a change rebuilds under the lock; no update runs during a build
   CacheMutex cacheMu_;
-  mutable std::vector<LabeledNode> labeledList_;
-  mutable uint64_t labeledListGen_ = 0, labeledListAdjVer_ = ~0ull;
+  // labeledList_ points into this object's adjacencyDatabases_: a copy starts empty with
+  // stamps that never match, so it rebuilds against its own databases (a move keeps the
+  // map's nodes, and the pointers with them)
+  struct LabeledListCache {
+    std::vector<LabeledNode> list;
+    uint64_t gen = 0, adjVer = ~0ull;
+    LabeledListCache() = default;
+    LabeledListCache(const LabeledListCache&) {}
+    LabeledListCache& operator=(const LabeledListCache&) {
+      list.clear();
+      gen = 0;
+      adjVer = ~0ull;
+      return *this;
+    }
+    LabeledListCache(LabeledListCache&&) noexcept = default;
+    LabeledListCache& operator=(LabeledListCache&&) noexcept = default;
+  };
+  mutable LabeledListCache labeledList_;
   mutable std::vector<int64_t> nodeLabelsById_;
   mutable uint64_t nodeLabelsGen_ = 0, nodeLabelsAdjVer_ = 0;
   uint64_t adjDbVersion_ = 0;  // bumped by every adjacency database update / delete

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
   const bool has_ign = GENERIC && has_ign_rt != 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_next;
-  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const uint32_t V = g.V, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = __lane_id();
   const BfsLayout lay = bfs_layout(V, g.L, has_ign, FB, ring_cap);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(BLOCK) void bfs_wide_kernel(DevGraph g, SolveArgs a
   constexpr int K = (int)kBfsEdgesPerLane;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_next;
-  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const uint32_t V = g.V, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = __lane_id();
   const WideLayout lay = wide_layout(V, nw);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;

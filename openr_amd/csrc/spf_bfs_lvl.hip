@@ -204,7 +204,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void
   __shared__ uint32_t s_next;
   using N = Nh<MODE>;
   using O = LvlOps<LT>;
-  const uint32_t V = g.V, tid = threadIdx.x, wave = tid >> 6, lane = __lane_id();
+  const uint32_t V = g.V, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = __lane_id();
   const uint32_t nh_words = N::words(V);
   const LvlLayout<LT> lay = lvl_layout<LT>(V, g.L, has_ign, nh_words, !ELECT, ring_cap);
   char* base = reinterpret_cast<char*>(smem);

@@ -1030,6 +1030,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.status.release();
     d.perm.release();
     d.part.release();
+    d.kkeep.release();
+    d.kpart.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.base_tin.p, d.win_links.p, d.win_src.p, d.wchanged.p, d.wchanged_t.p,
                      d.kbase.p,     d.krows.p,      d.krows16.p, d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,

@@ -353,6 +353,38 @@ static void ringKsp2Overload(bool v4) {
   EXPECT_EQ(at(m, "1", P(addr3, addr3V4)), NextHopSet({nhFromAdj(adj13, v4, 10, std::nullopt)}));
   EXPECT_TRUE(m.find({"1", P(addr2, addr2V4).toString()}) == m.end());
 }
+// An anycast KSP2 prefix that the building node also advertises with a prepend label
+// (ADVICE r5): the second-path loop of selectBestPathsKsp2 then reads getKthPaths(me, me,
+// 2), which is empty in the reference (traceOnePath(me, me) is the empty path) and which
+// the token rows of prefetchKthPaths do not stage. Routes and spf_runs with the device
+// prefetch must equal the call-by-call path's.
+TEST_GPU(SimpleRing_Ksp2EdEcmp_AnycastSelfPrependLabel) {
+  const auto anycast = pfx("fd00::a/128");
+  auto run = [&](const char* prefetch) {
+    setenv("OPENR_KSP2_PREFETCH", prefetch, 1);
+    Ring r(false, true);
+    for (auto const& [node, label] : {std::pair<std::string, int32_t>{"1", 60001}, {"4", 60004}}) {
+      auto e = createPrefixEntry(anycast, true);
+      e.prependLabel = label;
+      r.ps.updatePrefix(node, kDefaultArea, e);
+    }
+    SpfCounters::get().reset();
+    SpfSolver solver("1", false, true);
+    auto m = getRouteMap(solver, {"1", "2"}, r.als, r.ps);
+    return std::make_pair(m, SpfCounters::get().spfRuns());
+  };
+  auto off = run("0");
+  auto on = run("1");
+  unsetenv("OPENR_KSP2_PREFETCH");
+  EXPECT_TRUE(off.first == on.first);
+  EXPECT_EQ(off.second, on.second);
+  // node 1 reaches node 4's copy over both ring neighbours, under 4's prepend label
+  const auto push = [](std::vector<int32_t> l) { return mpls(MplsActionCode::PUSH, std::nullopt, l); };
+  EXPECT_EQ(at(on.first, "1", anycast),
+            NextHopSet({nhFromAdj(adj12, false, 20, push({60004, 4})), nhFromAdj(adj13, false, 20, push({60004, 4}))}));
+  EXPECT_EQ(at(on.first, "2", anycast).size(), at(off.first, "2", anycast).size());
+}
+
 TEST_GPU(SimpleRing_Ksp2EdEcmp_OverloadCorner_v6) { ringKsp2Overload(false); }
 TEST_GPU(SimpleRing_Ksp2EdEcmp_OverloadCorner_v4) { ringKsp2Overload(true); }
 

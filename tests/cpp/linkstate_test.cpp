@@ -388,6 +388,29 @@ TEST_CPU(LinkStateTest_LabeledNodeCount) {
   EXPECT_EQ(0u, (unsigned)ls.labeledNodeCount());
 }
 
+// A copy of a LinkState reads its own databases' names in labeledNodes(), not the
+// source's (the cached list holds pointers into adjacencyDatabases_)
+TEST_CPU(LinkStateTest_LabeledNodesSurviveCopy) {
+  std::unique_ptr<LinkState> src(new LinkState(kArea));
+  src->updateAdjacencyDatabase(createAdjDb("a", {createAdjacency("b", "a/b", "b/a", 3)}, 5), 0, 0);
+  src->updateAdjacencyDatabase(createAdjDb("b", {createAdjacency("a", "b/a", "a/b", 4)}, 7), 0, 0);
+  EXPECT_EQ(2u, (unsigned)src->labeledNodes().size());  // the source's cache is filled
+  LinkState copy(*src);
+  LinkState copy2(copy);  // a copy of a copy whose cache is filled too
+  (void)copy.labeledNodes();
+  src.reset();  // the source's databases (and the names its cache pointed at) are gone
+  for (LinkState* ls : {&copy, &copy2}) {
+    auto const& l = ls->labeledNodes();
+    EXPECT_EQ(2u, (unsigned)l.size());
+    std::set<std::pair<std::string, int32_t>> got;
+    for (auto const& n : l) {
+      EXPECT_TRUE(n.name == &ls->getAdjacencyDatabases().at(*n.name).thisNodeName);
+      got.emplace(*n.name, n.label);
+    }
+    EXPECT_TRUE(got == (std::set<std::pair<std::string, int32_t>>{{"a", 5}, {"b", 7}}));
+  }
+}
+
 // ParallelAdjRingTopologyFixture adjacencies (DecisionTest.cpp:3146-3203)
 static LinkState parallelRing() {
   LinkState ls(kArea);

@@ -786,6 +786,34 @@ def test_ksp2_tagged_rows_across_chunks(eng, monkeypatch, tag):
     check_ksp2_against_oracle(eng, g, [(int(a), int(b)) for a, b in rng.integers(0, g.num_nodes, (300, 2))])
 
 
+def skip_edge_graphs():
+    """Small graphs where ksp_select_pairs' row-length test is tight: the k = 1
+    paths of a pair use every link of src or of dst exactly when the row has no down link
+    and no self-loop. Two parallel links a=b (both up, or one down), an overloaded
+    destination behind parallel links, and a diamond whose middle node is overloaded."""
+    out = []
+    # 0 = 1 parallel pair, 1 - 2 - 3 chain with a parallel pair 2 = 3, 0 - 4 - 3 detour
+    links = np.array([(0, 1), (0, 1), (1, 2), (2, 3), (2, 3), (0, 4), (4, 3), (1, 4)])
+    m = np.ones(len(links), dtype=np.uint64)
+    for up in ([1] * 8, [1, 0, 1, 1, 1, 1, 1, 1], [1, 1, 1, 1, 0, 1, 1, 1]):
+        for ovl in ([0] * 5, [0, 0, 0, 1, 0], [0, 0, 1, 0, 0]):
+            out.append(T.csr_from_links([f"n{i}" for i in range(5)], links, m, m,
+                                        np.array(ovl, dtype=np.uint8), np.array(up, dtype=np.uint8)))
+    return out
+
+
+@pytest.mark.parametrize("skip", ["1", "0"], ids=["skip", "solve-all"])
+def test_ksp2_skip_parallel_down_and_overloaded_endpoints(eng, monkeypatch, skip):
+    """ksp_select_pairs' skip on and off against the oracle where its row-length test
+    decides: parallel links between one pair, a parallel link down (the row is longer
+    than the links a path can use, so the pair is kept), overloaded destinations and
+    transit nodes. Every ordered pair of every graph."""
+    monkeypatch.setenv("OPENR_SPF_KSP_SKIP", skip)
+    for g in skip_edge_graphs():
+        V = g.num_nodes
+        check_ksp2_against_oracle(eng, g, [(s, d) for s in range(V) for d in range(V)])
+
+
 @pytest.mark.parametrize("pack", ["1", "0"], ids=["arena-packed", "arena-wide"])
 @pytest.mark.parametrize("pull", ["1", "0"], ids=["pull-batched", "pull-per-wave"])
 @pytest.mark.parametrize("resume", ["1", "0"], ids=["resume", "regather"])
