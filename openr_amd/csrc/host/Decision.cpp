@@ -962,6 +962,7 @@ int SpfSolver::fastNextHopNodes(const std::string& me, uint32_t dst, Metric d) {
         }
         if (b == UINT32_MAX) {  // a neighbour's row on another mirror / map-backed: general path
           fast_.state = 2;
+          ++fastFallbacks_;
           return -1;
         }
         fast_.lfaBit.push_back(b);

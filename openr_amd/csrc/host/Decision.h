@@ -211,6 +211,9 @@ class SpfSolver {
   // tests: off = every route through the general createRouteForPrefix / label path (the
   // id-based fast path must build the same DBs)
   void setFastPathForTesting(bool on) { fastEnabled_ = on; }
+  // builds whose fast path handed the rest of the build to the general path (an LFA
+  // neighbour's row on another mirror)
+  uint64_t fastFallbacksForTesting() const { return fastFallbacks_; }
 
   // static MPLS routes (updateStaticRoutes): label -> next-hops
   void updateStaticMplsRoutes(const std::unordered_map<int32_t, std::vector<thrift::NextHopThrift>>& add,
@@ -334,6 +337,7 @@ class SpfSolver {
   mutable FastCtx fast_;
   bool fastSetup(std::unordered_map<std::string, LinkState> const& areaLinkStates, const std::string& me);
   bool fastEnabled_ = true;
+  uint64_t fastFallbacks_ = 0;
   int fastNextHopNodes(const std::string& me, uint32_t dst, Metric d);
   // the node-label MPLS route's next hops towards dst (getNextHopsWithMetric +
   // getNextHopsThrift with swapLabel = label, perDestination = false): 1 = *out built, 0 =

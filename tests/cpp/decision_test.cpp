@@ -1216,6 +1216,44 @@ TEST_GPU(RouteBuild_FastPath_MatchesGeneralPath) {
     }
 }
 
+// fastRoute's fallback: with LFA on, the fast path needs every
+// neighbour's row on my mirror. A neighbour whose memo row was kept on a retired mirror
+// snapshot (a new node nobody reciprocates rebuilds the mirror, not the memo) makes
+// fastNextHopNodes return -1, and the rest of the build takes the general path. Routes,
+// the best-route cache and the counters must equal an all-general build's.
+TEST_GPU(FastRoute_FallbackOnRetiredNeighbourRow) {
+  auto run = [&](bool fast, bool v4) {
+    Ring r(v4, false);
+    auto& ls = r.als.at(kDefaultArea);
+    (void)ls.getSpfResult("2");  // neighbour 2's memo row, on the current mirror
+    EXPECT_FALSE(ls.updateAdjacencyDatabase(createAdjDb("5", {createAdjacency("1", "5/1", "1/5", "fe80::1", "192.168.0.1", 10, 0)}, 5))
+                     .topologyChanged);
+    SpfSolver solver("1", v4, true);  // LFA: the build reads the neighbours' rows
+    solver.setFastPathForTesting(fast);
+    std::vector<std::string> flat{flatten(solver.buildRouteDb("1", r.als, r.ps))};
+    auto route = solver.createRouteForPrefix("1", r.als, r.ps, v4 ? addr4V4 : addr4);
+    flat.push_back(route ? flatten(DecisionRouteDb{{{route->prefix, *route}}, {}}) : "none");
+    std::string cache;
+    for (auto const& [p, b] : solver.getBestRoutesCache()) {
+      cache += p.toString() + (b.success ? "+" : "-") + b.bestNodeArea.first + ":";
+      for (auto const& na : b.allNodeAreas) cache += na.first + ",";
+    }
+    auto const& c = solver.counters();
+    std::vector<uint64_t> cnt{c.route_build_runs, c.get_route_for_prefix, c.no_route_to_prefix, c.skipped_unicast_route,
+                              c.skipped_mpls_route, c.duplicate_node_label, c.no_route_to_label};
+    return std::make_tuple(flat, cache, cnt, solver.fastFallbacksForTesting());
+  };
+  for (const bool v4 : {false, true}) {
+    const auto general = run(false, v4), fast = run(true, v4);
+    EXPECT_EQ(std::get<3>(general), 0u);
+    EXPECT_EQ(std::get<3>(fast), 1u);  // the fallback was taken
+    EXPECT_TRUE(std::get<0>(general) == std::get<0>(fast));
+    EXPECT_TRUE(std::get<1>(general) == std::get<1>(fast));
+    EXPECT_TRUE(std::get<2>(general) == std::get<2>(fast));
+    EXPECT_TRUE(std::get<0>(fast)[1] != "none");
+  }
+}
+
 // createRouteForPrefix outside buildRouteDb (Decision::rebuildRoutes on an
 // incremental prefix update, DecisionTest-style) after LinkState updates must read the
 // current SPF memo, not views a previous build cached: a new node with no up link (mirror
