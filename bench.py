@@ -74,6 +74,36 @@ def algorithmic_bytes(g, sources: np.ndarray) -> int:
     return int(per.sum())
 
 
+def hash_rows(a) -> str:
+    """64-bit digest (blake2b) of an array's bytes: the per-rank result checksum."""
+    import hashlib
+
+    return hashlib.blake2b(np.ascontiguousarray(a).view(np.uint8).tobytes(), digest_size=8).hexdigest()
+
+
+def gather_hashes(h: str, world: int, dev) -> list:
+    """all_gather of every rank's 64-bit digest (outside the timed region)."""
+    if world == 1:
+        return [h]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([int(h, 16) - (1 << 63)], dtype=torch.int64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [format(int(x.item()) + (1 << 63), "016x") for x in out]
+
+
+def token_prefix(row: np.ndarray) -> np.ndarray:
+    """The used prefix of a KSP2 token row ([n_paths, len, e.., len, e.., ...])."""
+    n, k = int(row[0]), 1
+    if n == 0xFFFFFFFF:
+        return row[:1]
+    for _ in range(n):
+        k += 1 + int(row[k])
+    return row[:k]
+
+
 def rows_check(g, d_dist, d_nh, lo: int, n_local: int, use_metric: bool, nrows: int = 8):
     """The post-run check of the all-sources line: `nrows` evenly spaced rows of the rank's
     result (u64 distances and every next-hop byte) compared with oracle runSpf rows
@@ -256,6 +286,56 @@ def whatif_main(args):
     units = L * V
     value = units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    # self-check outside the timed region: every rank's changed rows as a 64-bit digest,
+    # all-gathered; rank 0 re-solves a sampled shard (the last rank's links) on its own
+    # engine and compares digests, and at N = 1 checks 8 sources x its links against the
+    # oracle re-solves runSpf(src, true, {link})
+    mine = hash_rows(changed[:n_links].cpu().numpy().view(np.uint32))
+    hashes = gather_hashes(mine, world, dev)
+    check = None
+    if rank == 0:
+        r = world - 1
+        rlo, rhi = shard_range(L, r, world)
+        c_r, _ = eng.whatif(np.arange(rlo, rhi), np.arange(V), use_metric)
+        check = {"rank_digests": hashes, "recomputed_rank": r, "recomputed_digest": hash_rows(c_r),
+                 "recomputed_match": hash_rows(c_r) == hashes[r]}
+        if world == 1:
+            from oracle import Oracle
+
+            samp = np.linspace(0, V - 1, 8).astype(np.uint32)
+            want = Oracle(g).whatif(np.arange(llo, lhi, dtype=np.uint32), samp, use_metric)
+            got = changed[:n_links].cpu().numpy().view(np.uint32)[:, samp]
+            check.update(oracle_sample_units=int(want.size), oracle_sample_match=bool(np.array_equal(got, want)))
+        check["ok"] = bool(check["recomputed_match"] and check.get("oracle_sample_match", True))
+    # the delta leg (openr_spf_whatif_delta_device): the same sweep also writing each unit's
+    # changed nodes with their new distance and next-hop bytes into a device pool; its own
+    # clock, after the counts-only timed region
+    delta = None
+    if not args.no_delta:
+        nbh = eng.nh_bytes
+        cap = int(changed[:n_links].sum().item()) if n_links else 0
+        d_ptr = torch.empty(n_links * V + 1, dtype=torch.int64, device=dev)
+        d_node = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        d_dist = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        d_nh = torch.empty((max(cap, 1), nbh), dtype=torch.uint8, device=dev)
+
+        def dstep():
+            return eng.whatif_delta_device(links.data_ptr(), n_links, srcs.data_ptr(), V, changed.data_ptr(),
+                                           d_ptr.data_ptr(), d_node.data_ptr(), d_dist.data_ptr(), d_nh.data_ptr(),
+                                           cap, nbh, use_metric, stream=stream.cuda_stream)[0]
+
+        for _ in range(max(1, args.warmup)):
+            dstep()
+        barrier()
+        td = time.perf_counter()
+        for _ in range(args.steps):
+            used = dstep()
+        barrier()
+        dt = max_over_ranks(time.perf_counter() - td, dev)
+        delta = {"ms_per_step": dt / args.steps * 1e3, "units_per_s": units * args.steps / dt,
+                 "entries_per_step": int(used), "pool_bytes": int(used) * (4 + 8 + nbh),
+                 "note": "openr_spf_whatif_delta_device: counts + a CSR of every unit's changed nodes with their "
+                         "new u64 distance and next-hop bytes, from the repair overlays (no second solve)"}
     srcs_np = np.arange(V)
     per_src = algorithmic_bytes(g, srcs_np) / V  # mean B(src)
     bytes_step = per_src * units
@@ -309,6 +389,9 @@ def whatif_main(args):
         }
         if ucmp is not None:
             out["ucmp_routes"] = ucmp
+        out["check"] = check
+        if delta is not None:
+            out["delta"] = delta
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = whatif_cpu_baseline(g, min(args.cpu_seconds, 10.0), use_metric)
         print(json.dumps(out), flush=True)
@@ -456,6 +539,34 @@ def ksp2_main(args):
             s, d = int(s_np[last_b + p_np[i]]), int(d_np[i])
             assert decode_paths(t1[r]) == o.kth_paths(s, d, 1) and decode_paths(t2[r]) == o.kth_paths(s, d, 2), \
                 "ksp2 bench result check failed"
+    # self-check outside the timed region: 64 pairs of each rank's last block (what the
+    # token buffers hold after the loop), their token prefixes as a 64-bit digest per rank,
+    # all-gathered; rank 0 traces every rank's sample again with its own engine and
+    # compares digests
+    def sample_of(r):
+        rlo, rhi = shard_range(n_src_total, r, world)
+        rs = (np.arange(rlo, rhi, dtype=np.int64) * V // n_src_total).astype(np.uint32)
+        rn = rhi - rlo
+        lb = ((rn - 1) // blk) * blk
+        m_l = rn - lb
+        rows = np.linspace(0, m_l * V - 1, 64).astype(np.int64)
+        return rows, rs[lb + rows // V], (rows % V).astype(np.uint32)
+
+    rows, _, _ = sample_of(rank)
+    ridx = torch.from_numpy(rows).to(dev)
+    t1s = tok1.index_select(0, ridx).cpu().numpy().view(np.uint32)
+    t2s = tok2.index_select(0, ridx).cpu().numpy().view(np.uint32)
+    mine = hash_rows(np.concatenate([np.concatenate([token_prefix(a), token_prefix(b)]) for a, b in zip(t1s, t2s)]))
+    hashes = gather_hashes(mine, world, dev)
+    check = None
+    if rank == 0:
+        check = {"rank_digests": hashes, "pairs_per_rank": int(len(rows)), "recomputed_match": []}
+        for r in range(world):
+            _, ss, dd = sample_of(r)
+            a1, a2 = eng.ksp2_tokens(ss, dd, tok_cap)
+            d = hash_rows(np.concatenate([np.concatenate([token_prefix(a), token_prefix(b)]) for a, b in zip(a1, a2)]))
+            check["recomputed_match"].append(d == hashes[r])
+        check["ok"] = all(check["recomputed_match"])
     srcs_np = np.asarray(s_np, dtype=np.int64)
     per_pair = algorithmic_bytes(g, srcs_np) / max(nsrc, 1)  # B(src) per second SPF
     step_s = elapsed / args.steps
@@ -480,6 +591,7 @@ def ksp2_main(args):
                 pmc=pmc, scope="every engine kernel of a KSP2 step on the summary's sources, per pair, x this "
                               "step's pairs"),
         }
+        out["check"] = check
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ksp2_cpu_baseline(g, min(args.cpu_seconds, 10.0))
         print(json.dumps(out), flush=True)
@@ -771,6 +883,7 @@ def main():
                     help="strong scaling exchange: compact = u8/u16 level rows + next hops (uniform-cost graphs), "
                          "full = u64 dist + next hops")
     ap.add_argument("--no-ucmp", action="store_true", help="whatif: skip the UCMP route-build leg")
+    ap.add_argument("--no-delta", action="store_true", help="whatif: skip the delta-output leg")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="strong (default, BASELINE config 3): the V sources of ONE topology are split over the "
                          "ranks and the result shards all-gathered over RCCL; weak: every rank solves its own "

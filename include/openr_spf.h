@@ -20,6 +20,8 @@
  *                              (batched prefetch / benchmarks / multi-GPU shards)
  *   openr_spf_whatif           per-link-failure what-if sweep: runSpf(src, useLinkMetric, {link})
  *                              for every (link, source), reduced to changed-node counts
+ *   openr_spf_whatif_delta     the same sweep plus each unit's changed nodes with their
+ *                              new distance and next-hop bits
  *   openr_spf_ksp2             LinkState::getKthPaths(src, dst, 1 and 2) (LinkState.cpp:762-791)
  *                              for a batch of pairs, paths traced on the device
  *   openr_spf_patch_graph      attribute-only mirror updates (metric, Link::isUp, node
@@ -218,6 +220,46 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
                             uint32_t n_links, const uint32_t* d_sources, uint32_t n_sources,
                             uint32_t flags, uint32_t* d_changed, void* stream,
                             uint64_t* out_solved);
+
+/* What-if sweep with the per-unit delta (round 6): besides changed[], the nodes each
+   failure changes, with their new distance and next-hop bits, i.e. the part of
+   runSpf(sources[j], useLinkMetric, {links[i]}) (LinkState.cpp:808-882, SpfResult
+   LinkState.h:436-443) that differs from the no-failure SPF. A consumer builds
+   post-failure routes from it without solving again.
+   Host form: a CSR over units u = i * n_sources + j. Unit u's entries are
+   [ptr[u], ptr[u + 1]), with node ids ascending and ptr[n_units] = sum(changed).
+   dist[k] is UINT64_MAX for a node the failure makes unreachable. nh[k] holds nh_bytes
+   bytes in openr_spf_solve's row layout (bit b = the b-th distinct neighbour of the
+   source), zero past the graph's width. nh_bytes must be >= that width.
+   When sum(changed) > cap, ptr and changed are filled, the entries are not, and the call
+   returns OPENR_SPF_E2BIG. The entries come from the repair's own overlays (and from the
+   seeded re-solve of the few units too large for them): no second solve is run for them. */
+typedef struct {
+  uint64_t* ptr;     /* [n_links * n_sources + 1] */
+  uint32_t* node;    /* [cap] */
+  uint64_t* dist;    /* [cap] */
+  uint8_t* nh;       /* [cap][nh_bytes] */
+  uint64_t cap;      /* entries the caller allocated */
+  uint32_t nh_bytes; /* bytes per next-hop entry */
+} openr_spf_whatif_delta_t;
+int openr_spf_whatif_delta(openr_spf_ctx* ctx, const uint32_t* links, uint32_t n_links,
+                           const uint32_t* sources, uint32_t n_sources, uint32_t flags,
+                           uint32_t* changed, openr_spf_whatif_delta_t* delta,
+                           uint64_t* out_solved);
+
+/* Device-buffer form (every buffer device memory): the same CSR, d_ptr [n_units + 1],
+   with each unit's entries in the order the repair found them (not sorted). The repair
+   writes into library scratch, a few slots per unit from per-wave blocks; a scan of
+   changed and a gather then pack the caller's arrays. *out_total (host, nullable) =
+   sum(changed). d_ptr and d_changed are always filled; when the total exceeds cap the
+   entries are not, and the call returns OPENR_SPF_E2BIG (cap 0: counts and ptr only).
+   Synchronizes `stream`. */
+int openr_spf_whatif_delta_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_links,
+                                  uint32_t n_links, const uint32_t* d_sources, uint32_t n_sources,
+                                  uint32_t flags, uint32_t* d_changed, uint64_t* d_ptr,
+                                  uint32_t* d_node, uint64_t* d_dist, uint8_t* d_nh, uint64_t cap,
+                                  uint32_t nh_bytes, void* stream, uint64_t* out_total,
+                                  uint64_t* out_solved);
 
 /* LinkState::getKthPaths(src[i], dst[i], 1) and (.., 2) (LinkState.cpp:762-791, with
    traceOnePath :398-419) for a batch of pairs, traced on the device. Per pair, tok1 /

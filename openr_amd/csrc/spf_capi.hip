@@ -99,6 +99,15 @@ struct Device {
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
   DevBuf<uint32_t> kkeep, kpart;  // KSP pairs that need a second SPF; its count as a class partition
+  // what-if delta output of the host form (openr_spf_whatif_delta): per-unit pool offsets,
+  // the pool (node, distance, next-hop bytes) and its cursor
+  DevBuf<uint32_t> dl_off, dl_node;
+  DevBuf<unsigned long long> dl_dist, dl_used, dl_tsum;
+  DevBuf<uint8_t> dl_nh;
+  // ... and the host form's device-side CSR before it is copied out
+  DevBuf<unsigned long long> dlo_ptr, dlo_dist;
+  DevBuf<uint32_t> dlo_node;
+  DevBuf<uint8_t> dlo_nh;
   // incremental updates: patch records, the last patch's delta edges, refresh work list,
   // host-form refresh rows
   DevBuf<PatchRec> precs;
@@ -525,7 +534,8 @@ constexpr size_t kWhatifChunkBytes = size_t(1) << 30;
 // Reads the affected-unit count back (one stream sync) to size the chunks.
 hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, const Plan& ign_plan,
                             const uint32_t* d_links, uint32_t n_links, const uint32_t* d_sources, uint32_t n_src,
-                            uint32_t* d_changed, hipStream_t s, uint32_t* solved, bool use_link_metric) {
+                            uint32_t* d_changed, hipStream_t s, uint32_t* solved, bool use_link_metric,
+                            const WhatifDelta& dl = WhatifDelta{}) {
   const uint32_t V = ctx->V, tw = (ctx->E + 63u) / 64u;
   const uint32_t nb = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
   *solved = 0;
@@ -593,10 +603,11 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       if (fused) {
         b.seed_nh = d.base_nh.p;
         b.seed_changed = d_changed;
+        b.delta = dl;
       }
       if ((e2 = launch(ctx, d, ign_plan, b, s)) != hipSuccess) return e2;
       if (!fused && (e2 = launch_rows_compare(m, V, nb, d.wdist.p, d.wnh.p, d.base_dist.p, d.base_nh.p, d.wunit.p + off, n_src,
-                                    d_changed, d.num_cus, s)) != hipSuccess)
+                                    d_changed, dl, d.num_cus, s)) != hipSuccess)
         return e2;
     }
     return hipSuccess;
@@ -621,7 +632,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
                                     d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
                                     d_changed, d.wchanged_t.p, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p,
-                                    d.work.p + kIncrCtr, d.num_cus, s));
+                                    d.work.p + kIncrCtr, dl, d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));
       // Units past the slots are large (WAN: ~6 500 of 1.02 M affected units, ~150 dirty
       // nodes on average): re-solved, each starting from its source's base rows (the
@@ -649,6 +660,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
         b.seed_tin = base_tin ? d.base_tin.p : nullptr;
         b.seed_nh = d.base_nh.p;
         b.seed_changed = d_changed;
+        b.delta = dl;
         if (prof_enabled()) {
           OPENR_TRY(hipMallocAsync(reinterpret_cast<void**>(&b.prof_solve), 10 * units * sizeof(unsigned long long), s));
           OPENR_TRY(hipMemsetAsync(b.prof_solve, 0, 10 * units * sizeof(unsigned long long), s));
@@ -735,7 +747,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
   if (!count) return hipSuccess;
   // OPENR_SPF_WHATIF=incr: one wavefront per affected unit repairs it from the base rows it
   // re-reads (A set, distances inside A, dirty next hops); =solve re-solves every unit
-  if (!exact && !(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
+  if (!exact && !dl.node && !(mode && !std::strcmp(mode, "solve")) && whatif_incr_lds_bytes(V, nb, dist64)) {
     return launch_whatif_incr(d.g, d.wsrc.p, d.wlink.p, d.wunit.p, count, n_src, d.base_dist.p, d.base_nh.p, nb,
                               !use_link_metric, dist64, d_changed, d.work.p + kIncrCtr, d.num_cus, s);
   }
@@ -935,6 +947,68 @@ int whatif_plans(openr_spf_ctx* ctx, uint32_t flags, Plan* base_plan, Plan* ign_
   return make_plan(ctx, flags, true, ign_plan);
 }
 
+// openr_spf_whatif_delta[_device] on one device: the sweep with the delta into library
+// scratch (per-unit slots, WhatifDelta), the exclusive scan of changed into d_ptr, then
+// (when the total fits `cap`) every unit's entries gathered into the caller's CSR arrays.
+// Synchronizes s. *total = sum(changed); OPENR_SPF_E2BIG when it exceeds cap.
+int whatif_delta_on_device(openr_spf_ctx* ctx, Device& d, const uint32_t* d_links, uint32_t n_links,
+                           const uint32_t* d_sources, uint32_t n_src, uint32_t flags, uint32_t* d_changed,
+                           uint64_t* d_ptr, uint32_t* d_node, unsigned long long* d_dist, uint8_t* d_nh, uint64_t cap,
+                           uint32_t nhb, hipStream_t s, uint64_t* total, uint64_t* solved_out) {
+  const uint32_t nb = std::max<uint32_t>(1u, (ctx->nh_bits + 7u) / 8u);
+  if (nhb < nb) return fail(OPENR_SPF_EINVAL, "nh_bytes %u below the graph's next-hop width %u", nhb, nb);
+  Plan bp, ip;
+  int rc = whatif_plans(ctx, flags, &bp, &ip);
+  if (rc) return rc;
+  const size_t units = (size_t)n_links * n_src;
+  *total = 0;
+  *solved_out = 0;
+  unsigned long long* ptr = reinterpret_cast<unsigned long long*>(d_ptr);
+  if (!units) {
+    HIP_TRY(hipMemsetAsync(ptr, 0, sizeof(unsigned long long), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return OPENR_SPF_OK;
+  }
+  // scratch pool: room for the caller's cap twice over (gaps of the waves' slot blocks,
+  // grp_repair) plus one block per resident wave, at most 2^32 - 1 slots
+  const uint64_t want = std::min<uint64_t>(2u * cap + (uint64_t)d.num_cus * 32u * 256u + 1024u, 0xFFFFFFFFull);
+  HIP_TRY(d.dl_off.reserve(units));
+  HIP_TRY(d.dl_node.reserve(want));
+  HIP_TRY(d.dl_dist.reserve(want));
+  HIP_TRY(d.dl_nh.reserve(want * nhb));
+  HIP_TRY(d.dl_used.reserve(1));
+  HIP_TRY(d.dl_tsum.reserve(units / 4096u + 1u));
+  HIP_TRY(hipMemsetAsync(d.dl_used.p, 0, sizeof(unsigned long long), s));
+  WhatifDelta dl;
+  dl.off = d.dl_off.p;
+  dl.node = d.dl_node.p;
+  dl.dist = d.dl_dist.p;
+  dl.nh = d.dl_nh.p;
+  dl.cap = (uint32_t)want;
+  dl.nhb = nhb;
+  dl.used = d.dl_used.p;
+  uint32_t solved = 0;
+  HIP_TRY(whatif_on_device(ctx, d, bp, ip, d_links, n_links, d_sources, n_src, d_changed, s, &solved,
+                           (flags & OPENR_SPF_USE_LINK_METRIC) != 0, dl));
+  HIP_TRY(launch_delta_scan(d_changed, units, d.dl_tsum.p, ptr, s));
+  unsigned long long tu[2] = {0, 0};  // total entries, pool slots used
+  HIP_TRY(hipMemcpyAsync(&tu[0], ptr + units, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&tu[1], d.dl_used.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *total = tu[0];
+  *solved_out = (uint64_t)solved + n_src;
+  ctx->stats.spf_runs += *solved_out;
+  ctx->stats.batches += 1;
+  if (tu[1] > want)
+    return fail(OPENR_SPF_E2BIG, "delta needs %llu entries (%llu pool slots; scratch %llu for cap %llu)", tu[0], tu[1],
+                (unsigned long long)want, (unsigned long long)cap);
+  if (tu[0] > cap) return fail(OPENR_SPF_E2BIG, "delta needs %llu entries, cap %llu", tu[0], (unsigned long long)cap);
+  HIP_TRY(launch_delta_gather(d_changed, units, d.dl_off.p, ptr, dl, d_node, d_dist, d_nh, d.num_cus, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return OPENR_SPF_OK;
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -1032,6 +1106,16 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.part.release();
     d.kkeep.release();
     d.kpart.release();
+    d.dl_off.release();
+    d.dl_node.release();
+    d.dl_dist.release();
+    d.dl_used.release();
+    d.dl_nh.release();
+    d.dl_tsum.release();
+    d.dlo_ptr.release();
+    d.dlo_dist.release();
+    d.dlo_node.release();
+    d.dlo_nh.release();
     void* sweep[] = {d.base_dist.p, d.base_tight.p, d.wdist.p, d.base_nh.p, d.wnh.p, d.wsrc.p, d.wlink.p,
                      d.wunit.p,     d.wcount.p,     d.wiota.p, d.base_tin.p, d.win_links.p, d.win_src.p, d.wchanged.p, d.wchanged_t.p,
                      d.kbase.p,     d.krows.p,      d.krows16.p, d.kign.p,  d.kend.p, d.ksrc.p,      d.kptr.p,    d.kstatus.p,
@@ -1796,6 +1880,125 @@ int openr_spf_whatif_device(openr_spf_ctx* ctx, int device_index, const uint32_t
   ctx->stats.spf_runs += total;
   ctx->stats.batches += 1;
   if (out_solved) *out_solved = total;
+  return OPENR_SPF_OK;
+}
+
+int openr_spf_whatif_delta_device(openr_spf_ctx* ctx, int device_index, const uint32_t* d_links, uint32_t n_links,
+                                  const uint32_t* d_sources, uint32_t n_sources, uint32_t flags, uint32_t* d_changed,
+                                  uint64_t* d_ptr, uint32_t* d_node, uint64_t* d_dist, uint8_t* d_nh, uint64_t cap,
+                                  uint32_t nh_bytes, void* stream, uint64_t* out_total, uint64_t* out_solved) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (device_index < 0 || device_index >= (int)ctx->devs.size())
+    return fail(OPENR_SPF_EINVAL, "device_index %d out of range", device_index);
+  if ((n_links && !d_links) || (n_sources && !d_sources) || (n_links && n_sources && !d_changed) || !d_ptr)
+    return fail(OPENR_SPF_EINVAL, "null links, sources, changed or ptr");
+  if (cap && (!d_node || !d_dist || !d_nh)) return fail(OPENR_SPF_EINVAL, "null delta buffer");
+  Device& d = ctx->devs[device_index];
+  HIP_TRY(hipSetDevice(d.ordinal));
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : d.stream;
+  uint64_t total = 0, solved = 0;
+  const int rc = whatif_delta_on_device(ctx, d, d_links, n_links, d_sources, n_sources, flags, d_changed, d_ptr,
+                                        d_node, reinterpret_cast<unsigned long long*>(d_dist), d_nh, cap, nh_bytes,
+                                        s, &total, &solved);
+  if (out_total) *out_total = total;
+  if (out_solved) *out_solved = solved;
+  return rc;
+}
+
+int openr_spf_whatif_delta(openr_spf_ctx* ctx, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                           uint32_t n_sources, uint32_t flags, uint32_t* changed, openr_spf_whatif_delta_t* delta,
+                           uint64_t* out_solved) {
+  if (!ctx) return fail(OPENR_SPF_EINVAL, "null context");
+  if (!ctx->has_graph) return fail(OPENR_SPF_EINVAL, "no graph set (openr_spf_set_graph)");
+  if (!delta || !delta->ptr) return fail(OPENR_SPF_EINVAL, "null delta or delta->ptr");
+  if ((n_links && !links) || (n_sources && !sources) || (n_links && n_sources && !changed))
+    return fail(OPENR_SPF_EINVAL, "null links, sources or changed");
+  if (delta->cap && (!delta->node || !delta->dist || !delta->nh))
+    return fail(OPENR_SPF_EINVAL, "null delta->node, dist or nh");
+  for (uint32_t i = 0; i < n_sources; ++i)
+    if (sources[i] >= ctx->V) return fail(OPENR_SPF_EINVAL, "source %u out of range (V=%u)", sources[i], ctx->V);
+  for (uint32_t i = 0; i < n_links; ++i)
+    if (links[i] >= ctx->L) return fail(OPENR_SPF_EINVAL, "link %u out of range (L=%u)", links[i], ctx->L);
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t nhb = delta->nh_bytes;
+  // links split in contiguous blocks across the devices (openr_spf_whatif); each device's
+  // CSR is appended to the caller's at the running total
+  const uint32_t nd = (uint32_t)ctx->devs.size();
+  const uint32_t per = (n_links + nd - 1) / std::max<uint32_t>(nd, 1);
+  uint64_t solved_total = 0, at = 0;
+  bool over = false;
+  delta->ptr[0] = 0;
+  std::vector<uint64_t> ptr;
+  std::vector<uint32_t> idx;
+  for (uint32_t di = 0; di < nd; ++di) {
+    Device& d = ctx->devs[di];
+    const uint32_t b = std::min(n_links, di * per), e = std::min(n_links, b + per), m = e - b;
+    if (!m || !n_sources) continue;
+    const size_t mu = (size_t)m * n_sources;
+    HIP_TRY(hipSetDevice(d.ordinal));
+    HIP_TRY(d.win_links.reserve(m));
+    HIP_TRY(d.win_src.reserve(n_sources));
+    HIP_TRY(d.wchanged.reserve(mu));
+    HIP_TRY(d.dlo_ptr.reserve(mu + 1));
+    HIP_TRY(hipMemcpyAsync(d.win_links.p, links + b, m * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    HIP_TRY(hipMemcpyAsync(d.win_src.p, sources, n_sources * sizeof(uint32_t), hipMemcpyHostToDevice, d.stream));
+    // the device's entries land in library buffers sized to the room left in the caller's
+    const uint64_t room = delta->cap > at ? delta->cap - at : 0;
+    HIP_TRY(d.dlo_node.reserve(std::max<uint64_t>(room, 1)));
+    HIP_TRY(d.dlo_dist.reserve(std::max<uint64_t>(room, 1)));
+    HIP_TRY(d.dlo_nh.reserve(std::max<uint64_t>(room * nhb, 1)));
+    uint64_t total = 0, solved = 0;
+    int rc = whatif_delta_on_device(ctx, d, d.win_links.p, m, d.win_src.p, n_sources, flags, d.wchanged.p,
+                                    reinterpret_cast<uint64_t*>(d.dlo_ptr.p), d.dlo_node.p, d.dlo_dist.p, d.dlo_nh.p,
+                                    room, nhb, d.stream, &total, &solved);
+    if (rc && rc != OPENR_SPF_E2BIG) return rc;
+    over |= rc == OPENR_SPF_E2BIG;
+    solved_total += solved;
+    ptr.resize(mu + 1);
+    HIP_TRY(hipMemcpyAsync(changed + (size_t)b * n_sources, d.wchanged.p, mu * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           d.stream));
+    HIP_TRY(hipMemcpyAsync(ptr.data(), d.dlo_ptr.p, (mu + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    const bool fits = !over && total <= room;
+    if (fits && total) {
+      HIP_TRY(hipMemcpyAsync(delta->node + at, d.dlo_node.p, total * 4u, hipMemcpyDeviceToHost, d.stream));
+      HIP_TRY(hipMemcpyAsync(delta->dist + at, d.dlo_dist.p, total * 8u, hipMemcpyDeviceToHost, d.stream));
+      HIP_TRY(hipMemcpyAsync(delta->nh + at * nhb, d.dlo_nh.p, total * nhb, hipMemcpyDeviceToHost, d.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    for (size_t u = 0; u < mu; ++u) {
+      const size_t gu = (size_t)b * n_sources + u;
+      delta->ptr[gu + 1] = at + ptr[u + 1];
+      const uint32_t c = (uint32_t)(ptr[u + 1] - ptr[u]);
+      if (!fits || c < 2) continue;
+      // each unit's nodes ascending (the device keeps the repair's order)
+      const uint64_t o = at + ptr[u];
+      bool sorted = true;
+      for (uint32_t k = 1; k < c && sorted; ++k) sorted = delta->node[o + k - 1] < delta->node[o + k];
+      if (sorted) continue;
+      idx.resize(c);
+      for (uint32_t k = 0; k < c; ++k) idx[k] = k;
+      std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return delta->node[o + x] < delta->node[o + y]; });
+      std::vector<uint32_t> tn(c);
+      std::vector<uint64_t> td(c);
+      std::vector<uint8_t> th((size_t)c * nhb);
+      for (uint32_t k = 0; k < c; ++k) {
+        tn[k] = delta->node[o + idx[k]];
+        td[k] = delta->dist[o + idx[k]];
+        std::memcpy(&th[(size_t)k * nhb], delta->nh + (o + idx[k]) * nhb, nhb);
+      }
+      std::memcpy(delta->node + o, tn.data(), c * 4u);
+      std::memcpy(delta->dist + o, td.data(), c * 8u);
+      std::memcpy(delta->nh + o * nhb, th.data(), (size_t)c * nhb);
+    }
+    at += total;
+  }
+  ctx->stats.last_batch_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (out_solved) *out_solved = solved_total;
+  if (over || at > delta->cap)
+    return fail(OPENR_SPF_E2BIG, "delta needs %llu entries, cap %llu (ptr and changed are filled, entries are not)",
+                (unsigned long long)at, (unsigned long long)delta->cap);
   return OPENR_SPF_OK;
 }
 

@@ -90,6 +90,21 @@ struct LaunchInfo {
 void note_launch(const char* kernel);
 void clear_launch_trace();
 
+// Optional per-unit delta of a what-if sweep (openr_spf_whatif_delta): the nodes whose
+// distance or next-hop set a unit's failure changes, with their new values. Unit u's
+// entries are pool slots [off[u], off[u] + changed[u]) in no particular order; a unit
+// reserves its slots with one atomic on `used`, and slots past `cap` are not written
+// (used then exceeds cap: the caller reports OPENR_SPF_E2BIG).
+struct WhatifDelta {
+  uint32_t* off = nullptr;             // [units] (unit = link index * n_src + source index)
+  uint32_t* node = nullptr;            // [cap] node id; null: no delta output
+  unsigned long long* dist = nullptr;  // [cap] new distance (UINT64_MAX: not reached)
+  uint8_t* nh = nullptr;               // [cap][nhb] new next-hop bits, zero padded past the graph's width
+  uint32_t cap = 0, nhb = 0;
+  unsigned long long* used = nullptr;  // pool cursor (device counter, zeroed by the launcher)
+  __device__ uint32_t base_of(unsigned long long b) const { return b < 0xFFFFFFFFull ? (uint32_t)b : 0xFFFFFFFFu; }
+};
+
 struct SolveArgs {
   const uint32_t* sources;
   uint32_t n;
@@ -150,6 +165,7 @@ struct SolveArgs {
   // next-hop bytes differ at seed_changed[seed_unit[sid]] (the what-if unit's answer)
   const uint8_t* seed_nh;
   uint32_t* seed_changed;
+  WhatifDelta delta;  // with seed_changed: the unit's changed nodes and their new rows (node == null: off)
   // rounds kernel: tin_out (nullable, solves without a seed) receives each solve's tight
   // in-degree row [out_row][V] (u16); seed_tin (nullable, with seed_dist) is such a row set
   // for the base SPF, so a seeded start reads the counts instead of scanning every in-edge
@@ -232,9 +248,18 @@ hipError_t launch_whatif_filter(const DevGraph& g, const uint32_t* links, uint32
                                 uint32_t n_src, const uint64_t* base_tight, uint32_t* changed, uint32_t* wsrc,
                                 uint32_t* wlink, uint32_t* wunit, uint32_t* wcount, int num_cus, hipStream_t s);
 // changed[wunit[k]] = nodes whose dist / next-hop bytes differ from base row wunit[k] % n_src.
+// With dl.node: also the unit's changed nodes and their new rows (WhatifDelta).
 hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64_t* dist, const uint8_t* nh,
                                const uint64_t* base_dist, const uint8_t* base_nh, const uint32_t* wunit,
-                               uint32_t n_src, uint32_t* changed, int num_cus, hipStream_t s);
+                               uint32_t n_src, uint32_t* changed, const WhatifDelta& dl, int num_cus, hipStream_t s);
+// What-if delta compaction: ptr[0, n] = exclusive scan of changed (tsum: one u64 per
+// 4096 units of scratch), then every unit's entries from its pool slots (off) to its CSR
+// slots (ptr) in node / dist / nh.
+hipError_t launch_delta_scan(const uint32_t* changed, size_t n, unsigned long long* tsum, unsigned long long* ptr,
+                             hipStream_t s);
+hipError_t launch_delta_gather(const uint32_t* changed, size_t n, const uint32_t* off, const unsigned long long* ptr,
+                               const WhatifDelta& pool, uint32_t* node, unsigned long long* dist, uint8_t* nh,
+                               int num_cus, hipStream_t s);
 hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s);
 // Incremental what-if (spf_sweep.hip): changed[wunit[k]] for every listed unit from the
 // base rows alone (no full re-solve). Uses a.work-style counters `ctr` (2 slots).
@@ -247,16 +272,14 @@ uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
 // stages the source's base rows (dist, next hops, tight mask) in LDS once; its wavefronts
 // filter the links (no tight edge -> 0) and repair the affected ones on private overlays.
 // Writes every changed[i * n_src + j]; affected[0] = affected units, affected[1] = units
-// that outgrew the first pass's dirty slots (listed in ovf_*[0, affected[1])). With `list`
-// (= ovf_unit of the first pass, n_list = affected[1]) it is the list pass: it repairs the
-// listed units again with every slot and lists the ones that still outgrow them in
-// ovf_*[n_list, n_list + affected[2]) for a re-solve.
+// that outgrew the dirty slots (listed in ovf_*[0, affected[1]) for a re-solve). With
+// dl.node, every repaired unit also writes its delta (WhatifDelta).
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* changed_t, uint32_t* affected,
-                               uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus,
-                               hipStream_t s);
+                               uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr,
+                               const WhatifDelta& dl, int num_cus, hipStream_t s);
 // 0 when the grouped repair cannot run on the graph (ids, next-hop width, degree, LDS)
 uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64, uint32_t max_deg);
 

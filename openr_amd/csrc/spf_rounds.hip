@@ -416,16 +416,52 @@ __global__ __launch_bounds__(BLOCK) void rounds_kernel(DevGraph g, SolveArgs a, 
         const uint32_t unit = a.seed_unit[sid], j = unit % a.seed_nsrc, nb = a.nh_bytes;
         const uint64_t* bd = a.seed_dist + (size_t)j * V;
         const uint8_t* bh = a.seed_nh + (size_t)j * V * nb;
-        uint32_t c = 0;
-        for (uint32_t v = tid; v < V; v += BLOCK) {
+        auto differs = [&](uint32_t v) {
           const D dv = dist[v];
           bool diff = (dv == INF ? ~0ull : (uint64_t)dv) != bd[v];
           for (uint32_t b = 0; b < nb && !diff; ++b) diff = (uint8_t)N::byte(nh, v, b) != bh[(size_t)v * nb + b];
-          c += diff ? 1u : 0u;
-        }
+          return diff;
+        };
+        uint32_t c = 0;
+        for (uint32_t v = tid; v < V; v += BLOCK) c += differs(v) ? 1u : 0u;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
         if ((tid & 63u) == 0 && c) atomicAdd(&a.seed_changed[unit], c);  // zeroed by the seeded start
+        if (a.delta.node) {
+          // the unit's delta (WhatifDelta): one pool reservation for the workgroup, then each
+          // wave writes its differing nodes in order. The frontier queues are free now.
+          constexpr uint32_t W = BLOCK / 64u;
+          const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63u;
+          uint32_t* sc = reinterpret_cast<uint32_t*>(base + lay.fa);  // >= 8 words (fa, fb)
+          if (lane == 0) sc[wave] = c;
+          sync();
+          if (tid == 0) {
+            uint32_t total = 0;
+            for (uint32_t w = 0; w < W; ++w) total += sc[w];
+            const unsigned long long b = total ? atomicAdd(a.delta.used, (unsigned long long)total) : 0ull;
+            sc[4] = (uint32_t)b;
+            sc[5] = (uint32_t)(b >> 32);
+            if (total) a.delta.off[unit] = a.delta.base_of(b);
+          }
+          sync();
+          unsigned long long cur = (unsigned long long)sc[4] | ((unsigned long long)sc[5] << 32);
+          for (uint32_t w = 0; w < wave; ++w) cur += sc[w];
+          for (uint32_t v0 = wave * 64u; v0 < V; v0 += BLOCK) {
+            const uint32_t v = v0 + lane;
+            const bool diff = v < V && differs(v);
+            const unsigned long long m = __ballot(diff);
+            const unsigned long long pos =
+                cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (diff && pos < a.delta.cap) {
+              a.delta.node[pos] = v;
+              const D dv = dist[v];
+              a.delta.dist[pos] = dv == INF ? ~0ull : (unsigned long long)dv;
+              uint8_t* o = a.delta.nh + (size_t)pos * a.delta.nhb;
+              for (uint32_t b = 0; b < a.delta.nhb; ++b) o[b] = b < nb ? (uint8_t)N::byte(nh, v, b) : 0u;
+            }
+            cur += (uint32_t)__popcll(m);
+          }
+        }
         goto next_solve;
       }
       {

@@ -68,26 +68,54 @@ __global__ __launch_bounds__(256) void whatif_filter(const uint2* ledge, uint32_
 __global__ __launch_bounds__(256) void rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64_t* dist,
                                                     const uint8_t* nh, const uint64_t* base_dist,
                                                     const uint8_t* base_nh, const uint32_t* wunit, uint32_t n_src,
-                                                    uint32_t* changed) {
+                                                    uint32_t* changed, WhatifDelta dl) {
   __shared__ uint32_t part[4];
+  __shared__ unsigned long long s_base;
+  const uint32_t lane = __lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
     const uint32_t unit = wunit[k], j = unit % n_src;
     const uint64_t* d = dist + (size_t)k * V;
     const uint64_t* bd = base_dist + (size_t)j * V;
     const uint8_t* h = nh ? nh + (size_t)k * V * nb : nullptr;
     const uint8_t* bh = nh ? base_nh + (size_t)j * V * nb : nullptr;
-    uint32_t c = 0;
-    for (uint32_t v = threadIdx.x; v < V; v += 256u) {
+    auto differs = [&](uint32_t v) {
       bool diff = d[v] != bd[v];
       if (h)
         for (uint32_t b = 0; b < nb && !diff; ++b) diff = h[(size_t)v * nb + b] != bh[(size_t)v * nb + b];
-      c += diff ? 1u : 0u;
-    }
+      return diff;
+    };
+    uint32_t c = 0;
+    for (uint32_t v = threadIdx.x; v < V; v += 256u) c += differs(v) ? 1u : 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if (__lane_id() == 0) part[threadIdx.x >> 6] = c;
+    if (lane == 0) part[wave] = c;
     __syncthreads();
-    if (threadIdx.x == 0) changed[unit] = part[0] + part[1] + part[2] + part[3];
+    const uint32_t total = part[0] + part[1] + part[2] + part[3];
+    if (threadIdx.x == 0) changed[unit] = total;
+    if (dl.node) {  // the unit's delta: one pool reservation, then each wave's diffs in order
+      if (threadIdx.x == 0) {
+        const unsigned long long b = total ? atomicAdd(dl.used, (unsigned long long)total) : 0ull;
+        s_base = b;
+        if (total) dl.off[unit] = dl.base_of(b);
+      }
+      __syncthreads();
+      unsigned long long cur = s_base;
+      for (uint32_t w = 0; w < wave; ++w) cur += part[w];
+      for (uint32_t v0 = wave * 64u; v0 < V; v0 += 256u) {
+        const uint32_t v = v0 + lane;
+        const bool diff = v < V && differs(v);
+        const unsigned long long m = __ballot(diff);
+        const unsigned long long pos =
+            cur + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (diff && pos < dl.cap) {
+          dl.node[pos] = v;
+          dl.dist[pos] = d[v];
+          uint8_t* o = dl.nh + (size_t)pos * dl.nhb;
+          for (uint32_t b = 0; b < dl.nhb; ++b) o[b] = (h && b < nb) ? h[(size_t)v * nb + b] : 0u;
+        }
+        cur += (uint32_t)__popcll(m);
+      }
+    }
     __syncthreads();
   }
 }
@@ -665,6 +693,9 @@ struct GrpWave {
   uint32_t cap;            // dirty slots
   uint16_t *alist, *dlist;
   unsigned long long* prof;  // tuning (OPENR_SPF_PROF): per-phase cycles and sizes, or null
+  WhatifDelta dl;            // delta output (the DL kernel variant)
+  unsigned long long pcur, pend;  // DL: this wave's current block of pool slots [pcur, pend)
+  uint32_t uidx;             // the unit's index in the API rows (link index * n_src + source index)
   __device__ uint32_t w(const EdgeRec& r) const { return unit ? 1u : r.wout; }
   __device__ uint32_t wi(const EdgeRec& r) const { return unit ? 1u : r.win; }
   __device__ bool expands(uint32_t x) const { return x == src || !gv.ovl(x); }
@@ -700,7 +731,15 @@ constexpr uint32_t kGrpOverflow = UINT32_MAX;  // grp_repair: the unit outgrew t
 
 // One affected unit: returns the changed-node count (uniform across the wave), or
 // kGrpOverflow.
-template <typename D, bool LG, uint32_t W>
+// Delta output (DL): a wave takes pool slots in blocks of kDeltaBlock from the pool
+// cursor and hands them to its units in order, so the cursor sees one atomic per block
+// instead of one per unit (a million units on one address serialised: 12 ms against the
+// 2.5 ms repair). A unit that does not fit the rest of the block starts a new block (the
+// rest is a gap); a unit larger than half a block reserves its own slots. The pool is
+// library scratch: openr_spf_whatif_delta compacts it into the caller's CSR.
+constexpr uint32_t kDeltaBlock = 256;
+
+template <typename D, bool LG, uint32_t W, bool DL>
 __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, uint32_t bnode) {
   constexpr D INF = (D)~(D)0;
   const uint32_t vw = (V + 31u) / 32u, nb = c.nb;
@@ -944,6 +983,49 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
     lds_fence();
   }
   if (ovf) return kGrpOverflow;
+  if (DL && nchanged) {
+    // delta output: the changed dirty nodes (A members, and nodes whose set changed) with
+    // their new distance and next hops, from the overlays (slot k holds dlist[k])
+    unsigned long long b = 0;
+    if (nchanged > kDeltaBlock / 2u) {
+      if (lane == 0) b = atomicAdd(c.dl.used, (unsigned long long)nchanged);
+      b = readlane_t(b, 0);
+    } else {
+      if (c.pcur + nchanged > c.pend) {
+        unsigned long long nbk = 0;
+        if (lane == 0) nbk = atomicAdd(c.dl.used, (unsigned long long)kDeltaBlock);
+        nbk = readlane_t(nbk, 0);
+        c.pcur = nbk;
+        c.pend = nbk + kDeltaBlock;
+      }
+      b = c.pcur;
+      c.pcur += nchanged;
+    }
+    if (lane == 0) c.dl.off[c.uidx] = c.dl.base_of(b);
+    for (uint32_t k0 = 0; k0 < nd; k0 += 64u) {
+      const uint32_t k = k0 + lane;
+      uint32_t v = 0;
+      bool in_a = false, own = false;
+      if (k < nd) {
+        v = c.dlist[k];
+        in_a = bit_of(c.ina, v);
+        own = bit_of(c.nhm, v);
+      }
+      const bool ch = in_a || own;
+      const unsigned long long m = __ballot(ch);
+      const unsigned long long pos =
+          b + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (ch && pos < c.dl.cap) {
+        c.dl.node[pos] = v;
+        const D dv = in_a ? c.adist[k] : c.bdist[v];
+        c.dl.dist[pos] = dv == INF ? ~0ull : (unsigned long long)dv;
+        const uint8_t* h = own ? c.anh + (size_t)k * nb : c.bnh + (size_t)v * nb;
+        uint8_t* o = c.dl.nh + (size_t)pos * c.dl.nhb;
+        for (uint32_t q = 0; q < c.dl.nhb; ++q) o[q] = q < nb ? h[q] : 0u;
+      }
+      b += (uint32_t)__popcll(m);
+    }
+  }
   if (c.prof && lane == 0) {
     pt3 = (long long)__builtin_amdgcn_s_memtime();
     atomicAdd(&c.prof[0], (unsigned long long)(pt1 - pt0));
@@ -966,12 +1048,12 @@ constexpr uint32_t kGrpMaxBlock = 512;
 // LDS allows; 7 (its default since round 4) forces 72 VGPRs at the price of 140 B of
 // scratch spills per lane, and the 28 waves per CU the LDS layout allows win (kernel
 // 3.66 -> 2.81 ms on the WAN).
-template <typename D, bool LG, uint32_t W, int WPE>
+template <typename D, bool LG, uint32_t W, int WPE, bool DL>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
     uint32_t cap, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
-    uint32_t* ctr, unsigned long long* prof) {
+    uint32_t* ctr, unsigned long long* prof, WhatifDelta dl) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1015,6 +1097,8 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.nb = nb;
   c.unit = unit != 0;
   c.prof = prof;
+  c.dl = dl;
+  c.pcur = c.pend = 0;
   c.bdist = bdist;
   c.bnh = bnh;
   c.btight = btight;
@@ -1096,7 +1180,8 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
       const uint32_t ent = __builtin_amdgcn_readfirstlane(ulist[idx]);
       const uint32_t i = l0 + (ent >> 16);
       c.link = links[i];  // first needed in step (2): the load overlaps step (1)
-      const uint32_t cnt = grp_repair(c, lane, V, ent & 0xFFFFu);
+      c.uidx = i * n_src + j;
+      const uint32_t cnt = grp_repair<D, LG, W, DL>(c, lane, V, ent & 0xFFFFu);
       if (lane == 0) {
         // results source-major (changed_t[j][i]): an item's units share cache lines, where the
         // link-major API rows put every unit of an item on a line of its own (whatif_transpose)
@@ -1144,6 +1229,95 @@ __global__ __launch_bounds__(256) void whatif_transpose(const uint32_t* changed_
   }
 }
 
+// --- what-if delta compaction (openr_spf_whatif_delta) --------------------------------
+// ptr[0, n] = exclusive scan of changed[0, n) (u64), in three passes over tiles of
+// kScanTile units: tile sums, a scan of the sums in one workgroup, tile-local scans.
+constexpr uint32_t kScanTile = 4096;  // 256 threads x 16 units
+
+__device__ __forceinline__ unsigned long long block_excl_scan256(unsigned long long x, unsigned long long* tmp,
+                                                                 unsigned long long& total) {
+  const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+  unsigned long long inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) tmp[wave] = inc;
+  __syncthreads();
+  unsigned long long before = 0;
+  for (uint32_t w = 0; w < wave; ++w) before += tmp[w];
+  total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+  __syncthreads();
+  return before + inc - x;
+}
+
+__global__ __launch_bounds__(256) void delta_tile_sums(const uint32_t* c, size_t n, unsigned long long* tsum) {
+  __shared__ unsigned long long tmp[4];
+  const size_t t0 = (size_t)blockIdx.x * kScanTile;
+  unsigned long long x = 0;
+  for (uint32_t k = 0; k < kScanTile / 256u; ++k) {
+    const size_t u = t0 + (size_t)k * 256u + threadIdx.x;
+    if (u < n) x += c[u];
+  }
+  unsigned long long total;
+  (void)block_excl_scan256(x, tmp, total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void delta_scan_sums(unsigned long long* tsum, uint32_t nt) {
+  __shared__ unsigned long long tmp[4];
+  unsigned long long carry = 0;
+  for (uint32_t i0 = 0; i0 < nt; i0 += 256u) {
+    const uint32_t i = i0 + threadIdx.x;
+    const unsigned long long x = i < nt ? tsum[i] : 0ull;
+    unsigned long long total;
+    const unsigned long long ex = block_excl_scan256(x, tmp, total);
+    if (i < nt) tsum[i] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(256) void delta_tile_scan(const uint32_t* c, size_t n, const unsigned long long* tsum,
+                                                       unsigned long long* ptr) {
+  __shared__ unsigned long long tmp[4];
+  const size_t t0 = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * (kScanTile / 256u);
+  uint32_t v[kScanTile / 256u];
+  unsigned long long x = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanTile / 256u; ++k) {
+    v[k] = t0 + k < n ? c[t0 + k] : 0u;
+    x += v[k];
+  }
+  unsigned long long total;
+  unsigned long long at = tsum[blockIdx.x] + block_excl_scan256(x, tmp, total);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanTile / 256u; ++k) {
+    if (t0 + k < n) ptr[t0 + k] = at;
+    at += v[k];
+  }
+  if (t0 < n && t0 + kScanTile / 256u >= n) ptr[n] = at;  // the thread holding unit n - 1: the total
+}
+
+// unit u's entries from its pool slots [off[u], off[u] + changed[u]) to the CSR slots
+// [ptr[u], ptr[u + 1]) (a thread per unit; the order inside a unit is kept)
+__global__ __launch_bounds__(256) void delta_gather(const uint32_t* c, size_t n, const uint32_t* off,
+                                                    const unsigned long long* ptr, WhatifDelta pool,
+                                                    uint32_t* node, unsigned long long* dist, uint8_t* nh) {
+  for (size_t u = (size_t)blockIdx.x * 256u + threadIdx.x; u < n; u += (size_t)gridDim.x * 256u) {
+    const uint32_t k = c[u];
+    if (!k) continue;
+    const size_t src = off[u], dst = ptr[u];
+    for (uint32_t q = 0; q < k; ++q) {
+      node[dst + q] = pool.node[src + q];
+      dist[dst + q] = pool.dist[src + q];
+    }
+    const uint8_t* hs = pool.nh + src * pool.nhb;
+    uint8_t* hd = nh + dst * pool.nhb;
+    for (uint32_t q = 0; q < k * pool.nhb; ++q) hd[q] = hs[q];
+  }
+}
+
 __global__ __launch_bounds__(256) void iota_u32(uint32_t* p, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) p[i] = i;
 }
@@ -1171,10 +1345,10 @@ hipError_t launch_whatif_filter(const DevGraph& g, const uint32_t* links, uint32
 
 hipError_t launch_rows_compare(uint32_t n, uint32_t V, uint32_t nb, const uint64_t* dist, const uint8_t* nh,
                                const uint64_t* base_dist, const uint8_t* base_nh, const uint32_t* wunit,
-                               uint32_t n_src, uint32_t* changed, int num_cus, hipStream_t s) {
+                               uint32_t n_src, uint32_t* changed, const WhatifDelta& dl, int num_cus, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(rows_compare, dim3(grid_for(n, 1u, num_cus)), dim3(256), 0, s, n, V, nb, dist, nh, base_dist,
-                     base_nh, wunit, n_src, changed);
+                     base_nh, wunit, n_src, changed, dl);
   return hipGetLastError();
 }
 
@@ -1219,8 +1393,8 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
                                const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* changed_t, uint32_t* affected,
-                               uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr, int num_cus,
-                               hipStream_t s) {
+                               uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr,
+                               const WhatifDelta& dl, int num_cus, hipStream_t s) {
   // [0] affected units, [1] units listed for a re-solve
   hipError_t err = hipMemsetAsync(affected, 0, 2u * sizeof(uint32_t), s);
   if (err != hipSuccess || !n_links || !n_src) return err;
@@ -1281,13 +1455,16 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // 4 waves per SIMD; 5 waves: 4.56 ms), round 4
 #define OPENR_GRP_LAUNCH(DT, LGV)                                                                              \
   do {                                                                                                         \
-    auto k = nb <= 4u ? whatif_group_kernel<DT, LGV, 1, 7> : whatif_group_kernel<DT, LGV, kGrpNhWords, 1>;     \
+    auto k = dl.node ? (nb <= 4u ? whatif_group_kernel<DT, LGV, 1, 7, true>                                  \
+                                 : whatif_group_kernel<DT, LGV, kGrpNhWords, 1, true>)                         \
+                     : (nb <= 4u ? whatif_group_kernel<DT, LGV, 1, 7, false>                                 \
+                                 : whatif_group_kernel<DT, LGV, kGrpNhWords, 1, false>);                       \
     err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
                        base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed_t, affected, ovf_src, ovf_link, \
-                       ovf_unit, ctr, prof);                                                                   \
+                       ovf_unit, ctr, prof, dl);                                                               \
   } while (0)
   if (d16) {
     if (lg) OPENR_GRP_LAUNCH(uint16_t, true);
@@ -1321,6 +1498,26 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     }
   }
   return err;
+}
+
+hipError_t launch_delta_scan(const uint32_t* changed, size_t n, unsigned long long* tsum, unsigned long long* ptr,
+                             hipStream_t s) {
+  const size_t nt = (n + kScanTile - 1) / kScanTile;
+  if (nt > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  if (!n) return hipMemsetAsync(ptr, 0, sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(delta_tile_sums, dim3((uint32_t)nt), dim3(256), 0, s, changed, n, tsum);
+  hipLaunchKernelGGL(delta_scan_sums, dim3(1), dim3(256), 0, s, tsum, (uint32_t)nt);
+  hipLaunchKernelGGL(delta_tile_scan, dim3((uint32_t)nt), dim3(256), 0, s, changed, n, tsum, ptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_gather(const uint32_t* changed, size_t n, const uint32_t* off, const unsigned long long* ptr,
+                               const WhatifDelta& pool, uint32_t* node, unsigned long long* dist, uint8_t* nh,
+                               int num_cus, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<size_t>((n + 255u) / 256u, (size_t)num_cus * 16u);
+  hipLaunchKernelGGL(delta_gather, dim3(grid), dim3(256), 0, s, changed, n, off, ptr, pool, node, dist, nh);
+  return hipGetLastError();
 }
 
 hipError_t launch_iota(uint32_t* p, uint32_t n, int num_cus, hipStream_t s) {

@@ -44,6 +44,8 @@ EXPORTS = (
     "openr_spf_solve_device",
     "openr_spf_whatif",
     "openr_spf_whatif_device",
+    "openr_spf_whatif_delta",
+    "openr_spf_whatif_delta_device",
     "openr_spf_ksp2",
     "openr_spf_ksp2_device",
     "openr_spf_host_alloc",
@@ -88,6 +90,17 @@ class SpfPatch(ctypes.Structure):
         ("n_nodes", ctypes.c_uint32),
         ("node_ids", ctypes.c_void_p),
         ("node_overloaded", ctypes.c_void_p),
+    ]
+
+
+class WhatifDelta(ctypes.Structure):  # openr_spf_whatif_delta_t
+    _fields_ = [
+        ("ptr", ctypes.c_void_p),
+        ("node", ctypes.c_void_p),
+        ("dist", ctypes.c_void_p),
+        ("nh", ctypes.c_void_p),
+        ("cap", ctypes.c_uint64),
+        ("nh_bytes", ctypes.c_uint32),
     ]
 
 
@@ -137,6 +150,9 @@ def load_library():
     l.openr_spf_solve_device.argtypes = [vp, ctypes.c_int, vp, u32, u32, vp, vp, vp, vp, u32, vp, vp]
     l.openr_spf_whatif.argtypes = [vp, vp, u32, vp, u32, u32, vp, P(ctypes.c_uint64)]
     l.openr_spf_whatif_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, P(ctypes.c_uint64)]
+    l.openr_spf_whatif_delta.argtypes = [vp, vp, u32, vp, u32, u32, vp, P(WhatifDelta), P(ctypes.c_uint64)]
+    l.openr_spf_whatif_delta_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, u32, u32, vp, vp, vp, vp, vp,
+                                                ctypes.c_uint64, u32, vp, P(ctypes.c_uint64), P(ctypes.c_uint64)]
     l.openr_spf_ksp2.argtypes = [vp, vp, vp, u32, u32, vp, vp]
     l.openr_spf_ksp2_device.argtypes = [vp, ctypes.c_int, vp, u32, vp, vp, u32, u32, vp, vp, vp]
     l.openr_spf_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
@@ -300,6 +316,49 @@ class SpfEngine:
                                                  n_sources, flags, vp(d_changed), vp(stream or None),
                                                  ctypes.byref(solved)))
         return int(solved.value)
+
+    def whatif_delta(self, links: Sequence[int], sources: Sequence[int], use_link_metric: bool = True,
+                     cap: Optional[int] = None, nh_bytes: Optional[int] = None):
+        """Per-link-failure sweep with each unit's delta (openr_spf_whatif_delta):
+        (changed[n_links, n_sources] u32, ptr[n_units + 1] u64, node u32, dist u64,
+        nh[entries, nh_bytes] u8, SPFs run). Unit u = i * n_sources + j owns entries
+        [ptr[u], ptr[u + 1]), node ids ascending. cap None: sized from a count-only pass."""
+        lk = np.ascontiguousarray(links, dtype=np.uint32)
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        nb = nh_bytes if nh_bytes is not None else self.nh_bytes
+        if cap is None:
+            changed, _ = self.whatif(lk, src, use_link_metric)
+            cap = int(changed.sum(dtype=np.uint64))
+        changed = np.zeros((lk.shape[0], src.shape[0]), dtype=np.uint32)
+        ptr = np.zeros(lk.shape[0] * src.shape[0] + 1, dtype=np.uint64)
+        node = np.zeros(max(cap, 1), dtype=np.uint32)
+        dist = np.zeros(max(cap, 1), dtype=np.uint64)
+        nh = np.zeros((max(cap, 1), nb), dtype=np.uint8)
+        d = WhatifDelta(_p(ptr), _p(node), _p(dist), _p(nh), cap, nb)
+        solved = ctypes.c_uint64()
+        flags = USE_LINK_METRIC if use_link_metric else 0
+        _check(self._lib.openr_spf_whatif_delta(self._ctx, _p(lk), lk.shape[0], _p(src), src.shape[0], flags,
+                                                _p(changed), ctypes.byref(d), ctypes.byref(solved)))
+        n = int(ptr[-1])
+        return changed, ptr, node[:n], dist[:n], nh[:n], int(solved.value)
+
+    def whatif_delta_device(self, d_links: int, n_links: int, d_sources: int, n_sources: int, d_changed: int,
+                            d_ptr: int, d_node: int, d_dist: int, d_nh: int, cap: int, nh_bytes: int,
+                            use_link_metric: bool = True, stream: int = 0, device_index: int = 0,
+                            allow_overflow: bool = False) -> Tuple[int, int]:
+        """Device-pointer form: (total entries, SPFs run). d_ptr [n_units + 1] u64 CSR; unit
+        u's entries are [ptr[u], ptr[u + 1]) in the repair's order."""
+        vp = ctypes.c_void_p
+        total = ctypes.c_uint64()
+        solved = ctypes.c_uint64()
+        flags = USE_LINK_METRIC if use_link_metric else 0
+        rc = self._lib.openr_spf_whatif_delta_device(self._ctx, device_index, vp(d_links), n_links, vp(d_sources),
+                                                     n_sources, flags, vp(d_changed), vp(d_ptr), vp(d_node or None),
+                                                     vp(d_dist or None), vp(d_nh or None), cap, nh_bytes,
+                                                     vp(stream or None), ctypes.byref(total), ctypes.byref(solved))
+        if not (allow_overflow and rc == E2BIG):
+            _check(rc)
+        return int(total.value), int(solved.value)
 
     def ksp2_tokens(self, src: Sequence[int], dst: Sequence[int], tok_cap: int = 256,
                     allow_overflow: bool = False) -> Tuple[np.ndarray, np.ndarray]:

@@ -4,4 +4,4 @@ Restates /root/reference/openr/decision/LinkState.cpp:398-419, 762-882 in C
 (spf_oracle.c). Imported only by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py; never by the product package openr_amd.
 """
-from .oracle import Oracle, OracleGraph, SpfRun, U64_MAX, build, default_threads  # noqa: F401
+from .oracle import Oracle, OracleGraph, SpfRun, U64_MAX, build, default_threads, delta_digest  # noqa: F401

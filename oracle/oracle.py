@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Set
+from typing import Dict, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
 
@@ -74,6 +74,10 @@ def lib():
         l.oracle_whatif.restype = ctypes.c_int
         l.oracle_whatif.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                     ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        l.oracle_whatif_delta_digest.restype = ctypes.c_int
+        l.oracle_whatif_delta_digest.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                                 ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_uint32, ctypes.c_int]
         l.faithful_all_sources.restype = ctypes.c_int
         l.faithful_all_sources.argtypes = [P(OracleGraph), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -200,6 +204,22 @@ class Oracle:
             raise RuntimeError("oracle_whatif failed")
         return out
 
+    def whatif_delta_digest(self, links: Sequence[int], sources: Sequence[int], nh_bytes: int,
+                            use_link_metric: bool = True, nthreads: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+        """(changed[n_links, n_sources] u32, digest[n_links, n_sources] u64): each unit's
+        changed nodes hashed with their new distance and next-hop bytes (delta_digest()
+        computes the same from a delta)."""
+        lk = np.ascontiguousarray(links, dtype=np.uint32)
+        sr = np.ascontiguousarray(sources, dtype=np.uint32)
+        out = np.zeros((lk.shape[0], sr.shape[0]), dtype=np.uint32)
+        dig = np.zeros((lk.shape[0], sr.shape[0]), dtype=np.uint64)
+        rc = lib().oracle_whatif_delta_digest(ctypes.byref(self._s), _ptr(lk), lk.shape[0], _ptr(sr), sr.shape[0],
+                                              int(use_link_metric), _ptr(out), _ptr(dig), nh_bytes,
+                                              nthreads or default_threads())
+        if rc != 0:
+            raise RuntimeError("oracle_whatif_delta_digest failed")
+        return out, dig
+
     # --- helpers mirroring the reference's SpfResult view -------------------
     def next_hop_names(self, src: int, run: SpfRun, v: int) -> Set[str]:
         nbrs = self.g.distinct_neighbors(src)
@@ -223,3 +243,35 @@ class Oracle:
                 "pathLinks": [(int(self.g.link_id[e]), self.g.names[int(owner[e])]) for e in pls],
             }
         return res
+
+
+_M1, _M2, _G = np.uint64(0xBF58476D1CE4E5B9), np.uint64(0x94D049BB133111EB), np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + _G
+        x = (x ^ (x >> np.uint64(30))) * _M1
+        x = (x ^ (x >> np.uint64(27))) * _M2
+        return x ^ (x >> np.uint64(31))
+
+
+def delta_digest(ptr: np.ndarray, node: np.ndarray, dist: np.ndarray, nh: np.ndarray) -> np.ndarray:
+    """Per-unit digest of a CSR delta (openr_spf_whatif_delta's host form), as
+    oracle_whatif_delta_digest computes it: sum mod 2^64 of the entries' hashes."""
+    n, nb = nh.shape
+    pad = np.zeros((n, (nb + 7) // 8 * 8), dtype=np.uint8)
+    pad[:, :nb] = nh
+    chunks = pad.view(np.uint64).reshape(n, -1)
+    h = _mix64(node.astype(np.uint64) ^ np.uint64(0xD1B54A32D192ED03))
+    h = _mix64(h ^ dist.astype(np.uint64))
+    for k in range(chunks.shape[1]):
+        h = _mix64(h ^ chunks[:, k])
+    units = ptr.shape[0] - 1
+    out = np.zeros(units, dtype=np.uint64)
+    cnt = np.diff(ptr.astype(np.int64))
+    nz = np.nonzero(cnt)[0]
+    if len(nz):
+        with np.errstate(over="ignore"):
+            out[nz] = np.add.reduceat(h, ptr[:-1][nz].astype(np.int64))
+    return out

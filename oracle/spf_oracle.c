@@ -531,7 +531,31 @@ typedef struct {
   int use_link_metric;
   uint32_t* changed;
   int rc;
+  uint64_t* digest;   /* nullable: per-unit delta digest (oracle_whatif_delta_digest) */
+  uint32_t nh_bytes;
 } whatif_job_t;
+
+/* splitmix64 finaliser (Steele et al.): the mixing step of the delta digest */
+static uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+/* hash of one delta entry: node, new distance, new next-hop bytes in 8-byte chunks
+   (little-endian, zero past nh_bytes) -- the layout openr_spf_whatif_delta writes */
+static uint64_t delta_entry_hash(uint32_t v, uint64_t d, const uint64_t* nh, uint32_t nw, uint32_t nh_bytes) {
+  uint64_t h = mix64((uint64_t)v ^ 0xD1B54A32D192ED03ull);
+  h = mix64(h ^ d);
+  for (uint32_t k = 0; k < (nh_bytes + 7) / 8; ++k) {
+    uint64_t c = k < nw ? nh[k] : 0;
+    const uint32_t bytes = nh_bytes - 8 * k;
+    if (bytes < 8) c &= (((uint64_t)1) << (8 * bytes)) - 1;
+    h = mix64(h ^ c);
+  }
+  return h;
+}
 
 static void* whatif_worker(void* arg) {
   whatif_job_t* j = (whatif_job_t*)arg;
@@ -561,13 +585,16 @@ static void* whatif_worker(void* arg) {
       if (run_spf_ws(&w, g, src, j->use_link_metric, ign) < 0) j->rc = -1;
       ign[l >> 6] = 0;
       uint32_t cnt = 0;
+      uint64_t dig = 0;
       for (uint32_t v = 0; v < V; ++v) {
         const uint64_t d = w.settled[v] ? w.dist[v] : U64_MAX_;
         int diff = d != base_d[v];
         for (uint32_t k = 0; k < nw && !diff; ++k) diff = w.nh[(size_t)v * nw + k] != base_nh[(size_t)v * nw + k];
         cnt += (uint32_t)diff;
+        if (diff && j->digest) dig += delta_entry_hash(v, d, w.nh + (size_t)v * nw, nw, j->nh_bytes);
       }
       j->changed[(size_t)i * j->n_sources + s] = cnt;
+      if (j->digest) j->digest[(size_t)i * j->n_sources + s] = dig;
     }
   }
   free(base_d);
@@ -577,8 +604,9 @@ static void* whatif_worker(void* arg) {
   return NULL;
 }
 
-int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
-                  uint32_t n_sources, int use_link_metric, uint32_t* changed, int nthreads) {
+static int whatif_run(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                      uint32_t n_sources, int use_link_metric, uint32_t* changed, uint64_t* digest,
+                      uint32_t nh_bytes, int nthreads) {
   if (!g) return -1;
   for (uint32_t i = 0; i < n_links; ++i)
     if (links[i] >= g->num_links) return -1;
@@ -590,7 +618,7 @@ int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links
   whatif_job_t jobs[256];
   for (int t = 0; t < nthreads; ++t) {
     jobs[t] = (whatif_job_t){g, links, sources, n_links, n_sources, (uint32_t)t, (uint32_t)nthreads,
-                             use_link_metric, changed, 0};
+                             use_link_metric, changed, 0, digest, nh_bytes};
     if (t > 0) pthread_create(&th[t], NULL, whatif_worker, &jobs[t]);
   }
   whatif_worker(&jobs[0]);
@@ -600,6 +628,18 @@ int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links
     rc |= jobs[t].rc;
   }
   return rc;
+}
+
+int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
+                  uint32_t n_sources, int use_link_metric, uint32_t* changed, int nthreads) {
+  return whatif_run(g, links, n_links, sources, n_sources, use_link_metric, changed, NULL, 0, nthreads);
+}
+
+int oracle_whatif_delta_digest(const oracle_graph* g, const uint32_t* links, uint32_t n_links,
+                               const uint32_t* sources, uint32_t n_sources, int use_link_metric,
+                               uint32_t* changed, uint64_t* digest, uint32_t nh_bytes, int nthreads) {
+  if (!digest) return -1;
+  return whatif_run(g, links, n_links, sources, n_sources, use_link_metric, changed, digest, nh_bytes, nthreads);
 }
 
 /* ------------------------------------------------------------------------ */

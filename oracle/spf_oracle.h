@@ -98,6 +98,16 @@ int oracle_ksp2_batch(const oracle_graph* g, const uint32_t* src, const uint32_t
 int oracle_whatif(const oracle_graph* g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                   uint32_t n_sources, int use_link_metric, uint32_t* changed, int nthreads);
 
+/*
+ * The same sweep with a digest of each unit's delta (test infrastructure for
+ * openr_spf_whatif_delta): digest[i][j] = sum mod 2^64 over the changed nodes v of
+ * mix(v, new distance, new next-hop bytes [nh_bytes]) (delta_entry_hash, splitmix64
+ * steps), so a delta is checked without shipping rows. Order-independent by construction.
+ */
+int oracle_whatif_delta_digest(const oracle_graph* g, const uint32_t* links, uint32_t n_links,
+                               const uint32_t* sources, uint32_t n_sources, int use_link_metric,
+                               uint32_t* changed, uint64_t* digest, uint32_t nh_bytes, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -167,6 +167,50 @@ def test_config4_wan_whatif_full_workload(eng):
     assert changed.shape == (3000, 1000) and changed.sum() > 0
 
 
+def test_config4_wan_whatif_delta(eng):
+    """openr_spf_whatif_delta on the config-4 WAN: all 3 000 links x 16 sources, each
+    unit's changed nodes with their new u64 distance and next-hop bits, against oracle
+    re-solves runSpf(src, true, {link}) through the oracle's per-unit digest, plus entry
+    for entry on the first 150 links x 4 sources."""
+    from oracle import delta_digest
+    from test_gpu_parity import check_delta_rows
+
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    links = np.arange(g.num_links, dtype=np.uint32)
+    sources = np.linspace(0, g.num_nodes - 1, 16).astype(np.uint32)
+    changed, ptr, node, dist, nh, _ = eng.whatif_delta(links, sources, True)
+    want, dig = Oracle(g).whatif_delta_digest(links, sources, nh.shape[1], True)
+    np.testing.assert_array_equal(changed, want)
+    got = delta_digest(ptr, node, dist, nh).reshape(changed.shape)
+    bad = np.argwhere(got != dig)
+    assert bad.size == 0, f"{len(bad)} units' deltas differ: {bad[:8].tolist()}"
+    n150 = 150 * len(sources)
+    sub = [0, 5, 10, 15]
+    sel = np.array([i * len(sources) + j for i in range(150) for j in sub])
+    ptr2 = np.concatenate([[0], np.cumsum(changed.ravel()[sel])]).astype(np.uint64)
+    take = np.concatenate([np.arange(int(ptr[u]), int(ptr[u + 1])) for u in sel]).astype(np.int64)
+    check_delta_rows(g, links[:150], sources[sub], True, changed[:150][:, sub], ptr2, node[take], dist[take], nh[take])
+    assert n150 > 0 and changed.sum() > 0
+
+
+def test_config4_wan_whatif_delta_full_workload(eng):
+    """The whole config-4 workload (3 000 links x 1 000 sources, 3 M units) with the
+    delta: every unit's digest against the oracle's (host worker threads)."""
+    from oracle import delta_digest
+
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    links = np.arange(g.num_links, dtype=np.uint32)
+    sources = np.arange(g.num_nodes, dtype=np.uint32)
+    changed, ptr, node, dist, nh, _ = eng.whatif_delta(links, sources, True)
+    want, dig = Oracle(g).whatif_delta_digest(links, sources, nh.shape[1], True)
+    np.testing.assert_array_equal(changed, want)
+    got = delta_digest(ptr, node, dist, nh).reshape(changed.shape)
+    bad = np.argwhere(got != dig)
+    assert bad.size == 0, f"{len(bad)} units' deltas differ: {bad[:8].tolist()}"
+
+
 def test_config5_fabric_ksp2_more_sources(eng):
     """KSP2 on the fabric for 40 more sources spread over the id range (SSWs, FSWs and
     RSWs of many pods) x every destination: 199 680 pairs (0.8 % of the benchmarked 24.9 M),

@@ -586,6 +586,99 @@ def test_whatif_wan_sample_and_device_form(eng, whatif_mode):
     np.testing.assert_array_equal(d_c.cpu().numpy().view(np.uint32), changed)
 
 
+def check_delta_rows(g, links, sources, use_metric, changed, ptr, node, dist, nh):
+    """Every unit's delta entries against explicit oracle rows: the nodes whose distance
+    or next-hop set differ between runSpf(s) and runSpf(s, {link}), ascending, with the
+    re-solve's distance and next-hop bytes."""
+    o = Oracle(g)
+    base = {int(s): o.run_spf(int(s), use_metric) for s in sources}
+    nb = nh.shape[1]
+    for i, l in enumerate(links):
+        for j, s in enumerate(sources):
+            u = i * len(sources) + j
+            r = o.run_spf(int(s), use_metric, [int(l)])
+            b = base[int(s)]
+            ch = np.nonzero((r.dist != b.dist) | np.any(r.nh != b.nh, axis=1))[0]
+            a, e = int(ptr[u]), int(ptr[u + 1])
+            assert e - a == len(ch) == changed[i, j], (l, s)
+            np.testing.assert_array_equal(node[a:e], ch)
+            np.testing.assert_array_equal(dist[a:e], r.dist[ch])
+            want = np.zeros((len(ch), nb), dtype=np.uint8)
+            want[:, : min(nb, r.nh.shape[1])] = r.nh[ch, :nb]
+            np.testing.assert_array_equal(nh[a:e], want)
+
+
+@pytest.mark.parametrize("seed,max_metric", [(0, 64), (1, 1)])
+def test_whatif_delta_matches_oracle_rows(eng, seed, max_metric, whatif_mode):
+    """openr_spf_whatif_delta on random graphs with overloads, down and parallel links:
+    per unit, the changed nodes with their new distance (UINT64_MAX when the failure cuts
+    them off) and next-hop bytes, entry for entry against oracle re-solves, in every
+    what-if mode (repair overlays, seeded re-solves, full re-solves + row compare), with
+    link metrics and hop counts, and with next-hop entries wider than the graph's."""
+    g = random_graph(310 + seed, 110, 240, max_metric, p_ovl=0.05, p_down=0.05, p_par=0.1)
+    eng.set_graph(g)
+    links = list(range(g.num_links))
+    sources = list(range(0, g.num_nodes, 5))
+    changed, ptr, node, dist, nh, _ = eng.whatif_delta(links, sources, True)
+    np.testing.assert_array_equal(changed, whatif_oracle(g, links, sources, True))
+    check_delta_rows(g, links, sources, True, changed, ptr, node, dist, nh)
+    assert (dist == np.uint64(2**64 - 1)).any()  # some failures cut nodes off (tree links)
+    c2, p2, n2, d2, h2, _ = eng.whatif_delta(links[::4], sources[:6], False, nh_bytes=eng.nh_bytes + 5)
+    check_delta_rows(g, links[::4], sources[:6], False, c2, p2, n2, d2, h2)
+
+
+def test_whatif_delta_device_form_and_cap(eng, whatif_mode):
+    """The device form's CSR (entries in the repair's order) holds the host form's entries
+    (node ids ascending); a cap below the total returns E2BIG with changed and ptr filled."""
+    import torch
+
+    g = T.wan(1000, 3000, 64, seed=1)
+    eng.set_graph(g)
+    rng = np.random.default_rng(12)
+    links = np.sort(rng.choice(g.num_links, 60, replace=False)).astype(np.uint32)
+    sources = np.sort(rng.choice(g.num_nodes, 10, replace=False)).astype(np.uint32)
+    changed, ptr, node, dist, nh, _ = eng.whatif_delta(links, sources, True)
+    total = int(ptr[-1])
+    assert total == int(changed.sum())
+    nb = eng.nh_bytes
+    units = len(links) * len(sources)
+    dev = torch.device("cuda", 0)
+    d_l = torch.from_numpy(links.astype(np.int32)).to(dev)
+    d_s = torch.from_numpy(sources.astype(np.int32)).to(dev)
+    d_c = torch.zeros((len(links), len(sources)), dtype=torch.int32, device=dev)
+    d_ptr = torch.zeros(units + 1, dtype=torch.int64, device=dev)
+    d_node = torch.zeros(total, dtype=torch.int32, device=dev)
+    d_dist = torch.zeros(total, dtype=torch.int64, device=dev)
+    d_nh = torch.zeros((total, nb), dtype=torch.uint8, device=dev)
+    got, _ = eng.whatif_delta_device(d_l.data_ptr(), len(links), d_s.data_ptr(), len(sources), d_c.data_ptr(),
+                                     d_ptr.data_ptr(), d_node.data_ptr(), d_dist.data_ptr(), d_nh.data_ptr(), total, nb)
+    assert got == total
+    np.testing.assert_array_equal(d_c.cpu().numpy().view(np.uint32), changed)
+    p = d_ptr.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(p, ptr)
+    pn = d_node.cpu().numpy().view(np.uint32)
+    pd = d_dist.cpu().numpy().view(np.uint64)
+    ph = d_nh.cpu().numpy()
+    for u in range(units):
+        a, e = int(p[u]), int(p[u + 1])
+        k = np.argsort(pn[a:e], kind="stable")
+        np.testing.assert_array_equal(pn[a:e][k], node[a:e])
+        np.testing.assert_array_equal(pd[a:e][k], dist[a:e])
+        np.testing.assert_array_equal(ph[a:e][k], nh[a:e])
+    # cap below the total: E2BIG, counts and ptr still right
+    d_c.zero_()
+    d_ptr.zero_()
+    got2, _ = eng.whatif_delta_device(d_l.data_ptr(), len(links), d_s.data_ptr(), len(sources), d_c.data_ptr(),
+                                      d_ptr.data_ptr(), d_node.data_ptr(), d_dist.data_ptr(), d_nh.data_ptr(),
+                                      total // 2, nb, allow_overflow=True)
+    assert got2 == total
+    np.testing.assert_array_equal(d_c.cpu().numpy().view(np.uint32), changed)
+    np.testing.assert_array_equal(d_ptr.cpu().numpy().view(np.uint64), ptr)
+    with pytest.raises(SpfError) as ei:
+        eng.whatif_delta(links, sources, True, cap=total - 1)
+    assert ei.value.code == E2BIG
+
+
 def test_whatif_edge_cases(eng, whatif_mode):
     g = T.grid_fast(6)
     eng.set_graph(g)

@@ -32,7 +32,7 @@ MAX_LEAF_BLOCKS = 12
 def test_whatif_repair_loops_have_uniform_exits():
     res = uc.divergent_exit_cycles(os.path.join(ROOT, "openr_amd", "csrc", "spf_sweep.hip"), "whatif_group_kernel",
                                    [os.path.join(ROOT, "include")])
-    assert len(res) == 12, sorted(res)  # {u16, u32, u64 distances} x {global, LDS graph} x {1, 8 next-hop words}
+    assert len(res) == 24, sorted(res)  # {u16, u32, u64 distances} x {global, LDS graph} x {1, 8 words} x {delta}
     for name, cycles in res.items():
         big = [c for c in cycles if c[1] > MAX_LEAF_BLOCKS]
         assert not big, f"{name}: loops with divergent exits {big}"
