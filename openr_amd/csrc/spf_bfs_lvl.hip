@@ -540,9 +540,7 @@ __host__ __device__ inline LeanLayout lean_layout(uint32_t V, uint32_t nh_words,
 // in the CU's L1); a zero delta (no edge, down link, overloaded row) and a lane past the
 // level resolve to a node whose level is <= L, never tight.
 // WPE: the waves-per-SIMD target the compiler allocates registers for. LDS caps G100 at
-// 10 workgroups of 2 waves per CU (5 per SIMD); a target of 8 (default) squeezes the pass
-// into 78 SGPRs with 29 spilled to VGPR lanes (v_writelane / v_readlane in the level
-// loop), a target of 5 (OPENR_SPF_LEAN_WPE=5) leaves 106 SGPRs and 6 spills.
+// 10 workgroups of 2 waves per CU (5 per SIMD), and 5 is the default since round 6.
 template <int MODE, int BLOCK, bool PROF, bool DELTA, int WPE>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void bfs_ell_kernel(
     DevGraph g, SolveArgs a, uint64_t cost, uint32_t ring_cap, uint32_t* ctr, uint32_t* ovf_count, uint32_t nt,
@@ -824,8 +822,11 @@ hipError_t launch_lvl_lean(const DevGraph& g, const SolveArgs& a, uint64_t cost,
   const bool want_prof = prof_enabled();
   // OPENR_SPF_LEAN_DELTA=0: 16-byte ellv rows even when the delta rows exist
   const bool delta = g.elld && env_u32("OPENR_SPF_LEAN_DELTA", 1u, 0u, 1u) != 0;
-  auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true, 8> : bfs_ell_kernel<MODE, BLOCK, true, false, 8>)
-                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 8> : bfs_ell_kernel<MODE, BLOCK, false, false, 8>);
+  // registers for 5 waves per SIMD, the occupancy LDS allows G100 (10 workgroups of 2 waves
+  // per CU): 89 VGPRs, no scratch, 31 SGPR spills; a target of 8 spilled 21 VGPRs to
+  // scratch and 50 SGPRs (r06, interleaved A/B: 0.707 vs 0.715 ms median)
+  auto k = want_prof ? (delta ? bfs_ell_kernel<MODE, BLOCK, true, true, 5> : bfs_ell_kernel<MODE, BLOCK, true, false, 5>)
+                     : (delta ? bfs_ell_kernel<MODE, BLOCK, false, true, 5> : bfs_ell_kernel<MODE, BLOCK, false, false, 5>);
   hipError_t err =
       hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (err != hipSuccess) return err;

@@ -136,3 +136,72 @@ def test_context_over_repeated_device_list():
     finally:
         one.close()
         two.close()
+
+
+def _whatif_rank_main(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.init()
+    from openr_amd.engine import SpfEngine
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    g = T.wan(400, 1200, 64, seed=5)
+    V, L = g.num_nodes, g.num_links
+    eng = SpfEngine([0])
+    eng.set_graph(g)
+    # config 4's strong split (bench.py whatif_main): rank r takes links shard_range(L, r, N)
+    lo, hi = shard.shard_range(L, rank, world)
+    srcs = np.arange(0, V, 3, dtype=np.uint32)
+    changed, _ = eng.whatif(np.arange(lo, hi, dtype=np.uint32), srcs, True)
+    # bench.py's self-check: every rank's rows as a 64-bit digest, all-gathered
+    import hashlib
+
+    digest = hashlib.blake2b(changed.tobytes(), digest_size=8).hexdigest()
+    t = torch.tensor([int(digest, 16) - (1 << 63)], dtype=torch.int64)
+    digs = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(digs, t)
+    # the rows themselves, gathered to rank 0 (padded to the largest shard)
+    sizes = shard.shard_sizes(L, world)
+    buf = np.zeros((max(sizes), len(srcs)), dtype=np.int64)
+    buf[: hi - lo] = changed
+    parts = [torch.zeros(buf.shape, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, torch.from_numpy(buf))
+    if rank == 0:
+        full = np.concatenate([p.numpy()[:n] for p, n in zip(parts, sizes)]).astype(np.uint32)
+        np.save(os.path.join(out_dir, "whatif.npy"), full)
+        np.save(os.path.join(out_dir, "digests.npy"), np.array([int(x.item()) for x in digs], dtype=np.int64))
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_engine_ranks_whatif_link_shards(tmp_path, world):
+    """Config 4 across ranks: each rank sweeps its block of links (shard_range) for the
+    same sources on its own engine; the gathered changed rows equal the oracle's
+    re-solves runSpf(src, true, {link}), and each rank's all-gathered digest equals a
+    single-rank recomputation of that shard (the check bench.py's what-if line carries)."""
+    import hashlib
+
+    import torch.multiprocessing as mp
+
+    from openr_amd.engine import SpfEngine
+    from oracle import Oracle
+
+    mp.start_processes(_whatif_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    g = T.wan(400, 1200, 64, seed=5)
+    V, L = g.num_nodes, g.num_links
+    srcs = np.arange(0, V, 3, dtype=np.uint32)
+    full = np.load(tmp_path / "whatif.npy")
+    want = Oracle(g).whatif(np.arange(L, dtype=np.uint32), srcs, True)
+    np.testing.assert_array_equal(full, want)
+    digs = np.load(tmp_path / "digests.npy")
+    eng = SpfEngine([0])
+    eng.set_graph(g)
+    for r in range(world):
+        lo, hi = shard.shard_range(L, r, world)
+        c, _ = eng.whatif(np.arange(lo, hi, dtype=np.uint32), srcs, True)
+        d = hashlib.blake2b(c.tobytes(), digest_size=8).hexdigest()
+        assert int(d, 16) - (1 << 63) == int(digs[r]), f"rank {r} digest"
+    eng.close()
