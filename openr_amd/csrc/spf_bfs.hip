@@ -379,6 +379,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
                 put(t, near ? L + 1u : L + 2u);
                 atomicOr(&st[S::word(t)], (near ? cnext : level_code(L + 2u)) << S::shift(t));
               }
+              // the one-thread branch joins here, not at the level loop's exit (a divergent
+              // exit: per-lane exit masks around the whole level loop)
+              __builtin_amdgcn_wave_barrier();
               break;
             }
           }
@@ -583,6 +586,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
           // heads are settled at levels <= L), so the level is only settled here
           if (own_dist)
             for (uint32_t i = head + tid; i < tail; i += BLOCK) put(ring[RING ? (i & rmask) : i], L);
+          __builtin_amdgcn_wave_barrier();  // the per-thread loop joins before the break (uniform exit)
           break;
         }
         if (!SLICED && a.target && a.dist_only) {
@@ -591,6 +595,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(BLOCK >= 
           const uint32_t t = a.target[sid];
           if (t < V && (S::field(st, t) & kCodeMask) != 0u) {
             for (uint32_t i = head + tid; i < tail; i += BLOCK) put(ring[RING ? (i & rmask) : i], L);
+            __builtin_amdgcn_wave_barrier();
             break;
           }
         }

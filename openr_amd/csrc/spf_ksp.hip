@@ -98,7 +98,13 @@ __host__ __device__ inline KspLayout ksp_layout(uint32_t V, uint32_t L, uint32_t
 #ifdef OPENR_SPF_KSP_WAIT
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 #else
-__device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
+// ... and a convergent join (wave_barrier emits no instruction): the lane-0 stores before a
+// fence reconverge there, so the compiler does not merge their join into the exits of the
+// DFS and pair loops (which would make those exits divergent: per-lane exit masks)
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 #endif
 
 struct KspState {
@@ -183,7 +189,10 @@ __device__ void copy_row16_tagged(uint16_t* d16, const uint16_t* l16, uint32_t V
 }
 
 __device__ __forceinline__ void stat_add(const KspState& st, uint32_t i, uint64_t v) {
-  if (st.stats && threadIdx.x == 0) st.stats[i] += v;
+  if (st.stats) {
+    if (threadIdx.x == 0) st.stats[i] += v;
+    __builtin_amdgcn_wave_barrier();  // the lane-0 branch joins here, not at a caller's return or latch
+  }
 }
 
 // pathLinks(v) still worth trying -> arena[beg, beg + count) as (edge u->v, link, u):
@@ -731,6 +740,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
         if (bad) atomicOr(status, 1u);
       }
     }
+    __builtin_amdgcn_wave_barrier();  // the lane-0 branch joins here: the pair loop's latch is uniform
     if (st.stats) {
       stat_add(st, kStPaths, npaths);
       stat_add(st, kStCyc, clock64() - tp);
