@@ -400,7 +400,7 @@ def whatif_main(args):
     eng.close()
 
 
-PMC_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: the PMC summaries bench lines carry
+PMC_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest first: the PMC summaries bench lines carry
 
 
 def pmc_path(name):
