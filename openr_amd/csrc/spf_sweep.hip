@@ -12,6 +12,7 @@
 // Integer / byte work only: HBM-bound, coalesced row reads, one workgroup per unit.
 #include <algorithm>
 #include <cstdio>
+#include <vector>
 
 #include "spf_bfs_common.h"
 #include "spf_kernels.h"
@@ -1042,6 +1043,7 @@ __device__ uint32_t grp_repair(GrpWave<D, LG, W>& c, uint32_t lane, uint32_t V, 
 }
 
 constexpr uint32_t kGrpMaxBlock = 512;
+constexpr uint32_t kGrpProfWg = 4096;  // workgroups whose start / end times the profile keeps
 
 // WPE: waves per SIMD the compiler must fit registers for (1: no constraint). Unconstrained
 // the <= 32-bit-set variant takes 119 VGPRs, i.e. 4 waves per SIMD (16 per CU) whatever
@@ -1056,6 +1058,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     uint32_t* ctr, unsigned long long* prof, WhatifDelta dl) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long wt0 = prof ? wall_clock64() : 0ull;  // workgroup span (100 MHz), tail analysis
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ uint32_t s_item;
   const uint32_t V = g.V, E = g.E, tid = threadIdx.x, lane = __lane_id(), wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform to the compiler: per-wave LDS pointers stay scalar
@@ -1204,6 +1207,10 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }
+  if (prof && tid == 0 && blockIdx.x < kGrpProfWg) {
+    prof[16 + blockIdx.x] = wt0;
+    prof[16 + kGrpProfWg + blockIdx.x] = wall_clock64();
+  }
   bfs::retire_workgroup(ctr, nullptr);
 }
 
@@ -1300,21 +1307,41 @@ __global__ __launch_bounds__(256) void delta_tile_scan(const uint32_t* c, size_t
 }
 
 // unit u's entries from its pool slots [off[u], off[u] + changed[u]) to the CSR slots
-// [ptr[u], ptr[u + 1]) (a thread per unit; the order inside a unit is kept)
-__global__ __launch_bounds__(256) void delta_gather(const uint32_t* c, size_t n, const uint32_t* off,
-                                                    const unsigned long long* ptr, WhatifDelta pool,
-                                                    uint32_t* node, unsigned long long* dist, uint8_t* nh) {
-  for (size_t u = (size_t)blockIdx.x * 256u + threadIdx.x; u < n; u += (size_t)gridDim.x * 256u) {
-    const uint32_t k = c[u];
-    if (!k) continue;
-    const size_t src = off[u], dst = ptr[u];
-    for (uint32_t q = 0; q < k; ++q) {
-      node[dst + q] = pool.node[src + q];
-      dist[dst + q] = pool.dist[src + q];
+// [ptr[u], ptr[u + 1]) (the order inside a unit is kept). A wave takes 64 consecutive
+// units, whose CSR slots are one contiguous range, and gives each lane one slot of it at a
+// time: the lane finds its unit by a binary search over the 64 offsets in LDS. Writes are
+// coalesced and every lane has work whatever the units' sizes (a thread per unit left
+// most lanes idle on a WAN unit's ~6 entries: 0.76 ms per step, r06).
+__global__ __launch_bounds__(256) void delta_gather(size_t n, const uint32_t* off, const unsigned long long* ptr,
+                                                    WhatifDelta pool, uint32_t* node, unsigned long long* dist,
+                                                    uint8_t* nh) {
+  __shared__ unsigned long long sp[4][65];
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  unsigned long long* p = sp[wave];
+  const size_t groups = (n + 63u) / 64u;
+  for (size_t gi = (size_t)blockIdx.x * 4u + wave; gi < groups; gi += (size_t)gridDim.x * 4u) {
+    const size_t u0 = gi * 64u;
+    p[lane] = ptr[min(u0 + lane, n)];
+    if (lane == 0) p[64] = ptr[min(u0 + 64u, n)];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const unsigned long long b0 = p[0], b1 = p[64];
+    for (unsigned long long t = b0 + lane; t < b1; t += 64u) {
+      uint32_t lo = 0, hi = 63;  // the last unit whose first slot is <= t (empty units share it)
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (p[mid] <= t) lo = mid;
+        else hi = mid - 1u;
+      }
+      const size_t src = off[u0 + lo] + (size_t)(t - p[lo]);
+      node[t] = pool.node[src];
+      dist[t] = pool.dist[src];
+      const uint8_t* hs = pool.nh + src * pool.nhb;
+      uint8_t* hd = nh + (size_t)t * pool.nhb;
+      for (uint32_t q = 0; q < pool.nhb; ++q) hd[q] = hs[q];
     }
-    const uint8_t* hs = pool.nh + src * pool.nhb;
-    uint8_t* hd = nh + dst * pool.nhb;
-    for (uint32_t q = 0; q < k * pool.nhb; ++q) hd[q] = hs[q];
+    __builtin_amdgcn_wave_barrier();  // every lane's reads of p precede the next group's writes
   }
 }
 
@@ -1446,9 +1473,10 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   static unsigned long long* prof_buf = nullptr;
   unsigned long long* prof = nullptr;
   if (prof_enabled()) {
-    if (!prof_buf && hipMalloc(&prof_buf, 16 * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
+    const size_t words = 16u + 2u * kGrpProfWg;
+    if (!prof_buf && hipMalloc(&prof_buf, words * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
     prof = prof_buf;
-    if (prof) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
+    if (prof) (void)hipMemsetAsync(prof, 0, words * sizeof(unsigned long long), s);
   }
   // the <= 32-bit-set variant is compiled for 7 waves per SIMD, the occupancy its LDS
   // layout allows (28 waves per CU): WAN step 5.03 -> 4.17 ms (unconstrained: 119 VGPRs,
@@ -1495,6 +1523,34 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                    (int)lg, waves, grid, chunk, h[3], h[0] / u, h[1] / u, h[2] / u, h[4] / u, h[5] / u, h[6] / u,
                    h[7] / u, h[9] ? (double)h[8] / h[9] : 0.0, h[9],
                    h[8] ? (double)(h[0] + h[1] + h[2]) / (double)h[8] : 0.0);
+      // the launch's tail: workgroup end times against the last one (100 MHz clock)
+      const uint32_t nw = std::min<uint32_t>(grid, kGrpProfWg);
+      std::vector<unsigned long long> t((size_t)2 * nw);
+      if (hipMemcpy(t.data(), prof + 16, nw * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess &&
+          hipMemcpy(t.data() + nw, prof + 16 + kGrpProfWg, nw * sizeof(unsigned long long), hipMemcpyDeviceToHost) ==
+              hipSuccess && nw) {
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (uint32_t b = 0; b < nw; ++b) {
+          t0 = std::min(t0, t[b]);
+          t1 = std::max(t1, t[nw + b]);
+        }
+        std::vector<double> ends(nw), starts(nw);
+        double busy = 0.0;
+        for (uint32_t b = 0; b < nw; ++b) {
+          starts[b] = (double)(t[b] - t0) / 100.0;
+          ends[b] = (double)(t[nw + b] - t0) / 100.0;
+          busy += ends[b] - starts[b];
+        }
+        std::sort(ends.begin(), ends.end());
+        std::sort(starts.begin(), starts.end());
+        const double span = (double)(t1 - t0) / 100.0;
+        std::fprintf(stderr,
+                     "whatif_group tail: span %.1f us, workgroups %u; starts p50 %.1f p90 %.1f max %.1f; ends p10 %.1f "
+                     "p50 %.1f p90 %.1f p99 %.1f max %.1f us; workgroup-time / (span x resident %u) %.3f\n",
+                     span, nw, starts[nw / 2], starts[nw * 9 / 10], starts.back(), ends[nw / 10], ends[nw / 2],
+                     ends[nw * 9 / 10], ends[nw * 99 / 100], ends.back(), (uint32_t)std::min<uint64_t>(nw, slots),
+                     busy / (span * (double)std::min<uint64_t>(nw, slots)));
+      }
     }
   }
   return err;
@@ -1515,8 +1571,9 @@ hipError_t launch_delta_gather(const uint32_t* changed, size_t n, const uint32_t
                                const WhatifDelta& pool, uint32_t* node, unsigned long long* dist, uint8_t* nh,
                                int num_cus, hipStream_t s) {
   if (!n) return hipSuccess;
+  (void)changed;  // the unit sizes are ptr's differences
   const uint32_t grid = (uint32_t)std::min<size_t>((n + 255u) / 256u, (size_t)num_cus * 16u);
-  hipLaunchKernelGGL(delta_gather, dim3(grid), dim3(256), 0, s, changed, n, off, ptr, pool, node, dist, nh);
+  hipLaunchKernelGGL(delta_gather, dim3(grid), dim3(256), 0, s, n, off, ptr, pool, node, dist, nh);
   return hipGetLastError();
 }
 

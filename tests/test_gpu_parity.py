@@ -552,6 +552,44 @@ def whatif_mode(request, monkeypatch):
     return request.param
 
 
+def long_line_graph(seed, V=220, chords=24, w_lo=250, w_hi=297):
+    """A line of V nodes plus a few short chords, metrics up to w_hi with V * w_hi just under
+    0xFFFF: shortest distances reach ~60 000, the top of the rounds kernel's packed u16 rows."""
+    rng = np.random.default_rng(seed)
+    names = [f"l{i:04d}" for i in range(V)]
+    links = [(i, i + 1) for i in range(V - 1)]
+    while len(links) < V - 1 + chords:
+        a = int(rng.integers(0, V - 6))
+        links.append((a, a + int(rng.integers(2, 6))))  # short detours: distances stay long
+    m_uv = rng.integers(w_lo, w_hi + 1, len(links)).astype(np.uint64)
+    m_vu = rng.integers(w_lo, w_hi + 1, len(links)).astype(np.uint64)
+    up = np.ones(len(links), np.uint8)
+    ovl = np.zeros(V, np.uint8)
+    return T.csr_from_links(names, np.array(links), m_uv, m_vu, ovl, up)
+
+
+def test_rounds_long_distances(eng, monkeypatch):
+    """Distances near 0xFFFF (V * w_max = 65 340; the what-if repair's u16 rows hold them):
+    all-sources solves with pathLinks, ignore sets, and a what-if sweep whose affected units
+    all take the seeded re-solve (1 dirty slot), against the oracle."""
+    monkeypatch.setenv("OPENR_SPF_GENERAL", "rounds")
+    g = long_line_graph(5)
+    assert g.num_nodes * int(g.metric.max()) < 0xFFFF
+    o = Oracle(g)
+    assert max(int(d) for d in o.run_spf(0, True).dist if d != np.iinfo(np.uint64).max) > 40000
+    check_against_oracle(eng, g, list(range(g.num_nodes)), True)
+    rng = np.random.default_rng(7)
+    srcs = list(range(0, g.num_nodes, 5))
+    ign = [sorted(rng.choice(g.num_links, 2, replace=False).tolist()) for _ in srcs]
+    check_against_oracle(eng, g, srcs, True, ignore=ign)
+    monkeypatch.setenv("OPENR_SPF_WHATIF_CAP", "1")
+    eng.set_graph(g)
+    links = list(range(g.num_links))
+    sources = list(range(0, g.num_nodes, 11))
+    changed, _ = eng.whatif(links, sources, True)
+    np.testing.assert_array_equal(changed, whatif_oracle(g, links, sources, True))
+
+
 @pytest.mark.parametrize("seed,max_metric", [(0, 64), (1, 1), (2, 7)])
 def test_whatif_sweep_matches_oracle(eng, seed, max_metric, whatif_mode):
     g = random_graph(300 + seed, 120, 300, max_metric, p_ovl=0.05, p_down=0.05, p_par=0.1)
