@@ -173,6 +173,7 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
     return false;
   };
   for (auto const& [area, ls] : als) {  // one all-sources batch covers every node and its neighbours
+    HostPhase ph("buildRouteDbs: prefetch (one area)");
     std::vector<std::string> present;
     for (auto const& n : nodes)
       // also the self-only result of a node this area lacks but another has
@@ -189,6 +190,7 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
     }
     ls.prefetchSpfResults(present, true);
   }
+  HostPhase phBuild("buildRouteDbs: per-node builds");
   if (workers <= 1) {
     for (size_t i = 0; i < nodes.size(); ++i) {
       auto db = buildRouteDb(nodes[i], als, prefixState);
@@ -270,6 +272,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   }
 
   DecisionRouteDb routeDb;
+  routeDb.unicastRoutes.reserve(prefixState.prefixes().size());  // at most one route per prefix
   bestRoutesCache_.clear();
   bestLazy_.clear();
   // advertiser ids of the single-advertiser prefixes on the fast path's mirror, computed
@@ -370,6 +373,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
     }
   }
   std::sort(cand.begin(), cand.end(), [](auto const& x, auto const& y) { return x.second.label < y.second.label; });
+  routeDb.mplsRoutes.reserve(cand.size() + staticMplsRoutes_.size() + 64u);
   for (auto& [_, entry] : cand) {
     const int32_t label = entry.label;
     routeDb.mplsRoutes.emplace_hint(routeDb.mplsRoutes.end(), label, std::move(entry));
@@ -1006,7 +1010,7 @@ int SpfSolver::fastLabelNextHops(const std::string& me, uint32_t dst, int32_t la
 }
 
 bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries,
-                          uint32_t dstId, std::map<thrift::IpPrefix, RibUnicastEntry>& routes) {
+                          uint32_t dstId, UnicastRoutes& routes) {
   if (entries.size() != 1) return false;
   const auto& [na, e] = *entries.begin();
   if (na.second != *fast_.area || e.type == thrift::PrefixType::BGP ||
@@ -1044,10 +1048,15 @@ bool SpfSolver::fastRoute(const std::string& me, thrift::IpPrefix const& prefix,
   // getNextHopsThrift(me, {dst}, isV4, false, d, ...): every up link to a next-hop node
   NextHopSet nextHops;
   const bool v4 = prefix.isV4();
+  auto takes = [&](const FastLink& fl) {
+    return fast_.has[fl.nbrBit] && fl.up && (computeLfaPaths_ || fl.metric + fast_.val[fl.nbrBit] == d);
+  };
+  size_t want = 0;
+  for (auto const& fl : fast_.links) want += takes(fl) ? 1u : 0u;
+  nextHops.reserve(want);  // one allocation per route
   for (auto const& fl : fast_.links) {
-    if (!fast_.has[fl.nbrBit] || !fl.up) continue;
+    if (!takes(fl)) continue;
     const Metric over = fl.metric + fast_.val[fl.nbrBit];
-    if (!computeLfaPaths_ && over != d) continue;
     thrift::NextHopThrift nh = v4 ? fl.proto4 : fl.proto6;
     nh.metric = static_cast<int32_t>(over);
     nextHops.emplace_hint(nextHops.end(), std::move(nh));
@@ -1210,7 +1219,7 @@ bool RibPolicy::applyAction(RibUnicastEntry& route) const {
   return false;
 }
 
-std::vector<thrift::IpPrefix> RibPolicy::applyPolicy(std::map<thrift::IpPrefix, RibUnicastEntry>& entries) const {
+std::vector<thrift::IpPrefix> RibPolicy::applyPolicy(UnicastRoutes& entries) const {
   std::vector<thrift::IpPrefix> updated;
   if (!isActive()) return updated;
   for (auto& [prefix, route] : entries)

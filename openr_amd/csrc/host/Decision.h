@@ -18,12 +18,16 @@
 // hold timers (Decision event plumbing), thrift serialization.
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <optional>
+#include <stdexcept>
+#include <tuple>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -130,7 +134,86 @@ void maybeUpdate(CompareResult& target, CompareResult update);
 CompareResult compareMetricVectors(thrift::MetricVector const& l, thrift::MetricVector const& r);
 }  // namespace MetricVectorUtils
 
-using NextHopSet = std::set<thrift::NextHopThrift>;
+// The reference's unordered_set<NextHopThrift> as a sorted vector: set semantics, iteration
+// in NextHopThrift order (deterministic for tests), and one allocation per route instead
+// of one tree node per next hop (the all-node route build allocates ~200 M next hops).
+// Iterators are const, as a set's; an insert or erase invalidates them, as a vector's.
+class NextHopSet {
+ public:
+  using value_type = thrift::NextHopThrift;
+  using key_type = thrift::NextHopThrift;
+  using const_iterator = std::vector<value_type>::const_iterator;
+  using iterator = const_iterator;
+  using size_type = size_t;
+  using reference = const value_type&;
+  using const_reference = const value_type&;
+
+  NextHopSet() = default;
+  NextHopSet(std::initializer_list<value_type> il) {
+    v_.reserve(il.size());
+    for (auto const& x : il) insert(x);
+  }
+  template <class It>
+  NextHopSet(It b, It e) {
+    insert(b, e);
+  }
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  const_iterator cbegin() const { return v_.begin(); }
+  const_iterator cend() const { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  void clear() { v_.clear(); }
+  void reserve(size_t n) { v_.reserve(n); }
+
+  std::pair<iterator, bool> insert(const value_type& x) { return put(value_type(x)); }
+  std::pair<iterator, bool> insert(value_type&& x) { return put(std::move(x)); }
+  iterator insert(const_iterator hint, const value_type& x) { return putHint(hint, value_type(x)); }
+  iterator insert(const_iterator hint, value_type&& x) { return putHint(hint, std::move(x)); }
+  template <class It>
+  void insert(It b, It e) {
+    for (; b != e; ++b) insert(*b);
+  }
+  template <class... A>
+  std::pair<iterator, bool> emplace(A&&... a) {
+    return put(value_type(std::forward<A>(a)...));
+  }
+  template <class... A>
+  iterator emplace_hint(const_iterator hint, A&&... a) {
+    return putHint(hint, value_type(std::forward<A>(a)...));
+  }
+  iterator find(const value_type& x) const {
+    auto it = std::lower_bound(v_.begin(), v_.end(), x);
+    return it != v_.end() && !(x < *it) ? it : v_.end();
+  }
+  size_t count(const value_type& x) const { return find(x) != end() ? 1u : 0u; }
+  bool contains(const value_type& x) const { return find(x) != end(); }
+  iterator erase(const_iterator it) { return v_.erase(it); }
+  size_t erase(const value_type& x) {
+    auto it = find(x);
+    if (it == end()) return 0;
+    v_.erase(it);
+    return 1;
+  }
+  bool operator==(const NextHopSet& o) const { return v_ == o.v_; }
+  bool operator!=(const NextHopSet& o) const { return !(v_ == o.v_); }
+  bool operator<(const NextHopSet& o) const { return v_ < o.v_; }
+
+ private:
+  std::pair<iterator, bool> put(value_type&& x) {
+    if (v_.empty() || v_.back() < x) {  // in order (the route builds insert sorted)
+      v_.push_back(std::move(x));
+      return {v_.end() - 1, true};
+    }
+    auto it = std::lower_bound(v_.begin(), v_.end(), x);
+    if (it != v_.end() && !(x < *it)) return {it, false};
+    const auto at = it - v_.begin();
+    v_.insert(it, std::move(x));
+    return {v_.begin() + at, true};
+  }
+  iterator putHint(const_iterator, value_type&& x) { return put(std::move(x)).first; }
+  std::vector<value_type> v_;
+};
 using PrefixEntries = std::unordered_map<NodeAndArea, thrift::PrefixEntry>;
 
 struct RibUnicastEntry {  // RibEntry.h:37
@@ -146,9 +229,111 @@ struct RibMplsEntry {  // RibEntry.h:92
   NextHopSet nexthops;
 };
 
+// The reference's route maps (Decision.h:80: unordered_map<CIDRNetwork, RibUnicastEntry>,
+// unordered_map<int32_t, RibMplsEntry>) as sorted vectors of (key, value): map lookups,
+// iteration in key order (deterministic for tests), and no per-route node allocation. A
+// route build inserts in key order (an append); an insert elsewhere shifts the tail, and
+// like a vector's it invalidates iterators and references.
+template <class K, class V>
+class FlatMap {
+ public:
+  using key_type = K;
+  using mapped_type = V;
+  using value_type = std::pair<K, V>;
+  using iterator = typename std::vector<value_type>::iterator;
+  using const_iterator = typename std::vector<value_type>::const_iterator;
+  using size_type = size_t;
+
+  FlatMap() = default;
+  FlatMap(std::initializer_list<value_type> il) {
+    for (auto const& x : il) insert_or_assign(x.first, x.second);
+  }
+  iterator begin() { return v_.begin(); }
+  iterator end() { return v_.end(); }
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  void clear() { v_.clear(); }
+  void reserve(size_t n) { v_.reserve(n); }
+
+  iterator find(const K& k) {
+    auto it = lower(k);
+    return it != v_.end() && !(k < it->first) ? it : v_.end();
+  }
+  const_iterator find(const K& k) const { return const_cast<FlatMap*>(this)->find(k); }
+  size_t count(const K& k) const { return find(k) != end() ? 1u : 0u; }
+  bool contains(const K& k) const { return find(k) != end(); }
+  V& at(const K& k) {
+    auto it = find(k);
+    if (it == v_.end()) throw std::out_of_range("FlatMap::at");
+    return it->second;
+  }
+  const V& at(const K& k) const { return const_cast<FlatMap*>(this)->at(k); }
+  V& operator[](const K& k) { return emplace(std::piecewise_construct, std::forward_as_tuple(k), std::forward_as_tuple()).first->second; }
+
+  template <class M>
+  std::pair<iterator, bool> insert_or_assign(const K& k, M&& m) {
+    if (v_.empty() || v_.back().first < k) {  // in key order: an append
+      v_.emplace_back(k, std::forward<M>(m));
+      return {v_.end() - 1, true};
+    }
+    auto it = lower(k);
+    if (it != v_.end() && !(k < it->first)) {
+      it->second = std::forward<M>(m);
+      return {it, false};
+    }
+    const auto at = it - v_.begin();
+    v_.emplace(it, k, std::forward<M>(m));
+    return {v_.begin() + at, true};
+  }
+  template <class M>
+  iterator insert_or_assign(const_iterator, const K& k, M&& m) {
+    return insert_or_assign(k, std::forward<M>(m)).first;
+  }
+  std::pair<iterator, bool> insert(value_type x) { return put(std::move(x)); }
+  template <class... A>
+  std::pair<iterator, bool> emplace(A&&... a) {
+    return put(value_type(std::forward<A>(a)...));
+  }
+  template <class... A>
+  iterator emplace_hint(const_iterator, A&&... a) {
+    return put(value_type(std::forward<A>(a)...)).first;
+  }
+  iterator erase(const_iterator it) { return v_.erase(it); }
+  size_t erase(const K& k) {
+    auto it = find(k);
+    if (it == v_.end()) return 0;
+    v_.erase(it);
+    return 1;
+  }
+  bool operator==(const FlatMap& o) const { return v_ == o.v_; }
+  bool operator!=(const FlatMap& o) const { return !(v_ == o.v_); }
+
+ private:
+  iterator lower(const K& k) {
+    return std::lower_bound(v_.begin(), v_.end(), k, [](const value_type& a, const K& b) { return a.first < b; });
+  }
+  // inserts x unless its key is present; returns (the key's element, inserted)
+  std::pair<iterator, bool> put(value_type&& x) {
+    if (v_.empty() || v_.back().first < x.first) {  // in key order: an append
+      v_.push_back(std::move(x));
+      return {v_.end() - 1, true};
+    }
+    auto it = lower(x.first);
+    if (it != v_.end() && !(x.first < it->first)) return {it, false};
+    const auto at = it - v_.begin();
+    v_.insert(it, std::move(x));
+    return {v_.begin() + at, true};
+  }
+  std::vector<value_type> v_;
+};
+using UnicastRoutes = FlatMap<thrift::IpPrefix, RibUnicastEntry>;
+using MplsRoutes = FlatMap<int32_t, RibMplsEntry>;
+
 struct DecisionRouteDb {  // Decision.h:80
-  std::map<thrift::IpPrefix, RibUnicastEntry> unicastRoutes;
-  std::map<int32_t, RibMplsEntry> mplsRoutes;
+  UnicastRoutes unicastRoutes;
+  MplsRoutes mplsRoutes;
   void addUnicastRoute(RibUnicastEntry&& e) { unicastRoutes.insert_or_assign(e.prefix, std::move(e)); }
   void addMplsRoute(RibMplsEntry&& e) { mplsRoutes.insert_or_assign(e.label, std::move(e)); }
 };
@@ -346,7 +531,7 @@ class SpfSolver {
   // true when the prefix was served: its route, if any, is appended to `routes` (prefixes
   // arrive in key order, so the route is built in place at the end)
   bool fastRoute(const std::string& me, thrift::IpPrefix const& prefix, PrefixEntries const& entries, uint32_t dstId,
-                 std::map<thrift::IpPrefix, RibUnicastEntry>& routes);
+                 UnicastRoutes& routes);
   // selectBestPathsKsp2 on the staged token rows of one area (LinkState::kthPathTokens):
   // the same paths, pathAInPathB filter, label stacks, costs and next hops, on ids
   NextHopSet ksp2NextHopsFromTokens(const std::string& me, thrift::IpPrefix const& prefix,
@@ -405,7 +590,7 @@ class RibPolicy {
   bool isActive() const;
   bool applyAction(RibUnicastEntry& route) const;  // first matching statement wins
   // prefixes of the routes the policy transformed
-  std::vector<thrift::IpPrefix> applyPolicy(std::map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries) const;
+  std::vector<thrift::IpPrefix> applyPolicy(UnicastRoutes& unicastEntries) const;
 
  private:
   std::vector<RibPolicyStatement> statements_;

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <exception>
 #include <mutex>
@@ -71,6 +73,25 @@ void parallelFor(size_t n, size_t grain, unsigned workers, F&& f) {
   for (auto& t : pool) t.join();
   if (err) std::rethrow_exception(err);
 }
+
+// Tuning aid: OPENR_HOST_PROF=1 prints the wall time of the host phases of a route build
+// (prefetch, D2H, row store, per-node builds) to stderr.
+inline bool hostProf() {
+  static const bool on = [] {
+    const char* s = std::getenv("OPENR_HOST_PROF");
+    return s && *s == '1';
+  }();
+  return on;
+}
+struct HostPhase {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit HostPhase(const char* n) : name(n) {}
+  double ms() const { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+  ~HostPhase() {
+    if (hostProf() && name && *name) std::fprintf(stderr, "[host] %s %.1f ms\n", name, ms());
+  }
+};
 
 inline unsigned parallelWorkers(size_t n, size_t grain) {
   grain = std::max<size_t>(grain, 1);

@@ -719,18 +719,28 @@ void LinkState::prefetchSpfResults(const std::vector<std::string>& nodes, bool u
   if (d.src.empty()) d.nb = nb;
   const size_t r0 = d.src.size();
   d.V = V;
-  d.resizeRows(r0 + n);
+  {
+    HostPhase ph("prefetch: resize rows");
+    d.resizeRows(r0 + n);
+  }
   // the engine's u64 rows through a staging buffer of at most ~64 MB
   const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(n, (64u << 20) / (8u * (size_t)std::max(V, 1u))));
   std::vector<uint64_t> stage((size_t)chunk * V);
+  double msSolve = 0, msStore = 0;
   for (uint32_t c0 = 0; c0 < n; c0 += chunk) {
     const uint32_t k = std::min(chunk, n - c0);
+    HostPhase ps("");
     SpfEngineHandle::check(openr_spf_solve(engine_->ctx(), ids.data() + c0, k,
                                            useLinkMetric ? (uint32_t)OPENR_SPF_USE_LINK_METRIC : 0u, stage.data(),
                                            d.nh.data() + (r0 + c0) * V * d.nb, d.nb, nullptr),
                            "openr_spf_solve");
+    msSolve += ps.ms();
+    HostPhase pt("");
     d.store(r0 + c0, k, stage.data());
+    msStore += pt.ms();
   }
+  if (hostProf()) std::fprintf(stderr, "[host] prefetch: %u rows, solve + D2H %.1f ms, store %.1f ms\n", n, msSolve, msStore);
+  HostPhase pn("prefetch: neighbour maps + memo entries");
   d.nbrs.resize(r0 + n);
   std::vector<uint32_t> buf(V ? V : 1);
   for (uint32_t k = 0; k < n; ++k) {

@@ -288,9 +288,20 @@ uint64_t mix64(uint64_t h) {
   h *= 0xc4ceb9fe1a85ec53ULL;
   return h ^ (h >> 33);
 }
+// 8 bytes per step (the route tally hashes every next hop of 100 M routes on G100: a byte
+// at a time that was ~8 % of the route-build wall time)
 uint64_t hashStr(uint64_t h, const std::string& s) {
-  for (unsigned char c : s) h = (h ^ c) * 1099511628211ULL;
-  return mix64(h ^ s.size());
+  const char* p = s.data();
+  size_t n = s.size();
+  for (; n >= 8; p += 8, n -= 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    h = (h ^ w) * 0x9E3779B97F4A7C15ULL;
+    h ^= h >> 29;
+  }
+  uint64_t w = 0;
+  std::memcpy(&w, p, n);
+  return mix64(h ^ w ^ ((uint64_t)s.size() << 56));
 }
 }  // namespace
 

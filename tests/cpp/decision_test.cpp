@@ -886,7 +886,7 @@ TEST_CPU(RibPolicy_ApplyAction) {  // RibPolicy.cpp:61-111 (RibPolicyTest semant
   auto r3 = route;
   r3.prefix = addr2;
   EXPECT_FALSE(policy.applyAction(r3));
-  std::map<thrift::IpPrefix, RibUnicastEntry> db{{addr1, route}, {addr2, r3}};
+  UnicastRoutes db{{addr1, route}, {addr2, r3}};
   EXPECT_EQ(policy.applyPolicy(db).size(), 1u);
   bool threw = false;
   try {
@@ -1514,6 +1514,47 @@ TEST_GPU(BGPRedistribution_BasicOperation) {
   EXPECT_FALSE(routeTo("3").has_value());
 }
 
+// The route containers (sorted vectors with the reference's map / set semantics): keys
+// kept unique and ordered whatever the insertion order, insert_or_assign overwriting,
+// emplace not, lookups and erasure.
+TEST_CPU(RouteContainers_MapAndSetSemantics) {
+  MplsRoutes m;
+  for (int32_t k : {30, 10, 20, 40, 10}) m.emplace(k, RibMplsEntry{k, {}});
+  EXPECT_EQ(m.size(), 4u);
+  std::vector<int32_t> keys;
+  for (auto const& [k, e] : m) keys.push_back(k);
+  EXPECT_TRUE((keys == std::vector<int32_t>{10, 20, 30, 40}));
+  m.insert_or_assign(20, RibMplsEntry{99, {}});
+  EXPECT_EQ(m.at(20).label, 99);
+  m.emplace(20, RibMplsEntry{7, {}});  // present: unchanged
+  EXPECT_EQ(m.at(20).label, 99);
+  m.insert_or_assign(25, RibMplsEntry{25, {}});
+  EXPECT_EQ(std::next(m.begin(), 2)->first, 25);
+  EXPECT_EQ(m.count(25), 1u);
+  EXPECT_EQ(m.erase(25), 1u);
+  EXPECT_EQ(m.erase(25), 0u);
+  EXPECT_TRUE(m.find(25) == m.end());
+  EXPECT_THROW(m.at(25));
+  EXPECT_EQ(m[50].label, 0);  // default-constructed on first access
+  EXPECT_EQ(m.size(), 5u);
+
+  thrift::NextHopThrift a, b, c;
+  a.address.addr = "a";
+  b.address.addr = "b";
+  c.address.addr = "c";
+  NextHopSet s{c, a, b, a};
+  EXPECT_EQ(s.size(), 3u);
+  EXPECT_TRUE(s.begin()->address.addr == "a" && std::prev(s.end())->address.addr == "c");
+  EXPECT_FALSE(s.insert(b).second);
+  thrift::NextHopThrift b5 = b;
+  b5.metric = 5;  // a different next hop
+  EXPECT_TRUE(s.emplace(b5).second);
+  EXPECT_EQ(s.size(), 4u);
+  EXPECT_EQ(s.count(b5), 1u);
+  EXPECT_EQ(s.erase(b5), 1u);
+  EXPECT_TRUE((s == NextHopSet{b, c, a}));
+}
+
 TEST_CPU(RibPolicyTest_ApplyAction) {  // :180-236 only the first matching statement applies
   const auto stmt1 = policyStatement({pfx("fc01::/64")}, 1, {{"area1", 99}});
   const auto stmt2 = policyStatement({pfx("fc00::/64"), pfx("fc02::/64")}, 1, {{"area2", 99}});
@@ -1566,7 +1607,7 @@ TEST_CPU(RibPolicyTest_ApplyPolicy) {  // :238-301 neighbour > area > default, a
   e2.prefix = pfx("fc02::/64");
   e2.nexthops = {nh2};
   {
-    std::map<thrift::IpPrefix, RibUnicastEntry> entries{{e1.prefix, e1}, {e2.prefix, e2}};
+    UnicastRoutes entries{{e1.prefix, e1}, {e2.prefix, e2}};
     const uint64_t inv0 = RibPolicyCounters::get().invalidatedRoutes;
     const auto updated = policy.applyPolicy(entries);
     EXPECT_EQ(updated, std::vector<thrift::IpPrefix>({e1.prefix}));
@@ -1582,7 +1623,7 @@ TEST_CPU(RibPolicyTest_ApplyPolicy) {  // :238-301 neighbour > area > default, a
   std::this_thread::sleep_for(std::chrono::milliseconds(1100));  // the policy expires
   EXPECT_FALSE(policy.isActive());
   {
-    std::map<thrift::IpPrefix, RibUnicastEntry> entries{{e1.prefix, e1}, {e2.prefix, e2}};
+    UnicastRoutes entries{{e1.prefix, e1}, {e2.prefix, e2}};
     EXPECT_TRUE(policy.applyPolicy(entries).empty());
     EXPECT_EQ(entries.at(e1.prefix).nexthops, e1.nexthops);
   }
