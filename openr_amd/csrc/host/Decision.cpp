@@ -238,6 +238,57 @@ void SpfSolver::buildRouteDbs(const std::vector<std::string>& nodes,
   }
 }
 
+namespace {
+// label -> slot of a route build's node-label candidates: open addressing over valid MPLS
+// labels (never 0), one allocation per build instead of a hash node per label
+class LabelSlots {
+ public:
+  size_t size() const { return n_; }
+  void reserve(size_t n) {
+    if (2 * n <= keys_.size()) return;
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<int32_t> k(cap, 0);
+    std::vector<uint32_t> v(cap, 0);
+    const size_t m = cap - 1;
+    for (size_t i = 0; i < keys_.size(); ++i)
+      if (keys_[i]) {
+        size_t h = hash(keys_[i]) & m;
+        while (k[h]) h = (h + 1) & m;
+        k[h] = keys_[i];
+        v[h] = vals_[i];
+      }
+    keys_.swap(k);
+    vals_.swap(v);
+  }
+  const uint32_t* find(int32_t label) const {
+    if (keys_.empty()) return nullptr;
+    const size_t m = keys_.size() - 1;
+    for (size_t h = hash(label) & m;; h = (h + 1) & m) {
+      if (keys_[h] == label) return &vals_[h];
+      if (!keys_[h]) return nullptr;
+    }
+  }
+  std::pair<uint32_t*, bool> emplace(int32_t label, uint32_t slot) {
+    reserve(n_ + 1);
+    const size_t m = keys_.size() - 1;
+    size_t h = hash(label) & m;
+    for (; keys_[h]; h = (h + 1) & m)
+      if (keys_[h] == label) return {&vals_[h], false};
+    keys_[h] = label;
+    vals_[h] = slot;
+    ++n_;
+    return {&vals_[h], true};
+  }
+
+ private:
+  static size_t hash(int32_t label) { return (size_t)((uint32_t)label * 2654435761u); }
+  std::vector<int32_t> keys_;
+  std::vector<uint32_t> vals_;
+  size_t n_ = 0;
+};
+}  // namespace
+
 // Decision.cpp:568-734
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNodeName,
                                                        std::unordered_map<std::string, LinkState> const& als,
@@ -311,16 +362,16 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
   // MPLS routes for every node label (:593-680). The reference's label -> (node, route) map
   // is kept as label -> slot of `cand` (same visiting order, collisions and counters); the
   // winners then enter the DB in label order.
-  std::unordered_map<int32_t, uint32_t> labelToNode;
+  LabelSlots labelToNode;
   std::vector<std::pair<const std::string*, RibMplsEntry>> cand;
   auto put = [&](int32_t label, const std::string* node, RibMplsEntry&& entry) {
-    auto [it, fresh] = labelToNode.emplace(label, (uint32_t)cand.size());
+    auto [slot, fresh] = labelToNode.emplace(label, (uint32_t)cand.size());
     if (fresh) cand.emplace_back(node, std::move(entry));
-    else cand[it->second] = std::make_pair(node, std::move(entry));
+    else cand[*slot] = std::make_pair(node, std::move(entry));
   };
   for (auto const& [area, ls] : als) {
     if (!ls.labeledNodeCount()) continue;  // every label is 0 (non-SR mode): nothing to visit
-    labelToNode.reserve(labelToNode.size() + ls.labeledNodeCount());
+    labelToNode.reserve(labelToNode.size() + ls.labeledNodeCount() + 1u);
     // the labelled adjacency databases in getAdjacencyDatabases() order, with mirror ids
     // (the fast path reads my row's mirror: a retired snapshot's ids need the name lookup)
     const auto& labeled = ls.labeledNodes();
@@ -332,10 +383,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
         counters_.skipped_mpls_route++;
         continue;
       }
-      auto it = labelToNode.find(topLabel);
-      if (it != labelToNode.end()) {  // collision: the bigger node name keeps the label
+      if (const uint32_t* slot = labelToNode.find(topLabel)) {  // collision: the bigger node name keeps the label
         counters_.duplicate_node_label++;
-        if (*cand[it->second].first < nodeName) continue;
+        if (*cand[*slot].first < nodeName) continue;
       }
       if (nodeName == myNodeName) {
         thrift::NextHopThrift nh;
@@ -372,9 +422,13 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(const std::string& myNode
                                                    metricNhs.first, metricNhs.second, topLabel, als)});
     }
   }
-  std::sort(cand.begin(), cand.end(), [](auto const& x, auto const& y) { return x.second.label < y.second.label; });
+  // label order through (label, slot) words: the entries move once, into the DB
+  std::vector<uint64_t> order(cand.size());
+  for (size_t i = 0; i < cand.size(); ++i) order[i] = ((uint64_t)(uint32_t)cand[i].second.label << 32) | i;
+  std::sort(order.begin(), order.end());
   routeDb.mplsRoutes.reserve(cand.size() + staticMplsRoutes_.size() + 64u);
-  for (auto& [_, entry] : cand) {
+  for (const uint64_t o : order) {
+    RibMplsEntry& entry = cand[(uint32_t)o].second;
     const int32_t label = entry.label;
     routeDb.mplsRoutes.emplace_hint(routeDb.mplsRoutes.end(), label, std::move(entry));
   }
@@ -995,10 +1049,15 @@ int SpfSolver::fastLabelNextHops(const std::string& me, uint32_t dst, int32_t la
   if (d == UINT64_MAX) return 0;  // getMinCostNodes: dst not reached, no next-hop node
   const int nn = fastNextHopNodes(me, dst, d);
   if (nn <= 0) return nn;
+  auto takes = [&](const FastLink& fl) {
+    return fast_.has[fl.nbrBit] && fl.up && (computeLfaPaths_ || fl.metric + fast_.val[fl.nbrBit] == d);
+  };
+  size_t want = 0;
+  for (auto const& fl : fast_.links) want += takes(fl) ? 1u : 0u;
+  out->reserve(want);  // one allocation per label route
   for (auto const& fl : fast_.links) {  // getNextHopsThrift, in NextHopThrift order
-    if (!fast_.has[fl.nbrBit] || !fl.up) continue;
+    if (!takes(fl)) continue;
     const Metric over = fl.metric + fast_.val[fl.nbrBit];
-    if (!computeLfaPaths_ && over != d) continue;
     thrift::NextHopThrift nh = fl.proto6;
     nh.metric = static_cast<int32_t>(over);
     const bool php = fl.nbrId == dst;  // the next hop is the label's node
