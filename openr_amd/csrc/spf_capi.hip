@@ -630,7 +630,7 @@ hipError_t whatif_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan
       OPENR_TRY(d.wchanged_t.reserve(units));
       OPENR_TRY(hipEventRecord(d.ev_begin, s));  // the repair kernel's own time -> stats.last_kernel_ms
       OPENR_TRY(launch_whatif_group(d.g, d_links, n_links, d_sources, n_src, d.base_dist.p, d.base_nh.p,
-                                    d.base_tight.p, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
+                                    d.base_tight.p, base_tin ? d.base_tin.p : nullptr, nb, !use_link_metric, dist64, ctx->w_max, ctx->nh_bits,
                                     d_changed, d.wchanged_t.p, d.wcount.p, d.wsrc.p, d.wlink.p, d.wunit.p,
                                     d.work.p + kIncrCtr, dl, d.num_cus, s));
       OPENR_TRY(hipEventRecord(d.ev_end, s));

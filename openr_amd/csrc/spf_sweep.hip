@@ -1053,8 +1053,8 @@ constexpr uint32_t kGrpProfWg = 4096;  // workgroups whose start / end times the
 template <typename D, bool LG, uint32_t W, int WPE, bool DL>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
-    const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, uint32_t nb, uint32_t unit,
-    uint32_t cap, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
+    const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, const uint16_t* base_tin,
+    uint32_t nb, uint32_t unit, uint32_t cap, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
     uint32_t* ctr, unsigned long long* prof, WhatifDelta dl) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -1138,14 +1138,29 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     }
     const uint64_t* trow = base_tight + (size_t)j * tw;
     for (uint32_t i = tid; i < tw; i += block) btight[i] = trow[i];
-    for (uint32_t i = tid; i < (V + 4u) / 4u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
+    if (base_tin) {
+      // the base SPF's tight in-degree row (rounds plan), four nodes per word
+      const uint16_t* tr = base_tin + (size_t)j * V;
+      for (uint32_t i = tid; i < (V + 4u) / 4u; i += block) {
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          const uint32_t v = 4u * i + q;
+          w |= (v < V ? (uint32_t)tr[v] : 0u) << (8u * q);  // max_deg <= 255
+        }
+        reinterpret_cast<uint32_t*>(btin)[i] = w;
+      }
+    } else {
+      for (uint32_t i = tid; i < (V + 4u) / 4u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
+    }
     if (tid == 0) wctl[0] = wctl[1] = 0;  // [0] affected links listed, [1] next one to repair
     __syncthreads();
-    for (uint32_t e = tid; e < E; e += block)  // base-tight in-degrees
-      if ((btight[e >> 6] >> (e & 63u)) & 1ull) {
-        const uint32_t v = c.gv.rec(e).col;
-        atomicAdd(reinterpret_cast<uint32_t*>(btin) + (v >> 2), 1u << (8u * (v & 3u)));
-      }
+    if (!base_tin)
+      for (uint32_t e = tid; e < E; e += block)  // base-tight in-degrees from the tight mask
+        if ((btight[e >> 6] >> (e & 63u)) & 1ull) {
+          const uint32_t v = c.gv.rec(e).col;
+          atomicAdd(reinterpret_cast<uint32_t*>(btin) + (v >> 2), 1u << (8u * (v & 3u)));
+        }
     // fused filter, a thread per link: a link with no base-tight edge changes nothing;
     // the others are listed with b, the head of their tight edge a->b (at most one
     // direction of a link is tight), so a repair starts without dependent loads
@@ -1418,7 +1433,8 @@ uint32_t whatif_group_lds_bytes(uint32_t V, uint32_t E, uint32_t nb, bool dist64
 
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
-                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
+                               const uint64_t* base_tight, const uint16_t* base_tin, uint32_t nb, bool unit_cost,
+                               bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* changed_t, uint32_t* affected,
                                uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr,
                                const WhatifDelta& dl, int num_cus, hipStream_t s) {
@@ -1478,6 +1494,9 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     prof = prof_buf;
     if (prof) (void)hipMemsetAsync(prof, 0, words * sizeof(unsigned long long), s);
   }
+  // base-tight in-degrees from the base SPF's rows when it left them (OPENR_SPF_WHATIF_TIN=0:
+  // recounted from the tight mask per item, A/B)
+  const uint16_t* tin = bfs::env_u32("OPENR_SPF_WHATIF_TIN", 1u, 0u, 1u) ? base_tin : nullptr;
   // the <= 32-bit-set variant is compiled for 7 waves per SIMD, the occupancy its LDS
   // layout allows (28 waves per CU): WAN step 5.03 -> 4.17 ms (unconstrained: 119 VGPRs,
   // 4 waves per SIMD; 5 waves: 4.56 ms), round 4
@@ -1491,7 +1510,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
-                       base_nh, base_tight, nb, (uint32_t)unit_cost, cap, changed_t, affected, ovf_src, ovf_link, \
+                       base_nh, base_tight, tin, nb, (uint32_t)unit_cost, cap, changed_t, affected, ovf_src, ovf_link, \
                        ovf_unit, ctr, prof, dl);                                                               \
   } while (0)
   if (d16) {
