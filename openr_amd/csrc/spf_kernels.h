@@ -276,7 +276,7 @@ uint32_t whatif_incr_lds_bytes(uint32_t V, uint32_t nb, bool dist64);
 // dl.node, every repaired unit also writes its delta (WhatifDelta).
 hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_t n_links, const uint32_t* sources,
                                uint32_t n_src, const uint64_t* base_dist, const uint8_t* base_nh,
-                               const uint64_t* base_tight, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
+                               const uint64_t* base_tight, const uint16_t* base_tin, uint32_t nb, bool unit_cost, bool dist64, uint32_t w_max,
                                uint32_t nh_bits, uint32_t* changed, uint32_t* changed_t, uint32_t* affected,
                                uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit, uint32_t* ctr,
                                const WhatifDelta& dl, int num_cus, hipStream_t s);
