@@ -1099,7 +1099,9 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   }
   c.nb = nb;
   c.unit = unit != 0;
-  c.prof = prof;
+  // prof[15] != 0: workgroup start / end times only (no per-unit counters and their atomics)
+  const bool tail_only = prof && prof[15] != 0ull;
+  c.prof = tail_only ? nullptr : prof;
   c.dl = dl;
   c.pcur = c.pend = 0;
   c.bdist = bdist;
@@ -1218,7 +1220,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     __syncthreads();
     item = s_item;
   }
-  if (prof && lane == 0) {
+  if (prof && !tail_only && lane == 0) {
     atomicAdd(&prof[8], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - kt0));  // wave lifetime
     atomicAdd(&prof[9], 1ull);
   }
@@ -1456,7 +1458,7 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // 112 4.25, 128 4.16, 144 4.17, 160 4.15, 192 4.21 ms). A second pass repairing the
   // overflowed units with every slot on one wavefront each was slower than the re-solves
   // (5.34 vs 5.18 ms, round 3; 4.68 vs 4.16 ms, round 4) and was removed.
-  uint32_t waves = kGrpWaves;
+  uint32_t waves = bfs::env_u32("OPENR_SPF_WHATIF_WAVES", kGrpWaves, 1u, 8u);  // tuning / tests
   const uint32_t cap = bfs::env_u32("OPENR_SPF_WHATIF_CAP", kGrpCap1, 1u, kGrpMaxCap);  // tests force small caps
   auto layout_bytes = [&](bool l, uint32_t w, uint32_t ch) { return grp_layout(g.V, g.E, nb, db, l, w, ch, cap).total; };
   if (grp_lds_graph_ok(g, w_max, nh_bits)) {
@@ -1492,7 +1494,14 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     const size_t words = 16u + 2u * kGrpProfWg;
     if (!prof_buf && hipMalloc(&prof_buf, words * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
     prof = prof_buf;
-    if (prof) (void)hipMemsetAsync(prof, 0, words * sizeof(unsigned long long), s);
+    if (prof) {
+      (void)hipMemsetAsync(prof, 0, words * sizeof(unsigned long long), s);
+      // OPENR_SPF_WHATIF_TAIL=1: only the workgroup times (the per-unit counters' atomics
+      // slow the kernel ~40x and distort its tail)
+      static const unsigned long long one = 1ull;
+      if (bfs::env_u32("OPENR_SPF_WHATIF_TAIL", 0u, 0u, 1u))
+        (void)hipMemcpyAsync(prof + 15, &one, sizeof(one), hipMemcpyHostToDevice, s);
+    }
   }
   // base-tight in-degrees from the base SPF's rows when it left them (OPENR_SPF_WHATIF_TIN=0:
   // recounted from the tight mask per item, A/B)
