@@ -1054,7 +1054,7 @@ template <typename D, bool LG, uint32_t W, int WPE, bool DL>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, const uint16_t* base_tin,
-    uint32_t nb, uint32_t unit, uint32_t cap, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
+    uint32_t nb, uint32_t unit, uint32_t cap, uint32_t heavy_first, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
     uint32_t* ctr, unsigned long long* prof, WhatifDelta dl) {
   constexpr D INF = (D)~(D)0;
   const long long kt0 = prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     } else {
       for (uint32_t i = tid; i < (V + 4u) / 4u; i += block) reinterpret_cast<uint32_t*>(btin)[i] = 0;
     }
-    if (tid == 0) wctl[0] = wctl[1] = 0;  // [0] affected links listed, [1] next one to repair
+    if (tid == 0) wctl[0] = wctl[1] = wctl[2] = 0;  // [0] / [2] affected links listed, [1] next one to repair
     __syncthreads();
     if (!base_tin)
       for (uint32_t e = tid; e < E; e += block)  // base-tight in-degrees from the tight mask
@@ -1165,7 +1165,11 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
         }
     // fused filter, a thread per link: a link with no base-tight edge changes nothing;
     // the others are listed with b, the head of their tight edge a->b (at most one
-    // direction of a link is tight), so a repair starts without dependent loads
+    // direction of a link is tight), so a repair starts without dependent loads. With
+    // heavy_first, a unit whose b has no other base-tight in-edge (b's distance grows: A is
+    // not empty, the long repairs) is listed from the front (wctl[0]), the others from the
+    // back (wctl[2]): the item's last repairs are short ones, so its waves reach the item's
+    // barrier closer together
     for (uint32_t i0 = l0; i0 < l1; i0 += block) {
       const uint32_t i = i0 + tid;
       bool hit = false;
@@ -1180,16 +1184,23 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
         }
         if (!hit) changed_t[(size_t)j * n_links + i] = 0;
       }
-      const unsigned long long m = __ballot(hit);
-      uint32_t basei = 0;
+      const bool heavy = hit && (!heavy_first || btin[bnode] == 1u);
+      const unsigned long long m = __ballot(heavy), ml = __ballot(hit && !heavy);
+      uint32_t basei = 0, basel = 0;
       if (lane == 0 && m) basei = atomicAdd(&wctl[0], (uint32_t)__popcll(m));
+      if (lane == 0 && ml) basel = atomicAdd(&wctl[2], (uint32_t)__popcll(ml));
       basei = __builtin_amdgcn_readfirstlane(__shfl(basei, 0));
-      if (hit)
+      basel = __builtin_amdgcn_readfirstlane(__shfl(basel, 0));
+      if (heavy)
         ulist[basei + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+            ((i - l0) << 16) | bnode;
+      else if (hit)
+        ulist[chunk - 1u - (basel + __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u)))] =
             ((i - l0) << 16) | bnode;
     }
     __syncthreads();
-    const uint32_t n_hit = wctl[0];
+    const uint32_t n_front = wctl[0], n_hit = n_front + wctl[2];
     if (tid == 0 && n_hit) atomicAdd(affected, n_hit);  // per item: no counter live across the repairs
     // waves take the listed units one at a time: the item ends within one repair of balance
     for (;;) {
@@ -1197,7 +1208,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
       if (lane == 0) idx = atomicAdd(&wctl[1], 1u);
       idx = __builtin_amdgcn_readfirstlane(__shfl(idx, 0));
       if (idx >= n_hit) break;
-      const uint32_t ent = __builtin_amdgcn_readfirstlane(ulist[idx]);
+      const uint32_t ent = __builtin_amdgcn_readfirstlane(ulist[idx < n_front ? idx : chunk - 1u - (idx - n_front)]);
       const uint32_t i = l0 + (ent >> 16);
       c.link = links[i];  // first needed in step (2): the load overlaps step (1)
       c.uidx = i * n_src + j;
@@ -1506,6 +1517,8 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   // base-tight in-degrees from the base SPF's rows when it left them (OPENR_SPF_WHATIF_TIN=0:
   // recounted from the tight mask per item, A/B)
   const uint16_t* tin = bfs::env_u32("OPENR_SPF_WHATIF_TIN", 1u, 0u, 1u) ? base_tin : nullptr;
+  // long repairs first within an item (needs the staged in-degrees; OPENR_SPF_WHATIF_ORDER=0: link order)
+  const uint32_t heavy_first = tin && bfs::env_u32("OPENR_SPF_WHATIF_ORDER", 1u, 0u, 1u) ? 1u : 0u;
   // the <= 32-bit-set variant is compiled for 7 waves per SIMD, the occupancy its LDS
   // layout allows (28 waves per CU): WAN step 5.03 -> 4.17 ms (unconstrained: 119 VGPRs,
   // 4 waves per SIMD; 5 waves: 4.56 ms), round 4
@@ -1519,7 +1532,8 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
-                       base_nh, base_tight, tin, nb, (uint32_t)unit_cost, cap, changed_t, affected, ovf_src, ovf_link, \
+                       base_nh, base_tight, tin, nb, (uint32_t)unit_cost, cap, heavy_first, changed_t, affected,     \
+                       ovf_src, ovf_link,                                                                      \
                        ovf_unit, ctr, prof, dl);                                                               \
   } while (0)
   if (d16) {
