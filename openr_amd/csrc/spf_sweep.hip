@@ -1053,6 +1053,7 @@ constexpr uint32_t kGrpProfWg = 4096;  // workgroups whose start / end times the
 template <typename D, bool LG, uint32_t W, int WPE, bool DL>
 __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void whatif_group_kernel(
     DevGraph g, const uint32_t* links, uint32_t n_links, const uint32_t* sources, uint32_t n_src, uint32_t chunk,
+    uint32_t lbig, uint32_t schunk,
     const uint64_t* base_dist, const uint8_t* base_nh, const uint64_t* base_tight, const uint16_t* base_tin,
     uint32_t nb, uint32_t unit, uint32_t cap, uint32_t heavy_first, uint32_t* changed_t, uint32_t* affected, uint32_t* ovf_src, uint32_t* ovf_link, uint32_t* ovf_unit,
     uint32_t* ctr, unsigned long long* prof, WhatifDelta dl) {
@@ -1119,10 +1120,25 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
   c.anh = reinterpret_cast<uint8_t*>(wb + lay.w_anh);
   c.alist = reinterpret_cast<uint16_t*>(wb + lay.w_alist);
   c.dlist = reinterpret_cast<uint16_t*>(wb + lay.w_dlist);
-  const uint32_t chunks = (n_links + chunk - 1u) / chunk;
-  const uint32_t items = n_src * chunks;
+  // items: every source's links [0, lbig) in chunks of `chunk`, then (the queue's tail, so
+  // that the last workgroups finish together) its links [lbig, n_links) in chunks of `schunk`
+  const uint32_t bchunks = (lbig + chunk - 1u) / chunk;
+  const uint32_t schunks = lbig < n_links ? (n_links - lbig + schunk - 1u) / schunk : 0u;
+  const uint32_t nbig = n_src * bchunks, items = nbig + n_src * schunks;
+  unsigned long long* ist = tail_only ? prof + 16 + 2 * kGrpProfWg : nullptr;  // per-item stamps (tuning)
   for (uint32_t item = blockIdx.x; item < items;) {
-    const uint32_t j = item / chunks, l0 = (item - j * chunks) * chunk, l1 = min(n_links, l0 + chunk);
+    uint32_t j, l0, l1;
+    if (item < nbig) {
+      j = item / bchunks;
+      l0 = (item - j * bchunks) * chunk;
+      l1 = min(lbig, l0 + chunk);
+    } else {
+      const uint32_t k = item - nbig;
+      j = k / schunks;
+      l0 = lbig + (k - j * schunks) * schunk;
+      l1 = min(n_links, l0 + schunk);
+    }
+    if (ist && lane == 0) ist[(size_t)(item * waves + wave) * 4u + 0u] = __builtin_amdgcn_s_memtime();
     c.src = sources[j];
     // stage source j's base rows (read once per item)
     const uint64_t* drow = base_dist + (size_t)j * V;
@@ -1201,6 +1217,7 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
     }
     __syncthreads();
     const uint32_t n_front = wctl[0], n_hit = n_front + wctl[2];
+    if (ist && lane == 0) ist[(size_t)(item * waves + wave) * 4u + 1u] = __builtin_amdgcn_s_memtime();
     if (tid == 0 && n_hit) atomicAdd(affected, n_hit);  // per item: no counter live across the repairs
     // waves take the listed units one at a time: the item ends within one repair of balance
     for (;;) {
@@ -1226,7 +1243,9 @@ __global__ __launch_bounds__(kGrpMaxBlock) __attribute__((amdgpu_waves_per_eu(WP
       }
       __builtin_amdgcn_wave_barrier();  // the lane-0 branch joins here: the latch is taken by the whole wave
     }
+    if (ist && lane == 0) ist[(size_t)(item * waves + wave) * 4u + 2u] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // every wave is done with this item's shared rows and s_item
+    if (ist && lane == 0) ist[(size_t)(item * waves + wave) * 4u + 3u] = __builtin_amdgcn_s_memtime();
     if (tid == 0) s_item = gridDim.x + atomicAdd(&ctr[0], 1u);
     __syncthreads();
     item = s_item;
@@ -1489,20 +1508,38 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
   };
   // work items of (source, chunk of links): ~8 per resident workgroup, so the tail is short
   const uint64_t slots0 = slots_for(layout_bytes(lg, waves, kGrpMaxChunk));
-  uint64_t cps = (8u * slots0 + n_src - 1u) / n_src;
+  // ~3 full-size items per resident workgroup, then (below) the last fifth of every
+  // source's links in quarter-size chunks: an item ends at a workgroup barrier where the
+  // waves that are done wait for the last repair (~10 % of the wave time at 8 items per
+  // workgroup, OPENR_SPF_WHATIF_TAIL), so items are large while the queue is long and small
+  // at its end, where the workgroups must finish together. WAN step 3.486 -> 3.375 ms
+  // (IPW 8 / no tail split -> 3 / 20 % / 4, interleaved; r06)
+  const uint32_t ipw = bfs::env_u32("OPENR_SPF_WHATIF_IPW", 3u, 1u, 64u);
+  uint64_t cps = (ipw * slots0 + n_src - 1u) / n_src;
   cps = std::max<uint64_t>(1u, std::min<uint64_t>(cps, n_links));
   uint32_t chunk = (uint32_t)((n_links + cps - 1u) / cps);
   chunk = std::min(chunk, kGrpMaxChunk);
   const uint32_t lds = layout_bytes(lg, waves, chunk);  // the list sized to the chunk
   const uint64_t slots = slots_for(lds);
-  const uint64_t items = (uint64_t)n_src * ((n_links + chunk - 1u) / chunk);
+  // the last part of every source's links in smaller chunks at the queue's end
+  // (OPENR_SPF_WHATIF_TAILFRAC percent, 0: one chunk size; OPENR_SPF_WHATIF_TAILDIV: the split)
+  const uint32_t tail_pct = bfs::env_u32("OPENR_SPF_WHATIF_TAILFRAC", 20u, 0u, 100u);
+  const uint32_t tail_div = bfs::env_u32("OPENR_SPF_WHATIF_TAILDIV", 4u, 1u, 64u);
+  uint32_t lbig = n_links, schunk = chunk;
+  if (tail_pct && tail_div > 1u && chunk >= tail_div) {
+    const uint64_t keep = (uint64_t)n_links * (100u - tail_pct) / 100u;
+    lbig = (uint32_t)(keep / chunk * chunk);
+    schunk = (chunk + tail_div - 1u) / tail_div;
+  }
+  const uint64_t items = (uint64_t)n_src * ((lbig + chunk - 1u) / chunk) +
+                         (lbig < n_links ? (uint64_t)n_src * ((n_links - lbig + schunk - 1u) / schunk) : 0u);
   if (items >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(slots, items);
   // tuning aid: per-phase cycle sums and set sizes, printed after the launch
   static unsigned long long* prof_buf = nullptr;
   unsigned long long* prof = nullptr;
   if (prof_enabled()) {
-    const size_t words = 16u + 2u * kGrpProfWg;
+    const size_t words = 16u + 2u * kGrpProfWg + 4u * 8u * 65536u;  // + per-item stamps (<= 64 K items x 8 waves)
     if (!prof_buf && hipMalloc(&prof_buf, words * sizeof(unsigned long long)) != hipSuccess) prof_buf = nullptr;
     prof = prof_buf;
     if (prof) {
@@ -1531,7 +1568,8 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
     err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,    \
                               (int)lds);                                                                       \
     if (err != hipSuccess) return err;                                                                         \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, base_dist, \
+    hipLaunchKernelGGL(k, dim3(grid), dim3(block), lds, s, g, links, n_links, sources, n_src, chunk, lbig, schunk, \
+                       base_dist, \
                        base_nh, base_tight, tin, nb, (uint32_t)unit_cost, cap, heavy_first, changed_t, affected,     \
                        ovf_src, ovf_link,                                                                      \
                        ovf_unit, ctr, prof, dl);                                                               \
@@ -1586,6 +1624,23 @@ hipError_t launch_whatif_group(const DevGraph& g, const uint32_t* links, uint32_
         std::sort(ends.begin(), ends.end());
         std::sort(starts.begin(), starts.end());
         const double span = (double)(t1 - t0) / 100.0;
+        if (items <= 65536u) {
+          const size_t ns = (size_t)items * waves * 4u;
+          std::vector<unsigned long long> it(ns);
+          if (hipMemcpy(it.data(), prof + 16 + 2 * kGrpProfWg, ns * sizeof(unsigned long long), hipMemcpyDeviceToHost) ==
+              hipSuccess) {
+            double st = 0, un = 0, wt = 0, n = 0;
+            for (size_t q = 0; q + 3 < ns; q += 4) {
+              if (!it[q] || !it[q + 3]) continue;
+              st += (double)(it[q + 1] - it[q]);
+              un += (double)(it[q + 2] - it[q + 1]);
+              wt += (double)(it[q + 3] - it[q + 2]);
+              n += 1;
+            }
+            if (n) std::fprintf(stderr, "whatif_group items: %llu items, per wave-item cycles: stage+filter %.0f, units %.0f, barrier wait %.0f\n",
+                                (unsigned long long)items, st / n, un / n, wt / n);
+          }
+        }
         std::fprintf(stderr,
                      "whatif_group tail: span %.1f us, workgroups %u; starts p50 %.1f p90 %.1f max %.1f; ends p10 %.1f "
                      "p50 %.1f p90 %.1f p99 %.1f max %.1f us; workgroup-time / (span x resident %u) %.3f\n",

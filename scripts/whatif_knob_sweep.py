@@ -1,6 +1,7 @@
 """Interleaved A/B of a what-if tuning knob on the config-4 WAN (tuning aid).
 
   python scripts/whatif_knob_sweep.py OPENR_SPF_WHATIF_CAP 96,128,160,192 [rounds] [steps]
+  python scripts/whatif_knob_sweep.py - "A=1+B=2,A=4+B=0" ...   (several variables per value)
 
 Every round runs each value once, `steps` timed steps each. For each value the script prints
 the median step time and the median repair-kernel time. The `changed` rows of every value
@@ -41,7 +42,12 @@ step_ms = {v: [] for v in values}
 kern_ms = {v: [] for v in values}
 for r in range(rounds):
     for v in values:
-        os.environ[knob] = v
+        if knob == "-":
+            for kv in v.split("+"):
+                name, val = kv.split("=", 1)
+                os.environ[name] = val
+        else:
+            os.environ[knob] = v
         run()
         torch.cuda.synchronize()
         if ref is None:

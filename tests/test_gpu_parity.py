@@ -533,15 +533,20 @@ def whatif_oracle(g, links, sources, use_metric=True):
     return out
 
 
-@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "group-cap1", "incr", "solve"])
+@pytest.fixture(params=["group", "group-lds", "group-d32", "group-cap", "group-cap1", "group-items", "incr", "solve"])
 def whatif_mode(request, monkeypatch):
     """What-if units repaired from LDS-staged base rows per (source, link chunk) workgroup
     (default: graph read from global memory, u16 distances when they fit; or the graph
     staged in LDS too; or u32 / u64 distances), per-unit incremental repair, or full
     re-solves. group-cap: 3 dirty slots per wave, so most units are re-solved; group-cap1:
     1 slot, so nearly every affected unit takes the seeded re-solve (the rounds kernel
-    starting from the base rows)."""
+    starting from the base rows); group-items: 1 item per workgroup and 60 % of each
+    source's links in the queue's tail as third-size chunks (the split's bounds)."""
     mode = request.param
+    if mode == "group-items":
+        monkeypatch.setenv("OPENR_SPF_WHATIF_IPW", "1")
+        monkeypatch.setenv("OPENR_SPF_WHATIF_TAILFRAC", "60")
+        monkeypatch.setenv("OPENR_SPF_WHATIF_TAILDIV", "3")
     if mode == "group-lds":
         monkeypatch.setenv("OPENR_SPF_WHATIF_LDSG", "1")
     if mode == "group-d32":
