@@ -120,6 +120,26 @@ def test_grid_overload_toggle_benchmark_loop(eng):
         np.testing.assert_array_equal(nh, base_n)
 
 
+@pytest.mark.parametrize("delta", ["1", "0"], ids=["delta8", "ellv"])
+def test_grid_link_patches_lean_rows(eng, monkeypatch, delta):
+    """Links going down and up on a grid, solved by the lean level pass from each form of
+    its rows (byte deltas, 16-byte rows): the patched rows (a down link's slot becomes
+    delta 0) and the refreshed rows equal the oracle's."""
+    monkeypatch.setenv("OPENR_SPF_BFS_WAVE", "0")
+    monkeypatch.setenv("OPENR_SPF_LEAN_DELTA", delta)
+    g = T.grid_fast(40)
+    eng.set_graph(g)
+    srcs = np.arange(g.num_nodes, dtype=np.uint32)
+    dist, nh, _ = eng.solve(srcs, True)
+    rng = np.random.default_rng(int(delta) + 11)
+    sample = rng.choice(g.num_nodes, 16, replace=False).tolist()
+    for step in range(3):
+        lk = rng.choice(g.num_links, 6, replace=False)
+        eng.patch(links=lk, link_up=np.full(len(lk), step % 2, np.uint8))
+        eng.refresh(srcs, dist, nh)
+        check_rows(eng, eng.g, srcs, dist, nh, None, oracle_rows=sample)
+
+
 def test_fabric_rsw_overload_toggle(eng):
     """BM_DecisionFabric update loop (RoutingBenchmarkUtils.cpp:407-446): an RSW's overload
     bit affects only sources that transit it (SSWs, FSWs), not the RSWs."""
