@@ -293,6 +293,45 @@ static void ringShortestPath(bool v4, bool lfa) {
   validateAdjLabelRoutes(m, "4", r.db4.adjacencies);
 }
 
+// DecisionRouteDb::calculateUpdate's MPLS half as verifyRouteInUpdateNoDelete uses it
+// (DecisionTest.cpp:1785-1799): `label` is updated exactly once and nothing is withdrawn.
+static DecisionRouteDb mplsUpdateNoDelete(SpfSolver& solver, Ring& r, const char* node, int32_t label,
+                                          const DecisionRouteDb& comp) {
+  auto db = solver.buildRouteDb(node, r.als, r.ps).value();
+  int updates = 0;
+  for (const auto& [l, e] : db.mplsRoutes) {
+    auto it = comp.mplsRoutes.find(l);
+    if (l == label && (it == comp.mplsRoutes.end() || !(it->second.nexthops == e.nexthops))) ++updates;
+  }
+  size_t deletes = 0;
+  for (const auto& kv : comp.mplsRoutes) deletes += db.mplsRoutes.count(kv.first) ? 0 : 1;
+  EXPECT_EQ(updates, 1);
+  EXPECT_EQ(deletes, 0u);
+  return db;
+}
+
+TEST_GPU(SimpleRing_DuplicateMplsRoutes) {  // DecisionTest.cpp:1946-1993
+  Ring r(false, false);
+  SpfSolver solver("1", false, false);
+  const uint64_t dup0 = solver.counters().duplicate_node_label;
+  r.db1.nodeLabel = 2;  // node 1 now shares node 2's label
+  r.als.at(kDefaultArea).updateAdjacencyDatabase(r.db1);
+  const DecisionRouteDb empty;
+  for (auto node : {"1", "2", "3"}) mplsUpdateNoDelete(solver, r, node, 2, empty);
+  EXPECT_EQ(dup0 + 3, solver.counters().duplicate_node_label);  // one collision noticed per build
+  auto comp1 = solver.buildRouteDb("1", r.als, r.ps).value();
+  auto comp2 = solver.buildRouteDb("2", r.als, r.ps).value();
+  auto comp3 = solver.buildRouteDb("3", r.als, r.ps).value();
+  EXPECT_EQ(dup0 + 6, solver.counters().duplicate_node_label);
+  for (auto* db : {&comp1, &comp2, &comp3}) EXPECT_EQ(db->mplsRoutes.count(1), 0u);  // label 1 is unused
+  r.db1.nodeLabel = 1;  // back to distinct labels: label 2 changes owner, nothing withdrawn
+  r.als.at(kDefaultArea).updateAdjacencyDatabase(r.db1);
+  mplsUpdateNoDelete(solver, r, "1", 2, comp1);
+  mplsUpdateNoDelete(solver, r, "2", 2, comp2);
+  mplsUpdateNoDelete(solver, r, "3", 2, comp3);
+  EXPECT_EQ(dup0 + 6, solver.counters().duplicate_node_label);
+}
+
 TEST_GPU(SimpleRing_ShortestPathTest_v6) { ringShortestPath(false, false); }
 TEST_GPU(SimpleRing_ShortestPathTest_v4) { ringShortestPath(true, false); }
 TEST_GPU(SimpleRing_MultiPathTest_LFA_v6) { ringShortestPath(false, true); }
