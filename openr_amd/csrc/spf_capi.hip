@@ -806,9 +806,6 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   // the kept list. OPENR_SPF_KSP_SKIP=0: every pair solved and traced (A/B, tests).
   const char* skip_env = std::getenv("OPENR_SPF_KSP_SKIP");
   const bool skip = rows16 && !(skip_env && std::atoi(skip_env) == 0);
-  // tagged rows: the second SPF grows from both ends and writes the path nodes only
-  // (launch_ksp_bidir); OPENR_SPF_KSP_BIDIR=0: the forward, target-bounded solve (A/B, tests)
-  const bool bidir = tagged && ksp_bidir_lds_bytes(V, d.g.L) != 0u && !(std::getenv("OPENR_SPF_KSP_BIDIR") && std::atoi(std::getenv("OPENR_SPF_KSP_BIDIR")) == 0);
   // pairs per chunk from a byte budget for the chunk's rows and ignore slots: 8 GiB of the
   // 288 GB, capped at half the device memory free at the call, and halved again
   // when a reservation still fails. Fabric, 512 sources x all destinations, ms per step by
@@ -841,8 +838,8 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     if ((e2 = d.ksrc.reserve(c)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)c * ctx->nsl_max())) != hipSuccess) return e2;
     if (skip && (e2 = d.kkeep.reserve(c)) != hipSuccess) return e2;
-    if ((e2 = d.kpart.reserve(4u * kMaxClasses)) != hipSuccess) return e2;
-    return d.kretry.reserve(8u + 3u * (size_t)c);
+    if (skip && (e2 = d.kpart.reserve(2u * kMaxClasses)) != hipSuccess) return e2;
+    return d.kretry.reserve(8u + 2u * (size_t)c);
   };
   for (;;) {
     err = reserve_chunk(chunk);
@@ -871,8 +868,6 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     uint32_t* wctr = d.kretry.p + 2;
     uint32_t* rlist1 = d.kretry.p + 8;
     uint32_t* rlist2 = rlist1 + chunk;
-    uint32_t* rlist3 = rlist2 + chunk;  // bidirectional second SPFs handed to the forward kernel
-    uint32_t* rpart3 = d.kpart.p + 2u * kMaxClasses;  // their count as the kCls8 partition
     OPENR_TRY(hipMemsetAsync(rcount, 0, 8u * sizeof(uint32_t), ls));
     // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
@@ -883,8 +878,8 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
                                nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u));
     const uint32_t* keep = nullptr;  // chunk-local pairs left for the second SPF (skip)
     const uint32_t* keep_count = nullptr;
-    if (skip || bidir) OPENR_TRY(hipMemsetAsync(d.kpart.p, 0, 4u * kMaxClasses * sizeof(uint32_t), ls));
     if (skip) {
+      OPENR_TRY(hipMemsetAsync(d.kpart.p, 0, 2u * kMaxClasses * sizeof(uint32_t), ls));
       OPENR_TRY(launch_ksp_select_pairs(d.g, d_sources, d_prow, d_pdst, first, m, d_tok1, d_tok2, tok_cap, d.ksrc.p,
                                         d.kkeep.p, d.kpart.p + kCls8, d.num_cus, ls));
       keep = d.kkeep.p;
@@ -915,13 +910,6 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
     b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
-    if (bidir) {
-      OPENR_TRY(launch_ksp_bidir(d.g, b.sources, b.target, keep, keep_count, m, b.ign_ptr, b.ign_end, b.ign_links,
-                                 b.lvl16, b.lvl_tag << b.lvl_shift, rlist3, rpart3 + kCls8, d.kretry.p + 6,
-                                 d.num_cus, ls));
-      b.perm = rlist3;  // the pairs it handed back (usually none): the forward solve
-      b.part = rpart3;
-    }
     OPENR_TRY(launch(ctx, d, ign_plan, b, ls));
     const uint64_t* r2 = rows16 ? nullptr : d.krows.p;
     const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;

@@ -357,16 +357,6 @@ hipError_t launch_ksp_select_pairs(const DevGraph& g, const uint32_t* sources, c
                                    uint32_t* tok2, uint32_t tok_cap, uint32_t* out_src, uint32_t* list,
                                    uint32_t* count, int num_cus, hipStream_t s);
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg);
-// KSP2 second SPF, bidirectional (round 6): for chunk-local pair k (list[0 .. *list_count)
-// when list is set) the tagged u16 row rows16[k][V] gets (ltag | level) for exactly the
-// nodes on shortest srcs[k] -> tgts[k] paths with ign_links[ign_ptr[k], ign_end[k])
-// ignored; a pair deeper than the byte levels allow is appended to retry_list (count
-// *retry_count) for the forward kernel. work_ctr: zeroed dynamic-scheduling counter.
-uint32_t ksp_bidir_lds_bytes(uint32_t V, uint32_t L);  // 0: the graph does not fit
-hipError_t launch_ksp_bidir(const DevGraph& g, const uint32_t* srcs, const uint32_t* tgts, const uint32_t* list,
-                            const uint32_t* list_count, uint32_t n, const uint32_t* ign_ptr, const uint32_t* ign_end,
-                            const uint32_t* ign_links, uint16_t* rows16, uint32_t ltag, uint32_t* retry_list,
-                            uint32_t* retry_count, uint32_t* work_ctr, int num_cus, hipStream_t s);
 
 // Exact-order kernel (spf_exact.hip): LinkState::runSpf's heap process replayed per solve
 // (one wavefront per solve) for graphs outside the fast kernels' domain — zero or

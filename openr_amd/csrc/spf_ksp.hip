@@ -802,277 +802,6 @@ __global__ __launch_bounds__(256) void ksp_select_pairs(DevGraph g, const uint32
   }
 }
 
-// ---------------------------------------------------------------------------
-// KSP2 second SPF, bidirectional (round 6): runSpf(src, true, ignore) as the k = 2 trace
-// reads it (LinkState.cpp:776-788 -> traceOnePath :398-419). The trace walks tight
-// in-edges back from dest, so it reads only nodes on some shortest src -> dest path (a
-// tight in-neighbour of such a node is on one too); every other node may read unreached.
-// The forward solve settled every node nearer than dest instead — on the fabric ~24 k
-// (RSW -> FSW) to ~74 k (RSW -> SSW) edge checks per pair, nearly all off the paths.
-//
-// Here one workgroup per pair grows a BFS level from src (forward) or from dest
-// (backward, over the same symmetric records: Link::isUp and the ignore set are per
-// link) — whichever frontier has fewer edges — until the two meet. Level-synchronous
-// with no meeting before the last expansion, the meeting gives D = fa + bb exactly
-// (fa / bb = forward / backward depth), and the nodes known to both sides are exactly the
-// path nodes of level fa. The path nodes of lower levels are the forward nodes with a
-// usable edge to a path node one level up (descending), those of higher levels the
-// backward nodes with a usable edge from a path node one level down (ascending). Only
-// path nodes are written (tagged rows: every other entry reads unreached).
-// Transit rules as runSpf: a sink (overloaded node) is reached but never expanded unless
-// it is src; the backward side therefore never enters a sink other than src.
-// Levels are stored as level + 1 in a byte; a side deeper than max_lvl hands the pair
-// to the forward kernel (retry list, SolveArgs::perm / part of class kCls8).
-constexpr uint32_t kBdCtl = 16;
-enum : uint32_t { kBdFTail = 0, kBdBTail = 1, kBdD = 2, kBdWork0 = 3 /* 3 rotating slots */, kBdUnit = 6 };
-
-struct BidirLayout {
-  uint32_t fl, bl, onp, q, ign, lvf, lvb, total;
-};
-__host__ __device__ inline BidirLayout bidir_layout(uint32_t V, uint32_t L) {
-  BidirLayout l;
-  uint32_t off = kBdCtl * 4u;
-  auto take = [&](uint32_t bytes) {
-    const uint32_t o = off;
-    off += (bytes + 15u) & ~15u;
-    return o;
-  };
-  l.fl = take((V + 3u) & ~3u);         // forward level + 1 per node (0: not reached)
-  l.bl = take((V + 3u) & ~3u);         // backward level + 1 per node
-  l.onp = take(4u * ((V + 31u) / 32u));  // path nodes
-  l.q = take(2u * V);                  // forward queue from 0 up, backward from V - 1 down
-  l.ign = take(4u * ((L + 31u) / 32u));
-  l.lvf = take(4u * 257u);             // queue index where each forward level starts
-  l.lvb = take(4u * 257u);
-  l.total = off;
-  return l;
-}
-
-template <int BLOCK, int G>
-__global__ __launch_bounds__(BLOCK) void ksp_bidir_kernel(DevGraph g, const uint32_t* srcs, const uint32_t* tgts,
-                                                         const uint32_t* list, const uint32_t* list_count,
-                                                         uint32_t n, const uint32_t* ign_ptr, const uint32_t* ign_end,
-                                                         const uint32_t* ign_links, uint16_t* rows16, uint32_t ltag,
-                                                         uint32_t max_lvl, uint32_t* retry_list,
-                                                         uint32_t* retry_count, uint32_t* work_ctr) {
-  static_assert(BLOCK % 64 == 0 && 64 % G == 0, "groups of G lanes inside a wavefront");
-  constexpr uint32_t NG = BLOCK / G;  // frontier nodes per pass
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t V = g.V, L = g.L, tid = threadIdx.x, lane = __lane_id();
-  const BidirLayout lay = bidir_layout(V, L);
-  char* base = reinterpret_cast<char*>(smem);
-  uint32_t* ctl = smem;
-  uint32_t* flw = reinterpret_cast<uint32_t*>(base + lay.fl);
-  uint32_t* blw = reinterpret_cast<uint32_t*>(base + lay.bl);
-  uint32_t* onp = reinterpret_cast<uint32_t*>(base + lay.onp);
-  uint16_t* q = reinterpret_cast<uint16_t*>(base + lay.q);
-  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
-  uint32_t* lvf = reinterpret_cast<uint32_t*>(base + lay.lvf);
-  uint32_t* lvb = reinterpret_cast<uint32_t*>(base + lay.lvb);
-  const uint32_t vw4 = (V + 3u) / 4u, vw32 = (V + 31u) / 32u, lw = (L + 31u) / 32u;
-  const uint32_t grp = tid / G, lg = tid % G;
-  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << (G & 63)) - 1ull)) << ((lane / G) * G);
-  auto byte_of = [](const uint32_t* w, uint32_t v) { return (w[v >> 2] >> (8u * (v & 3u))) & 0xFFu; };
-  const uint32_t units = list ? *list_count : n;
-  for (uint32_t unit = blockIdx.x; unit < units;) {
-    const uint32_t k = list ? list[unit] : unit;
-    const uint32_t s = srcs[k], d = tgts[k];
-    uint16_t* lrow = rows16 + (size_t)k * V;
-    if (s < V && d < V) {  // block-uniform
-      for (uint32_t i = tid; i < vw4; i += BLOCK) {
-        flw[i] = 0;
-        blw[i] = 0;
-      }
-      for (uint32_t i = tid; i < vw32; i += BLOCK) onp[i] = 0;
-      for (uint32_t i = tid; i < lw; i += BLOCK) ign[i] = 0;
-      if (tid < kBdCtl && tid != kBdUnit) ctl[tid] = 0;
-      __syncthreads();
-      for (uint32_t i = ign_ptr[k] + tid, e = ign_end[k]; i < e; i += BLOCK) {
-        const uint32_t l = ign_links[i];
-        if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
-      }
-      if (tid == 0) {
-        atomicOr(&flw[s >> 2], 1u << (8u * (s & 3u)));
-        atomicOr(&blw[d >> 2], 1u << (8u * (d & 3u)));
-        q[0] = (uint16_t)s;
-        q[V - 1u] = (uint16_t)d;  // V == 1: s == d, both slots the same node
-        ctl[kBdFTail] = 1;
-        ctl[kBdBTail] = 1;
-        ctl[kBdD] = s == d ? 0u : 0xFFFFFFFFu;
-        lvf[0] = 0;
-        lvf[1] = 1;
-        lvb[0] = 0;
-        lvb[1] = 1;
-      }
-      __syncthreads();
-      const uint2 rs0 = g.row2[s], rd0 = g.row2[d];
-      uint32_t fa = 0, bb = 0, fhead = 0, ftail = 1, bhead = 0, btail = 1;
-      uint32_t fwork = rs0.y - rs0.x, bwork = rd0.y - rd0.x, step = 0;
-      uint32_t D = __builtin_amdgcn_readfirstlane(ctl[kBdD]);
-      bool overflow = false, last_fwd = false;  // block-uniform
-      while (D == 0xFFFFFFFFu && fhead < ftail && bhead < btail) {
-        const bool fwd = fwork <= bwork;
-        const uint32_t depth = fwd ? fa : bb;
-        if (depth + 1u > max_lvl) {
-          overflow = true;
-          break;
-        }
-        const uint32_t nv = depth + 2u;  // stored value of the new level
-        uint32_t* mine = fwd ? flw : blw;
-        const uint32_t* other = fwd ? blw : flw;
-        uint32_t* work = &ctl[kBdWork0 + step % 3u];
-        if (tid == 0) ctl[kBdWork0 + (step + 1u) % 3u] = 0;  // last read two barriers ago
-        const uint32_t head = fwd ? fhead : bhead, tail = fwd ? ftail : btail;
-        for (uint32_t b0 = head; b0 < tail; b0 += NG) {
-          const uint32_t idx = b0 + grp;
-          uint32_t beg = 0, end = 0;
-          if (idx < tail) {
-            const uint32_t u = q[fwd ? idx : V - 1u - idx];
-            const uint2 r = g.row2[u];
-            beg = r.x;
-            end = r.y;
-          }
-          for (uint32_t e = beg + lg; __any(e < end); e += G) {
-            bool app = false;
-            uint32_t v = 0;
-            if (e < end) {
-              const uint4 rec = g.erec[e];  // u->v: {v | down | v overloaded, ., link, .}
-              v = rec.x & ~(kEdgeDown | kNodeSink);
-              const bool sink = (rec.x & kNodeSink) != 0u;
-              // backward: v would transit on the way to dest, so it must be able to expand
-              if (!(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && (fwd || !sink || v == s)) {
-                const uint32_t sh = 8u * (v & 3u);
-                if (((mine[v >> 2] >> sh) & 0xFFu) == 0u) {
-                  const uint32_t old = atomicOr(&mine[v >> 2], nv << sh);
-                  if (((old >> sh) & 0xFFu) == 0u) {  // first arrival (all arrivals write nv)
-                    const uint32_t ob = (other[v >> 2] >> sh) & 0xFFu;
-                    if (ob) atomicMin(&ctl[kBdD], (nv - 1u) + (ob - 1u));  // the sides meet at v
-                    else app = fwd ? !sink : true;  // a forward sink is reached, never expanded
-                  }
-                }
-              }
-            }
-            const uint32_t slot = wave_append(app, &ctl[fwd ? kBdFTail : kBdBTail]);
-            if (app) {
-              q[fwd ? slot : V - 1u - slot] = (uint16_t)v;
-              const uint2 rv = g.row2[v];
-              atomicAdd(work, rv.y - rv.x);
-            }
-          }
-        }
-        __syncthreads();
-        const uint32_t nt = __builtin_amdgcn_readfirstlane(ctl[fwd ? kBdFTail : kBdBTail]);
-        const uint32_t nwork = __builtin_amdgcn_readfirstlane(*work);
-        D = __builtin_amdgcn_readfirstlane(ctl[kBdD]);
-        if (fwd) {
-          fhead = ftail;
-          ftail = nt;
-          fwork = nwork;
-          ++fa;
-          if (tid == 0) lvf[fa + 1u] = nt;
-        } else {
-          bhead = btail;
-          btail = nt;
-          bwork = nwork;
-          ++bb;
-          if (tid == 0) lvb[bb + 1u] = nt;
-        }
-        last_fwd = fwd;
-        ++step;
-      }
-      if (overflow) {
-        if (tid == 0) retry_list[atomicAdd(retry_count, 1u)] = k;
-        __builtin_amdgcn_wave_barrier();
-      } else if (D != 0xFFFFFFFFu) {
-        // level fa: the nodes both sides know (the segment of the side not expanded last)
-        if (D == 0u) {
-          if (tid == 0) {
-            atomicOr(&onp[s >> 5], 1u << (s & 31u));
-            lrow[s] = (uint16_t)ltag;
-          }
-          __builtin_amdgcn_wave_barrier();
-        } else {
-          const uint32_t h = last_fwd ? bhead : fhead, t = last_fwd ? btail : ftail;
-          for (uint32_t i = h + tid; i < t; i += BLOCK) {
-            const uint32_t v = q[last_fwd ? V - 1u - i : i];
-            if (byte_of(last_fwd ? flw : blw, v)) {
-              atomicOr(&onp[v >> 5], 1u << (v & 31u));
-              lrow[v] = (uint16_t)(ltag | fa);
-            }
-          }
-        }
-        __syncthreads();
-        // levels fa - 1 .. 0: forward nodes with a usable edge to a path node one level up
-        // (rows are symmetric; a queued node may expand)
-        for (uint32_t l = fa; l-- > 0u;) {
-          const uint32_t h = __builtin_amdgcn_readfirstlane(lvf[l]), t = __builtin_amdgcn_readfirstlane(lvf[l + 1u]);
-          for (uint32_t b0 = h; b0 < t; b0 += NG) {
-            const uint32_t idx = b0 + grp;
-            uint32_t u = 0, beg = 0, end = 0;
-            if (idx < t) {
-              u = q[idx];
-              const uint2 r = g.row2[u];
-              beg = r.x;
-              end = r.y;
-            }
-            bool hit = false;
-            for (uint32_t e = beg + lg; __any(e < end && !hit); e += G) {
-              bool x = false;
-              if (e < end && !hit) {
-                const uint4 rec = g.erec[e];
-                const uint32_t w = rec.x & ~(kEdgeDown | kNodeSink);
-                x = !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && test_bit(onp, w) && byte_of(flw, w) == l + 2u;
-              }
-              const bool gh = (__ballot(x) & gmask) != 0u;  // the whole wave ballots
-              hit = hit || gh;
-            }
-            if (hit && lg == 0u) {
-              atomicOr(&onp[u >> 5], 1u << (u & 31u));
-              lrow[u] = (uint16_t)(ltag | l);
-            }
-          }
-          __syncthreads();
-        }
-        // levels fa + 1 .. D (backward levels bb - 1 .. 0): backward nodes with a usable
-        // edge from a path node one level down (that node is src or not overloaded)
-        for (uint32_t j = bb; j-- > 0u;) {
-          const uint32_t h = __builtin_amdgcn_readfirstlane(lvb[j]), t = __builtin_amdgcn_readfirstlane(lvb[j + 1u]);
-          for (uint32_t b0 = h; b0 < t; b0 += NG) {
-            const uint32_t idx = b0 + grp;
-            uint32_t x0 = 0, beg = 0, end = 0;
-            if (idx < t) {
-              x0 = q[V - 1u - idx];
-              const uint2 r = g.row2[x0];
-              beg = r.x;
-              end = r.y;
-            }
-            bool hit = false;
-            for (uint32_t e = beg + lg; __any(e < end && !hit); e += G) {
-              bool x = false;
-              if (e < end && !hit) {
-                const uint4 rec = g.erec[e];
-                const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-                x = !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && test_bit(onp, u) && byte_of(blw, u) == j + 2u;
-              }
-              const bool gh = (__ballot(x) & gmask) != 0u;  // the whole wave ballots
-              hit = hit || gh;
-            }
-            if (hit && lg == 0u) {
-              atomicOr(&onp[x0 >> 5], 1u << (x0 & 31u));
-              lrow[x0] = (uint16_t)(ltag | (D - j));
-            }
-          }
-          __syncthreads();
-        }
-      }
-    }
-    __syncthreads();  // every thread is done with this pair's LDS before the next one's zeroing
-    if (tid == 0) ctl[kBdUnit] = gridDim.x + atomicAdd(work_ctr, 1u);
-    __syncthreads();
-    unit = __builtin_amdgcn_readfirstlane(ctl[kBdUnit]);
-  }
-}
-
 }  // namespace
 
 // A u16 copy of the pair's distance row in LDS was measured slower on the fabric (fewer
@@ -1177,37 +906,6 @@ hipError_t launch_ksp_select_pairs(const DevGraph& g, const uint32_t* sources, c
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((n + 255u) / 256u, (uint32_t)num_cus * 8u));
   hipLaunchKernelGGL(ksp_select_pairs, dim3(grid), dim3(256), 0, s, g, sources, prow, pdst, first, n, tok1, tok2,
                      tok_cap, out_src, list, count);
-  return hipGetLastError();
-}
-
-}  // namespace openr_spf
-
-namespace openr_spf {
-
-uint32_t ksp_bidir_lds_bytes(uint32_t V, uint32_t L) {
-  const uint32_t t = bidir_layout(V, L).total;
-  return V <= 65535u && t <= kMaxLds ? t : 0u;
-}
-
-hipError_t launch_ksp_bidir(const DevGraph& g, const uint32_t* srcs, const uint32_t* tgts, const uint32_t* list,
-                            const uint32_t* list_count, uint32_t n, const uint32_t* ign_ptr, const uint32_t* ign_end,
-                            const uint32_t* ign_links, uint16_t* rows16, uint32_t ltag, uint32_t* retry_list,
-                            uint32_t* retry_count, uint32_t* work_ctr, int num_cus, hipStream_t s) {
-  if (!n) return hipSuccess;
-  const uint32_t lds = ksp_bidir_lds_bytes(g.V, g.L);
-  if (!lds || !work_ctr || !retry_list || !retry_count) return hipErrorInvalidValue;
-  // OPENR_SPF_KSP_BIDIR_LVL (tests): a smaller depth cap sends pairs to the forward re-run
-  const uint32_t max_lvl = bfs::env_u32("OPENR_SPF_KSP_BIDIR_LVL", 254u, 1u, 254u);
-  const uint32_t gl = bfs::env_u32("OPENR_SPF_KSP_BIDIR_G", 16u, 4u, 64u);  // lanes per frontier node (tuning)
-  auto k = gl == 4 ? ksp_bidir_kernel<256, 4> : gl == 8 ? ksp_bidir_kernel<256, 8>
-         : gl == 32 ? ksp_bidir_kernel<256, 32> : gl == 64 ? ksp_bidir_kernel<256, 64> : ksp_bidir_kernel<256, 16>;
-  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-  if (err != hipSuccess) return err;
-  const uint32_t grid = blocks_for(n, lds, num_cus, 256u);
-  note_launch("ksp_bidir_kernel");
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, s, g, srcs, tgts, list, list_count, n, ign_ptr, ign_end,
-                     ign_links, rows16, ltag, max_lvl, retry_list, retry_count, work_ctr);
   return hipGetLastError();
 }
 

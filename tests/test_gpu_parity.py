@@ -978,34 +978,3 @@ def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip, resume, pull, p
     check_ksp2_against_oracle(eng, gf, [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (400, 2))])
     gr = random_graph(77, 90, 140, 1, p_ovl=0.08, p_down=0.08, p_par=0.2)
     check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 3) for d in range(gr.num_nodes)])
-
-
-@pytest.mark.parametrize("mode", [{}, {"OPENR_SPF_KSP_BIDIR": "0"}, {"OPENR_SPF_KSP_BIDIR_LVL": "1"},
-                                  {"OPENR_SPF_KSP_BIDIR_LVL": "2"}, {"OPENR_SPF_KSP_BIDIR_G": "4"},
-                                  {"OPENR_SPF_KSP_BIDIR_G": "64"}, {"OPENR_SPF_KSP_SKIP": "0"}],
-                         ids=["bidir", "forward", "depth1-retry", "depth2-retry", "g4", "g64", "solve-all"])
-def test_ksp2_second_spf_bidirectional(eng, monkeypatch, mode, bfs_family):
-    """The KSP2 second SPF grown from both ends (launch_ksp_bidir): only the nodes on
-    shortest src -> dest paths get tagged levels, which is all the k = 2 trace reads.
-    Against the oracle on the fabric (RSW / FSW / SSW endpoints), the fabric with sinks and
-    down links, leaves and hubs of a random uniform-cost multigraph, the small parallel /
-    down / overloaded graphs, and pairs with src == dest; also with the forward solve, with
-    a depth cap of 1 or 2 levels per side (pairs deeper than that re-run in the forward
-    kernel), other lanes-per-node widths, and with every pair solved (no skip list)."""
-    for k, v in mode.items():
-        monkeypatch.setenv(k, v)
-    rng = np.random.default_rng(23)
-    g = T.fabric(288 + 2 * 56)
-    V = g.num_nodes
-    pairs = [(int(s), d) for s in rng.integers(0, V, 6) for d in range(0, V, 3)] + [(5, 5), (V - 1, V - 1)]
-    check_ksp2_against_oracle(eng, g, pairs)
-    if mode.get("OPENR_SPF_KSP_BIDIR") != "0" and bfs_family[0] == "code":  # tagged rows: code family only
-        assert "ksp_bidir_kernel" in eng.last_kernels()
-    gf, ovl = fabric_with_faults(4)
-    pairs = [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (300, 2))]
-    pairs += [(int(rng.integers(0, gf.num_nodes)), int(x)) for x in ovl] + [(int(x), int(rng.integers(0, gf.num_nodes))) for x in ovl]
-    check_ksp2_against_oracle(eng, gf, pairs)
-    gr = random_graph(91, 120, 260, 1, p_ovl=0.08, p_down=0.08, p_par=0.2)
-    check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 7) for d in range(gr.num_nodes)])
-    for gs in skip_edge_graphs()[:4]:
-        check_ksp2_against_oracle(eng, gs, [(s, d) for s in range(gs.num_nodes) for d in range(gs.num_nodes)])
