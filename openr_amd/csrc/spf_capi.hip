@@ -99,6 +99,8 @@ struct Device {
   DevBuf<uint32_t> kign, kend, ksrc, kptr, kstatus, kin_src, kin_row, kin_dst, ktok1, ktok2, kq;
   DevBuf<uint32_t> kretry;  // KSP small-tier overflows: [0,1] counts (k = 1, k = 2), lists after
   DevBuf<uint32_t> kkeep, kpart;  // KSP pairs that need a second SPF; its count as a class partition
+  DevBuf<uint32_t> ktloff;  // KSP2 k = 1: per base row, pathLinks list offsets [V + 1]
+  DevBuf<uint2> ktlent;     // ... and entries [E] (launch_ksp_path_lists)
   // what-if delta output of the host form (openr_spf_whatif_delta): per-unit pool offsets,
   // the pool (node, distance, next-hop bytes) and its cursor
   DevBuf<uint32_t> dl_off, dl_node;
@@ -790,6 +792,21 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   a.ovf_list = d.ovf.p;
   a.work = d.work.p;
   OPENR_TRY(launch(ctx, d, base_plan, a, s));
+  // uniform cost: the base rows' pathLinks as lists, read by the k = 1 trace's frames
+  // (a list read instead of a record row plus its tails' distances); up to 16 GiB
+  const uint32_t* tl_off = nullptr;
+  const uint2* tl_ent = nullptr;
+  if (base_plan.bfs && base_plan.cost && ksp_path_lists_ok(d.g) &&
+      (size_t)n_src * d.g.E * sizeof(uint2) <= (size_t(16) << 30)) {
+    if (d.ktloff.reserve((size_t)n_src * (V + 1u)) == hipSuccess &&
+        d.ktlent.reserve((size_t)n_src * d.g.E) == hipSuccess) {
+      OPENR_TRY(launch_ksp_path_lists(d.g, d_sources, n_src, d.kbase.p, d.ktloff.p, d.ktlent.p, d.num_cus, s));
+      tl_off = d.ktloff.p;
+      tl_ent = d.ktlent.p;
+    } else {
+      (void)hipGetLastError();  // no room: the trace gathers from the records
+    }
+  }
   const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
   // uniform-cost second SPFs on the code family are distance-only: u16 level rows, tagged
   // (SolveArgs::lvl_tag: a solve writes only the nodes it settles — it stops at the pair's
@@ -872,10 +889,10 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, nullptr, nullptr, rlist1,
-                               rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u));
+                               rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent));
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, rlist1, rcount, nullptr,
-                               nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u));
+                               nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent));
     const uint32_t* keep = nullptr;  // chunk-local pairs left for the second SPF (skip)
     const uint32_t* keep_count = nullptr;
     if (skip) {
@@ -1105,6 +1122,8 @@ void openr_spf_destroy(openr_spf_ctx* ctx) {
     d.perm.release();
     d.part.release();
     d.kkeep.release();
+    d.ktloff.release();
+    d.ktlent.release();
     d.kpart.release();
     d.dl_off.release();
     d.dl_node.release();

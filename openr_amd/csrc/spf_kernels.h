@@ -342,7 +342,17 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             const uint16_t* rows16 = nullptr,  // kind 2: u16 level rows (SolveArgs::lvl16)
                             uint64_t lcost = 0,   // instead of `rows`: dist = level * lcost; non-zero lcost
                                                   // also marks a uniform-cost graph (rank by name / edge)
-                            uint32_t ltag = 0);   // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
+                            uint32_t ltag = 0,    // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
+                            // kind 1, uniform cost: the sources' pathLinks lists (launch_ksp_path_lists),
+                            // row prow[pair] of each, instead of gathering from the records and rows
+                            const uint32_t* tl_off = nullptr, const uint2* tl_ent = nullptr);
+// The k = 1 trace's pathLinks lists: for base row j (source sources[j], distances rows[j]),
+// off[j][0 .. V] (V + 1 u32) and ent[j][off[v] .. off[v + 1]) = node v's tight in-edges in
+// rank order as {u->v edge, link | u << 16} (ent holds E entries per source). Needs
+// DevGraph::erecs and ids below 2^16 (ksp_path_lists_ok; OPENR_SPF_KSP_TL=0 turns it off).
+bool ksp_path_lists_ok(const DevGraph& g);
+hipError_t launch_ksp_path_lists(const DevGraph& g, const uint32_t* sources, uint32_t n_src, const uint64_t* rows,
+                                 uint32_t* off, uint2* ent, int num_cus, hipStream_t s);
 uint32_t ksp_stats_count();  // counters a stats buffer holds (OPENR_SPF_PROF tuning only)
 uint32_t ksp_max_grid(const DevGraph& g, int num_cus);  // qbuf must hold ksp_max_grid * (V + ceil(V / 32)) u32
 hipError_t launch_strided_iota(uint32_t* p, uint32_t n, uint32_t stride, int num_cus, hipStream_t s);

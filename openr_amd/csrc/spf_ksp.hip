@@ -129,6 +129,10 @@ struct KspState {
   const uint16_t* l16;  // non-null: the pair's row is u16 levels (0xFFFF unreached), dist = level * lcost
   uint64_t lcost;       // non-zero: every usable edge costs lcost (uniform-cost graph)
   uint32_t ltag, lshift;  // ltag != 0: l16 entries are ltag << lshift | level, other tags unreached
+  // k = 1 (round 6): the source's pathLinks as lists (ksp_path_lists_kernel): node v's tight
+  // in-edges in rank order are tl_ent[tl_off[v], tl_off[v + 1]) = {u->v edge, link | u << 16}
+  const uint32_t* tl_off;
+  const uint2* tl_ent;
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -284,7 +288,44 @@ __device__ __forceinline__ void rank_against(uint64_t m, const PathCand& src, co
 
 __device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_t beg);
 
+// pathLinks(v) from the source's lists: the tight in-edges are already filtered and in
+// rank order, so a frame reads its list (one offset pair, then the entries) and keeps the
+// ones whose link is unvisited and whose tail is not dead, at their ballot positions
+// (no record rows, no distance reads)
+__device__ uint32_t load_path_links_tl(const KspState& st, uint32_t v, uint32_t beg) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t0 = st.stats ? clock64() : 0;
+  const uint32_t b = st.tl_off[v], n = st.tl_off[v + 1u] - b;
+  uint32_t cnt = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    bool ok = false;
+    uint2 t = make_uint2(0u, 0u);
+    if (i < n) {
+      t = st.tl_ent[b + i];
+      ok = !test_bit(st.vis, t.y & 0xFFFFu) && !test_bit(st.dead, t.y >> 16);
+    }
+    const uint64_t m = __ballot(ok);
+    const uint32_t r = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    cnt += (uint32_t)__popcll(m);
+    if (beg + cnt > st.arena_cap) return UINT32_MAX;
+    if (ok) {
+      st.ar_e[beg + r] = t.x;
+      st.ar_l[beg + r] = t.y;
+    }
+  }
+  lds_fence();
+  if (st.stats) {
+    const uint64_t t2 = clock64();
+    stat_add(st, kStEntries, 1);
+    stat_add(st, kStCands, cnt);
+    stat_add(st, kStCycLoad, t2 - t0);
+  }
+  return cnt;
+}
+
 __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg) {
+  if (st.tl_off) return load_path_links_tl(st, v, beg);
   const uint2 r = st.g->row2[v];
   if (r.y - r.x > 2u * kWave) return load_path_links_long(st, v, beg);
   const uint32_t lane = threadIdx.x;
@@ -609,7 +650,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           const uint32_t* list_count, uint32_t* retry_list,
                                                           uint32_t* retry_count, uint32_t* work_ctr,
                                                           const uint16_t* rows16, uint64_t lcost,
-                                                          uint32_t ltag) {
+                                                          uint32_t ltag, const uint32_t* tl_off,
+                                                          const uint2* tl_ent) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay =
@@ -659,6 +701,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     st.src = src;
     st.drow = rows + (size_t)(KIND == 1 ? row : k) * V;
     st.l16 = (KIND == 2 && rows16) ? rows16 + (size_t)k * V : nullptr;
+    st.tl_off = (KIND == 1 && tl_off) ? tl_off + (size_t)row * (V + 1u) : nullptr;
+    st.tl_ent = (KIND == 1 && tl_off) ? tl_ent + (size_t)row * g.E : nullptr;
     st.lcost = lcost;
     st.ltag = ltag >> 8;
     st.lshift = ltag & 0xFFu;
@@ -802,6 +846,90 @@ __global__ __launch_bounds__(256) void ksp_select_pairs(DevGraph g, const uint32
   }
 }
 
+// The k = 1 trace's pathLinks (round 6): per source of the batch, every node's tight
+// in-edges over the base row in rank order (DevGraph::erecs order; uniform cost), as the
+// reference's SpfResult holds them (LinkState.h:203-260, built in runSpf :867-872). Same
+// test as gather_cand_sorted without the pair's visited / dead sets: edge up, tail may
+// expand (the source or not overloaded), dist[u] + w(u->v) == dist[v]. One workgroup per
+// source: counts into off[1 .. V], an exclusive scan over off, then the entries.
+__device__ __forceinline__ bool tl_tight(const DevGraph& g, const uint64_t* drow, uint32_t src, uint4 rec,
+                                         uint64_t dv) {
+  const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+  if ((rec.x & kEdgeDown) || (u != src && (rec.x & kNodeSink))) return false;
+  const uint64_t du = drow[u];
+  return du != kNoKey && du + rec.y == dv;
+}
+
+__global__ __launch_bounds__(256) void ksp_path_lists_kernel(DevGraph g, const uint32_t* sources, uint32_t n_src,
+                                                             const uint64_t* rows, uint32_t* off_all,
+                                                             uint2* ent_all) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t carry;
+  const uint32_t V = g.V, tid = threadIdx.x, lane = __lane_id(), wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (uint32_t j = blockIdx.x; j < n_src; j += gridDim.x) {
+    const uint32_t src = sources[j];
+    const uint64_t* drow = rows + (size_t)j * V;
+    uint32_t* off = off_all + (size_t)j * (V + 1u);
+    uint2* ent = ent_all + (size_t)j * g.E;
+    // counts: one wavefront per node, 64 in-edges per step
+    for (uint32_t v = wave; v < V; v += 4u) {
+      const uint2 r = g.row2[v];
+      const uint64_t dv = drow[v];
+      uint32_t c = 0;
+      for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+        const uint32_t e = e0 + lane;
+        c += (uint32_t)__popcll(__ballot(e < r.y && src < V && tl_tight(g, drow, src, g.erecs[e], dv)));
+      }
+      if (lane == 0) off[v + 1u] = c;
+    }
+    if (tid == 0) {
+      off[0] = 0;
+      carry = 0;
+    }
+    __syncthreads();
+    // inclusive scan of off[1 .. V] in 256-entry chunks
+    for (uint32_t b = 1; b <= V; b += 256u) {
+      const uint32_t i = b + tid;
+      uint32_t x = i <= V ? off[i] : 0u;
+      for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      if (lane == 63u) wsum[wave] = x;
+      __syncthreads();
+      uint32_t pre = carry;
+      for (uint32_t w = 0; w < wave; ++w) pre += wsum[w];
+      if (i <= V) off[i] = x + pre;
+      __syncthreads();
+      if (tid == 255u) carry = x + pre;
+      __syncthreads();
+    }
+    // entries at their scanned positions, in row order
+    for (uint32_t v = wave; v < V; v += 4u) {
+      const uint2 r = g.row2[v];
+      const uint64_t dv = drow[v];
+      uint32_t at = off[v];
+      for (uint32_t e0 = r.x; e0 < r.y; e0 += 64u) {
+        const uint32_t e = e0 + lane;
+        uint4 rec = make_uint4(kEdgeDown, 0u, 0u, 0u);
+        bool t = false;
+        if (e < r.y && src < V) {
+          rec = g.erecs[e];
+          t = tl_tight(g, drow, src, rec, dv);
+        }
+        const uint64_t m = __ballot(t);
+        if (t) {
+          const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+          ent[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              make_uint2(rec.w, rec.z | (u << 16));
+        }
+        at += (uint32_t)__popcll(m);
+      }
+    }
+    __syncthreads();  // off / ent of this source done before the next one's counts
+  }
+}
+
 }  // namespace
 
 // A u16 copy of the pair's distance row in LDS was measured slower on the fabric (fewer
@@ -848,6 +976,18 @@ uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
 
 uint32_t ksp_stats_count() { return kKspStats; }
 
+bool ksp_path_lists_ok(const DevGraph& g) {
+  return g.erecs != nullptr && ksp_pack(g.V, g.L) && bfs::env_u32("OPENR_SPF_KSP_TL", 1u, 0u, 1u) != 0u;
+}
+
+hipError_t launch_ksp_path_lists(const DevGraph& g, const uint32_t* sources, uint32_t n_src, const uint64_t* rows,
+                                 uint32_t* off, uint2* ent, int num_cus, hipStream_t s) {
+  if (!n_src) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>(n_src, (uint32_t)num_cus * 8u);
+  hipLaunchKernelGGL(ksp_path_lists_kernel, dim3(grid), dim3(256), 0, s, g, sources, n_src, rows, off, ent);
+  return hipGetLastError();
+}
+
 uint32_t ksp_lds_bytes(uint32_t V, uint32_t L, uint32_t max_deg) {
   const uint32_t t =
       ksp_layout(V, L, max_deg, kKspMaxDepth, kKspArena, ksp_use_d16(1) || ksp_use_d16(2), ksp_pack(V, L)).total;
@@ -860,8 +1000,9 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
                             const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
                             uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost,
-                            uint32_t ltag) {
+                            uint32_t ltag, const uint32_t* tl_off, const uint2* tl_ent) {
   if (!n) return hipSuccess;
+  if (tl_off && (kind != 1 || !lcost || !g.erecs || !ksp_pack(g.V, g.L))) return hipErrorInvalidValue;
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
   const KspCaps caps = ksp_caps(g, full);
@@ -879,7 +1020,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                      (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1) |
                          (ksp_pack(g.V, g.L) ? 8u : 0u),
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
-                     lcost, ltag);
+                     lcost, ltag, tl_off, tl_ent);
   return hipGetLastError();
 }
 

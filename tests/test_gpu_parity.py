@@ -978,3 +978,29 @@ def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip, resume, pull, p
     check_ksp2_against_oracle(eng, gf, [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (400, 2))])
     gr = random_graph(77, 90, 140, 1, p_ovl=0.08, p_down=0.08, p_par=0.2)
     check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 3) for d in range(gr.num_nodes)])
+
+
+@pytest.mark.parametrize("tier", [{}, {"OPENR_SPF_KSP_SMALL_FRAMES": "3", "OPENR_SPF_KSP_SMALL_ARENA": "8"}],
+                         ids=["tiers", "tiny-small-tier"])
+@pytest.mark.parametrize("tl", ["1", "0"], ids=["path-lists", "record-rows"])
+def test_ksp2_k1_path_lists(eng, monkeypatch, tl, tier):
+    """The k = 1 trace's frames read the source's pathLinks as lists built once per base
+    row (launch_ksp_path_lists: tight in-edges in rank order, the tail's sink rule and the
+    edge's up flag applied) instead of gathering record rows and their tails' distances.
+    Against the oracle with the lists on and off: the fabric with sinks and down links,
+    hub rows of 130 in-edges (lists longer than a wavefront), a uniform-cost random
+    multigraph with parallel links, and a weighted one (no lists: not uniform cost); also
+    with a tiny small tier, so list gathers overflow the arena and re-run in the full tier."""
+    monkeypatch.setenv("OPENR_SPF_KSP_TL", tl)
+    for k, v in tier.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(29)
+    gf, ovl = fabric_with_faults(6)
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (300, 2))]
+    pairs += [(int(x), int(rng.integers(0, gf.num_nodes))) for x in ovl] + [(3, 3)]
+    check_ksp2_against_oracle(eng, gf, pairs)
+    gh = hub_graph(22, V=220, L=500)
+    check_ksp2_against_oracle(eng, gh, [(int(s), h) for h in range(3) for s in rng.integers(0, gh.num_nodes, 40)])
+    for mm in (1, 9):
+        gr = random_graph(93 + mm, 100, 220, mm, p_ovl=0.08, p_down=0.08, p_par=0.2)
+        check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 9) for d in range(gr.num_nodes)])
