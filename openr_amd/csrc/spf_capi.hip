@@ -807,6 +807,13 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
       (void)hipGetLastError();  // no room: the trace gathers from the records
     }
   }
+  // the k = 2 trace also reads them where its pair's row keeps the base distance (same
+  // uniform cost in both solves); OPENR_SPF_KSP_TL2=0: record rows only (A/B, tests)
+  const char* tl2_env = std::getenv("OPENR_SPF_KSP_TL2");
+  const uint32_t* tl2_off = tl_off && ign_plan.bfs && ign_plan.cost == base_plan.cost &&
+                                    !(tl2_env && std::atoi(tl2_env) == 0)
+                                ? tl_off
+                                : nullptr;
   const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
   // uniform-cost second SPFs on the code family are distance-only: u16 level rows, tagged
   // (SolveArgs::lvl_tag: a solve writes only the nodes it settles — it stops at the pair's
@@ -889,10 +896,12 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, nullptr, nullptr, rlist1,
-                               rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent));
+                               rcount, wctr, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent,
+                               d.kbase.p));
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
                                d_tok1, tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst, rlist1, rcount, nullptr,
-                               nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent));
+                               nullptr, wctr + 1, nullptr, base_plan.bfs ? base_plan.cost : 0u, 0u, tl_off, tl_ent,
+                               d.kbase.p));
     const uint32_t* keep = nullptr;  // chunk-local pairs left for the second SPF (skip)
     const uint32_t* keep_count = nullptr;
     if (skip) {
@@ -933,11 +942,11 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, keep, keep_count,
                                rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u,
-                               tagged ? (b.lvl_tag << 8 | lshift) : 0u));
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, rlist2,
                                rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u,
-                               tagged ? (b.lvl_tag << 8 | lshift) : 0u));
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);

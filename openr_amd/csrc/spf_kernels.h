@@ -343,9 +343,12 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint64_t lcost = 0,   // instead of `rows`: dist = level * lcost; non-zero lcost
                                                   // also marks a uniform-cost graph (rank by name / edge)
                             uint32_t ltag = 0,    // rows16 tagged (SolveArgs::lvl_tag): tag << 8 | lvl_shift
-                            // kind 1, uniform cost: the sources' pathLinks lists (launch_ksp_path_lists),
-                            // row prow[pair] of each, instead of gathering from the records and rows
-                            const uint32_t* tl_off = nullptr, const uint2* tl_ent = nullptr);
+                            // uniform cost: the sources' pathLinks lists (launch_ksp_path_lists), row
+                            // prow[pair] of each. Kind 1 reads them instead of gathering from the records
+                            // and rows; kind 2 reads them for the nodes its pair's row leaves at their
+                            // base distance (tl_rows: the base rows the lists were built from)
+                            const uint32_t* tl_off = nullptr, const uint2* tl_ent = nullptr,
+                            const uint64_t* tl_rows = nullptr);
 // The k = 1 trace's pathLinks lists: for base row j (source sources[j], distances rows[j]),
 // off[j][0 .. V] (V + 1 u32) and ent[j][off[v] .. off[v + 1]) = node v's tight in-edges in
 // rank order as {u->v edge, link | u << 16} (ent holds E entries per source). Needs

@@ -133,6 +133,9 @@ struct KspState {
   // in-edges in rank order are tl_ent[tl_off[v], tl_off[v + 1]) = {u->v edge, link | u << 16}
   const uint32_t* tl_off;
   const uint2* tl_ent;
+  // k = 2: the source's base row. Where the pair's second SPF left v's distance as in the
+  // base row, v's tight in-edges are a subset of its base list (see load_path_links)
+  const uint64_t* tl_brow;
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -292,10 +295,11 @@ __device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_
 // rank order, so a frame reads its list (one offset pair, then the entries) and keeps the
 // ones whose link is unvisited and whose tail is not dead, at their ballot positions
 // (no record rows, no distance reads)
-__device__ uint32_t load_path_links_tl(const KspState& st, uint32_t v, uint32_t beg) {
+// CHECK_DV (k = 2): an entry also needs dist[u] + cost == dv in the pair's own row.
+template <bool CHECK_DV>
+__device__ uint32_t load_path_links_tl(const KspState& st, uint32_t beg, uint32_t b, uint32_t n, uint64_t dv) {
   const uint32_t lane = threadIdx.x;
   const uint64_t t0 = st.stats ? clock64() : 0;
-  const uint32_t b = st.tl_off[v], n = st.tl_off[v + 1u] - b;
   uint32_t cnt = 0;
   for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
     const uint32_t i = i0 + lane;
@@ -304,6 +308,10 @@ __device__ uint32_t load_path_links_tl(const KspState& st, uint32_t v, uint32_t 
     if (i < n) {
       t = st.tl_ent[b + i];
       ok = !test_bit(st.vis, t.y & 0xFFFFu) && !test_bit(st.dead, t.y >> 16);
+      if (CHECK_DV && ok) {
+        const uint64_t du = dist_of(st, t.y >> 16);
+        ok = du != kNoKey && du + st.lcost == dv;
+      }
     }
     const uint64_t m = __ballot(ok);
     const uint32_t r = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -325,7 +333,17 @@ __device__ uint32_t load_path_links_tl(const KspState& st, uint32_t v, uint32_t 
 }
 
 __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg) {
-  if (st.tl_off) return load_path_links_tl(st, v, beg);
+  if (st.tl_off) {
+    const uint32_t b = st.tl_off[v], n = st.tl_off[v + 1u] - b;
+    if (!st.tl_brow) return load_path_links_tl<false>(st, beg, b, n, 0);  // k = 1: the base row's own lists
+    // k = 2 (uniform cost c): if the second SPF left dist[v] as in the base row, every
+    // tight in-edge u->v of the pair's row is in v's base list: dist2[u] = dist2[v] - c =
+    // dist1[v] - c, and dist1[u] <= dist2[u] (ignoring links only lengthens) while
+    // dist1[u] >= dist1[v] - c (u is v's neighbour in the base graph too), so dist1[u] =
+    // dist1[v] - c. The list keeps rank order; the pair's own level test filters it.
+    const uint64_t dv = dist_of(st, v);
+    if (dv == st.tl_brow[v]) return load_path_links_tl<true>(st, beg, b, n, dv);
+  }
   const uint2 r = st.g->row2[v];
   if (r.y - r.x > 2u * kWave) return load_path_links_long(st, v, beg);
   const uint32_t lane = threadIdx.x;
@@ -651,7 +669,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t* retry_count, uint32_t* work_ctr,
                                                           const uint16_t* rows16, uint64_t lcost,
                                                           uint32_t ltag, const uint32_t* tl_off,
-                                                          const uint2* tl_ent) {
+                                                          const uint2* tl_ent, const uint64_t* tl_rows) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay =
@@ -701,8 +719,9 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     st.src = src;
     st.drow = rows + (size_t)(KIND == 1 ? row : k) * V;
     st.l16 = (KIND == 2 && rows16) ? rows16 + (size_t)k * V : nullptr;
-    st.tl_off = (KIND == 1 && tl_off) ? tl_off + (size_t)row * (V + 1u) : nullptr;
-    st.tl_ent = (KIND == 1 && tl_off) ? tl_ent + (size_t)row * g.E : nullptr;
+    st.tl_off = tl_off ? tl_off + (size_t)row * (V + 1u) : nullptr;
+    st.tl_ent = tl_off ? tl_ent + (size_t)row * g.E : nullptr;
+    st.tl_brow = (KIND == 2 && tl_off) ? tl_rows + (size_t)row * V : nullptr;
     st.lcost = lcost;
     st.ltag = ltag >> 8;
     st.lshift = ltag & 0xFFu;
@@ -1000,9 +1019,9 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
                             const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
                             uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost,
-                            uint32_t ltag, const uint32_t* tl_off, const uint2* tl_ent) {
+                            uint32_t ltag, const uint32_t* tl_off, const uint2* tl_ent, const uint64_t* tl_rows) {
   if (!n) return hipSuccess;
-  if (tl_off && (kind != 1 || !lcost || !g.erecs || !ksp_pack(g.V, g.L))) return hipErrorInvalidValue;
+  if (tl_off && (!lcost || !g.erecs || !ksp_pack(g.V, g.L) || (kind == 2 && !tl_rows))) return hipErrorInvalidValue;
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
   const KspCaps caps = ksp_caps(g, full);
@@ -1020,7 +1039,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                      (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1) |
                          (ksp_pack(g.V, g.L) ? 8u : 0u),
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
-                     lcost, ltag, tl_off, tl_ent);
+                     lcost, ltag, tl_off, tl_ent, tl_rows);
   return hipGetLastError();
 }
 

@@ -982,7 +982,7 @@ def test_ksp2_empty_second_paths_skipped(eng, monkeypatch, skip, resume, pull, p
 
 @pytest.mark.parametrize("tier", [{}, {"OPENR_SPF_KSP_SMALL_FRAMES": "3", "OPENR_SPF_KSP_SMALL_ARENA": "8"}],
                          ids=["tiers", "tiny-small-tier"])
-@pytest.mark.parametrize("tl", ["1", "0"], ids=["path-lists", "record-rows"])
+@pytest.mark.parametrize("tl", [("1", "1"), ("1", "0"), ("0", "0")], ids=["path-lists-k12", "path-lists-k1", "record-rows"])
 def test_ksp2_k1_path_lists(eng, monkeypatch, tl, tier):
     """The k = 1 trace's frames read the source's pathLinks as lists built once per base
     row (launch_ksp_path_lists: tight in-edges in rank order, the tail's sink rule and the
@@ -990,8 +990,11 @@ def test_ksp2_k1_path_lists(eng, monkeypatch, tl, tier):
     Against the oracle with the lists on and off: the fabric with sinks and down links,
     hub rows of 130 in-edges (lists longer than a wavefront), a uniform-cost random
     multigraph with parallel links, and a weighted one (no lists: not uniform cost); also
-    with a tiny small tier, so list gathers overflow the arena and re-run in the full tier."""
-    monkeypatch.setenv("OPENR_SPF_KSP_TL", tl)
+    with a tiny small tier, so list gathers overflow the arena and re-run in the full tier.
+    The k = 2 trace reads the same lists for nodes its pair's row leaves at their base
+    distance (OPENR_SPF_KSP_TL2), else the record rows."""
+    monkeypatch.setenv("OPENR_SPF_KSP_TL", tl[0])
+    monkeypatch.setenv("OPENR_SPF_KSP_TL2", tl[1])
     for k, v in tier.items():
         monkeypatch.setenv(k, v)
     rng = np.random.default_rng(29)
