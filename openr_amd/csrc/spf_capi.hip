@@ -815,6 +815,9 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
                                 ? tl_off
                                 : nullptr;
   const uint32_t ign_cap = tok_cap;  // the k = 1 paths' links fit their tokens (slot; ends in kend)
+  // the second SPF as a repair of the base rows (launch_ksp_repair): needs the k = 2 lists'
+  // conditions, tagged rows, and a level mask no real level reaches; OPENR_SPF_KSP_REPAIR=0:
+  // the forward, target-bounded solve (A/B, tests)
   // uniform-cost second SPFs on the code family are distance-only: u16 level rows, tagged
   // (SolveArgs::lvl_tag: a solve writes only the nodes it settles — it stops at the pair's
   // target — and the trace reads other entries as unreached) when levels leave >= 2 tag bits
@@ -830,6 +833,9 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
   // the kept list. OPENR_SPF_KSP_SKIP=0: every pair solved and traced (A/B, tests).
   const char* skip_env = std::getenv("OPENR_SPF_KSP_SKIP");
   const bool skip = rows16 && !(skip_env && std::atoi(skip_env) == 0);
+  const char* rep_env = std::getenv("OPENR_SPF_KSP_REPAIR");
+  const bool repair = tagged && tl_off && ign_plan.bfs && ign_plan.cost == base_plan.cost && (1u << lshift) > V && ksp_repair_lds_bytes(V, d.g.L) != 0u &&
+                      !(rep_env && std::atoi(rep_env) == 0);
   // pairs per chunk from a byte budget for the chunk's rows and ignore slots: 8 GiB of the
   // 288 GB, capped at half the device memory free at the call, and halved again
   // when a reservation still fails. Fabric, 512 sources x all destinations, ms per step by
@@ -862,8 +868,8 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     if ((e2 = d.ksrc.reserve(c)) != hipSuccess) return e2;
     if ((e2 = d.ovf.reserve((size_t)c * ctx->nsl_max())) != hipSuccess) return e2;
     if (skip && (e2 = d.kkeep.reserve(c)) != hipSuccess) return e2;
-    if (skip && (e2 = d.kpart.reserve(2u * kMaxClasses)) != hipSuccess) return e2;
-    return d.kretry.reserve(8u + 2u * (size_t)c);
+    if ((e2 = d.kpart.reserve(4u * kMaxClasses)) != hipSuccess) return e2;
+    return d.kretry.reserve(8u + 4u * (size_t)c);
   };
   for (;;) {
     err = reserve_chunk(chunk);
@@ -892,6 +898,9 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     uint32_t* wctr = d.kretry.p + 2;
     uint32_t* rlist1 = d.kretry.p + 8;
     uint32_t* rlist2 = rlist1 + chunk;
+    uint32_t* rlist3 = rlist2 + chunk;  // repaired second SPFs handed to the forward solve
+    uint32_t* rmode = rlist3 + chunk;   // per pair: 0 repaired row, 1 forward row
+    uint32_t* rpart3 = d.kpart.p + 2u * kMaxClasses;  // rlist3's count as the kCls8 partition
     OPENR_TRY(hipMemsetAsync(rcount, 0, 8u * sizeof(uint32_t), ls));
     // small tier (occupancy), then the full tier over the pairs it could not hold
     OPENR_TRY(launch_ksp_trace(1, d.g, d_sources, d_prow, d_pdst, first, m, d.kbase.p, d.kign.p, d.kend.p, ign_cap,
@@ -904,8 +913,8 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
                                d.kbase.p));
     const uint32_t* keep = nullptr;  // chunk-local pairs left for the second SPF (skip)
     const uint32_t* keep_count = nullptr;
+    if (skip || repair) OPENR_TRY(hipMemsetAsync(d.kpart.p, 0, 4u * kMaxClasses * sizeof(uint32_t), ls));
     if (skip) {
-      OPENR_TRY(hipMemsetAsync(d.kpart.p, 0, 2u * kMaxClasses * sizeof(uint32_t), ls));
       OPENR_TRY(launch_ksp_select_pairs(d.g, d_sources, d_prow, d_pdst, first, m, d_tok1, d_tok2, tok_cap, d.ksrc.p,
                                         d.kkeep.p, d.kpart.p + kCls8, d.num_cus, ls));
       keep = d.kkeep.p;
@@ -936,17 +945,27 @@ hipError_t ksp2_on_device(openr_spf_ctx* ctx, Device& d, const Plan& base_plan, 
     b.ovf_list = d.ovf.p;
     b.work = d.work.p;
     b.target = d_pdst + first;  // the k = 2 trace reads nodes no farther than dest
+    if (repair) {
+      OPENR_TRY(launch_ksp_repair(d.g, b.sources, d_prow + first, b.target, keep, keep_count, m, b.ign_ptr, b.ign_end,
+                                  b.ign_links, d.kbase.p, tl_off, base_plan.cost, b.lvl16, b.lvl_tag << b.lvl_shift,
+                                  (1u << b.lvl_shift) - 1u, rmode, rlist3, rpart3 + kCls8, d.kretry.p + 6,
+                                  d.num_cus, ls));
+      b.perm = rlist3;  // the pairs it handed back: the forward solve
+      b.part = rpart3;
+    }
     OPENR_TRY(launch(ctx, d, ign_plan, b, ls));
     const uint64_t* r2 = rows16 ? nullptr : d.krows.p;
     const uint16_t* r16 = rows16 ? d.krows16.p : nullptr;
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, keep, keep_count,
                                rlist2, rcount + 1, wctr + 2, r16, ign_plan.bfs ? ign_plan.cost : 0u,
-                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p));
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p,
+                               repair ? rmode : nullptr));
     OPENR_TRY(launch_ksp_trace(2, d.g, d_sources, d_prow, d_pdst, first, m, r2, d.kign.p, d.kend.p, ign_cap, d_tok2,
                                tok_cap, d.kstatus.p, d.kq.p, d.num_cus, ls, kst ? kst + nst : nullptr, rlist2,
                                rcount + 1, nullptr, nullptr, wctr + 3, r16, ign_plan.bfs ? ign_plan.cost : 0u,
-                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p));
+                               tagged ? (b.lvl_tag << 8 | lshift) : 0u, tl2_off, tl_ent, d.kbase.p,
+                               repair ? rmode : nullptr));
   }
   if (kst) {
     std::vector<unsigned long long> h(2 * nst);

@@ -348,7 +348,25 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             // and rows; kind 2 reads them for the nodes its pair's row leaves at their
                             // base distance (tl_rows: the base rows the lists were built from)
                             const uint32_t* tl_off = nullptr, const uint2* tl_ent = nullptr,
-                            const uint64_t* tl_rows = nullptr);
+                            const uint64_t* tl_rows = nullptr,
+                            // kind 2: rows16 from launch_ksp_repair where rmode[k] == 0 (base fallback)
+                            const uint32_t* rmode = nullptr);
+// KSP2 second SPF as a repair of the base SPF (uniform cost `cost`): for chunk-local pair k
+// (list[0 .. *list_count) when list is set), source srcs[k] of base row prow[k] (base_rows,
+// pathLinks list offsets tl_off: launch_ksp_path_lists), dest tgts[k], ignoring
+// ign_links[ign_ptr[k], ign_end[k]): rows16[k][v] = ltag | level for the nodes whose
+// distance the ignored links change (lmask: unreached or at / beyond dest's level); every
+// other node keeps its base distance (the k = 2 trace's `repaired` mode reads it there).
+// Requires levels < lmask. A pair whose affected set outgrows a cap gets mode[k] = 1 and
+// is appended to retry_list (*retry_count) for the forward solve; else mode[k] = 0.
+// work_ctr: zeroed dynamic-scheduling counter.
+uint32_t ksp_repair_lds_bytes(uint32_t V, uint32_t L);  // 0: the graph does not fit
+hipError_t launch_ksp_repair(const DevGraph& g, const uint32_t* srcs, const uint32_t* prow, const uint32_t* tgts,
+                             const uint32_t* list, const uint32_t* list_count, uint32_t n, const uint32_t* ign_ptr,
+                             const uint32_t* ign_end, const uint32_t* ign_links, const uint64_t* base_rows,
+                             const uint32_t* tl_off, uint64_t cost, uint16_t* rows16, uint32_t ltag, uint32_t lmask,
+                             uint32_t* mode, uint32_t* retry_list, uint32_t* retry_count, uint32_t* work_ctr,
+                             int num_cus, hipStream_t s);
 // The k = 1 trace's pathLinks lists: for base row j (source sources[j], distances rows[j]),
 // off[j][0 .. V] (V + 1 u32) and ent[j][off[v] .. off[v + 1]) = node v's tight in-edges in
 // rank order as {u->v edge, link | u << 16} (ent holds E entries per source). Needs

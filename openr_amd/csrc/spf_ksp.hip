@@ -136,6 +136,9 @@ struct KspState {
   // k = 2: the source's base row. Where the pair's second SPF left v's distance as in the
   // base row, v's tight in-edges are a subset of its base list (see load_path_links)
   const uint64_t* tl_brow;
+  // k = 2 over repaired rows (ksp_repair_kernel): an entry with another tag is the base
+  // distance (this source's base row), level lmask reads as unreached
+  const uint64_t* rbrow;
 };
 
 // dist[u] of the pair's row. With the LDS copy (dist[dest] < 0xFFFF) a saturated entry
@@ -147,6 +150,13 @@ __device__ __forceinline__ uint64_t dist_of(const KspState& st, uint32_t u) {
     return d == 0xFFFFu ? kNoKey : (uint64_t)d;
   }
   if (st.l16) {
+    if (st.rbrow) {  // both loads in flight together
+      const uint32_t l = st.l16[u];
+      const uint64_t b = st.rbrow[u];
+      if ((l >> st.lshift) != st.ltag) return b;
+      const uint32_t m = (1u << st.lshift) - 1u, lev = l & m;
+      return lev == m ? kNoKey : (uint64_t)lev * st.lcost;
+    }
     const uint32_t l = st.l16[u];
     if (st.ltag) return (l >> st.lshift) != st.ltag ? kNoKey : (uint64_t)(l & ((1u << st.lshift) - 1u)) * st.lcost;
     return l == 0xFFFFu ? kNoKey : (uint64_t)l * st.lcost;
@@ -669,7 +679,8 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
                                                           uint32_t* retry_count, uint32_t* work_ctr,
                                                           const uint16_t* rows16, uint64_t lcost,
                                                           uint32_t ltag, const uint32_t* tl_off,
-                                                          const uint2* tl_ent, const uint64_t* tl_rows) {
+                                                          const uint2* tl_ent, const uint64_t* tl_rows,
+                                                          const uint32_t* rmode) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t V = g.V;
   const KspLayout lay =
@@ -722,6 +733,7 @@ __global__ __launch_bounds__(kWave) void ksp_trace_kernel(DevGraph g, const uint
     st.tl_off = tl_off ? tl_off + (size_t)row * (V + 1u) : nullptr;
     st.tl_ent = tl_off ? tl_ent + (size_t)row * g.E : nullptr;
     st.tl_brow = (KIND == 2 && tl_off) ? tl_rows + (size_t)row * V : nullptr;
+    st.rbrow = (KIND == 2 && tl_rows && rmode && rmode[k] == 0u) ? tl_rows + (size_t)row * V : nullptr;
     st.lcost = lcost;
     st.ltag = ltag >> 8;
     st.lshift = ltag & 0xFFu;
@@ -949,6 +961,257 @@ __global__ __launch_bounds__(256) void ksp_path_lists_kernel(DevGraph g, const u
   }
 }
 
+// ---------------------------------------------------------------------------
+// KSP2 second SPF as a repair of the base SPF (round 6). runSpf(src, true, ignore) differs
+// from the memoized getSpfResult(src) (LinkState.cpp:776-788) only where every shortest
+// path used an ignored link. With uniform cost c and base distances B:
+//  * a node is *affected* (its distance grows) iff each of its base pathLinks u->v is
+//    ignored or comes from an affected u. Induction on B: an unaffected node keeps a tight
+//    in-edge from an unaffected node, so its distance stays; an affected node's every
+//    shortest-path predecessor would have to be unaffected and tight, and none is.
+//  * the affected set A is the closure of that rule from the ignored links: each node
+//    counts its base pathLinks lost (ignored, or from a node found affected) against
+//    its list length (the k = 1 lists, ksp_path_lists_kernel) and joins A at zero.
+//  * A's new distances: a BFS over A seeded by its unaffected in-neighbours (B[u] + c),
+//    in increasing level, until dest's level is settled (dest in A) or up to dest's base
+//    level (dest unaffected). Only A is written: tagged level, or `lmask` (no level:
+//    unreached, or not needed — at or beyond dest). The k = 2 trace reads every other
+//    node's distance from the base row (dist_of with KspState::rbrow).
+// On the fabric A is a few nodes to one plane (~120 nodes) where the forward solve
+// expanded 11 k - 74 k edges per pair.
+constexpr uint32_t kRpCtl = 16;
+enum : uint32_t { kRpQTail = 0, kRpMin = 1, kRpUnit = 2 };
+constexpr uint32_t kRpAff = 0xFFu, kRpDone = 0xFEu;  // state byte: 0 unaffected, affected, settled
+constexpr uint32_t kRpNone = 0xFFFFu;                // tent: no level yet
+
+struct RepairLayout {
+  uint32_t cnt, st, ign, q, total;
+};
+__host__ __device__ inline RepairLayout repair_layout(uint32_t V, uint32_t L) {
+  RepairLayout l;
+  uint32_t off = kRpCtl * 4u;
+  auto take = [&](uint32_t bytes) {
+    const uint32_t o = off;
+    off += (bytes + 15u) & ~15u;
+    return o;
+  };
+  l.cnt = take(4u * ((V + 1u) / 2u));  // u16 per node: pathLinks lost; for A, level + 1 (tent)
+  l.st = take((V + 3u) & ~3u);         // u8 per node: state
+  l.ign = take(4u * ((L + 31u) / 32u));
+  l.q = take(2u * V);                  // A in discovery order
+  l.total = off;
+  return l;
+}
+
+__device__ __forceinline__ uint32_t rp_level(uint64_t b, uint64_t cost) {
+  return cost == 1u ? (uint32_t)b : (uint32_t)((double)b / (double)cost);  // exact: b is a multiple
+}
+
+template <int BLOCK, int G>
+__global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uint32_t* srcs, const uint32_t* prow,
+                                                          const uint32_t* tgts, const uint32_t* list,
+                                                          const uint32_t* list_count, uint32_t n,
+                                                          const uint32_t* ign_ptr, const uint32_t* ign_end,
+                                                          const uint32_t* ign_links, const uint64_t* base_rows,
+                                                          const uint32_t* tl_off_all, uint64_t cost,
+                                                          uint16_t* rows16, uint32_t ltag, uint32_t lmask,
+                                                          uint32_t cap, uint32_t* mode, uint32_t* retry_list,
+                                                          uint32_t* retry_count, uint32_t* work_ctr) {
+  static_assert(BLOCK % 64 == 0 && 64 % G == 0, "groups of G lanes inside a wavefront");
+  constexpr uint32_t NG = BLOCK / G;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t V = g.V, L = g.L, tid = threadIdx.x;
+  const RepairLayout lay = repair_layout(V, L);
+  char* base = reinterpret_cast<char*>(smem);
+  uint32_t* ctl = smem;
+  uint32_t* cntw = reinterpret_cast<uint32_t*>(base + lay.cnt);
+  uint16_t* tent = reinterpret_cast<uint16_t*>(base + lay.cnt);
+  uint32_t* stw = reinterpret_cast<uint32_t*>(base + lay.st);
+  uint8_t* stb = reinterpret_cast<uint8_t*>(base + lay.st);
+  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
+  uint16_t* q = reinterpret_cast<uint16_t*>(base + lay.q);
+  const uint32_t cw = (V + 1u) / 2u, sw = (V + 3u) / 4u, lw = (L + 31u) / 32u;
+  const uint32_t grp = tid / G, lg = tid % G;
+  const uint32_t units = list ? *list_count : n;
+  for (uint32_t unit = blockIdx.x; unit < units;) {
+    const uint32_t k = list ? list[unit] : unit;
+    const uint32_t s = srcs[k], d = tgts[k];
+    if (!(s < V && d < V && s != d) && tid == 0) mode[k] = 0u;
+    if (s < V && d < V && s != d) {  // block-uniform (src == dest is never traced)
+      const uint32_t row = prow[k];
+      const uint64_t* B = base_rows + (size_t)row * V;
+      const uint32_t* toff = tl_off_all + (size_t)row * (V + 1u);
+      uint16_t* lrow = rows16 + (size_t)k * V;
+      for (uint32_t i = tid; i < cw; i += BLOCK) cntw[i] = 0;
+      for (uint32_t i = tid; i < sw; i += BLOCK) stw[i] = 0;
+      for (uint32_t i = tid; i < lw; i += BLOCK) ign[i] = 0;
+      if (tid < kRpCtl && tid != kRpUnit) ctl[tid] = 0;
+      __syncthreads();
+      const uint32_t ib = ign_ptr[k], ie = ign_end[k];
+      for (uint32_t i = ib + tid; i < ie; i += BLOCK) {
+        const uint32_t l = ign_links[i];
+        if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
+      }
+      // one lost pathLink of y; the arrival that loses the last one puts y into A
+      auto lose = [&](bool hit, uint32_t y) {
+        bool aff = false;
+        if (hit) {
+          const uint32_t sh = 16u * (y & 1u);
+          const uint32_t old = (atomicAdd(&cntw[y >> 1], 1u << sh) >> sh) & 0xFFFFu;
+          aff = old + 1u == toff[y + 1u] - toff[y];
+          if (aff) atomicOr(&stw[y >> 2], kRpAff << (8u * (y & 3u)));
+        }
+        const uint32_t slot = wave_append(aff, &ctl[kRpQTail]);
+        if (aff) q[slot] = (uint16_t)y;
+      };
+      // the ignored links' base pathLinks (either direction: tail may expand, edge up, tight)
+      for (uint32_t i0 = ib; i0 < ie; i0 += BLOCK / 2u) {
+        const uint32_t i = i0 + tid / 2u;
+        bool hit = false;
+        uint32_t y = 0;
+        if (i < ie) {
+          const uint32_t l = ign_links[i];
+          const uint2 ab = l < L ? g.ledge[l] : make_uint2(UINT32_MAX, UINT32_MAX);
+          if (ab.x != UINT32_MAX) {
+            const uint32_t e = (tid & 1u) ? ab.y : ab.x, r = (tid & 1u) ? ab.x : ab.y;
+            const uint4 re = g.erec[e], rr = g.erec[r];  // e = x->y, r = y->x (its col x, x's sink flag)
+            const uint32_t x = rr.x & ~(kEdgeDown | kNodeSink);
+            y = re.x & ~(kEdgeDown | kNodeSink);
+            if (!(re.x & kEdgeDown) && (x == s || !(rr.x & kNodeSink))) {
+              const uint64_t bx = B[x], by = B[y];
+              hit = bx != kNoKey && bx + cost == by;
+            }
+          }
+        }
+        lose(hit, y);
+      }
+      __syncthreads();
+      // closure: the base pathLinks out of every node put into A
+      uint32_t head = 0, tail = __builtin_amdgcn_readfirstlane(ctl[kRpQTail]);
+      while (head < tail && tail <= cap) {
+        for (uint32_t b0 = head; b0 < tail; b0 += NG) {
+          const uint32_t idx = b0 + grp;
+          uint32_t beg = 0, end = 0;
+          uint64_t bx = 0;
+          if (idx < tail) {
+            const uint32_t x = q[idx];
+            if (!g.ovl[x]) {  // a sink (other than src, never in A) has no pathLinks out
+              const uint2 r = g.row2[x];
+              beg = r.x;
+              end = r.y;
+              bx = B[x];
+            }
+          }
+          for (uint32_t e = beg + lg; __any(e < end); e += G) {
+            bool hit = false;
+            uint32_t y = 0;
+            if (e < end) {
+              const uint4 rec = g.erec[e];
+              y = rec.x & ~(kEdgeDown | kNodeSink);
+              hit = !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && bx + cost == B[y];
+            }
+            lose(hit, y);
+          }
+        }
+        __syncthreads();
+        head = tail;
+        tail = __builtin_amdgcn_readfirstlane(ctl[kRpQTail]);
+      }
+      const uint32_t nA = tail;
+      const bool d_aff = ((stw[d >> 2] >> (8u * (d & 3u))) & 0xFFu) != 0u;
+      const uint64_t bd = B[d];
+      const bool over = nA > cap;  // block-uniform: A outgrew the cap, the forward solve takes the pair
+      if (tid == 0) {
+        mode[k] = over ? 1u : 0u;
+        if (over) retry_list[atomicAdd(retry_count, 1u)] = k;
+      }
+      if (!over && nA && bd != kNoKey) {  // block-uniform; dest unreached in the base: nothing is traced
+        // seeds: each node of A from its unaffected in-neighbours (usable, not ignored, able
+        // to expand): base level + 1, the group's minimum
+        for (uint32_t b0 = 0; b0 < nA; b0 += NG) {
+          const uint32_t idx = b0 + grp;
+          uint32_t y = 0, beg = 0, end = 0;
+          if (idx < nA) {
+            y = q[idx];
+            const uint2 r = g.row2[y];
+            beg = r.x;
+            end = r.y;
+          }
+          uint32_t best = kRpNone;
+          for (uint32_t e = beg + lg; e < end; e += G) {
+            const uint4 rec = g.erec[e];  // y->u, the mirror of u->y
+            const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
+            if (!(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && (u == s || !(rec.x & kNodeSink)) &&
+                stb[u] == 0u) {
+              const uint64_t bu = B[u];
+              if (bu != kNoKey) best = min(best, rp_level(bu, cost) + 2u);  // level + 1, stored + 1
+            }
+          }
+#pragma unroll
+          for (uint32_t m = 1; m < (uint32_t)G; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, (int)m));
+          if (idx < nA && lg == 0u) tent[y] = (uint16_t)min(best, kRpNone);
+        }
+        __syncthreads();
+        // settle A level by level: the smallest open tent, then its nodes relax their A
+        // neighbours; up to dest's base level - 1 (dest unaffected) or dest's own level
+        const uint32_t dlim = d_aff ? 0xFFFFFFFFu : rp_level(bd, cost);  // levels below it are needed
+        for (;;) {
+          if (tid == 0) ctl[kRpMin] = kRpNone;
+          __syncthreads();
+          for (uint32_t i = tid; i < nA; i += BLOCK) {
+            const uint32_t y = q[i];
+            if (stb[y] == kRpAff && tent[y] != kRpNone) atomicMin(&ctl[kRpMin], (uint32_t)tent[y]);
+          }
+          __syncthreads();
+          const uint32_t t = __builtin_amdgcn_readfirstlane(ctl[kRpMin]);  // level + 1
+          if (t == kRpNone || t - 1u >= dlim) break;
+          const bool d_now = d_aff && stb[d] == kRpAff && tent[d] == t;
+          // settle the bucket (its nodes keep tent = t)
+          for (uint32_t b0 = 0; b0 < nA; b0 += NG) {
+            const uint32_t idx = b0 + grp;
+            uint32_t y = 0, beg = 0, end = 0;
+            if (idx < nA) {
+              y = q[idx];
+              if (stb[y] == kRpAff && tent[y] == t) {
+                if (lg == 0u) atomicAnd(&stw[y >> 2], ~((kRpAff ^ kRpDone) << (8u * (y & 3u))));
+                if (!d_now && !g.ovl[y]) {  // relax out of it (a sink does not expand)
+                  const uint2 r = g.row2[y];
+                  beg = r.x;
+                  end = r.y;
+                }
+              }
+            }
+            // (a bucket node of a later pass still reads open with tent == t: never lowered)
+            for (uint32_t e = beg + lg; e < end; e += G) {
+              const uint4 rec = g.erec[e];
+              const uint32_t z = rec.x & ~(kEdgeDown | kNodeSink);
+              if (!(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && stb[z] == kRpAff && tent[z] > t + 1u)
+                tent[z] = (uint16_t)(t + 1u);  // every writer of this level writes the same value
+            }
+          }
+          __syncthreads();
+          if (d_now) break;
+        }
+        // write A: the settled levels below dest's, dest's own, lmask for the rest
+        const uint32_t dl = d_aff ? (stb[d] == kRpDone ? (uint32_t)tent[d] - 1u : 0xFFFFFFFFu) : rp_level(bd, cost);
+        for (uint32_t i = tid; i < nA; i += BLOCK) {
+          const uint32_t y = q[i];
+          uint32_t lev = lmask;
+          if (stb[y] == kRpDone) {
+            const uint32_t l = (uint32_t)tent[y] - 1u;
+            if (l < dl || y == d) lev = l;
+          }
+          lrow[y] = (uint16_t)(ltag | lev);
+        }
+      }
+    }
+    __syncthreads();  // every thread is done with this pair's LDS before the next one's zeroing
+    if (tid == 0) ctl[kRpUnit] = gridDim.x + atomicAdd(work_ctr, 1u);
+    __syncthreads();
+    unit = __builtin_amdgcn_readfirstlane(ctl[kRpUnit]);
+  }
+}
+
 }  // namespace
 
 // A u16 copy of the pair's distance row in LDS was measured slower on the fabric (fewer
@@ -995,6 +1258,36 @@ uint32_t ksp_max_grid(const DevGraph& g, int num_cus) {
 
 uint32_t ksp_stats_count() { return kKspStats; }
 
+uint32_t ksp_repair_lds_bytes(uint32_t V, uint32_t L) {
+  const uint32_t t = repair_layout(V, L).total;
+  return V < 65535u && t <= kMaxLds ? t : 0u;
+}
+
+hipError_t launch_ksp_repair(const DevGraph& g, const uint32_t* srcs, const uint32_t* prow, const uint32_t* tgts,
+                             const uint32_t* list, const uint32_t* list_count, uint32_t n, const uint32_t* ign_ptr,
+                             const uint32_t* ign_end, const uint32_t* ign_links, const uint64_t* base_rows,
+                             const uint32_t* tl_off, uint64_t cost, uint16_t* rows16, uint32_t ltag, uint32_t lmask,
+                             uint32_t* mode, uint32_t* retry_list, uint32_t* retry_count, uint32_t* work_ctr,
+                             int num_cus, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (!mode || !retry_list || !retry_count) return hipErrorInvalidValue;
+  // a pair whose affected set outgrows the cap is solved forward (OPENR_SPF_KSP_REPAIR_CAP)
+  const uint32_t cap = bfs::env_u32("OPENR_SPF_KSP_REPAIR_CAP", 128u, 0u, 1u << 30);
+  const uint32_t lds = ksp_repair_lds_bytes(g.V, g.L);
+  if (!lds || !work_ctr || !cost) return hipErrorInvalidValue;
+  const uint32_t gl = bfs::env_u32("OPENR_SPF_KSP_REPAIR_G", 16u, 4u, 64u);  // lanes per node (tuning)
+  auto k = gl == 4 ? ksp_repair_kernel<256, 4> : gl == 8 ? ksp_repair_kernel<256, 8>
+         : gl == 32 ? ksp_repair_kernel<256, 32> : gl == 64 ? ksp_repair_kernel<256, 64> : ksp_repair_kernel<256, 16>;
+  hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+  if (err != hipSuccess) return err;
+  note_launch("ksp_repair_kernel");
+  hipLaunchKernelGGL(k, dim3(blocks_for(n, lds, num_cus, 256u)), dim3(256), lds, s, g, srcs, prow, tgts, list,
+                     list_count, n, ign_ptr, ign_end, ign_links, base_rows, tl_off, cost, rows16, ltag, lmask, cap,
+                     mode, retry_list, retry_count, work_ctr);
+  return hipGetLastError();
+}
+
 bool ksp_path_lists_ok(const DevGraph& g) {
   return g.erecs != nullptr && ksp_pack(g.V, g.L) && bfs::env_u32("OPENR_SPF_KSP_TL", 1u, 0u, 1u) != 0u;
 }
@@ -1019,9 +1312,11 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                             uint32_t* qbuf, int num_cus, hipStream_t s, unsigned long long* stats,
                             const uint32_t* list, const uint32_t* list_count, uint32_t* retry_list,
                             uint32_t* retry_count, uint32_t* work_ctr, const uint16_t* rows16, uint64_t lcost,
-                            uint32_t ltag, const uint32_t* tl_off, const uint2* tl_ent, const uint64_t* tl_rows) {
+                            uint32_t ltag, const uint32_t* tl_off, const uint2* tl_ent, const uint64_t* tl_rows,
+                            const uint32_t* rmode) {
   if (!n) return hipSuccess;
   if (tl_off && (!lcost || !g.erecs || !ksp_pack(g.V, g.L) || (kind == 2 && !tl_rows))) return hipErrorInvalidValue;
+  if (rmode && (kind != 2 || !tl_rows || !rows16 || !ltag)) return hipErrorInvalidValue;
   if (!work_ctr) return hipErrorInvalidValue;
   const bool full = retry_list == nullptr;  // the small tier hands overflows to a full-tier re-run
   const KspCaps caps = ksp_caps(g, full);
@@ -1039,7 +1334,7 @@ hipError_t launch_ksp_trace(int kind, const DevGraph& g, const uint32_t* sources
                      (ksp_use_d16(kind) ? 1u : 0u) | (bfs::env_u32("OPENR_SPF_KSP_RESUME", 1u, 0u, 1u) << 1) |
                          (ksp_pack(g.V, g.L) ? 8u : 0u),
                      stats, caps.frames, caps.arena, list, list_count, retry_list, retry_count, work_ctr, rows16,
-                     lcost, ltag, tl_off, tl_ent, tl_rows);
+                     lcost, ltag, tl_off, tl_ent, tl_rows, rmode);
   return hipGetLastError();
 }
 

@@ -1007,3 +1007,42 @@ def test_ksp2_k1_path_lists(eng, monkeypatch, tl, tier):
     for mm in (1, 9):
         gr = random_graph(93 + mm, 100, 220, mm, p_ovl=0.08, p_down=0.08, p_par=0.2)
         check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 9) for d in range(gr.num_nodes)])
+
+
+@pytest.mark.parametrize("mode", [{}, {"OPENR_SPF_KSP_REPAIR": "0"}, {"OPENR_SPF_KSP_REPAIR_G": "4"},
+                                  {"OPENR_SPF_KSP_REPAIR_G": "64"}, {"OPENR_SPF_KSP_SKIP": "0"},
+                                  {"OPENR_SPF_KSP_TL2": "0"}, {"OPENR_SPF_KSP_CHUNK": "7"},
+                                  {"OPENR_SPF_KSP_REPAIR_CAP": "0"}, {"OPENR_SPF_KSP_REPAIR_CAP": "6"}],
+                         ids=["repair", "forward", "g4", "g64", "solve-all", "k2-record-rows", "chunks-of-7",
+                              "cap0-all-forward", "cap6-mixed"])
+def test_ksp2_second_spf_repair(eng, monkeypatch, mode, bfs_family):
+    """The KSP2 second SPF as a repair of the base SPF (launch_ksp_repair): the nodes whose
+    every base pathLink is ignored or comes from such a node get new levels (a BFS over
+    them seeded by their unaffected neighbours, up to dest's level); the k = 2 trace reads
+    every other node's distance from the base row. Against the oracle on the fabric (RSW,
+    FSW and SSW endpoints, src == dest), the fabric with sinks and down links, a
+    uniform-cost random multigraph with parallel links, the small parallel / down /
+    overloaded graphs and hub rows; with the forward solve, other lanes-per-node widths,
+    every pair solved, the k = 2 record-row gather, chunks of 7 pairs (tags wrap), and
+    affected-set caps of 0 and 6 nodes (pairs over the cap are solved forward, and the
+    trace reads each pair's row in its own form)."""
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(31)
+    g = T.fabric(288 + 2 * 56)
+    V = g.num_nodes
+    pairs = [(int(s), d) for s in rng.integers(0, V, 5) for d in range(0, V, 3)] + [(5, 5)]
+    pairs += [(s, int(d)) for s in range(0, 16 * 2 + 16, 7) for d in rng.integers(0, V, 30)]  # SSW / FSW sources
+    check_ksp2_against_oracle(eng, g, pairs)
+    if mode.get("OPENR_SPF_KSP_REPAIR") != "0" and bfs_family[0] == "code":  # tagged rows: code family only
+        assert "ksp_repair_kernel" in eng.last_kernels()
+    gf, ovl = fabric_with_faults(8)
+    pairs = [(int(a), int(b)) for a, b in rng.integers(0, gf.num_nodes, (300, 2))]
+    pairs += [(int(rng.integers(0, gf.num_nodes)), int(x)) for x in ovl] + [(int(x), int(rng.integers(0, gf.num_nodes))) for x in ovl]
+    check_ksp2_against_oracle(eng, gf, pairs)
+    gr = random_graph(97, 120, 260, 1, p_ovl=0.08, p_down=0.08, p_par=0.2)
+    check_ksp2_against_oracle(eng, gr, [(s, d) for s in range(0, gr.num_nodes, 7) for d in range(gr.num_nodes)])
+    for gs in skip_edge_graphs()[:5]:
+        check_ksp2_against_oracle(eng, gs, [(s, d) for s in range(gs.num_nodes) for d in range(gs.num_nodes)])
+    gh = hub_graph(23, V=220, L=500)
+    check_ksp2_against_oracle(eng, gh, [(h, int(d)) for h in range(3) for d in rng.integers(0, gh.num_nodes, 30)])
