@@ -980,12 +980,17 @@ __global__ __launch_bounds__(256) void ksp_path_lists_kernel(DevGraph g, const u
 // On the fabric A is a few nodes to one plane (~120 nodes) where the forward solve
 // expanded 11 k - 74 k edges per pair.
 constexpr uint32_t kRpCtl = 16;
-enum : uint32_t { kRpQTail = 0, kRpMin = 1, kRpUnit = 2 };
-constexpr uint32_t kRpAff = 0xFFu, kRpDone = 0xFEu;  // state byte: 0 unaffected, affected, settled
-constexpr uint32_t kRpNone = 0xFFFFu;                // tent: no level yet
+enum : uint32_t { kRpQTail = 0, kRpMin = 1, kRpUnit = 2, kRpOvf = 3 };
+constexpr uint32_t kRpNone = 0xFFFFu;  // tent: no level yet
+constexpr uint32_t kRpMaxCap = 254u;   // A's index + 1 fits the node's state byte
 
+// LDS of one pair: per node a lost-pathLink count (u8; a node with more than 255 base
+// pathLinks hands the pair to the forward solve) and a state byte (0: unaffected, else
+// its index in A + 1); the ignore bitmap; per A entry its node, tentative level + 1, and a
+// settled flag. A is capped (kRpMaxCap), so the per-A arrays are small: ~17 KB per pair
+// on the fabric, 9 pairs per CU.
 struct RepairLayout {
-  uint32_t cnt, st, ign, q, total;
+  uint32_t cnt, st, ign, q, tent, done, total;
 };
 __host__ __device__ inline RepairLayout repair_layout(uint32_t V, uint32_t L) {
   RepairLayout l;
@@ -995,10 +1000,12 @@ __host__ __device__ inline RepairLayout repair_layout(uint32_t V, uint32_t L) {
     off += (bytes + 15u) & ~15u;
     return o;
   };
-  l.cnt = take(4u * ((V + 1u) / 2u));  // u16 per node: pathLinks lost; for A, level + 1 (tent)
-  l.st = take((V + 3u) & ~3u);         // u8 per node: state
+  l.cnt = take((V + 3u) & ~3u);
+  l.st = take((V + 3u) & ~3u);
   l.ign = take(4u * ((L + 31u) / 32u));
-  l.q = take(2u * V);                  // A in discovery order
+  l.q = take(2u * kRpMaxCap);
+  l.tent = take(2u * kRpMaxCap);
+  l.done = take(kRpMaxCap);
   l.total = off;
   return l;
 }
@@ -1025,12 +1032,13 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
   uint32_t* cntw = reinterpret_cast<uint32_t*>(base + lay.cnt);
-  uint16_t* tent = reinterpret_cast<uint16_t*>(base + lay.cnt);
   uint32_t* stw = reinterpret_cast<uint32_t*>(base + lay.st);
   uint8_t* stb = reinterpret_cast<uint8_t*>(base + lay.st);
   uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
   uint16_t* q = reinterpret_cast<uint16_t*>(base + lay.q);
-  const uint32_t cw = (V + 1u) / 2u, sw = (V + 3u) / 4u, lw = (L + 31u) / 32u;
+  uint16_t* tent = reinterpret_cast<uint16_t*>(base + lay.tent);
+  uint8_t* done = reinterpret_cast<uint8_t*>(base + lay.done);
+  const uint32_t vw = (V + 3u) / 4u, lw = (L + 31u) / 32u;
   const uint32_t grp = tid / G, lg = tid % G;
   const uint32_t units = list ? *list_count : n;
   for (uint32_t unit = blockIdx.x; unit < units;) {
@@ -1042,8 +1050,10 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
       const uint64_t* B = base_rows + (size_t)row * V;
       const uint32_t* toff = tl_off_all + (size_t)row * (V + 1u);
       uint16_t* lrow = rows16 + (size_t)k * V;
-      for (uint32_t i = tid; i < cw; i += BLOCK) cntw[i] = 0;
-      for (uint32_t i = tid; i < sw; i += BLOCK) stw[i] = 0;
+      for (uint32_t i = tid; i < vw; i += BLOCK) {
+        cntw[i] = 0;
+        stw[i] = 0;
+      }
       for (uint32_t i = tid; i < lw; i += BLOCK) ign[i] = 0;
       if (tid < kRpCtl && tid != kRpUnit) ctl[tid] = 0;
       __syncthreads();
@@ -1056,13 +1066,19 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
       auto lose = [&](bool hit, uint32_t y) {
         bool aff = false;
         if (hit) {
-          const uint32_t sh = 16u * (y & 1u);
-          const uint32_t old = (atomicAdd(&cntw[y >> 1], 1u << sh) >> sh) & 0xFFFFu;
-          aff = old + 1u == toff[y + 1u] - toff[y];
-          if (aff) atomicOr(&stw[y >> 2], kRpAff << (8u * (y & 3u)));
+          const uint32_t tin = toff[y + 1u] - toff[y];
+          if (tin > 255u) {
+            ctl[kRpOvf] = 1u;  // the u8 count cannot hold it
+          } else {
+            const uint32_t sh = 8u * (y & 3u);
+            aff = ((atomicAdd(&cntw[y >> 2], 1u << sh) >> sh) & 0xFFu) + 1u == tin;
+          }
         }
         const uint32_t slot = wave_append(aff, &ctl[kRpQTail]);
-        if (aff) q[slot] = (uint16_t)y;
+        if (aff && slot < cap) {
+          q[slot] = (uint16_t)y;
+          stb[y] = (uint8_t)(slot + 1u);
+        }
       };
       // the ignored links' base pathLinks (either direction: tail may expand, edge up, tight)
       for (uint32_t i0 = ib; i0 < ie; i0 += BLOCK / 2u) {
@@ -1118,9 +1134,9 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
         tail = __builtin_amdgcn_readfirstlane(ctl[kRpQTail]);
       }
       const uint32_t nA = tail;
-      const bool d_aff = ((stw[d >> 2] >> (8u * (d & 3u))) & 0xFFu) != 0u;
+      const uint32_t di = stb[d];  // dest's index in A + 1, 0: unaffected
       const uint64_t bd = B[d];
-      const bool over = nA > cap;  // block-uniform: A outgrew the cap, the forward solve takes the pair
+      const bool over = nA > cap || ctl[kRpOvf] != 0u;  // block-uniform: the forward solve takes the pair
       if (tid == 0) {
         mode[k] = over ? 1u : 0u;
         if (over) retry_list[atomicAdd(retry_count, 1u)] = k;
@@ -1130,10 +1146,9 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
         // to expand): base level + 1, the group's minimum
         for (uint32_t b0 = 0; b0 < nA; b0 += NG) {
           const uint32_t idx = b0 + grp;
-          uint32_t y = 0, beg = 0, end = 0;
+          uint32_t beg = 0, end = 0;
           if (idx < nA) {
-            y = q[idx];
-            const uint2 r = g.row2[y];
+            const uint2 r = g.row2[q[idx]];
             beg = r.x;
             end = r.y;
           }
@@ -1149,56 +1164,55 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
           }
 #pragma unroll
           for (uint32_t m = 1; m < (uint32_t)G; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, (int)m));
-          if (idx < nA && lg == 0u) tent[y] = (uint16_t)min(best, kRpNone);
+          if (idx < nA && lg == 0u) {
+            tent[idx] = (uint16_t)min(best, kRpNone);
+            done[idx] = 0;
+          }
         }
         __syncthreads();
         // settle A level by level: the smallest open tent, then its nodes relax their A
         // neighbours; up to dest's base level - 1 (dest unaffected) or dest's own level
-        const uint32_t dlim = d_aff ? 0xFFFFFFFFu : rp_level(bd, cost);  // levels below it are needed
+        const uint32_t dlim = di ? 0xFFFFFFFFu : rp_level(bd, cost);  // levels below it are needed
         for (;;) {
           if (tid == 0) ctl[kRpMin] = kRpNone;
           __syncthreads();
-          for (uint32_t i = tid; i < nA; i += BLOCK) {
-            const uint32_t y = q[i];
-            if (stb[y] == kRpAff && tent[y] != kRpNone) atomicMin(&ctl[kRpMin], (uint32_t)tent[y]);
-          }
+          if (tid < nA && !done[tid] && tent[tid] != kRpNone) atomicMin(&ctl[kRpMin], (uint32_t)tent[tid]);
           __syncthreads();
           const uint32_t t = __builtin_amdgcn_readfirstlane(ctl[kRpMin]);  // level + 1
           if (t == kRpNone || t - 1u >= dlim) break;
-          const bool d_now = d_aff && stb[d] == kRpAff && tent[d] == t;
-          // settle the bucket (its nodes keep tent = t)
+          const bool d_now = di && !done[di - 1u] && tent[di - 1u] == t;
+          __syncthreads();  // every thread has read done[] before the bucket is marked
           for (uint32_t b0 = 0; b0 < nA; b0 += NG) {
             const uint32_t idx = b0 + grp;
-            uint32_t y = 0, beg = 0, end = 0;
-            if (idx < nA) {
-              y = q[idx];
-              if (stb[y] == kRpAff && tent[y] == t) {
-                if (lg == 0u) atomicAnd(&stw[y >> 2], ~((kRpAff ^ kRpDone) << (8u * (y & 3u))));
-                if (!d_now && !g.ovl[y]) {  // relax out of it (a sink does not expand)
-                  const uint2 r = g.row2[y];
-                  beg = r.x;
-                  end = r.y;
-                }
+            uint32_t beg = 0, end = 0;
+            if (idx < nA && !done[idx] && tent[idx] == t) {
+              if (lg == 0u) done[idx] = 1;
+              const uint32_t y = q[idx];
+              if (!d_now && !g.ovl[y]) {  // relax out of it (a sink does not expand)
+                const uint2 r = g.row2[y];
+                beg = r.x;
+                end = r.y;
               }
             }
             // (a bucket node of a later pass still reads open with tent == t: never lowered)
             for (uint32_t e = beg + lg; e < end; e += G) {
               const uint4 rec = g.erec[e];
               const uint32_t z = rec.x & ~(kEdgeDown | kNodeSink);
-              if (!(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && stb[z] == kRpAff && tent[z] > t + 1u)
-                tent[z] = (uint16_t)(t + 1u);  // every writer of this level writes the same value
+              const uint32_t zi = stb[z];
+              if (zi && !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && !done[zi - 1u] && tent[zi - 1u] > t + 1u)
+                tent[zi - 1u] = (uint16_t)(t + 1u);  // every writer of this level writes the same value
             }
           }
           __syncthreads();
           if (d_now) break;
         }
         // write A: the settled levels below dest's, dest's own, lmask for the rest
-        const uint32_t dl = d_aff ? (stb[d] == kRpDone ? (uint32_t)tent[d] - 1u : 0xFFFFFFFFu) : rp_level(bd, cost);
-        for (uint32_t i = tid; i < nA; i += BLOCK) {
-          const uint32_t y = q[i];
+        const uint32_t dl = di ? (done[di - 1u] ? (uint32_t)tent[di - 1u] - 1u : 0xFFFFFFFFu) : rp_level(bd, cost);
+        if (tid < nA) {
+          const uint32_t y = q[tid];
           uint32_t lev = lmask;
-          if (stb[y] == kRpDone) {
-            const uint32_t l = (uint32_t)tent[y] - 1u;
+          if (done[tid]) {
+            const uint32_t l = (uint32_t)tent[tid] - 1u;
             if (l < dl || y == d) lev = l;
           }
           lrow[y] = (uint16_t)(ltag | lev);
@@ -1272,7 +1286,7 @@ hipError_t launch_ksp_repair(const DevGraph& g, const uint32_t* srcs, const uint
   if (!n) return hipSuccess;
   if (!mode || !retry_list || !retry_count) return hipErrorInvalidValue;
   // a pair whose affected set outgrows the cap is solved forward (OPENR_SPF_KSP_REPAIR_CAP)
-  const uint32_t cap = bfs::env_u32("OPENR_SPF_KSP_REPAIR_CAP", 128u, 0u, 1u << 30);
+  const uint32_t cap = bfs::env_u32("OPENR_SPF_KSP_REPAIR_CAP", 128u, 0u, kRpMaxCap);
   const uint32_t lds = ksp_repair_lds_bytes(g.V, g.L);
   if (!lds || !work_ctr || !cost) return hipErrorInvalidValue;
   const uint32_t gl = bfs::env_u32("OPENR_SPF_KSP_REPAIR_G", 16u, 4u, 64u);  // lanes per node (tuning)
