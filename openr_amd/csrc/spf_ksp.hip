@@ -305,8 +305,10 @@ __device__ uint32_t load_path_links_long(const KspState& st, uint32_t v, uint32_
 // rank order, so a frame reads its list (one offset pair, then the entries) and keeps the
 // ones whose link is unvisited and whose tail is not dead, at their ballot positions
 // (no record rows, no distance reads)
-// CHECK_DV (k = 2): an entry also needs dist[u] + cost == dv in the pair's own row.
-template <bool CHECK_DV>
+// CHECK (k = 2): 1, an entry also needs dist[u] + cost == dv in the pair's own row; 2 (the
+// row repairs the base row, ksp_repair_kernel), u must be unaffected — no entry of this
+// row's tag — since v is, and u is one of v's base pathLinks.
+template <int CHECK>
 __device__ uint32_t load_path_links_tl(const KspState& st, uint32_t beg, uint32_t b, uint32_t n, uint64_t dv) {
   const uint32_t lane = threadIdx.x;
   const uint64_t t0 = st.stats ? clock64() : 0;
@@ -318,10 +320,11 @@ __device__ uint32_t load_path_links_tl(const KspState& st, uint32_t beg, uint32_
     if (i < n) {
       t = st.tl_ent[b + i];
       ok = !test_bit(st.vis, t.y & 0xFFFFu) && !test_bit(st.dead, t.y >> 16);
-      if (CHECK_DV && ok) {
+      if (CHECK == 1 && ok) {
         const uint64_t du = dist_of(st, t.y >> 16);
         ok = du != kNoKey && du + st.lcost == dv;
       }
+      if (CHECK == 2 && ok) ok = (uint32_t)(st.l16[t.y >> 16] >> st.lshift) != st.ltag;
     }
     const uint64_t m = __ballot(ok);
     const uint32_t r = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -345,14 +348,20 @@ __device__ uint32_t load_path_links_tl(const KspState& st, uint32_t beg, uint32_
 __device__ uint32_t load_path_links(const KspState& st, uint32_t v, uint32_t beg) {
   if (st.tl_off) {
     const uint32_t b = st.tl_off[v], n = st.tl_off[v + 1u] - b;
-    if (!st.tl_brow) return load_path_links_tl<false>(st, beg, b, n, 0);  // k = 1: the base row's own lists
-    // k = 2 (uniform cost c): if the second SPF left dist[v] as in the base row, every
-    // tight in-edge u->v of the pair's row is in v's base list: dist2[u] = dist2[v] - c =
-    // dist1[v] - c, and dist1[u] <= dist2[u] (ignoring links only lengthens) while
-    // dist1[u] >= dist1[v] - c (u is v's neighbour in the base graph too), so dist1[u] =
-    // dist1[v] - c. The list keeps rank order; the pair's own level test filters it.
-    const uint64_t dv = dist_of(st, v);
-    if (dv == st.tl_brow[v]) return load_path_links_tl<true>(st, beg, b, n, dv);
+    if (!st.tl_brow) return load_path_links_tl<0>(st, beg, b, n, 0);  // k = 1: the base row's own lists
+    if (st.rbrow) {
+      // repaired row (ksp_repair_kernel): v keeps its base distance iff the row holds no
+      // entry of its tag for v
+      if ((uint32_t)(st.l16[v] >> st.lshift) != st.ltag) return load_path_links_tl<2>(st, beg, b, n, 0);
+    } else {
+      // k = 2 (uniform cost c): if the second SPF left dist[v] as in the base row, every
+      // tight in-edge u->v of the pair's row is in v's base list: dist2[u] = dist2[v] - c =
+      // dist1[v] - c, and dist1[u] <= dist2[u] (ignoring links only lengthens) while
+      // dist1[u] >= dist1[v] - c (u is v's neighbour in the base graph too), so dist1[u] =
+      // dist1[v] - c. The list keeps rank order; the pair's own level test filters it.
+      const uint64_t dv = dist_of(st, v);
+      if (dv == st.tl_brow[v]) return load_path_links_tl<1>(st, beg, b, n, dv);
+    }
   }
   const uint2 r = st.g->row2[v];
   if (r.y - r.x > 2u * kWave) return load_path_links_long(st, v, beg);
