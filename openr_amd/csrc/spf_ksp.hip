@@ -991,15 +991,16 @@ __global__ __launch_bounds__(256) void ksp_path_lists_kernel(DevGraph g, const u
 constexpr uint32_t kRpCtl = 16;
 enum : uint32_t { kRpQTail = 0, kRpMin = 1, kRpUnit = 2, kRpOvf = 3 };
 constexpr uint32_t kRpNone = 0xFFFFu;  // tent: no level yet
-constexpr uint32_t kRpMaxCap = 254u;   // A's index + 1 fits the node's state byte
+constexpr uint32_t kRpMaxCap = 127u;   // A's index fits the node byte's low 7 bits
+constexpr uint32_t kRpHash = 512u;     // ignored-link hash slots (a pair ignoring more goes forward)
 
-// LDS of one pair: per node a lost-pathLink count (u8; a node with more than 255 base
-// pathLinks hands the pair to the forward solve) and a state byte (0: unaffected, else
-// its index in A + 1); the ignore bitmap; per A entry its node, tentative level + 1, and a
-// settled flag. A is capped (kRpMaxCap), so the per-A arrays are small: ~17 KB per pair
-// on the fabric, 9 pairs per CU.
+// LDS of one pair (~8 KB on the fabric, 16 pairs of 128 threads per CU): one byte per
+// node — its lost-pathLink count while unaffected (a node with more than 127 base
+// pathLinks hands the pair to the forward solve), 0x80 | its index in A once in A (no
+// pathLink is lost after the last one); the ignored links as an open-addressing hash;
+// per A entry its node, tentative level + 1 and a settled flag (A is capped).
 struct RepairLayout {
-  uint32_t cnt, st, ign, q, tent, done, total;
+  uint32_t nb, hsh, q, tent, done, total;
 };
 __host__ __device__ inline RepairLayout repair_layout(uint32_t V, uint32_t L) {
   RepairLayout l;
@@ -1009,9 +1010,8 @@ __host__ __device__ inline RepairLayout repair_layout(uint32_t V, uint32_t L) {
     off += (bytes + 15u) & ~15u;
     return o;
   };
-  l.cnt = take((V + 3u) & ~3u);
-  l.st = take((V + 3u) & ~3u);
-  l.ign = take(4u * ((L + 31u) / 32u));
+  l.nb = take((V + 3u) & ~3u);
+  l.hsh = take(4u * kRpHash);
   l.q = take(2u * kRpMaxCap);
   l.tent = take(2u * kRpMaxCap);
   l.done = take(kRpMaxCap);
@@ -1040,14 +1040,21 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
   const RepairLayout lay = repair_layout(V, L);
   char* base = reinterpret_cast<char*>(smem);
   uint32_t* ctl = smem;
-  uint32_t* cntw = reinterpret_cast<uint32_t*>(base + lay.cnt);
-  uint32_t* stw = reinterpret_cast<uint32_t*>(base + lay.st);
-  uint8_t* stb = reinterpret_cast<uint8_t*>(base + lay.st);
-  uint32_t* ign = reinterpret_cast<uint32_t*>(base + lay.ign);
+  uint32_t* nbw = reinterpret_cast<uint32_t*>(base + lay.nb);
+  uint8_t* nb = reinterpret_cast<uint8_t*>(base + lay.nb);
+  uint32_t* hsh = reinterpret_cast<uint32_t*>(base + lay.hsh);
+  auto slot_of = [](uint32_t l) { return (l * 2654435761u) >> 23; };  // 9 bits: kRpHash
+  auto is_ign = [&](uint32_t l) {
+    for (uint32_t h = slot_of(l);; h = (h + 1u) & (kRpHash - 1u)) {
+      const uint32_t x = hsh[h];
+      if (x == l) return true;
+      if (x == 0xFFFFFFFFu) return false;
+    }
+  };
   uint16_t* q = reinterpret_cast<uint16_t*>(base + lay.q);
   uint16_t* tent = reinterpret_cast<uint16_t*>(base + lay.tent);
   uint8_t* done = reinterpret_cast<uint8_t*>(base + lay.done);
-  const uint32_t vw = (V + 3u) / 4u, lw = (L + 31u) / 32u;
+  const uint32_t vw = (V + 3u) / 4u;
   const uint32_t grp = tid / G, lg = tid % G;
   const uint32_t units = list ? *list_count : n;
   for (uint32_t unit = blockIdx.x; unit < units;) {
@@ -1059,34 +1066,38 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
       const uint64_t* B = base_rows + (size_t)row * V;
       const uint32_t* toff = tl_off_all + (size_t)row * (V + 1u);
       uint16_t* lrow = rows16 + (size_t)k * V;
-      for (uint32_t i = tid; i < vw; i += BLOCK) {
-        cntw[i] = 0;
-        stw[i] = 0;
-      }
-      for (uint32_t i = tid; i < lw; i += BLOCK) ign[i] = 0;
+      for (uint32_t i = tid; i < vw; i += BLOCK) nbw[i] = 0;
+      for (uint32_t i = tid; i < kRpHash; i += BLOCK) hsh[i] = 0xFFFFFFFFu;
       if (tid < kRpCtl && tid != kRpUnit) ctl[tid] = 0;
       __syncthreads();
       const uint32_t ib = ign_ptr[k], ie = ign_end[k];
-      for (uint32_t i = ib + tid; i < ie; i += BLOCK) {
-        const uint32_t l = ign_links[i];
-        if (l < L) atomicOr(&ign[l >> 5], 1u << (l & 31u));
+      if (ie - ib > kRpHash / 2u) {  // a half-full table at most (short probes)
+        if (tid == 0) ctl[kRpOvf] = 1u;
+      } else {
+        for (uint32_t i = ib + tid; i < ie; i += BLOCK) {
+          const uint32_t l = ign_links[i];
+          for (uint32_t h = slot_of(l);; h = (h + 1u) & (kRpHash - 1u)) {
+            const uint32_t old = atomicCAS(&hsh[h], 0xFFFFFFFFu, l);
+            if (old == 0xFFFFFFFFu || old == l) break;
+          }
+        }
       }
       // one lost pathLink of y; the arrival that loses the last one puts y into A
       auto lose = [&](bool hit, uint32_t y) {
         bool aff = false;
         if (hit) {
           const uint32_t tin = toff[y + 1u] - toff[y];
-          if (tin > 255u) {
-            ctl[kRpOvf] = 1u;  // the u8 count cannot hold it
+          if (tin > 127u) {
+            ctl[kRpOvf] = 1u;  // the count byte cannot hold it
           } else {
             const uint32_t sh = 8u * (y & 3u);
-            aff = ((atomicAdd(&cntw[y >> 2], 1u << sh) >> sh) & 0xFFu) + 1u == tin;
+            aff = ((atomicAdd(&nbw[y >> 2], 1u << sh) >> sh) & 0xFFu) + 1u == tin;
           }
         }
         const uint32_t slot = wave_append(aff, &ctl[kRpQTail]);
         if (aff && slot < cap) {
           q[slot] = (uint16_t)y;
-          stb[y] = (uint8_t)(slot + 1u);
+          nb[y] = (uint8_t)(0x80u | slot);  // no arrival touches y's count after its last loss
         }
       };
       // the ignored links' base pathLinks (either direction: tail may expand, edge up, tight)
@@ -1113,7 +1124,8 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
       __syncthreads();
       // closure: the base pathLinks out of every node put into A
       uint32_t head = 0, tail = __builtin_amdgcn_readfirstlane(ctl[kRpQTail]);
-      while (head < tail && tail <= cap) {
+      const bool ovf0 = __builtin_amdgcn_readfirstlane(ctl[kRpOvf]) != 0u;
+      while (!ovf0 && head < tail && tail <= cap) {
         for (uint32_t b0 = head; b0 < tail; b0 += NG) {
           const uint32_t idx = b0 + grp;
           uint32_t beg = 0, end = 0;
@@ -1133,7 +1145,7 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
             if (e < end) {
               const uint4 rec = g.erec[e];
               y = rec.x & ~(kEdgeDown | kNodeSink);
-              hit = !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && bx + cost == B[y];
+              hit = !(rec.x & kEdgeDown) && bx + cost == B[y] && !is_ign(rec.z);
             }
             lose(hit, y);
           }
@@ -1143,7 +1155,7 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
         tail = __builtin_amdgcn_readfirstlane(ctl[kRpQTail]);
       }
       const uint32_t nA = tail;
-      const uint32_t di = stb[d];  // dest's index in A + 1, 0: unaffected
+      const uint32_t di = nb[d] >= 0x80u ? (nb[d] & 0x7Fu) + 1u : 0u;  // dest's index in A + 1, 0: unaffected
       const uint64_t bd = B[d];
       const bool over = nA > cap || ctl[kRpOvf] != 0u;  // block-uniform: the forward solve takes the pair
       if (tid == 0) {
@@ -1165,8 +1177,8 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
           for (uint32_t e = beg + lg; e < end; e += G) {
             const uint4 rec = g.erec[e];  // y->u, the mirror of u->y
             const uint32_t u = rec.x & ~(kEdgeDown | kNodeSink);
-            if (!(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && (u == s || !(rec.x & kNodeSink)) &&
-                stb[u] == 0u) {
+            if (!(rec.x & kEdgeDown) && (u == s || !(rec.x & kNodeSink)) && nb[u] < 0x80u &&
+                !is_ign(rec.z)) {
               const uint64_t bu = B[u];
               if (bu != kNoKey) best = min(best, rp_level(bu, cost) + 2u);  // level + 1, stored + 1
             }
@@ -1207,9 +1219,9 @@ __global__ __launch_bounds__(BLOCK) void ksp_repair_kernel(DevGraph g, const uin
             for (uint32_t e = beg + lg; e < end; e += G) {
               const uint4 rec = g.erec[e];
               const uint32_t z = rec.x & ~(kEdgeDown | kNodeSink);
-              const uint32_t zi = stb[z];
-              if (zi && !(rec.x & kEdgeDown) && !test_bit(ign, rec.z) && !done[zi - 1u] && tent[zi - 1u] > t + 1u)
-                tent[zi - 1u] = (uint16_t)(t + 1u);  // every writer of this level writes the same value
+              const uint32_t zb = nb[z], zi = zb & 0x7Fu;
+              if (zb >= 0x80u && !(rec.x & kEdgeDown) && !done[zi] && tent[zi] > t + 1u && !is_ign(rec.z))
+                tent[zi] = (uint16_t)(t + 1u);  // every writer of this level writes the same value
             }
           }
           __syncthreads();
@@ -1295,17 +1307,17 @@ hipError_t launch_ksp_repair(const DevGraph& g, const uint32_t* srcs, const uint
   if (!n) return hipSuccess;
   if (!mode || !retry_list || !retry_count) return hipErrorInvalidValue;
   // a pair whose affected set outgrows the cap is solved forward (OPENR_SPF_KSP_REPAIR_CAP)
-  const uint32_t cap = bfs::env_u32("OPENR_SPF_KSP_REPAIR_CAP", 128u, 0u, kRpMaxCap);
+  const uint32_t cap = bfs::env_u32("OPENR_SPF_KSP_REPAIR_CAP", kRpMaxCap, 0u, kRpMaxCap);
   const uint32_t lds = ksp_repair_lds_bytes(g.V, g.L);
   if (!lds || !work_ctr || !cost) return hipErrorInvalidValue;
   const uint32_t gl = bfs::env_u32("OPENR_SPF_KSP_REPAIR_G", 16u, 4u, 64u);  // lanes per node (tuning)
-  auto k = gl == 4 ? ksp_repair_kernel<256, 4> : gl == 8 ? ksp_repair_kernel<256, 8>
-         : gl == 32 ? ksp_repair_kernel<256, 32> : gl == 64 ? ksp_repair_kernel<256, 64> : ksp_repair_kernel<256, 16>;
+  auto k = gl == 4 ? ksp_repair_kernel<128, 4> : gl == 8 ? ksp_repair_kernel<128, 8>
+         : gl == 32 ? ksp_repair_kernel<128, 32> : gl == 64 ? ksp_repair_kernel<128, 64> : ksp_repair_kernel<128, 16>;
   hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
   if (err != hipSuccess) return err;
   note_launch("ksp_repair_kernel");
-  hipLaunchKernelGGL(k, dim3(blocks_for(n, lds, num_cus, 256u)), dim3(256), lds, s, g, srcs, prow, tgts, list,
+  hipLaunchKernelGGL(k, dim3(blocks_for(n, lds, num_cus, 128u)), dim3(128), lds, s, g, srcs, prow, tgts, list,
                      list_count, n, ign_ptr, ign_end, ign_links, base_rows, tl_off, cost, rows16, ltag, lmask, cap,
                      mode, retry_list, retry_count, work_ctr);
   return hipGetLastError();
